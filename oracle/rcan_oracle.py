@@ -1,0 +1,277 @@
+"""CPU oracle for the RCAN / EDSR tiled super-resolution hot path.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module, and only as the
+checker / the timed CPU baseline -- never as the thing measured or shipped.  The
+product path (``srmi``) never imports it and fails loudly when its HIP library
+is missing.
+
+This is a plain PyTorch-CPU restatement (fp32 or fp64) of the reference's
+algorithm, written independently and pinned against golden vectors generated
+from the imported reference (``tests/golden/make_golden.py``):
+
+* RCAN network ......... sres/model/rcan/network.py:7-77, blocks.py:58-76
+* EDSR network ......... sres/model/edsr/network.py:9-32,
+                         sres/model/common/residual.py:26-50, upsample.py:32-66
+* parameter plumbing ... sres/model/common/common.py:9-48 (defaults, scale)
+* default_conv ......... sres/model/common/cnn.py:8-9 (3x3, padding k//2)
+* downsample/upsample .. sres/base/util/array.py:72-87 (bicubic, 'cubic')
+* l2loss (RMSE) ........ sres/controller/stats.py:5-8
+* train step ........... sres/controller/dual_trainer.py:310-323, :557-571
+* Adam ................. torch.optim.Adam defaults used at dual_trainer.py:126
+
+State-dict keys are identical to the reference model's.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+# ---------------------------------------------------------------------------
+# hyper-parameters (sres/model/common/common.py:9-20 defaults;
+# config/model/rcan-10-20-64.yaml values)
+# ---------------------------------------------------------------------------
+COMMON_DEFAULTS = dict(nchannels_in=1, nchannels_out=1, nfeatures=64, kernel_size=3,
+                       nlayers=16, downscale_factors=[2, 2], bias=True, batch_norm=False,
+                       res_scale=1.0, ups_mode="bicubic")
+RCAN_DEFAULTS = dict(cbottleneck=2, nblocks=20)
+
+
+def _conv(cin: int, cout: int, k: int, bias: bool = True) -> nn.Conv2d:
+    # sres/model/common/cnn.py:8-9
+    return nn.Conv2d(cin, cout, k, padding=k // 2, bias=bias)
+
+
+class _CA(nn.Module):
+    """Channel attention: sres/model/rcan/network.py:31-47."""
+
+    def __init__(self, nf: int, reduction: int):
+        super().__init__()
+        self.conv_du = nn.Sequential(nn.Conv2d(nf, nf // reduction, 1, padding=0, bias=True), nn.ReLU(),
+                                     nn.Conv2d(nf // reduction, nf, 1, padding=0, bias=True), nn.Sigmoid())
+
+    def forward(self, x):
+        return x * self.conv_du(x.mean(dim=(2, 3), keepdim=True))
+
+
+class _RCAB(nn.Module):
+    """sres/model/rcan/network.py:50-64 (conv-ReLU-conv-CA + skip)."""
+
+    def __init__(self, nf: int, k: int, reduction: int):
+        super().__init__()
+        self.body = nn.Sequential(_conv(nf, nf, k), nn.ReLU(), _conv(nf, nf, k), _CA(nf, reduction))
+
+    def forward(self, x):
+        return self.body(x) + x
+
+
+class _RG(nn.Module):
+    """sres/model/rcan/network.py:67-77 (nblocks RCAB + conv, skip)."""
+
+    def __init__(self, nf: int, k: int, reduction: int, nblocks: int):
+        super().__init__()
+        self.body = nn.Sequential(*[_RCAB(nf, k, reduction) for _ in range(nblocks)], _conv(nf, nf, k))
+
+    def forward(self, x):
+        return self.body(x) + x
+
+
+def _upsampler(scale: int, nf: int) -> nn.Sequential:
+    """sres/model/rcan/blocks.py:58-76 and sres/model/common/upsample.py:32-66."""
+    m: List[nn.Module] = []
+    if scale & (scale - 1) == 0:
+        for _ in range(int(math.log2(scale))):
+            m += [_conv(nf, 4 * nf, 3), nn.PixelShuffle(2)]
+    elif scale == 3:
+        m += [_conv(nf, 9 * nf, 3), nn.PixelShuffle(3)]
+    else:
+        raise NotImplementedError(scale)
+    return nn.Sequential(*m)
+
+
+def resolve_parms(model: str, **kw) -> Dict:
+    """init_parms (sres/model/common/common.py:22-28): defaults <- model yaml <- kwargs."""
+    p = dict(COMMON_DEFAULTS)
+    if model == "rcan":
+        p.update(RCAN_DEFAULTS)
+    p.update({k: v for k, v in kw.items() if v is not None})
+    p["scale"] = int(math.prod(p["downscale_factors"]))
+    return p
+
+
+class RCANOracle(nn.Module):
+    """RCAN (sres/model/rcan/network.py:7-27) with identical state-dict keys."""
+
+    def __init__(self, **kw):
+        super().__init__()
+        p = resolve_parms("rcan", **kw)
+        self.parms = p
+        nf, k = p["nfeatures"], p["kernel_size"]
+        self.head = nn.Sequential(_conv(p["nchannels_in"], nf, k))
+        self.body = nn.Sequential(*[_RG(nf, k, p["cbottleneck"], p["nblocks"]) for _ in range(p["nlayers"])],
+                                  _conv(nf, nf, k))
+        self.tail = nn.Sequential(_upsampler(p["scale"], nf), _conv(nf, p["nchannels_out"], k))
+
+    def forward(self, x):
+        x = self.head(x)
+        res = self.body(x) + x
+        return self.tail(res)
+
+
+class _ResBlock(nn.Module):
+    """sres/model/common/residual.py:26-50."""
+
+    def __init__(self, nf: int, k: int, res_scale: float):
+        super().__init__()
+        self.body = nn.Sequential(_conv(nf, nf, k), nn.ReLU(), _conv(nf, nf, k))
+        self.res_scale = res_scale
+
+    def forward(self, x):
+        return self.body(x).mul(self.res_scale) + x
+
+
+class EDSROracle(nn.Module):
+    """EDSR (sres/model/edsr/network.py:9-32) with identical state-dict keys."""
+
+    def __init__(self, **kw):
+        super().__init__()
+        p = resolve_parms("edsr", **kw)
+        self.parms = p
+        nf, k = p["nfeatures"], p["kernel_size"]
+        self.head = nn.Sequential(_conv(p["nchannels_in"], nf, k))
+        self.body = nn.Sequential(*[_ResBlock(nf, k, p["res_scale"]) for _ in range(p["nlayers"])],
+                                  _conv(nf, nf, k))
+        self.tail = nn.Sequential(_upsampler(p["scale"], nf), _conv(nf, p["nchannels_out"], k))
+
+    def forward(self, x):
+        x = self.head(x)
+        res = self.body(x) + x
+        return self.tail(res)
+
+
+def build(model: str, **kw) -> nn.Module:
+    return {"rcan": RCANOracle, "edsr": EDSROracle}[model](**kw)
+
+
+# ---------------------------------------------------------------------------
+# deterministic parameter init: the distribution of PyTorch's default Conv2d
+# init (kaiming_uniform a=sqrt(5) -> U(-1/sqrt(fan_in), 1/sqrt(fan_in)); bias
+# the same bound), drawn from numpy RandomState so it is stream-stable.
+# ---------------------------------------------------------------------------
+def init_params_numpy(model: nn.Module, seed: int) -> None:
+    rs = np.random.RandomState(seed)
+    with torch.no_grad():
+        for name, mod in model.named_modules():
+            if isinstance(mod, nn.Conv2d):
+                fan_in = mod.in_channels * mod.kernel_size[0] * mod.kernel_size[1]
+                bound = 1.0 / math.sqrt(fan_in)
+                w = rs.uniform(-bound, bound, size=tuple(mod.weight.shape))
+                mod.weight.copy_(torch.from_numpy(w))
+                if mod.bias is not None:
+                    b = rs.uniform(-bound, bound, size=tuple(mod.bias.shape))
+                    mod.bias.copy_(torch.from_numpy(b))
+
+
+# ---------------------------------------------------------------------------
+# data path pieces on the hot path
+# ---------------------------------------------------------------------------
+def downsample(hr: torch.Tensor, scale: int) -> torch.Tensor:
+    """array.py:72-76: F.interpolate(scale_factor=1/scale, mode='bicubic')."""
+    return F.interpolate(hr, scale_factor=1.0 / scale, mode="bicubic")
+
+
+def downsample_explicit(hr: np.ndarray, scale: int) -> np.ndarray:
+    """Closed form of the bicubic (A=-0.75, align_corners=False) 1/scale
+    resampling: src = scale*d + (scale-1)/2 is exactly half-way between two
+    samples, so each output is the separable 4-tap [-3,19,19,-3]/32 filter over
+    rows/cols scale*d + scale/2 - 2 .. +1 (never clamped for scale >= 4)."""
+    w = np.array([-3.0, 19.0, 19.0, -3.0]) / 32.0
+    B, C, H, W = hr.shape
+    h, wd = H // scale, W // scale
+    o = scale // 2 - 2
+    ys = np.arange(h)[:, None] * scale + o + np.arange(4)[None, :]
+    xs = np.arange(wd)[:, None] * scale + o + np.arange(4)[None, :]
+    rows = np.einsum("bchkx,k->bchx", hr[:, :, ys, :], w)          # [B,C,h,W]
+    return np.einsum("bchwk,k->bchw", rows[:, :, :, xs], w)         # [B,C,h,w]
+
+
+def upsample(lr: torch.Tensor, scale: int) -> torch.Tensor:
+    """array.py:84-87: interp baseline, bicubic xscale."""
+    return F.interpolate(lr, scale_factor=scale, mode="bicubic")
+
+
+def l2loss(prd: torch.Tensor, tar: torch.Tensor, squared: bool = False) -> torch.Tensor:
+    """stats.py:5-8 -- RMSE unless squared."""
+    loss = ((prd - tar) ** 2).mean()
+    return loss if squared else torch.sqrt(loss)
+
+
+def lnorm(x: np.ndarray) -> np.ndarray:
+    """Per-tile, per-channel normalisation to mean 0 / std 1 (ddof 0), the
+    statistics of the reference's 'lnorm' tiles (sres/base/source/swot/raw.py:177-181)."""
+    m = x.mean(axis=(2, 3), keepdims=True)
+    s = x.std(axis=(2, 3), keepdims=True)
+    return (x - m) / s
+
+
+def synthetic_hr(batch: int, nchan: int, size: int, seed: int = 1234) -> np.ndarray:
+    """HR tiles ~ N(0,1) from RandomState(seed), lnorm-normalised."""
+    rs = np.random.RandomState(seed)
+    return lnorm(rs.standard_normal((batch, nchan, size, size))).astype(np.float32)
+
+
+# ---------------------------------------------------------------------------
+# Adam (torch.optim.Adam defaults: betas (0.9,0.999), eps 1e-8, no amsgrad)
+# ---------------------------------------------------------------------------
+class AdamOracle:
+    def __init__(self, params: Sequence[torch.Tensor], lr: float, betas=(0.9, 0.999), eps=1e-8,
+                 weight_decay: float = 0.0):
+        self.params = list(params)
+        self.lr, self.b1, self.b2, self.eps, self.wd = lr, betas[0], betas[1], eps, weight_decay
+        self.m = [torch.zeros_like(p) for p in self.params]
+        self.v = [torch.zeros_like(p) for p in self.params]
+        self.t = 0
+
+    @torch.no_grad()
+    def step(self):
+        self.t += 1
+        bc1 = 1 - self.b1 ** self.t
+        bc2 = 1 - self.b2 ** self.t
+        for p, m, v in zip(self.params, self.m, self.v):
+            g = p.grad
+            if g is None:
+                continue
+            if self.wd != 0:
+                g = g + self.wd * p
+            m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+            v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+            denom = (v.sqrt() / math.sqrt(bc2)).add_(self.eps)
+            p.addcdiv_(m, denom, value=-self.lr / bc1)
+
+    def zero_grad(self):
+        for p in self.params:
+            p.grad = None
+
+
+def train_step(model: nn.Module, opt: AdamOracle, hr: torch.Tensor, scale: int,
+               interp_loss: bool = False) -> Tuple[float, Optional[float], torch.Tensor]:
+    """One step of dual_trainer.py:310-323 with apply_network (:557-571):
+    HR (requires_grad, as array2tensor does) -> downsample -> model -> RMSE ->
+    backward -> Adam.  Returns (loss, interp_loss, output)."""
+    opt.zero_grad()
+    hr = hr.detach().clone().requires_grad_(True)          # array2tensor, array.py:70
+    lr_in = downsample(hr, scale)
+    out = model(lr_in)
+    loss = l2loss(out, hr)
+    iloss = None
+    if interp_loss:
+        with torch.no_grad():
+            iloss = float(l2loss(hr, upsample(lr_in, scale)))
+    loss.backward()
+    opt.step()
+    return float(loss), iloss, out.detach()
