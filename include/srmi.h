@@ -1,0 +1,137 @@
+/* srmi -- MI355X-native (gfx950) engine for the RCAN / EDSR tiled
+ * super-resolution hot path of nasa-nccs-hpda/super-resolution-climate.
+ *
+ * C ABI: plain pointers, sizes and a hipStream_t (passed as void*).  No torch
+ * types.  All device memory is owned by the caller (PyTorch's caching
+ * allocator on the Python side); the library allocates nothing persistent
+ * except what the caller hands it as workspace.  Every entry point returns 0
+ * on success or a negative status (SRMI_ERR_*, or -hipError_t), which the
+ * Python binding raises as RuntimeError (the reference raises Python
+ * exceptions; sres/controller/dual_trainer.py:557 @exception_handled).
+ *
+ * Reference interface each group replaces (paths relative to the reference):
+ *   srmi_param_*, srmi_engine_*  -> sres/model/manager.py:93-96 get_model plugin
+ *                                   + sres/model/common/common.py:22-48 FModule
+ *   srmi_forward                 -> RCAN.forward sres/model/rcan/network.py:22-27,
+ *                                   EDSR.forward sres/model/edsr/network.py:27-32
+ *   srmi_backward                -> autograd of the above (dual_trainer.py:322)
+ *   srmi_rmse_*                  -> l2loss sres/controller/stats.py:5-8
+ *   srmi_downsample/_upsample    -> sres/base/util/array.py:72-76 / :84-87
+ *   srmi_adam_step               -> torch.optim.Adam, dual_trainer.py:126,323
+ *   srmi_conv3x3* / srmi_wgrad*  -> nn.Conv2d of default_conv
+ *                                   sres/model/common/cnn.py:8-9 (op level)
+ *   srmi_ca_*                    -> CALayer sres/model/rcan/network.py:31-47
+ */
+#ifndef SRMI_H
+#define SRMI_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRMI_OK 0
+#define SRMI_ERR_ARG (-10001)
+#define SRMI_ERR_SHAPE (-10002)
+#define SRMI_ERR_WORKSPACE (-10003)
+#define SRMI_ERR_UNSUPPORTED (-10004)
+
+#define SRMI_ARCH_RCAN 0
+#define SRMI_ARCH_EDSR 1
+
+typedef struct srmi_model_config {
+  int arch;          /* SRMI_ARCH_RCAN | SRMI_ARCH_EDSR                     */
+  int nchannels_in;  /* len(task.input_variables)   (1..4)                  */
+  int nchannels_out; /* len(task.target_variables)  (== nchannels_in)       */
+  int nfeatures;     /* model.nfeatures (64)                                */
+  int nlayers;       /* RCAN residual groups / EDSR resblocks               */
+  int nblocks;       /* RCAN RCABs per group (ignored for EDSR)             */
+  int reduction;     /* RCAN model.cbottleneck (channel-attention reduction) */
+  int scale;         /* prod(model.downscale_factors): 2, 4 or 8            */
+  float res_scale;   /* EDSR model.res_scale                                */
+  int batch;         /* max tiles per call (workspace capacity)             */
+  int lr_h, lr_w;    /* LR tile size, e.g. 48 x 48                          */
+} srmi_model_config;
+
+typedef struct srmi_param_info {
+  long long offset; /* element offset in the flat fp32 parameter buffer     */
+  long long numel;
+  int ndim;
+  int shape[4];
+} srmi_param_info;
+
+typedef struct srmi_engine srmi_engine;
+
+int srmi_version(void);
+
+/* parameters, in state_dict order (identical keys to the reference model) */
+int srmi_param_count(const srmi_model_config* cfg, long long* n_params, int* n_tensors);
+int srmi_param_table(const srmi_model_config* cfg, srmi_param_info* out, int cap);
+
+/* workspace for `train` (saves activations) or inference */
+int srmi_workspace_size(const srmi_model_config* cfg, int train, size_t* bytes);
+int srmi_engine_create(const srmi_model_config* cfg, void* workspace, size_t ws_bytes, int train,
+                       srmi_engine** out);
+int srmi_engine_destroy(srmi_engine* e);
+
+/* fp32 master weights -> bf16 MFMA filter packs (call after every update) */
+int srmi_pack_weights(srmi_engine* e, const float* params, void* stream);
+
+/* lr: NCHW fp32 [n][Cin][lr_h][lr_w] -> sr: NCHW fp32 [n][Cout][lr_h*s][lr_w*s] */
+int srmi_forward(srmi_engine* e, const float* params, const float* lr, float* sr, int n, void* stream);
+
+/* backward of the last forward (train engines).  Either
+ *   dy != NULL : upstream gradient NCHW fp32 like sr, or
+ *   dy == NULL : RMSE gradient (sr - hr) * loss4[2] formed on the fly.
+ * Writes every parameter gradient into grads (flat, state_dict order).
+ * One event per residual group is recorded into group_events[g] (if not NULL,
+ * hipEvent_t*) as soon as that group's gradients are final -- the hook for
+ * bucketed all-reduce overlapped with the rest of backward. */
+int srmi_backward(srmi_engine* e, const float* params, const float* lr, const float* sr, const float* hr,
+                  const float* loss4, const float* dy, float* grads, void** group_events, void* stream);
+
+/* RMSE (l2loss, squared=False).  loss4[0] = sum of squares (this rank),
+ * loss4[1] = global element count; after the optional all-reduce of loss4[0],
+ * srmi_rmse_finalize sets loss4[3] = L = sqrt(S/count), loss4[2] = 1/(count L). */
+int srmi_rmse_partial(srmi_engine* e, const float* pred, const float* target, size_t n, double count_global,
+                      float* loss4, void* stream);
+int srmi_rmse_finalize(float* loss4, void* stream);
+
+/* interp baseline / data path */
+int srmi_downsample(const float* hr, int N, int C, int H, int W, int scale, float* lr, void* stream);
+int srmi_upsample(const float* lr, int N, int C, int h, int w, int scale, float* hr, void* stream);
+
+/* Adam on flat buffers, step counted from 1 */
+int srmi_adam_step(float* p, const float* g, float* m, float* v, size_t n, int step, float lr, float beta1,
+                   float beta2, float eps, float weight_decay, void* stream);
+
+/* ---- op-level entry points (kernel parity tests, custom graphs) ---------- */
+/* forward conv: x NHWC bf16 [N][H][W][Cin], packed filters (srmi_pack_conv),
+ * epi: 0 relu->bf16, 1 bf16+channel sums (part[N][strips][64]), 2 alpha*(y+b)+r1
+ * -> yf fp32 (opt) + yb bf16, 3 PixelShuffle(2) bf16, 6 plain bf16           */
+int srmi_conv3x3(const void* x, const void* wpack, const float* bias, int N, int H, int W, int Cin, int Cout,
+                 int in_unshuffle, int epi, void* yb, float* yf, const float* r1, const float* r2, const float* r3,
+                 const void* aux, float* part, float alpha, void* stream);
+int srmi_conv3x3_nstrips(int H, int W);
+/* fp32 torch filter [Cout][Cin][3][3] -> bf16 packs: fwd [Cin/64][9][Cout][64],
+ * dgrad [Cout/64][9][Cin][64] (flipped), bias [Cout]; ps != 0 permutes the
+ * PixelShuffle channel order (packed c'' = 64q + c <- torch 4c + q)         */
+int srmi_pack_conv(const float* w, const float* b, int Cout, int Cin, int ps, void* fpack, void* dpack, float* pbias,
+                   void* stream);
+int srmi_wgrad3x3(const void* x, const void* dy, int N, int H, int W, int Cout, int dy_unshuffle, int row_splits,
+                  float* slab, size_t slab_bytes, int ps, float alpha, float* gw, float* gb, void* stream);
+int srmi_ca_forward(const void* u, const float* part, int nstrips, const float* w1, const float* b1, const float* w2,
+                    const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, void* hb_out,
+                    float* rec, void* stream);
+int srmi_ca_backward(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
+                     const float* w2, int N, int HW, int C, int R, void* du, float* brec, void* stream);
+int srmi_head_forward(const float* lr, const float* w, const float* b, int N, int C, int H, int W, float* x0f,
+                      void* x0b, void* stream);
+int srmi_tail_forward(const void* x, const float* w, const float* b, int N, int C, int H, int W, float* y,
+                      void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SRMI_H */

@@ -1,0 +1,79 @@
+// Shared device helpers for the srmi CDNA4 (gfx950) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace srmi {
+
+typedef uint16_t bf16_t;                                        // raw bf16 bits
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;      // MFMA A/B fragment
+typedef __attribute__((ext_vector_type(4))) float f32x4;        // 16x16 accumulator
+typedef __attribute__((ext_vector_type(4))) short s16x4;        // ds_read_b64_tr_b16 result
+
+__device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// round-to-nearest-even f32 -> bf16 (v_cvt_pk_bf16_f32 on gfx950; NaN stays NaN)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+// 16-byte chunk swizzle for an LDS image of 128-byte rows (64 bf16 channels per
+// pixel/row).  Chunk c of row q lives at slot c ^ ((q >> 1) & 7): 16 consecutive
+// rows read at one logical chunk by ds_read_b128 land on 16 distinct 16-B slots
+// of the 256-B bank row (conflict-free), see DESIGN.md §3.
+__device__ __forceinline__ uint32_t swz128(uint32_t q, uint32_t c) {
+  return q * 128u + ((c ^ ((q >> 1) & 7u)) << 4);
+}
+// swizzle used by the transposed-read (ds_read_b64_tr_b16) images of the wgrad
+// kernel: rows q..q+3 and q+8..q+11 of one 32-lane half hit distinct banks.
+__device__ __forceinline__ uint32_t swz128t(uint32_t q, uint32_t c) {
+  return q * 128u + ((c ^ ((((q >> 1) & 1u) << 1) | (((q >> 3) & 1u) << 2))) << 4);
+}
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 lds_frag(const char* lds, uint32_t byte_off) {
+  uint4 v = *reinterpret_cast<const uint4*>(lds + byte_off);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ s16x4 lds_tr(const char* lds, uint32_t byte_off) {
+  typedef short v4i16 __attribute__((ext_vector_type(4)));
+  v4i16 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (v4i16 __attribute__((address_space(3)))*)(lds + byte_off));
+  return __builtin_bit_cast(s16x4, r);
+}
+
+__device__ __forceinline__ bf16x8 cat_tr(s16x4 lo, s16x4 hi) {
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// sum over the 16 lanes that share (lane >> 4)
+__device__ __forceinline__ float sum16(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
+}
+
+}  // namespace srmi
+
+#define SRMI_CHECK_LAUNCH()                                  \
+  do {                                                       \
+    hipError_t _e = hipGetLastError();                       \
+    if (_e != hipSuccess) return -(int)_e;                   \
+  } while (0)

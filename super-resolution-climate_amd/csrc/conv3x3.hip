@@ -1,0 +1,303 @@
+// 3x3 "same" convolution as an MFMA implicit GEMM on gfx950 (CDNA4).
+//
+// Replaces nn.Conv2d(k=3, padding=1) built by default_conv
+// (reference sres/model/common/cnn.py:8-9) for every 64->64 / 64->256 conv of
+// RCAN (sres/model/rcan/network.py:13-16,55,71; blocks.py:64-65) and EDSR,
+// forward AND data-gradient (dgrad = the same conv on dY with the flipped,
+// transposed filter bank packed by pack.hip).
+//
+// Layout: activations NHWC bf16, 64 channels per 128-byte pixel row.
+// One workgroup = 4 waves = one strip of TH=4 output rows x TW (32|48) columns of
+// one image, one 64-wide block of output channels.  Per 64-channel input chunk
+// the (TH+2)x(TW+2) halo is staged once in LDS (swizzled, conflict-free
+// ds_read_b128); the 9 per-tap [64 co][64 ci] filter slices stream through a
+// double-buffered LDS ring.  Wave w computes output row w:  A = filters
+// (M = co), B = halo pixels (N = px), K = ci, with v_mfma_f32_16x16x32_bf16, so
+// each lane ends up owning 4 consecutive channels of one pixel -> vectorised,
+// fused epilogues (bias, ReLU, channel-attention pooling, residual add,
+// PixelShuffle scatter, ReLU-mask for dgrad, residual-stream gradient add with
+// the CA reductions).
+#include "common.hpp"
+#include "srmi_internal.hpp"
+
+namespace srmi {
+
+constexpr int kTH = 4;
+constexpr int kThreads = 256;
+
+template <int TW>
+struct ConvSmem {
+  static constexpr int HALO_PIX = (kTH + 2) * (TW + 2);
+  static constexpr int HALO_BYTES = HALO_PIX * 128;
+  static constexpr int W_BYTES = 64 * 128;  // one tap slice [64 co][64 ci]
+  static constexpr int TOTAL = HALO_BYTES + 2 * W_BYTES;
+};
+
+__device__ __forceinline__ void load_halo_chunk(char* halo, const bf16_t* __restrict__ x, int mode, int n, int H,
+                                                int W, int Cin, int cc, int y0, int x0, int TWp2, int npix) {
+  const int tid = threadIdx.x;
+  const int nch = npix * 8;
+  for (int i = tid; i < nch; i += kThreads) {
+    const int q = i >> 3, c = i & 7;
+    const int hy = q / TWp2, hx = q - hy * TWp2;
+    const int y = y0 - 1 + hy, xx = x0 - 1 + hx;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (y >= 0 && y < H && xx >= 0 && xx < W) {
+      const bf16_t* src;
+      if (mode == IN_PLAIN) {
+        src = x + ((size_t)((size_t)n * H + y) * W + xx) * Cin + cc * 64 + c * 8;
+      } else {  // IN_UNSHUF: logical [H][W][4*64] view of a physical [2H][2W][64] map
+        src = x + ((size_t)((size_t)n * 2 * H + 2 * y + (cc >> 1)) * (2 * W) + 2 * xx + (cc & 1)) * 64 + c * 8;
+      }
+      v = *reinterpret_cast<const uint4*>(src);
+    }
+    *reinterpret_cast<uint4*>(halo + swz128(q, c)) = v;
+  }
+}
+
+template <int TW, int EPI>
+__global__ void __launch_bounds__(kThreads, 2) conv3x3_kernel(ConvParams p) {
+  using S = ConvSmem<TW>;
+  constexpr int NPT = TW / 16;  // 16-pixel tiles per row
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* halo = smem;
+  char* wbuf = smem + S::HALO_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int strips_x = p.W / TW;
+  const int sy = blockIdx.x / strips_x, sx = blockIdx.x - sy * strips_x;
+  const int y0 = sy * kTH, x0 = sx * TW;
+  const int cb = blockIdx.y, n = blockIdx.z;
+  const int nchunks = p.Cin >> 6;
+  const bf16_t* __restrict__ wsrc = p.w;
+
+  f32x4 acc[NPT][4];
+#pragma unroll
+  for (int i = 0; i < NPT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // lane-constant fragment coordinates
+  const int fr = lane & 15;   // A row (co within tile) / B column (pixel within tile)
+  const int fk = lane >> 4;   // 8-wide k group
+
+  for (int cc = 0; cc < nchunks; ++cc) {
+    if (cc) __syncthreads();
+    load_halo_chunk(halo, p.x, p.in_mode, n, p.H, p.W, p.Cin, cc, y0, x0, TW + 2, S::HALO_PIX);
+    // tap 0 filter slice
+    {
+      const bf16_t* ws = wsrc + ((size_t)(cc * 9 + 0) * p.Cout + cb * 64) * 64;
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int i = tid + r * kThreads;
+        const int row = i >> 3, c = i & 7;
+        *reinterpret_cast<uint4*>(wbuf + swz128(row, c)) =
+            *reinterpret_cast<const uint4*>(ws + row * 64 + c * 8);
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      uint4 nxt[2];
+      if (tap < 8) {
+        const bf16_t* ws = wsrc + ((size_t)(cc * 9 + tap + 1) * p.Cout + cb * 64) * 64;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const int i = tid + r * kThreads;
+          nxt[r] = *reinterpret_cast<const uint4*>(ws + (i >> 3) * 64 + (i & 7) * 8);
+        }
+      }
+      const char* wb = wbuf + (tap & 1) * S::W_BYTES;
+      const int ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int chunk = kk * 4 + fk;
+        bf16x8 a[4];
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) a[ct] = lds_frag(wb, swz128(ct * 16 + fr, chunk));
+#pragma unroll
+        for (int pt = 0; pt < NPT; ++pt) {
+          const int q = (wave + ky) * (TW + 2) + pt * 16 + fr + kx;
+          const bf16x8 b = lds_frag(halo, swz128(q, chunk));
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = mfma16(a[ct], b, acc[pt][ct]);
+        }
+      }
+      if (tap < 8) {
+        char* wn = wbuf + ((tap + 1) & 1) * S::W_BYTES;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const int i = tid + r * kThreads;
+          *reinterpret_cast<uint4*>(wn + swz128(i >> 3, i & 7)) = nxt[r];
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // ------------------------------------------------------------------ epilogue
+  const int y = y0 + wave;
+  const int HW = p.H * p.W;
+  constexpr bool kPart1 = (EPI == EPI_POOL_BF16);
+  constexpr bool kPart2 = (EPI == EPI_DG_ACC);
+  float ps0[4][4], ps1[4][4];  // per (ct, r) partial sums over this lane's pixels
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ps0[ct][r] = ps1[ct][r] = 0.f;
+
+#pragma unroll
+  for (int pt = 0; pt < NPT; ++pt) {
+    const int xx = x0 + pt * 16 + fr;
+    const size_t pix = (size_t)n * HW + (size_t)y * p.W + xx;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int col = ct * 16 + fk * 4;           // channel within the 64-block
+      const int co = cb * 64 + col;               // packed output channel
+      f32x4 v = acc[pt][ct];
+      if constexpr (EPI == EPI_RELU_BF16 || EPI == EPI_POOL_BF16 || EPI == EPI_RESID || EPI == EPI_PS_BF16) {
+        const float4 bb = *reinterpret_cast<const float4*>(p.bias + co);
+        v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+      } else if constexpr (EPI == EPI_PLAIN_BF16) {
+        if (p.bias) {
+          const float4 bb = *reinterpret_cast<const float4*>(p.bias + co);
+          v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+        }
+      }
+      if constexpr (EPI == EPI_RELU_BF16) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if constexpr (EPI == EPI_RESID) {
+        const size_t o = pix * p.Cout + co;
+        const float4 rr = *reinterpret_cast<const float4*>(p.r1 + o);
+        v[0] = p.alpha * v[0] + rr.x; v[1] = p.alpha * v[1] + rr.y;
+        v[2] = p.alpha * v[2] + rr.z; v[3] = p.alpha * v[3] + rr.w;
+        if (p.yf) *reinterpret_cast<float4*>(p.yf + o) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+      if constexpr (EPI == EPI_DG_RELUMASK) {
+        const size_t o = pix * p.Cout + co;
+        const uint2 tt = *reinterpret_cast<const uint2*>(p.aux + o);
+        v[0] = (tt.x & 0xFFFFu) && !(tt.x & 0x8000u) ? v[0] : 0.f;
+        v[1] = (tt.x >> 16) && !(tt.x & 0x80000000u) ? v[1] : 0.f;
+        v[2] = (tt.y & 0xFFFFu) && !(tt.y & 0x8000u) ? v[2] : 0.f;
+        v[3] = (tt.y >> 16) && !(tt.y & 0x80000000u) ? v[3] : 0.f;
+        v[0] *= p.alpha; v[1] *= p.alpha; v[2] *= p.alpha; v[3] *= p.alpha;
+      }
+      if constexpr (EPI == EPI_DG_ACC) {
+        const size_t o = pix * p.Cout + co;
+        if (p.r1) {
+          const float4 rr = *reinterpret_cast<const float4*>(p.r1 + o);
+          v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
+        }
+        if (p.r2) {
+          const float4 rr = *reinterpret_cast<const float4*>(p.r2 + o);
+          v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
+        }
+        if (p.r3) {
+          const float4 rr = *reinterpret_cast<const float4*>(p.r3 + o);
+          v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
+        }
+        *reinterpret_cast<float4*>(p.yf + o) = make_float4(v[0], v[1], v[2], v[3]);
+        if (p.part) {
+          const uint2 uu = *reinterpret_cast<const uint2*>(p.aux + o);
+          ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
+          ps1[ct][0] += v[0] * bf2f(uu.x & 0xFFFFu);
+          ps1[ct][1] += v[1] * bf2f(uu.x >> 16);
+          ps1[ct][2] += v[2] * bf2f(uu.y & 0xFFFFu);
+          ps1[ct][3] += v[3] * bf2f(uu.y >> 16);
+        }
+      }
+      if constexpr (kPart1) {
+        ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
+      }
+      // bf16 store
+      uint2 packed = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      if constexpr (EPI == EPI_PS_BF16) {
+        // PixelShuffle(2): packed channel block cb = 2i+j -> output pixel (2y+i, 2x+j)
+        const int oy = 2 * y + (cb >> 1), ox = 2 * xx + (cb & 1);
+        const size_t o = ((size_t)n * (2 * p.H) + oy) * (size_t)(2 * p.W) + ox;
+        *reinterpret_cast<uint2*>(p.yb + o * 64 + col) = packed;
+      } else {
+        if (p.yb) *reinterpret_cast<uint2*>(p.yb + pix * p.Cout + co) = packed;
+      }
+    }
+  }
+
+  if constexpr (kPart1 || kPart2) {
+    // reduce over the 16 pixel-lanes, then over the 4 waves via LDS
+    __syncthreads();  // halo no longer needed
+    float* red = reinterpret_cast<float*>(smem);  // [4 waves][2][64]
+    if (!kPart2 || p.part) {
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float s0 = sum16(ps0[ct][r]);
+          float s1 = 0.f;
+          if constexpr (kPart2) s1 = sum16(ps1[ct][r]);
+          if (fr == 0) {
+            red[(wave * 2 + 0) * 64 + ct * 16 + fk * 4 + r] = s0;
+            if constexpr (kPart2) red[(wave * 2 + 1) * 64 + ct * 16 + fk * 4 + r] = s1;
+          }
+        }
+    }
+    __syncthreads();
+    if (!kPart2 || p.part) {
+      const int nstrips = gridDim.x;
+      if (tid < 64) {
+        const float s = red[0 * 128 + tid] + red[1 * 128 + tid] + red[2 * 128 + tid] + red[3 * 128 + tid];
+        p.part[((size_t)n * nstrips + blockIdx.x) * p.part_stride + cb * 64 + tid] = s;
+      } else if (kPart2 && tid < 128) {
+        const int c = tid - 64;
+        const float s = red[0 * 128 + 64 + c] + red[1 * 128 + 64 + c] + red[2 * 128 + 64 + c] + red[3 * 128 + 64 + c];
+        p.part[((size_t)n * nstrips + blockIdx.x) * p.part_stride + 64 + c] = s;
+      }
+    }
+  }
+}
+
+template <int TW, int EPI>
+static int launch_tw(const ConvParams& p, hipStream_t st) {
+  dim3 grid((p.H / kTH) * (p.W / TW), p.Cout / 64, p.N);
+  const int smem = ConvSmem<TW>::TOTAL;
+  hipLaunchKernelGGL((conv3x3_kernel<TW, EPI>), grid, dim3(kThreads), smem, st, p);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int EPI>
+static int launch_epi(const ConvParams& p, hipStream_t st) {
+  if (p.W % 48 == 0 && p.H % kTH == 0) return launch_tw<48, EPI>(p, st);
+  if (p.W % 32 == 0 && p.H % kTH == 0) return launch_tw<32, EPI>(p, st);
+  return SRMI_ERR_SHAPE;
+}
+
+int conv3x3_tw(const ConvParams& p) {
+  if (p.W % 48 == 0) return 48;
+  if (p.W % 32 == 0) return 32;
+  return 0;
+}
+
+int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
+  if (p.Cin % 64 || p.Cout % 64 || p.N <= 0 || p.H % kTH) return SRMI_ERR_SHAPE;
+  if (epi == EPI_PS_BF16 && p.Cout != 256) return SRMI_ERR_SHAPE;
+  if (p.in_mode == IN_UNSHUF && p.Cin != 256) return SRMI_ERR_SHAPE;
+  switch (epi) {
+    case EPI_RELU_BF16: return launch_epi<EPI_RELU_BF16>(p, st);
+    case EPI_POOL_BF16: return launch_epi<EPI_POOL_BF16>(p, st);
+    case EPI_RESID: return launch_epi<EPI_RESID>(p, st);
+    case EPI_PS_BF16: return launch_epi<EPI_PS_BF16>(p, st);
+    case EPI_DG_RELUMASK: return launch_epi<EPI_DG_RELUMASK>(p, st);
+    case EPI_DG_ACC: return launch_epi<EPI_DG_ACC>(p, st);
+    case EPI_PLAIN_BF16: return launch_epi<EPI_PLAIN_BF16>(p, st);
+    default: return SRMI_ERR_ARG;
+  }
+}
+
+int conv3x3_nstrips(int H, int W) {
+  const int tw = (W % 48 == 0) ? 48 : 32;
+  return (H / kTH) * (W / tw);
+}
+
+}  // namespace srmi

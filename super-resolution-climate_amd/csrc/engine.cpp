@@ -1,0 +1,733 @@
+// srmi engine: the RCAN / EDSR network plan, workspace layout and the
+// forward / backward / optimizer orchestration behind the C ABI of
+// include/srmi.h.  Every launch is asynchronous on the caller's stream; the
+// engine never synchronises and allocates nothing (graph-capturable).
+//
+// Network structure follows the reference exactly:
+//   RCAN  sres/model/rcan/network.py:7-77, blocks.py:58-76
+//   EDSR  sres/model/edsr/network.py:9-32, common/residual.py:26-50,
+//         common/upsample.py:32-66
+// Parameter order = the reference state_dict order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "srmi_internal.hpp"
+
+using namespace srmi;
+
+namespace {
+
+struct ConvRef {
+  long long w = -1, b = -1;  // param offsets
+  int cin = 0, cout = 0, ps = 0;
+  long long f_off = -1, d_off = -1, pb_off = -1;  // pack offsets (MFMA convs only)
+};
+
+struct RCABRef {
+  ConvRef c1, c2;
+  long long ca_w1, ca_b1, ca_w2, ca_b2;
+};
+
+struct Plan {
+  srmi_model_config cfg;
+  std::vector<srmi_param_info> params;
+  long long n_params = 0;
+  ConvRef head, body_tail, tail;
+  std::vector<std::vector<RCABRef>> groups;  // RCAN
+  std::vector<ConvRef> group_tail;            // RCAN
+  std::vector<ConvRef> res1, res2;            // EDSR
+  std::vector<ConvRef> ups;
+  std::vector<ConvRef*> mfma_convs;
+  long long pack_elems = 0, pbias_elems = 0;
+  int nups = 0;
+};
+
+long long add_param(Plan& P, std::initializer_list<int> shape) {
+  srmi_param_info pi{};
+  pi.offset = P.n_params;
+  pi.ndim = (int)shape.size();
+  long long n = 1;
+  int k = 0;
+  for (int s : shape) {
+    pi.shape[k++] = s;
+    n *= s;
+  }
+  pi.numel = n;
+  P.params.push_back(pi);
+  P.n_params += n;
+  return pi.offset;
+}
+
+ConvRef add_conv(Plan& P, int cin, int cout, int k) {
+  ConvRef c;
+  c.cin = cin;
+  c.cout = cout;
+  c.w = add_param(P, {cout, cin, k, k});
+  c.b = add_param(P, {cout});
+  return c;
+}
+
+int build_plan(const srmi_model_config* cfg, Plan& P) {
+  if (!cfg) return SRMI_ERR_ARG;
+  const srmi_model_config& c = *cfg;
+  if (c.nfeatures != 64) return SRMI_ERR_UNSUPPORTED;
+  if (c.nchannels_in < 1 || c.nchannels_in > 4 || c.nchannels_out < 1 || c.nchannels_out > 4) return SRMI_ERR_UNSUPPORTED;
+  if (c.scale != 2 && c.scale != 4 && c.scale != 8) return SRMI_ERR_UNSUPPORTED;
+  if (c.nlayers < 1 || c.batch < 1 || c.lr_h < 4 || c.lr_w < 16) return SRMI_ERR_ARG;
+  if (c.arch == SRMI_ARCH_RCAN && (c.nblocks < 1 || c.reduction < 1 || 64 % c.reduction)) return SRMI_ERR_ARG;
+  if (c.arch != SRMI_ARCH_RCAN && c.arch != SRMI_ARCH_EDSR) return SRMI_ERR_ARG;
+  P = Plan();
+  P.cfg = c;
+  const int F = 64;
+  P.head = add_conv(P, c.nchannels_in, F, 3);
+  if (c.arch == SRMI_ARCH_RCAN) {
+    P.groups.resize(c.nlayers);
+    for (int g = 0; g < c.nlayers; ++g) {
+      for (int b = 0; b < c.nblocks; ++b) {
+        RCABRef r;
+        r.c1 = add_conv(P, F, F, 3);
+        r.c2 = add_conv(P, F, F, 3);
+        r.ca_w1 = add_param(P, {F / c.reduction, F, 1, 1});
+        r.ca_b1 = add_param(P, {F / c.reduction});
+        r.ca_w2 = add_param(P, {F, F / c.reduction, 1, 1});
+        r.ca_b2 = add_param(P, {F});
+        P.groups[g].push_back(r);
+      }
+      P.group_tail.push_back(add_conv(P, F, F, 3));
+    }
+  } else {
+    for (int i = 0; i < c.nlayers; ++i) {
+      P.res1.push_back(add_conv(P, F, F, 3));
+      P.res2.push_back(add_conv(P, F, F, 3));
+    }
+  }
+  P.body_tail = add_conv(P, F, F, 3);
+  P.nups = (int)std::lround(std::log2((double)c.scale));
+  for (int k = 0; k < P.nups; ++k) {
+    ConvRef u = add_conv(P, F, 4 * F, 3);
+    u.ps = 1;
+    P.ups.push_back(u);
+  }
+  P.tail = add_conv(P, F, c.nchannels_out, 3);
+  // MFMA convs get bf16 packs
+  for (auto& grp : P.groups)
+    for (auto& r : grp) {
+      P.mfma_convs.push_back(&r.c1);
+      P.mfma_convs.push_back(&r.c2);
+    }
+  for (auto& t : P.group_tail) P.mfma_convs.push_back(&t);
+  for (size_t i = 0; i < P.res1.size(); ++i) {
+    P.mfma_convs.push_back(&P.res1[i]);
+    P.mfma_convs.push_back(&P.res2[i]);
+  }
+  P.mfma_convs.push_back(&P.body_tail);
+  for (auto& u : P.ups) P.mfma_convs.push_back(&u);
+  for (ConvRef* cr : P.mfma_convs) {
+    const long long n = (long long)cr->cout * cr->cin * 9;
+    cr->f_off = P.pack_elems;
+    P.pack_elems += n;
+    cr->d_off = P.pack_elems;
+    P.pack_elems += n;
+    cr->pb_off = P.pbias_elems;
+    P.pbias_elems += cr->cout;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------- workspace
+struct Carver {
+  size_t off = 0;
+  char* base = nullptr;
+  template <class T>
+  T* take(size_t count) {
+    off = (off + 255) & ~(size_t)255;
+    T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+    off += count * sizeof(T);
+    return p;
+  }
+};
+
+int choose_row_splits(int N, int H, int Cout) {
+  // aim at >= 256 workgroups (one per CU) with >= 4 rows per workgroup
+  const int want = std::max(1, (256 + N * (Cout / 64) - 1) / (N * (Cout / 64)));
+  int best = 1;
+  for (int rs = 1; rs <= H / 2; ++rs) {
+    if (H % rs || (H / rs) % 2) continue;
+    if (H / rs < 4 && rs > 1) break;
+    best = rs;
+    if (rs >= want) break;
+  }
+  return best;
+}
+
+}  // namespace
+
+struct srmi_engine {
+  Plan P;
+  int train = 0;
+  int N = 0, h = 0, w = 0, C = 0, Co = 0, S = 0;
+  size_t mapn = 0;  // elements of one [N][h][w][64] map
+  // forward state
+  float *X0f, *Rf, *Hf;
+  bf16_t* HB;    // hb maps
+  int n_hb;      // number of hb slots
+  bf16_t *T, *U; // train: [nl*nb] maps; infer: 1 each
+  bf16_t* RESb;
+  bf16_t* PS[3];  // pixel-shuffle outputs (scale s: [N][h*2^k][w*2^k][64])
+  float *rec, *brec;
+  float *ppool, *pacc;
+  // backward
+  float *GAf, *GBf, *dRESf;
+  bf16_t *GAb, *GBb, *DU, *DZ, *dRESb;
+  bf16_t* dPS[3];
+  float *slab, *bslab;
+  size_t slab_floats, bslab_floats;
+  float* lpart;
+  int lpart_n;
+  // packs
+  bf16_t* packs;
+  float* pbias;
+  PackEntry* d_entries;
+  long long* d_caoffs;
+  std::vector<PackEntry> h_entries;
+  std::vector<long long> h_caoffs;
+  long long max_pack_elems = 0;
+  bool tables_uploaded = false;
+  int last_n = 0;
+
+  bf16_t* hb(int g, int b) const {
+    const int nb1 = P.cfg.arch == SRMI_ARCH_RCAN ? P.cfg.nblocks + 1 : 1;
+    const int k = g * nb1 + b;
+    return HB + (size_t)(train ? k : (k % n_hb)) * mapn;
+  }
+  int nbe() const { return P.cfg.arch == SRMI_ARCH_RCAN ? P.cfg.nblocks : 1; }
+  bf16_t* Tm(int g, int b) const { return train ? T + (size_t)(g * nbe() + (b - 1)) * mapn : T; }
+  bf16_t* Um(int g, int b) const { return train ? U + (size_t)(g * P.cfg.nblocks + (b - 1)) * mapn : U; }
+  float* recp(int g, int b) const {
+    return train ? rec + (size_t)(g * P.cfg.nblocks + (b - 1)) * N * 160 : rec;
+  }
+  float* brecp(int g, int b) const { return brec + (size_t)(g * P.cfg.nblocks + (b - 1)) * N * 160; }
+};
+
+static size_t carve(srmi_engine* e, char* base) {
+  Carver cv;
+  cv.base = base;
+  const Plan& P = e->P;
+  const int N = e->N;
+  const size_t m = e->mapn;
+  const bool rcan = P.cfg.arch == SRMI_ARCH_RCAN;
+  const int nl = P.cfg.nlayers, nb = rcan ? P.cfg.nblocks : 0;
+  e->X0f = cv.take<float>(m);
+  e->Rf = cv.take<float>(m);
+  e->Hf = cv.take<float>(m);
+  const int nslots = rcan ? nl * (nb + 1) + 1 : nl + 1;
+  e->n_hb = e->train ? nslots : 3;
+  e->HB = cv.take<bf16_t>(m * e->n_hb);
+  const int nconv1 = rcan ? nl * nb : nl;
+  e->T = cv.take<bf16_t>(m * (e->train ? nconv1 : 1));
+  e->U = rcan ? cv.take<bf16_t>(m * (e->train ? nconv1 : 1)) : nullptr;
+  e->RESb = cv.take<bf16_t>(m);
+  for (int k = 0; k < 3; ++k) e->PS[k] = nullptr;
+  for (int k = 0; k < P.nups; ++k) e->PS[k] = cv.take<bf16_t>(m << (2 * (k + 1)));
+  const int nstrips = conv3x3_nstrips(e->h, e->w);
+  if (rcan) {
+    e->rec = cv.take<float>((size_t)(e->train ? nl * nb : 1) * N * 160);
+    e->brec = e->train ? cv.take<float>((size_t)nl * nb * N * 160) : nullptr;
+    e->ppool = cv.take<float>((size_t)N * nstrips * 64);
+    e->pacc = cv.take<float>((size_t)N * nstrips * 128);
+  }
+  e->lpart_n = 1024;
+  e->lpart = cv.take<float>(e->lpart_n);
+  if (e->train) {
+    e->GAf = cv.take<float>(m);
+    e->GBf = cv.take<float>(m);
+    e->dRESf = cv.take<float>(m);
+    e->GAb = cv.take<bf16_t>(m);
+    e->GBb = cv.take<bf16_t>(m);
+    e->DU = cv.take<bf16_t>(m);
+    e->DZ = cv.take<bf16_t>(m);
+    e->dRESb = cv.take<bf16_t>(m);
+    for (int k = 0; k < 3; ++k) e->dPS[k] = nullptr;
+    for (int k = 0; k < P.nups; ++k) e->dPS[k] = cv.take<bf16_t>(m << (2 * (k + 1)));
+    // slab: max over all wgrads
+    size_t sf = 0, bf = 0;
+    auto upd = [&](int H, int W, int Cout) {
+      const int rs = choose_row_splits(N, H, Cout);
+      const size_t ns = (size_t)N * rs;
+      sf = std::max(sf, ns * Cout * 576);
+      bf = std::max(bf, ns * Cout);
+    };
+    upd(e->h, e->w, 64);
+    for (int k = 0; k < P.nups; ++k) upd(e->h << k, e->w << k, 256);
+    // head / tail slabs
+    const int Hs = e->h * e->S;
+    sf = std::max(sf, (size_t)N * (e->h / 4) * 64 * (9 * e->C + 1));
+    sf = std::max(sf, (size_t)N * (Hs / 16) * e->Co * 577);
+    e->slab_floats = sf;
+    e->bslab_floats = bf;
+    e->slab = cv.take<float>(sf);
+    e->bslab = cv.take<float>(bf);
+  }
+  e->packs = cv.take<bf16_t>(P.pack_elems);
+  e->pbias = cv.take<float>(P.pbias_elems);
+  e->d_entries = cv.take<PackEntry>(P.mfma_convs.size());
+  e->d_caoffs = cv.take<long long>((size_t)std::max(1, nl * nb) * 5);
+  return cv.off + 256;
+}
+
+static int init_engine(srmi_engine* e, const srmi_model_config* cfg, int train) {
+  int rc = build_plan(cfg, e->P);
+  if (rc) return rc;
+  e->train = train;
+  e->N = cfg->batch;
+  e->h = cfg->lr_h;
+  e->w = cfg->lr_w;
+  e->C = cfg->nchannels_in;
+  e->Co = cfg->nchannels_out;
+  e->S = cfg->scale;
+  e->mapn = (size_t)e->N * e->h * e->w * 64;
+  if (e->h % 4 || (e->w % 32 && e->w % 48)) return SRMI_ERR_SHAPE;
+  const int Hs = e->h * e->S;
+  if (Hs % 16 || ((e->w * e->S) % 32)) return SRMI_ERR_SHAPE;
+  return 0;
+}
+
+static void build_tables(srmi_engine* e) {
+  e->h_entries.clear();
+  e->max_pack_elems = 0;
+  for (ConvRef* c : e->P.mfma_convs) {
+    PackEntry pe{};
+    pe.w_off = c->w;
+    pe.b_off = c->b;
+    pe.f_off = c->f_off;
+    pe.d_off = c->d_off;
+    pe.pb_off = c->pb_off;
+    pe.Cout = c->cout;
+    pe.Cin = c->cin;
+    pe.ps = c->ps;
+    e->h_entries.push_back(pe);
+    e->max_pack_elems = std::max(e->max_pack_elems, (long long)c->cout * c->cin * 9);
+  }
+  e->h_caoffs.clear();
+  for (auto& grp : e->P.groups)
+    for (auto& r : grp) {
+      e->h_caoffs.push_back(r.ca_w1);
+      e->h_caoffs.push_back(r.ca_b1);
+      e->h_caoffs.push_back(r.ca_w2);
+      e->h_caoffs.push_back(r.ca_b2);
+      e->h_caoffs.push_back(r.c2.b);
+    }
+}
+
+static inline hipStream_t S_(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// --------------------------------------------------------------- conv helpers
+static int conv_fwd(srmi_engine* e, const ConvRef& c, const bf16_t* x, int n, int H, int W, int epi, bf16_t* yb,
+                    float* yf, const float* r1, float* part, float alpha, hipStream_t st) {
+  ConvParams p{};
+  p.x = x;
+  p.w = e->packs + c.f_off;
+  p.bias = e->pbias + c.pb_off;
+  p.N = n;
+  p.H = H;
+  p.W = W;
+  p.Cin = c.cin;
+  p.Cout = c.cout;
+  p.in_mode = IN_PLAIN;
+  p.yb = yb;
+  p.yf = yf;
+  p.r1 = r1;
+  p.part = part;
+  p.part_stride = 64;
+  p.alpha = alpha;
+  return conv3x3_launch(p, epi, st);
+}
+
+// dgrad of conv c: input dy (Cout channels, PS layout if c.ps), output Cin channels
+static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n, int H, int W, int epi, bf16_t* yb,
+                      float* yf, const float* r1, const float* r2, const float* r3, const bf16_t* aux, float* part,
+                      float alpha, hipStream_t st) {
+  ConvParams p{};
+  p.x = dy;
+  p.w = e->packs + c.d_off;
+  p.bias = nullptr;
+  p.N = n;
+  p.H = H;
+  p.W = W;
+  p.Cin = c.cout;
+  p.Cout = c.cin;
+  p.in_mode = c.ps ? IN_UNSHUF : IN_PLAIN;
+  p.yb = yb;
+  p.yf = yf;
+  p.r1 = r1;
+  p.r2 = r2;
+  p.r3 = r3;
+  p.aux = aux;
+  p.part = part;
+  p.part_stride = 128;
+  p.alpha = alpha;
+  return conv3x3_launch(p, epi, st);
+}
+
+static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const bf16_t* dy, int n, int H, int W,
+                      float* grads, bool with_bias, float alpha, hipStream_t st) {
+  WgradParams p{};
+  p.x = x;
+  p.dy = dy;
+  p.N = n;
+  p.H = H;
+  p.W = W;
+  p.Cout = c.cout;
+  p.dy_mode = c.ps ? IN_UNSHUF : IN_PLAIN;
+  p.imgs_per_wg = 1;
+  p.row_splits = choose_row_splits(n, H, c.cout);
+  p.slab = e->slab;
+  p.bslab = e->bslab;
+  const size_t ns = (size_t)wgrad3x3_nslabs(p);
+  if (ns * c.cout * 576 > e->slab_floats || ns * c.cout > e->bslab_floats) return SRMI_ERR_WORKSPACE;
+  int rc = wgrad3x3_launch(p, st);
+  if (rc) return rc;
+  return wgrad_reduce_launch(e->slab, e->bslab, (int)ns, c.cout, c.ps, alpha, grads + c.w,
+                             with_bias ? grads + c.b : nullptr, st);
+}
+
+#define RC(x)              \
+  do {                     \
+    int _rc = (x);         \
+    if (_rc) return _rc;   \
+  } while (0)
+
+static int upload_tables(srmi_engine* e, hipStream_t st) {
+  if (e->tables_uploaded) return 0;
+  build_tables(e);
+  hipError_t err = hipMemcpyAsync(e->d_entries, e->h_entries.data(), e->h_entries.size() * sizeof(PackEntry),
+                                  hipMemcpyHostToDevice, st);
+  if (err != hipSuccess) return -(int)err;
+  if (!e->h_caoffs.empty()) {
+    err = hipMemcpyAsync(e->d_caoffs, e->h_caoffs.data(), e->h_caoffs.size() * sizeof(long long),
+                         hipMemcpyHostToDevice, st);
+    if (err != hipSuccess) return -(int)err;
+  }
+  // the host vectors must outlive the async copies: keep them in the engine
+  e->tables_uploaded = true;
+  return 0;
+}
+
+// ------------------------------------------------------------------ forward
+static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float* sr, int n, hipStream_t st) {
+  const Plan& P = e->P;
+  const int h = e->h, w = e->w, HW = h * w;
+  const int nstrips = conv3x3_nstrips(h, w);
+  RC(head_fwd_launch(lr, prm + P.head.w, prm + P.head.b, n, e->C, h, w, e->X0f, e->hb(0, 0), st));
+  if (P.cfg.arch == SRMI_ARCH_RCAN) {
+    const int nl = P.cfg.nlayers, nb = P.cfg.nblocks, R = P.cfg.reduction;
+    for (int g = 0; g < nl; ++g) {
+      const float* rin = g == 0 ? e->X0f : e->Rf;
+      for (int b = 1; b <= nb; ++b) {
+        const RCABRef& r = P.groups[g][b - 1];
+        RC(conv_fwd(e, r.c1, e->hb(g, b - 1), n, h, w, EPI_RELU_BF16, e->Tm(g, b), nullptr, nullptr, nullptr, 1.f, st));
+        RC(conv_fwd(e, r.c2, e->Tm(g, b), n, h, w, EPI_POOL_BF16, e->Um(g, b), nullptr, nullptr, e->ppool, 1.f, st));
+        RC(ca_fwd_launch(e->Um(g, b), e->ppool, nstrips, prm + r.ca_w1, prm + r.ca_b1, prm + r.ca_w2, prm + r.ca_b2, n,
+                         HW, 64, R, b == 1 ? rin : e->Hf, e->Hf, e->hb(g, b), e->recp(g, b), st));
+      }
+      RC(conv_fwd(e, P.group_tail[g], e->hb(g, nb), n, h, w, EPI_RESID, e->hb(g + 1, 0), e->Rf, rin, nullptr, 1.f,
+                  st));
+    }
+    RC(conv_fwd(e, P.body_tail, e->hb(nl, 0), n, h, w, EPI_RESID, e->RESb, nullptr, e->X0f, nullptr, 1.f, st));
+  } else {
+    const int nl = P.cfg.nlayers;
+    for (int i = 0; i < nl; ++i) {
+      const float* rin = i == 0 ? e->X0f : e->Rf;
+      RC(conv_fwd(e, P.res1[i], e->hb(i, 0), n, h, w, EPI_RELU_BF16, e->Tm(i, 1), nullptr, nullptr, nullptr, 1.f, st));
+      RC(conv_fwd(e, P.res2[i], e->Tm(i, 1), n, h, w, EPI_RESID, e->hb(i + 1, 0), e->Rf, rin, nullptr,
+                  P.cfg.res_scale, st));
+    }
+    RC(conv_fwd(e, P.body_tail, e->hb(nl, 0), n, h, w, EPI_RESID, e->RESb, nullptr, e->X0f, nullptr, 1.f, st));
+  }
+  const bf16_t* cur = e->RESb;
+  int H = h, W = w;
+  for (int k = 0; k < P.nups; ++k) {
+    RC(conv_fwd(e, P.ups[k], cur, n, H, W, EPI_PS_BF16, e->PS[k], nullptr, nullptr, nullptr, 1.f, st));
+    cur = e->PS[k];
+    H *= 2;
+    W *= 2;
+  }
+  RC(tail_fwd_launch(cur, prm + P.tail.w, prm + P.tail.b, n, e->Co, H, W, sr, st));
+  e->last_n = n;
+  return 0;
+}
+
+// ----------------------------------------------------------------- backward
+static int backward_impl(srmi_engine* e, const float* prm, const float* lr, const float* sr, const float* hr,
+                         const float* loss4, const float* dy, float* grads, void** group_events, hipStream_t st) {
+  const Plan& P = e->P;
+  const int n = e->last_n, h = e->h, w = e->w, HW = h * w;
+  const int nstrips = conv3x3_nstrips(h, w);
+  int H = h << P.nups, W = w << P.nups;
+  // tail conv 64 -> C
+  const bf16_t* xlast = e->PS[P.nups - 1];
+  const float* yv = dy ? dy : sr;
+  const float* tv = dy ? nullptr : hr;
+  const float* lv = dy ? nullptr : loss4;
+  RC(tail_dgrad_launch(yv, tv, lv, prm + P.tail.w, n, e->Co, H, W, e->dPS[P.nups - 1], st));
+  int nsl = 0;
+  RC(tail_wgrad_launch(yv, tv, lv, xlast, n, e->Co, H, W, e->slab, &nsl, st));
+  RC(tail_wgrad_reduce_launch(e->slab, nsl, e->Co, grads + P.tail.w, grads + P.tail.b, st));
+  // upsamplers, last to first
+  for (int k = P.nups - 1; k >= 0; --k) {
+    H /= 2;
+    W /= 2;
+    const bf16_t* xin = k == 0 ? e->RESb : e->PS[k - 1];
+    RC(conv_wgrad(e, P.ups[k], xin, e->dPS[k], n, H, W, grads, true, 1.f, st));
+    if (k > 0)
+      RC(conv_dgrad(e, P.ups[k], e->dPS[k], n, H, W, EPI_PLAIN_BF16, e->dPS[k - 1], nullptr, nullptr, nullptr, nullptr,
+                    nullptr, nullptr, 1.f, st));
+    else
+      RC(conv_dgrad(e, P.ups[k], e->dPS[k], n, H, W, EPI_DG_ACC, e->dRESb, e->dRESf, nullptr, nullptr, nullptr,
+                    nullptr, nullptr, 1.f, st));
+  }
+  // body tail: res = conv(hb_last) + x0
+  const int nl = P.cfg.nlayers;
+  float *gRf = e->GAf, *ghf = e->GBf;
+  bf16_t *gRb = e->GAb, *ghb = e->GBb;
+  if (P.cfg.arch == SRMI_ARCH_RCAN) {
+    const int nb = P.cfg.nblocks, R = P.cfg.reduction;
+    RC(conv_wgrad(e, P.body_tail, e->hb(nl, 0), e->dRESb, n, h, w, grads, true, 1.f, st));
+    RC(conv_dgrad(e, P.body_tail, e->dRESb, n, h, w, EPI_DG_ACC, gRb, gRf, nullptr, nullptr, nullptr, nullptr, nullptr,
+                  1.f, st));
+    for (int g = nl - 1; g >= 0; --g) {
+      const ConvRef& gt = P.group_tail[g];
+      RC(conv_wgrad(e, gt, e->hb(g, nb), gRb, n, h, w, grads, true, 1.f, st));
+      RC(conv_dgrad(e, gt, gRb, n, h, w, EPI_DG_ACC, nullptr, ghf, nullptr, nullptr, nullptr, e->Um(g, nb), e->pacc,
+                    1.f, st));
+      for (int b = nb; b >= 1; --b) {
+        const RCABRef& r = P.groups[g][b - 1];
+        RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, e->DU,
+                            e->brecp(g, b), st));
+        RC(conv_wgrad(e, r.c2, e->Tm(g, b), e->DU, n, h, w, grads, false, 1.f, st));
+        RC(conv_dgrad(e, r.c2, e->DU, n, h, w, EPI_DG_RELUMASK, e->DZ, nullptr, nullptr, nullptr, nullptr, e->Tm(g, b),
+                      nullptr, 1.f, st));
+        RC(conv_wgrad(e, r.c1, e->hb(g, b - 1), e->DZ, n, h, w, grads, true, 1.f, st));
+        const bool last = (b == 1);
+        RC(conv_dgrad(e, r.c1, e->DZ, n, h, w, EPI_DG_ACC, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
+                      (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
+                      last ? nullptr : e->pacc, 1.f, st));
+      }
+      RC(ca_param_grads_batched_launch(e->recp(g, 1), e->brecp(g, 1), nb, n, 64, R, e->d_caoffs + (size_t)g * nb * 5,
+                                       grads, st));
+      std::swap(gRf, ghf);
+      std::swap(gRb, ghb);
+      if (group_events && group_events[g]) {
+        hipError_t er = hipEventRecord(reinterpret_cast<hipEvent_t>(group_events[g]), st);
+        if (er != hipSuccess) return -(int)er;
+      }
+    }
+  } else {
+    const float rsc = P.cfg.res_scale;
+    RC(conv_wgrad(e, P.body_tail, e->hb(nl, 0), e->dRESb, n, h, w, grads, true, 1.f, st));
+    RC(conv_dgrad(e, P.body_tail, e->dRESb, n, h, w, EPI_DG_ACC, gRb, gRf, nullptr, nullptr, nullptr, nullptr, nullptr,
+                  1.f, st));
+    for (int i = nl - 1; i >= 0; --i) {
+      // block i: out = rsc * (conv2(relu(conv1(x)))) + x, grad wrt out = gR
+      RC(conv_wgrad(e, P.res2[i], e->Tm(i, 1), gRb, n, h, w, grads, true, rsc, st));
+      RC(conv_dgrad(e, P.res2[i], gRb, n, h, w, EPI_DG_RELUMASK, e->DZ, nullptr, nullptr, nullptr, nullptr,
+                    e->Tm(i, 1), nullptr, rsc, st));
+      RC(conv_wgrad(e, P.res1[i], e->hb(i, 0), e->DZ, n, h, w, grads, true, 1.f, st));
+      RC(conv_dgrad(e, P.res1[i], e->DZ, n, h, w, EPI_DG_ACC, ghb, ghf, gRf, i == 0 ? e->dRESf : nullptr, nullptr,
+                    nullptr, nullptr, 1.f, st));
+      std::swap(gRf, ghf);
+      std::swap(gRb, ghb);
+    }
+  }
+  // head: only the weight gradient (the input gradient is never read)
+  RC(head_wgrad_launch(lr, gRf, n, e->C, h, w, e->slab, &nsl, st));
+  RC(head_wgrad_reduce_launch(e->slab, nsl, e->C, grads + P.head.w, grads + P.head.b, st));
+  return 0;
+}
+
+// =================================================================== C ABI
+extern "C" {
+
+int srmi_version(void) { return 100; }
+
+int srmi_param_count(const srmi_model_config* cfg, long long* n_params, int* n_tensors) {
+  Plan P;
+  RC(build_plan(cfg, P));
+  if (n_params) *n_params = P.n_params;
+  if (n_tensors) *n_tensors = (int)P.params.size();
+  return 0;
+}
+
+int srmi_param_table(const srmi_model_config* cfg, srmi_param_info* out, int cap) {
+  Plan P;
+  RC(build_plan(cfg, P));
+  if (!out || cap < (int)P.params.size()) return SRMI_ERR_ARG;
+  std::memcpy(out, P.params.data(), P.params.size() * sizeof(srmi_param_info));
+  return (int)P.params.size();
+}
+
+int srmi_workspace_size(const srmi_model_config* cfg, int train, size_t* bytes) {
+  srmi_engine e;
+  RC(init_engine(&e, cfg, train));
+  *bytes = carve(&e, nullptr);
+  return 0;
+}
+
+int srmi_engine_create(const srmi_model_config* cfg, void* workspace, size_t ws_bytes, int train, srmi_engine** out) {
+  if (!out || !workspace) return SRMI_ERR_ARG;
+  srmi_engine* e = new (std::nothrow) srmi_engine();
+  if (!e) return SRMI_ERR_ARG;
+  int rc = init_engine(e, cfg, train);
+  if (rc) {
+    delete e;
+    return rc;
+  }
+  const size_t need = carve(e, nullptr);
+  if (ws_bytes < need) {
+    delete e;
+    return SRMI_ERR_WORKSPACE;
+  }
+  char* base = reinterpret_cast<char*>(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  if ((size_t)(base - (char*)workspace) + need - 256 > ws_bytes) {
+    delete e;
+    return SRMI_ERR_WORKSPACE;
+  }
+  carve(e, base);
+  *out = e;
+  return 0;
+}
+
+int srmi_engine_destroy(srmi_engine* e) {
+  delete e;
+  return 0;
+}
+
+int srmi_pack_weights(srmi_engine* e, const float* params, void* stream) {
+  if (!e || !params) return SRMI_ERR_ARG;
+  RC(upload_tables(e, S_(stream)));
+  return pack_launch(params, e->d_entries, (int)e->h_entries.size(), e->max_pack_elems, e->packs, e->pbias,
+                     S_(stream));
+}
+
+int srmi_forward(srmi_engine* e, const float* params, const float* lr, float* sr, int n, void* stream) {
+  if (!e || !params || !lr || !sr || n < 1 || n > e->N) return SRMI_ERR_ARG;
+  if (!e->tables_uploaded) return SRMI_ERR_ARG;  // srmi_pack_weights first
+  return forward_impl(e, params, lr, sr, n, S_(stream));
+}
+
+int srmi_backward(srmi_engine* e, const float* params, const float* lr, const float* sr, const float* hr,
+                  const float* loss4, const float* dy, float* grads, void** group_events, void* stream) {
+  if (!e || !e->train || !params || !lr || !grads || e->last_n < 1) return SRMI_ERR_ARG;
+  if (!dy && (!sr || !hr || !loss4)) return SRMI_ERR_ARG;
+  return backward_impl(e, params, lr, sr, hr, loss4, dy, grads, group_events, S_(stream));
+}
+
+int srmi_rmse_partial(srmi_engine* e, const float* pred, const float* target, size_t n, double count_global,
+                      float* loss4, void* stream) {
+  if (!e || !pred || !target || !loss4) return SRMI_ERR_ARG;
+  RC(sqerr_partial_launch(pred, target, n, e->lpart, e->lpart_n, S_(stream)));
+  return sqerr_finish_launch(e->lpart, e->lpart_n, count_global, loss4, S_(stream));
+}
+
+int srmi_rmse_finalize(float* loss4, void* stream) { return loss_finalize_launch(loss4, S_(stream)); }
+
+int srmi_downsample(const float* hr, int N, int C, int H, int W, int scale, float* lr, void* stream) {
+  return downsample_launch(hr, N, C, H, W, scale, lr, S_(stream));
+}
+
+int srmi_upsample(const float* lr, int N, int C, int h, int w, int scale, float* hr, void* stream) {
+  return upsample_launch(lr, N, C, h, w, scale, hr, S_(stream));
+}
+
+int srmi_adam_step(float* p, const float* g, float* m, float* v, size_t n, int step, float lr, float beta1,
+                   float beta2, float eps, float weight_decay, void* stream) {
+  if (step < 1) return SRMI_ERR_ARG;
+  const double bc1 = 1.0 - std::pow((double)beta1, step);
+  const double bc2 = 1.0 - std::pow((double)beta2, step);
+  const float step_size = (float)(lr / bc1);
+  const float bc2_sqrt = (float)std::sqrt(bc2);
+  return adam_launch(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt, S_(stream));
+}
+
+// ---------------------------------------------------------------- op level
+int srmi_conv3x3(const void* x, const void* wpack, const float* bias, int N, int H, int W, int Cin, int Cout,
+                 int in_unshuffle, int epi, void* yb, float* yf, const float* r1, const float* r2, const float* r3,
+                 const void* aux, float* part, float alpha, void* stream) {
+  ConvParams p{};
+  p.x = (const bf16_t*)x;
+  p.w = (const bf16_t*)wpack;
+  p.bias = bias;
+  p.N = N;
+  p.H = H;
+  p.W = W;
+  p.Cin = Cin;
+  p.Cout = Cout;
+  p.in_mode = in_unshuffle ? IN_UNSHUF : IN_PLAIN;
+  p.yb = (bf16_t*)yb;
+  p.yf = yf;
+  p.r1 = r1;
+  p.r2 = r2;
+  p.r3 = r3;
+  p.aux = (const bf16_t*)aux;
+  p.part = part;
+  p.part_stride = (epi == EPI_DG_ACC) ? 128 : Cout;
+  p.alpha = alpha;
+  return conv3x3_launch(p, epi, S_(stream));
+}
+
+int srmi_conv3x3_nstrips(int H, int W) { return conv3x3_nstrips(H, W); }
+
+int srmi_pack_conv(const float* w, const float* b, int Cout, int Cin, int ps, void* fpack, void* dpack, float* pbias,
+                   void* stream) {
+  return pack_one_launch(w, b, Cout, Cin, ps, (bf16_t*)fpack, (bf16_t*)dpack, pbias, S_(stream));
+}
+
+int srmi_wgrad3x3(const void* x, const void* dy, int N, int H, int W, int Cout, int dy_unshuffle, int row_splits,
+                  float* slab, size_t slab_bytes, int ps, float alpha, float* gw, float* gb, void* stream) {
+  WgradParams p{};
+  p.x = (const bf16_t*)x;
+  p.dy = (const bf16_t*)dy;
+  p.N = N;
+  p.H = H;
+  p.W = W;
+  p.Cout = Cout;
+  p.dy_mode = dy_unshuffle ? IN_UNSHUF : IN_PLAIN;
+  p.imgs_per_wg = 1;
+  p.row_splits = row_splits > 0 ? row_splits : choose_row_splits(N, H, Cout);
+  const size_t ns = (size_t)wgrad3x3_nslabs(p);
+  const size_t need = ns * Cout * 577 * sizeof(float);
+  if (slab_bytes < need) return SRMI_ERR_WORKSPACE;
+  p.slab = slab;
+  p.bslab = slab + ns * Cout * 576;
+  RC(wgrad3x3_launch(p, S_(stream)));
+  return wgrad_reduce_launch(p.slab, p.bslab, (int)ns, Cout, ps, alpha, gw, gb, S_(stream));
+}
+
+int srmi_ca_forward(const void* u, const float* part, int nstrips, const float* w1, const float* b1, const float* w2,
+                    const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, void* hb_out,
+                    float* rec, void* stream) {
+  return ca_fwd_launch((const bf16_t*)u, part, nstrips, w1, b1, w2, b2, N, HW, C, R, h_in, h_out, (bf16_t*)hb_out,
+                       rec, S_(stream));
+}
+
+int srmi_ca_backward(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
+                     const float* w2, int N, int HW, int C, int R, void* du, float* brec, void* stream) {
+  return ca_bwd_du_launch(g, part, nstrips, rec, w1, w2, N, HW, C, R, (bf16_t*)du, brec, S_(stream));
+}
+
+int srmi_head_forward(const float* lr, const float* w, const float* b, int N, int C, int H, int W, float* x0f,
+                      void* x0b, void* stream) {
+  return head_fwd_launch(lr, w, b, N, C, H, W, x0f, (bf16_t*)x0b, S_(stream));
+}
+
+int srmi_tail_forward(const void* x, const float* w, const float* b, int N, int C, int H, int W, float* y,
+                      void* stream) {
+  return tail_fwd_launch((const bf16_t*)x, w, b, N, C, H, W, y, S_(stream));
+}
+
+}  // extern "C"

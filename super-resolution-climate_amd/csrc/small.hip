@@ -1,0 +1,835 @@
+// Memory-bound / small-channel kernels of the RCAN hot path on gfx950:
+//  * head conv C->64 (sres/model/rcan/network.py:13) fwd + weight grad
+//  * tail conv 64->C (network.py:16) fwd, data grad (with the RMSE gradient
+//    formed on the fly) and weight grad
+//  * bicubic 1/scale downsample (sres/base/util/array.py:72-76) and xscale
+//    upsample (array.py:84-87, the interp baseline)
+//  * RMSE loss partial sums (sres/controller/stats.py:5-8)
+//  * channel attention forward (CALayer, network.py:31-47 + RCAB skip :61-64)
+//    and backward, fused with the residual stream
+//  * Adam (torch.optim.Adam defaults, dual_trainer.py:126,323)
+//  * fp32 -> bf16 filter packing for the MFMA conv kernels
+#include <math.h>
+
+#include "common.hpp"
+#include "srmi_internal.hpp"
+
+namespace srmi {
+
+// =========================================================================== head
+// x0[n][y][x][co] = b[co] + sum_{c,tap} lr[n][c][y+ky-1][x+kx-1] * w[co][c][tap]
+__global__ void __launch_bounds__(256) head_fwd_kernel(const float* __restrict__ lr, const float* __restrict__ w,
+                                                       const float* __restrict__ b, int C, int H, int W,
+                                                       float* __restrict__ x0f, bf16_t* __restrict__ x0b) {
+  extern __shared__ float hs[];  // [C][6][W+2] halo, then [64][9C] weights
+  const int n = blockIdx.y, y0 = blockIdx.x * 4, tid = threadIdx.x;
+  const int Wp = W + 2;
+  float* halo = hs;
+  const int hsz = C * 6 * Wp;
+  for (int i = tid; i < hsz; i += 256) {
+    const int c = i / (6 * Wp), r = (i / Wp) % 6, xx = i % Wp;
+    const int y = y0 - 1 + r, x = xx - 1;
+    halo[i] = (y >= 0 && y < H && x >= 0 && x < W) ? lr[(((size_t)n * C + c) * H + y) * W + x] : 0.f;
+  }
+  __syncthreads();
+  const int co = tid & 63, grp = tid >> 6;
+  float wr[36];
+#pragma unroll
+  for (int k = 0; k < 36; ++k) wr[k] = (k < 9 * C) ? w[co * 9 * C + k] : 0.f;
+  const float bb = b[co];
+  for (int px = grp; px < 4 * W; px += 4) {
+    const int r = px / W, x = px - r * W;
+    float s = bb;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c < C) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+          s += halo[(c * 6 + r + t / 3) * Wp + x + t % 3] * wr[c * 9 + t];
+      }
+    }
+    const size_t o = (((size_t)n * H + y0 + r) * W + x) * 64 + co;
+    x0f[o] = s;
+    x0b[o] = f2bf(s);
+  }
+}
+
+int head_fwd_launch(const float* lr, const float* w, const float* b, int N, int C, int H, int W, float* x0f,
+                    bf16_t* x0b, hipStream_t st) {
+  if (C < 1 || C > 4 || H % 4) return SRMI_ERR_SHAPE;
+  const int smem = C * 6 * (W + 2) * 4;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(H / 4, N), dim3(256), smem, st, lr, w, b, C, H, W, x0f, x0b);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// dW[co][c][tap] = sum_p g[p][co] * lr[c][p+off];  db[co] = sum_p g[p][co]
+// one workgroup per (image, 4-row strip); slab [co][9C + 1]
+__global__ void __launch_bounds__(256) head_wgrad_kernel(const float* __restrict__ lr, const float* __restrict__ g,
+                                                         int C, int H, int W, float* __restrict__ slab) {
+  extern __shared__ float hs[];
+  const int n = blockIdx.y, y0 = blockIdx.x * 4, tid = threadIdx.x;
+  const int Wp = W + 2;
+  const int hsz = C * 6 * Wp;
+  for (int i = tid; i < hsz; i += 256) {
+    const int c = i / (6 * Wp), r = (i / Wp) % 6, xx = i % Wp;
+    const int y = y0 - 1 + r, x = xx - 1;
+    hs[i] = (y >= 0 && y < H && x >= 0 && x < W) ? lr[(((size_t)n * C + c) * H + y) * W + x] : 0.f;
+  }
+  __syncthreads();
+  const int co = tid & 63, grp = tid >> 6;
+  const int nj = 9 * C + 1;  // last = bias
+  float acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = 0.f;
+  for (int px = 0; px < 4 * W; ++px) {
+    const int r = px / W, x = px - r * W;
+    const float gv = g[(((size_t)n * H + y0 + r) * W + x) * 64 + co];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const int j = grp + 4 * k;
+      if (j < nj - 1) {
+        const int c = j / 9, t = j % 9;
+        acc[k] += gv * hs[(c * 6 + r + t / 3) * Wp + x + t % 3];
+      } else if (j == nj - 1) {
+        acc[k] += gv;
+      }
+    }
+  }
+  float* out = slab + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 64 * nj;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    const int j = grp + 4 * k;
+    if (j < nj) out[co * nj + j] = acc[k];
+  }
+}
+
+int head_wgrad_launch(const float* lr, const float* g, int N, int C, int H, int W, float* slab, int* nslab,
+                      hipStream_t st) {
+  if (C < 1 || C > 4 || H % 4) return SRMI_ERR_SHAPE;
+  const int smem = C * 6 * (W + 2) * 4;
+  hipLaunchKernelGGL(head_wgrad_kernel, dim3(H / 4, N), dim3(256), smem, st, lr, g, C, H, W, slab);
+  SRMI_CHECK_LAUNCH();
+  *nslab = N * (H / 4);
+  return 0;
+}
+
+__global__ void head_wgrad_reduce_kernel(const float* __restrict__ slab, int nslab, int C, float* __restrict__ gw,
+                                         float* __restrict__ gb) {
+  const int nj = 9 * C + 1, per = 64 * nj;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= per) return;
+  float s = 0.f;
+  for (int k = 0; k < nslab; ++k) s += slab[(size_t)k * per + idx];
+  const int co = idx / nj, j = idx % nj;
+  if (j < nj - 1)
+    gw[co * 9 * C + j] = s;
+  else
+    gb[co] = s;
+}
+
+int head_wgrad_reduce_launch(const float* slab, int nslab, int C, float* gw, float* gb, hipStream_t st) {
+  const int per = 64 * (9 * C + 1);
+  hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((per + 255) / 256), dim3(256), 0, st, slab, nslab, C, gw, gb);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// =========================================================================== tail
+// y[n][c][yy][xx] = b[c] + sum_{tap,ci} x[n][yy+ky-1][xx+kx-1][ci] * w[c][ci][tap]
+template <int TWT>
+__global__ void __launch_bounds__(4 * TWT) tail_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ b, int C, int H, int W,
+                                                          float* __restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) char ts[];
+  constexpr int NT = 4 * TWT, WP = TWT + 2, HP = 6 * WP;
+  const int n = blockIdx.z, y0 = blockIdx.y * 4, x0 = blockIdx.x * TWT, tid = threadIdx.x;
+  for (int i = tid; i < HP * 8; i += NT) {
+    const int q = i >> 3, c = i & 7;
+    const int hy = q / WP, hx = q - hy * WP;
+    const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+      v = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + c * 8);
+    *reinterpret_cast<uint4*>(ts + swz128(q, c)) = v;
+  }
+  __syncthreads();
+  const int r = tid / TWT, px = tid - r * TWT;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < 9; ++t) {
+    const int q = (r + t / 3) * WP + px + t % 3;
+#pragma unroll
+    for (int c8 = 0; c8 < 8; ++c8) {
+      const uint4 v = *reinterpret_cast<const uint4*>(ts + swz128(q, c8));
+      const float xv[8] = {bf2f(v.x & 0xFFFF), bf2f(v.x >> 16), bf2f(v.y & 0xFFFF), bf2f(v.y >> 16),
+                           bf2f(v.z & 0xFFFF), bf2f(v.z >> 16), bf2f(v.w & 0xFFFF), bf2f(v.w >> 16)};
+#pragma unroll
+      for (int co = 0; co < 4; ++co) {
+        if (co < C) {
+          const float* wp = w + ((size_t)co * 64 + c8 * 8) * 9 + t;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[co] += xv[e] * wp[e * 9];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int co = 0; co < 4; ++co)
+    if (co < C) y[(((size_t)n * C + co) * H + y0 + r) * W + x0 + px] = acc[co] + b[co];
+}
+
+int tail_fwd_launch(const bf16_t* x, const float* w, const float* b, int N, int C, int H, int W, float* y,
+                    hipStream_t st) {
+  if (C < 1 || C > 4 || H % 4) return SRMI_ERR_SHAPE;
+  if (W % 64 == 0) {
+    hipLaunchKernelGGL(tail_fwd_kernel<64>, dim3(W / 64, H / 4, N), dim3(256), 6 * 66 * 128, st, x, w, b, C, H, W, y);
+  } else if (W % 32 == 0) {
+    hipLaunchKernelGGL(tail_fwd_kernel<32>, dim3(W / 32, H / 4, N), dim3(128), 6 * 34 * 128, st, x, w, b, C, H, W, y);
+  } else {
+    return SRMI_ERR_SHAPE;
+  }
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// dx[n][yy][xx][ci] = sum_{tap,c} dy[n][c][yy-ky+1][xx-kx+1] * w[c][ci][tap],
+// dy = (y - hr) * loss[2]   (gradient of the RMSE, stats.py:5-8)
+template <int TWT>
+__global__ void __launch_bounds__(256) tail_dgrad_kernel(const float* __restrict__ yv, const float* __restrict__ hr,
+                                                        const float* __restrict__ loss, const float* __restrict__ w,
+                                                        int C, int H, int W, bf16_t* __restrict__ dx) {
+  extern __shared__ __attribute__((aligned(16))) float tds[];
+  constexpr int WP = TWT + 2;
+  const int n = blockIdx.z, y0 = blockIdx.y * 4, x0 = blockIdx.x * TWT, tid = threadIdx.x;
+  float* dyl = tds;                   // [C][6][WP]
+  float* wl = tds + 4 * 6 * WP;       // [C][9][64]  (tap-major, ci contiguous)
+  const float sc = loss ? loss[2] : 1.f;
+  for (int i = tid; i < C * 6 * WP; i += 256) {
+    const int c = i / (6 * WP), r = (i / WP) % 6, xx = i % WP;
+    const int yy = y0 - 1 + r, xg = x0 - 1 + xx;
+    float v = 0.f;
+    if (yy >= 0 && yy < H && xg >= 0 && xg < W) {
+      const size_t o = (((size_t)n * C + c) * H + yy) * W + xg;
+      v = hr ? (yv[o] - hr[o]) * sc : yv[o] * sc;
+    }
+    dyl[i] = v;
+  }
+  for (int i = tid; i < C * 576; i += 256) {
+    const int c = i / 576, t = (i / 64) % 9, ci = i % 64;
+    wl[i] = w[((size_t)c * 64 + ci) * 9 + t];
+  }
+  __syncthreads();
+  const int ck = tid & 7;
+  for (int px = tid >> 3; px < 4 * TWT; px += 32) {
+    const int r = px / TWT, xx = px - r * TWT;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int c = 0; c < C; ++c) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int ky = t / 3, kx = t % 3;
+        const float d = dyl[(c * 6 + r + 2 - ky) * WP + xx + 2 - kx];
+        const float4 w0 = *reinterpret_cast<const float4*>(wl + (c * 9 + t) * 64 + ck * 8);
+        const float4 w1 = *reinterpret_cast<const float4*>(wl + (c * 9 + t) * 64 + ck * 8 + 4);
+        acc[0] += d * w0.x; acc[1] += d * w0.y; acc[2] += d * w0.z; acc[3] += d * w0.w;
+        acc[4] += d * w1.x; acc[5] += d * w1.y; acc[6] += d * w1.z; acc[7] += d * w1.w;
+      }
+    }
+    uint4 o;
+    o.x = pack2(acc[0], acc[1]); o.y = pack2(acc[2], acc[3]);
+    o.z = pack2(acc[4], acc[5]); o.w = pack2(acc[6], acc[7]);
+    *reinterpret_cast<uint4*>(dx + (((size_t)n * H + y0 + r) * W + x0 + xx) * 64 + ck * 8) = o;
+  }
+}
+
+int tail_dgrad_launch(const float* y, const float* hr, const float* loss, const float* w, int N, int C, int H, int W,
+                      bf16_t* dx, hipStream_t st) {
+  if (C < 1 || C > 4 || H % 4) return SRMI_ERR_SHAPE;
+  if (W % 64 == 0) {
+    const int smem = (4 * 6 * 66 + 4 * 576) * 4;
+    hipLaunchKernelGGL(tail_dgrad_kernel<64>, dim3(W / 64, H / 4, N), dim3(256), smem, st, y, hr, loss, w, C, H, W, dx);
+  } else if (W % 32 == 0) {
+    const int smem = (4 * 6 * 34 + 4 * 576) * 4;
+    hipLaunchKernelGGL(tail_dgrad_kernel<32>, dim3(W / 32, H / 4, N), dim3(256), smem, st, y, hr, loss, w, C, H, W, dx);
+  } else {
+    return SRMI_ERR_SHAPE;
+  }
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// dW[c][ci][tap] = sum_p dy[c][p] * x[p+off][ci];  db[c] = sum_p dy[c][p]
+// workgroup = (image, 16-row band); slab [C][577]
+constexpr int kTailRows = 16;
+template <int TWT>
+__global__ void __launch_bounds__(256) tail_wgrad_kernel(const float* __restrict__ yv, const float* __restrict__ hr,
+                                                        const float* __restrict__ loss, const bf16_t* __restrict__ x,
+                                                        int C, int H, int W, float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) char tws[];
+  constexpr int WP = TWT + 2, HP = 6 * WP;
+  char* halo = tws;
+  float* dyl = reinterpret_cast<float*>(tws + HP * 128);  // [C][4][TWT]
+  const int n = blockIdx.y, band = blockIdx.x, tid = threadIdx.x;
+  const int ci = tid & 63, grp = tid >> 6;
+  const float sc = loss ? loss[2] : 1.f;
+  float acc[3][4];
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[a][c] = 0.f;
+  float bacc = 0.f;
+  const int ntx = W / TWT;
+  for (int tile = 0; tile < (kTailRows / 4) * ntx; ++tile) {
+    const int y0 = band * kTailRows + (tile / ntx) * 4, x0 = (tile % ntx) * TWT;
+    __syncthreads();
+    for (int i = tid; i < HP * 8; i += 256) {
+      const int q = i >> 3, c = i & 7;
+      const int hy = q / WP, hx = q - hy * WP;
+      const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+        v = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + c * 8);
+      *reinterpret_cast<uint4*>(halo + swz128(q, c)) = v;
+    }
+    for (int i = tid; i < C * 4 * TWT; i += 256) {
+      const int c = i / (4 * TWT), r = (i / TWT) % 4, xx = i % TWT;
+      const size_t o = (((size_t)n * C + c) * H + y0 + r) * W + x0 + xx;
+      dyl[i] = hr ? (yv[o] - hr[o]) * sc : yv[o] * sc;
+    }
+    __syncthreads();
+    for (int px = 0; px < 4 * TWT; ++px) {
+      const int r = px / TWT, xx = px - r * TWT;
+      float d[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) d[c] = (c < C) ? dyl[(c * 4 + r) * TWT + xx] : 0.f;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const int t = grp + 4 * a;
+        if (t < 9) {
+          const int q = (r + t / 3) * WP + xx + t % 3;
+          const float xv = bf2f(*reinterpret_cast<const bf16_t*>(halo + swz128(q, ci >> 3) + (ci & 7) * 2));
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[a][c] += d[c] * xv;
+        }
+      }
+      if (tid < C) bacc += dyl[(tid * 4 + r) * TWT + xx];
+    }
+  }
+  float* out = slab + ((size_t)n * gridDim.x + band) * C * 577;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const int t = grp + 4 * a;
+    if (t < 9)
+      for (int c = 0; c < C; ++c) out[c * 577 + ci * 9 + t] = acc[a][c];
+  }
+  if (tid < C) out[tid * 577 + 576] = bacc;
+}
+
+int tail_wgrad_launch(const float* y, const float* hr, const float* loss, const bf16_t* x, int N, int C, int H,
+                      int W, float* slab, int* nslab, hipStream_t st) {
+  if (C < 1 || C > 4 || H % kTailRows) return SRMI_ERR_SHAPE;
+  const dim3 grid(H / kTailRows, N);
+  if (W % 64 == 0) {
+    const int smem = 6 * 66 * 128 + 4 * 4 * 64 * 4;
+    hipLaunchKernelGGL(tail_wgrad_kernel<64>, grid, dim3(256), smem, st, y, hr, loss, x, C, H, W, slab);
+  } else if (W % 32 == 0) {
+    const int smem = 6 * 34 * 128 + 4 * 4 * 32 * 4;
+    hipLaunchKernelGGL(tail_wgrad_kernel<32>, grid, dim3(256), smem, st, y, hr, loss, x, C, H, W, slab);
+  } else {
+    return SRMI_ERR_SHAPE;
+  }
+  SRMI_CHECK_LAUNCH();
+  *nslab = N * (H / kTailRows);
+  return 0;
+}
+
+__global__ void tail_wgrad_reduce_kernel(const float* __restrict__ slab, int nslab, int C, float* __restrict__ gw,
+                                         float* __restrict__ gb) {
+  const int per = C * 577;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= per) return;
+  float s = 0.f;
+  for (int k = 0; k < nslab; ++k) s += slab[(size_t)k * per + idx];
+  const int c = idx / 577, j = idx % 577;
+  if (j < 576)
+    gw[c * 576 + j] = s;  // [c][ci][tap] == torch [C][64][3][3]
+  else
+    gb[c] = s;
+}
+
+int tail_wgrad_reduce_launch(const float* slab, int nslab, int C, float* gw, float* gb, hipStream_t st) {
+  const int per = C * 577;
+  hipLaunchKernelGGL(tail_wgrad_reduce_kernel, dim3((per + 255) / 256), dim3(256), 0, st, slab, nslab, C, gw, gb);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// ====================================================================== resampling
+// bicubic (A = -0.75, align_corners = False) at 1/scale: the source coordinate
+// scale*d + (scale-1)/2 is half-way between samples -> separable [-3,19,19,-3]/32
+__global__ void downsample_kernel(const float* __restrict__ hr, int NC, int H, int W, int scale,
+                                  float* __restrict__ lr) {
+  const int h = H / scale, w = W / scale;
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)NC * h * w) return;
+  const int x = idx % w, y = (idx / w) % h;
+  const size_t nc = idx / ((size_t)w * h);
+  const float k[4] = {-3.f / 32.f, 19.f / 32.f, 19.f / 32.f, -3.f / 32.f};
+  const int sy = y * scale + scale / 2 - 2, sx = x * scale + scale / 2 - 2;
+  const float* src = hr + nc * H * W;
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int yy = min(max(sy + i, 0), H - 1);
+    float rsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int xx = min(max(sx + j, 0), W - 1);
+      rsum += k[j] * src[(size_t)yy * W + xx];
+    }
+    acc += k[i] * rsum;
+  }
+  lr[idx] = acc;
+}
+
+int downsample_launch(const float* hr, int N, int C, int H, int W, int scale, float* lr, hipStream_t st) {
+  if (scale < 2 || H % scale || W % scale) return SRMI_ERR_SHAPE;
+  const size_t tot = (size_t)N * C * (H / scale) * (W / scale);
+  hipLaunchKernelGGL(downsample_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, hr, N * C, H, W, scale, lr);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+__device__ __forceinline__ void cubic_w(float t, float* c) {
+  const float A = -0.75f;
+  float x1 = t + 1.f;
+  c[0] = ((A * x1 - 5.f * A) * x1 + 8.f * A) * x1 - 4.f * A;
+  float x = t;
+  c[1] = ((A + 2.f) * x - (A + 3.f)) * x * x + 1.f;
+  x = 1.f - t;
+  c[2] = ((A + 2.f) * x - (A + 3.f)) * x * x + 1.f;
+  float x2 = 2.f - t;
+  c[3] = ((A * x2 - 5.f * A) * x2 + 8.f * A) * x2 - 4.f * A;
+}
+
+__global__ void upsample_kernel(const float* __restrict__ lr, int NC, int h, int w, int scale,
+                                float* __restrict__ hr) {
+  const int H = h * scale, W = w * scale;
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)NC * H * W) return;
+  const int X = idx % W, Y = (idx / W) % H;
+  const size_t nc = idx / ((size_t)W * H);
+  const float inv = 1.f / (float)scale;
+  const float sy = inv * (Y + 0.5f) - 0.5f, sx = inv * (X + 0.5f) - 0.5f;
+  const int iy = (int)floorf(sy), ix = (int)floorf(sx);
+  float wy[4], wx[4];
+  cubic_w(sy - iy, wy);
+  cubic_w(sx - ix, wx);
+  const float* src = lr + nc * h * w;
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int yy = min(max(iy - 1 + i, 0), h - 1);
+    float rsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int xx = min(max(ix - 1 + j, 0), w - 1);
+      rsum += wx[j] * src[(size_t)yy * w + xx];
+    }
+    acc += wy[i] * rsum;
+  }
+  hr[idx] = acc;
+}
+
+int upsample_launch(const float* lr, int N, int C, int h, int w, int scale, float* hr, hipStream_t st) {
+  const size_t tot = (size_t)N * C * h * scale * w * scale;
+  hipLaunchKernelGGL(upsample_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, lr, N * C, h, w, scale, hr);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// ============================================================================ loss
+__global__ void __launch_bounds__(256) sqerr_partial_kernel(const float* __restrict__ y, const float* __restrict__ t,
+                                                            size_t n, float* __restrict__ partial) {
+  __shared__ float red[4];
+  float s = 0.f;
+  const size_t n4 = n / 4;
+  const float4* y4 = reinterpret_cast<const float4*>(y);
+  const float4* t4 = reinterpret_cast<const float4*>(t);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const float4 a = y4[i], b = t4[i];
+    const float d0 = a.x - b.x, d1 = a.y - b.y, d2 = a.z - b.z, d3 = a.w - b.w;
+    s += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+  }
+  if (blockIdx.x == 0)
+    for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) {
+      const float d = y[i] - t[i];
+      s += d * d;
+    }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+int sqerr_partial_launch(const float* y, const float* t, size_t n, float* partial, int nblk, hipStream_t st) {
+  hipLaunchKernelGGL(sqerr_partial_kernel, dim3(nblk), dim3(256), 0, st, y, t, n, partial);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void sqerr_finish_kernel(const float* __restrict__ partial, int nblk, double count, float* loss) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nblk; i += 256) s += partial[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    loss[0] = (float)red[0];
+    loss[1] = (float)count;
+  }
+}
+
+int sqerr_finish_launch(const float* partial, int nblk, double count, float* loss, hipStream_t st) {
+  hipLaunchKernelGGL(sqerr_finish_kernel, dim3(1), dim3(256), 0, st, partial, nblk, count, loss);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// loss[3] = L = sqrt(S / count), loss[2] = dL/dy scale = 1 / (count * L)
+__global__ void loss_finalize_kernel(float* loss) {
+  const float L = sqrtf(loss[0] / loss[1]);
+  loss[3] = L;
+  loss[2] = 1.f / (loss[1] * L);
+}
+
+int loss_finalize_launch(float* loss, hipStream_t st) {
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1), 0, st, loss);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// =============================================================== channel attention
+// rec layout per image: m[C] z1[C/R] s[C]   (C = 64, C/R = 32)
+__device__ void ca_mlp(const float* __restrict__ part, int nstrips, int pstride, int n, int HW,
+                       const float* __restrict__ w1, const float* __restrict__ b1, const float* __restrict__ w2,
+                       const float* __restrict__ b2, int C, int CR, float* sm /* [C] m | [CR] z1 | [C] s */) {
+  const int tid = threadIdx.x;
+  if (tid < C) {
+    float s = 0.f;
+    for (int k = 0; k < nstrips; ++k) s += part[((size_t)n * nstrips + k) * pstride + tid];
+    sm[tid] = s / (float)HW;
+  }
+  __syncthreads();
+  if (tid < CR) {
+    float z = b1[tid];
+    for (int c = 0; c < C; ++c) z += w1[tid * C + c] * sm[c];
+    sm[C + tid] = z;
+  }
+  __syncthreads();
+  if (tid < C) {
+    float z = b2[tid];
+    for (int j = 0; j < CR; ++j) z += w2[tid * CR + j] * fmaxf(sm[C + j], 0.f);
+    sm[C + CR + tid] = 1.f / (1.f + expf(-z));
+  }
+  __syncthreads();
+}
+
+// h_out = u * s + h_in  (fp32 + bf16 copy); grid (chunks, N)
+__global__ void __launch_bounds__(256) ca_fwd_kernel(const bf16_t* __restrict__ u, const float* __restrict__ part,
+                                                     int nstrips, const float* __restrict__ w1,
+                                                     const float* __restrict__ b1, const float* __restrict__ w2,
+                                                     const float* __restrict__ b2, int HW, int C, int CR,
+                                                     const float* __restrict__ h_in, float* __restrict__ h_out,
+                                                     bf16_t* __restrict__ hb_out, float* __restrict__ rec) {
+  __shared__ float sm[64 + 32 + 64];
+  const int n = blockIdx.y;
+  ca_mlp(part, nstrips, C, n, HW, w1, b1, w2, b2, C, CR, sm);
+  if (blockIdx.x == 0 && threadIdx.x < 2 * C + CR) rec[(size_t)n * (2 * C + CR) + threadIdx.x] = sm[threadIdx.x];
+  const float* s = sm + C + CR;
+  const size_t base = (size_t)n * HW * C;
+  const size_t nv = (size_t)HW * C / 8;
+  for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (size_t)gridDim.x * blockDim.x) {
+    const size_t e = base + v * 8;
+    const int c0 = (int)((v * 8) % C);
+    const uint4 uu = *reinterpret_cast<const uint4*>(u + e);
+    const float4 h0 = *reinterpret_cast<const float4*>(h_in + e);
+    const float4 h1 = *reinterpret_cast<const float4*>(h_in + e + 4);
+    float o[8];
+    o[0] = bf2f(uu.x & 0xFFFF) * s[c0 + 0] + h0.x;
+    o[1] = bf2f(uu.x >> 16) * s[c0 + 1] + h0.y;
+    o[2] = bf2f(uu.y & 0xFFFF) * s[c0 + 2] + h0.z;
+    o[3] = bf2f(uu.y >> 16) * s[c0 + 3] + h0.w;
+    o[4] = bf2f(uu.z & 0xFFFF) * s[c0 + 4] + h1.x;
+    o[5] = bf2f(uu.z >> 16) * s[c0 + 5] + h1.y;
+    o[6] = bf2f(uu.w & 0xFFFF) * s[c0 + 6] + h1.z;
+    o[7] = bf2f(uu.w >> 16) * s[c0 + 7] + h1.w;
+    *reinterpret_cast<float4*>(h_out + e) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4*>(h_out + e + 4) = make_float4(o[4], o[5], o[6], o[7]);
+    uint4 ob;
+    ob.x = pack2(o[0], o[1]); ob.y = pack2(o[2], o[3]); ob.z = pack2(o[4], o[5]); ob.w = pack2(o[6], o[7]);
+    *reinterpret_cast<uint4*>(hb_out + e) = ob;
+  }
+}
+
+static int ca_grid_x(int HW, int C) {
+  const int nv = HW * C / 8;
+  int gx = (nv + 255) / 256;
+  return gx < 1 ? 1 : gx;
+}
+
+int ca_fwd_launch(const bf16_t* u, const float* part, int nstrips, const float* w1, const float* b1, const float* w2,
+                  const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, bf16_t* hb_out,
+                  float* rec, hipStream_t st) {
+  if (C != 64 || C % R || (HW * C) % 8) return SRMI_ERR_SHAPE;
+  hipLaunchKernelGGL(ca_fwd_kernel, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, u, part, nstrips, w1, b1, w2, b2,
+                     HW, C, C / R, h_in, h_out, hb_out, rec);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// CA backward per image + du = g * s + dm / HW  (bf16).  part[n][strip][2C] holds
+// sum_p g (0..C-1) and sum_p g*u (C..2C-1) from the producer of g.
+// brec per image: dz2[C] dz1[CR] dbconv2[C]
+__global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict__ g, const float* __restrict__ part,
+                                                        int nstrips, const float* __restrict__ rec,
+                                                        const float* __restrict__ w1, const float* __restrict__ w2,
+                                                        int HW, int C, int CR, bf16_t* __restrict__ du,
+                                                        float* __restrict__ brec) {
+  __shared__ float sm[64 * 4 + 32 * 2];
+  const int n = blockIdx.y, tid = threadIdx.x;
+  const float* r = rec + (size_t)n * (2 * C + CR);
+  float* G = sm;            // [C]
+  float* dsv = sm + C;      // [C]
+  float* dz2 = sm + 2 * C;  // [C]
+  float* dm = sm + 3 * C;   // [C]
+  float* dz1 = sm + 4 * C;  // [CR]
+  if (tid < C) {
+    float a = 0.f, b = 0.f;
+    for (int k = 0; k < nstrips; ++k) {
+      const float* pp = part + ((size_t)n * nstrips + k) * (2 * C);
+      a += pp[tid];
+      b += pp[C + tid];
+    }
+    G[tid] = a;
+    dsv[tid] = b;
+    const float s = r[C + CR + tid];
+    dz2[tid] = b * s * (1.f - s);
+  }
+  __syncthreads();
+  if (tid < CR) {
+    float a = 0.f;
+    for (int c = 0; c < C; ++c) a += w2[c * CR + tid] * dz2[c];
+    dz1[tid] = (r[C + tid] > 0.f) ? a : 0.f;
+  }
+  __syncthreads();
+  if (tid < C) {
+    float a = 0.f;
+    for (int j = 0; j < CR; ++j) a += w1[j * C + tid] * dz1[j];
+    dm[tid] = a;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    float* br = brec + (size_t)n * (2 * C + CR);
+    if (tid < C) {
+      br[tid] = dz2[tid];
+      br[C + CR + tid] = r[C + CR + tid] * G[tid] + dm[tid];
+    } else if (tid < C + CR) {
+      br[tid] = dz1[tid - C];
+    }
+  }
+  const float* s = r + C + CR;
+  const float inv = 1.f / (float)HW;
+  const size_t base = (size_t)n * HW * C;
+  const size_t nv = (size_t)HW * C / 8;
+  for (size_t v = (size_t)blockIdx.x * blockDim.x + tid; v < nv; v += (size_t)gridDim.x * blockDim.x) {
+    const size_t e = base + v * 8;
+    const int c0 = (int)((v * 8) % C);
+    const float4 g0 = *reinterpret_cast<const float4*>(g + e);
+    const float4 g1 = *reinterpret_cast<const float4*>(g + e + 4);
+    uint4 ob;
+    ob.x = pack2(g0.x * s[c0 + 0] + dm[c0 + 0] * inv, g0.y * s[c0 + 1] + dm[c0 + 1] * inv);
+    ob.y = pack2(g0.z * s[c0 + 2] + dm[c0 + 2] * inv, g0.w * s[c0 + 3] + dm[c0 + 3] * inv);
+    ob.z = pack2(g1.x * s[c0 + 4] + dm[c0 + 4] * inv, g1.y * s[c0 + 5] + dm[c0 + 5] * inv);
+    ob.w = pack2(g1.z * s[c0 + 6] + dm[c0 + 6] * inv, g1.w * s[c0 + 7] + dm[c0 + 7] * inv);
+    *reinterpret_cast<uint4*>(du + e) = ob;
+  }
+}
+
+int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
+                     const float* w2, int N, int HW, int C, int R, bf16_t* du, float* brec, hipStream_t st) {
+  if (C != 64 || C % R || (HW * C) % 8) return SRMI_ERR_SHAPE;
+  hipLaunchKernelGGL(ca_bwd_du_kernel, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, g, part, nstrips, rec, w1, w2,
+                     HW, C, C / R, du, brec);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// CA parameter grads of `nblocks` RCABs (summed over images, fixed order), plus
+// the conv2 bias grad.  offs[k*5 + {0..4}] = grad offsets of
+// conv_du.0.weight, conv_du.0.bias, conv_du.2.weight, conv_du.2.bias, conv2.bias
+__global__ void __launch_bounds__(256) ca_param_grads_kernel(const float* __restrict__ recs,
+                                                             const float* __restrict__ brecs, int N, int C, int CR,
+                                                             const long long* __restrict__ offs,
+                                                             float* __restrict__ grads) {
+  const int k = blockIdx.x;
+  const int rs = 2 * C + CR;
+  const float* rec = recs + (size_t)k * N * rs;
+  const float* brec = brecs + (size_t)k * N * rs;
+  float* gw1 = grads + offs[k * 5 + 0];
+  float* gb1 = grads + offs[k * 5 + 1];
+  float* gw2 = grads + offs[k * 5 + 2];
+  float* gb2 = grads + offs[k * 5 + 3];
+  float* gbc = grads + offs[k * 5 + 4];
+  for (int o = threadIdx.x; o < 2 * C * CR; o += 256) {
+    if (o < C * CR) {  // dW2[c][j] = sum_n dz2[n][c] * relu(z1[n][j])
+      const int c = o / CR, j = o % CR;
+      float s = 0.f;
+      for (int n = 0; n < N; ++n) s += brec[n * rs + c] * fmaxf(rec[n * rs + C + j], 0.f);
+      gw2[o] = s;
+    } else {  // dW1[j][c] = sum_n dz1[n][j] * m[n][c]
+      const int oo = o - C * CR;
+      const int j = oo / C, c = oo % C;
+      float s = 0.f;
+      for (int n = 0; n < N; ++n) s += brec[n * rs + C + j] * rec[n * rs + c];
+      gw1[oo] = s;
+    }
+  }
+  for (int o = threadIdx.x; o < 2 * C + CR; o += 256) {
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += brec[n * rs + o];
+    if (o < C)
+      gb2[o] = s;
+    else if (o < C + CR)
+      gb1[o - C] = s;
+    else
+      gbc[o - C - CR] = s;
+  }
+}
+
+int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int C, int R,
+                                  const long long* offs, float* grads, hipStream_t st) {
+  hipLaunchKernelGGL(ca_param_grads_kernel, dim3(nblocks), dim3(256), 0, st, recs, brecs, N, C, C / R, offs, grads);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// ============================================================================ Adam
+// torch.optim.Adam (foreach path): m.lerp_(g, 1-b1); v = b2 v + (1-b2) g^2;
+// p -= step_size * m / (sqrt(v)/sqrt(bc2) + eps)
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, size_t n, float b1, float b2, float eps, float wd,
+                            float step_size, float bc2_sqrt) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float gi = g[i];
+    const float pi = p[i];
+    if (wd != 0.f) gi += wd * pi;
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi - step_size * (mi / (sqrtf(vi) / bc2_sqrt + eps));
+  }
+}
+
+int adam_launch(float* p, const float* g, float* m, float* v, size_t n, float lr, float b1, float b2, float eps,
+                float wd, float step_size, float bc2_sqrt, hipStream_t st) {
+  (void)lr;
+  size_t blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, st, p, g, m, v, n, b1, b2, eps, wd, step_size,
+                     bc2_sqrt);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// ========================================================================= packing
+// forward pack [Cin/64][9][Cout][64]; dgrad pack [Cout/64][9][Cin][64] with the
+// taps flipped (dgrad == forward conv of dY with W'[ci][co][8-tap]); PixelShuffle
+// convs store output channel c'' = 64q + c for torch channel 4c + q, so each
+// 64-wide output block is one sub-pixel position.
+__device__ __forceinline__ void pack_elem(const float* __restrict__ W, const float* __restrict__ B, int Cout, int Cin,
+                                          int ps, int which, long long idx, bf16_t* __restrict__ fpack,
+                                          bf16_t* __restrict__ dpack, float* __restrict__ pbias) {
+  if (which == 0) {
+    const int ci_l = idx & 63;
+    long long rest = idx >> 6;
+    const int cop = rest % Cout;
+    rest /= Cout;
+    const int tap = rest % 9, cc = (int)(rest / 9);
+    const int cot = ps ? (4 * (cop & 63) + (cop >> 6)) : cop;
+    fpack[idx] = f2bf(W[((size_t)cot * Cin + cc * 64 + ci_l) * 9 + tap]);
+  } else if (which == 1) {
+    const int co_l = idx & 63;
+    long long rest = idx >> 6;
+    const int ci = rest % Cin;
+    rest /= Cin;
+    const int tapd = rest % 9, ccd = (int)(rest / 9);
+    const int cop = ccd * 64 + co_l;
+    const int cot = ps ? (4 * (cop & 63) + (cop >> 6)) : cop;
+    dpack[idx] = f2bf(W[((size_t)cot * Cin + ci) * 9 + (8 - tapd)]);
+  } else if (idx < Cout) {
+    const int cop = (int)idx;
+    const int cot = ps ? (4 * (cop & 63) + (cop >> 6)) : cop;
+    pbias[cop] = B[cot];
+  }
+}
+
+__global__ void pack_kernel(const float* __restrict__ params, const PackEntry* __restrict__ ents,
+                            bf16_t* __restrict__ packs, float* __restrict__ pbias) {
+  const PackEntry e = ents[blockIdx.y];
+  const long long total = (long long)e.Cout * e.Cin * 9;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x)
+    pack_elem(params + e.w_off, params + e.b_off, e.Cout, e.Cin, e.ps, blockIdx.z, idx, packs + e.f_off,
+              packs + e.d_off, pbias + e.pb_off);
+}
+
+int pack_launch(const float* params, const PackEntry* dev_entries, int nentries, long long max_elems, bf16_t* packs,
+                float* pbias, hipStream_t st) {
+  long long bx = (max_elems + 255) / 256;
+  if (bx > 1024) bx = 1024;
+  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)bx, nentries, 3), dim3(256), 0, st, params, dev_entries, packs,
+                     pbias);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void pack_one_kernel(const float* __restrict__ W, const float* __restrict__ B, int Cout, int Cin, int ps,
+                                bf16_t* __restrict__ fpack, bf16_t* __restrict__ dpack, float* __restrict__ pbias) {
+  const long long total = (long long)Cout * Cin * 9;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x)
+    pack_elem(W, B, Cout, Cin, ps, blockIdx.y, idx, fpack, dpack, pbias);
+}
+
+int pack_one_launch(const float* w, const float* b, int Cout, int Cin, int ps, bf16_t* fpack, bf16_t* dpack,
+                    float* pbias, hipStream_t st) {
+  if (Cout % 64 || Cin % 64) return SRMI_ERR_SHAPE;
+  long long bx = ((long long)Cout * Cin * 9 + 255) / 256;
+  if (bx > 1024) bx = 1024;
+  hipLaunchKernelGGL(pack_one_kernel, dim3((unsigned)bx, 3), dim3(256), 0, st, w, b, Cout, Cin, ps, fpack, dpack,
+                     pbias);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void scale_add_kernel(float* y, const float* x, float a, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    y[i] += a * x[i];
+}
+
+int scale_add_launch(float* y, const float* x, float a, size_t n, hipStream_t st) {
+  size_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(scale_add_kernel, dim3(blocks), dim3(256), 0, st, y, x, a, n);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace srmi

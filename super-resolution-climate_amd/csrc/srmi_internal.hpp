@@ -1,0 +1,116 @@
+// Internal (C++) interface between the kernel translation units and the engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/srmi.h"
+
+namespace srmi {
+
+typedef uint16_t bf16_t;
+
+enum InMode { IN_PLAIN = 0, IN_UNSHUF = 1 };
+
+enum Epi {
+  EPI_RELU_BF16 = 0,   // y = relu(acc + b)                       -> bf16
+  EPI_POOL_BF16 = 1,   // y = acc + b  (+ per-strip channel sums)   -> bf16
+  EPI_RESID = 2,       // y = alpha*(acc + b) + r1                  -> fp32 (opt) + bf16
+  EPI_PS_BF16 = 3,     // y = acc + b, PixelShuffle(2) scatter      -> bf16 [2H][2W][64]
+  EPI_DG_RELUMASK = 4, // dz = acc * (aux > 0)                      -> bf16
+  EPI_DG_ACC = 5,      // g = acc + r1 + r2 + r3 (+ sums of g, g*aux) -> fp32 + bf16
+  EPI_PLAIN_BF16 = 6,  // y = acc (+ b)                              -> bf16
+};
+
+struct ConvParams {
+  const bf16_t* x;     // input (logical NHWC [N][H][W][Cin])
+  const bf16_t* w;     // packed filters [Cin/64][9][Cout][64]
+  const float* bias;   // [Cout] packed order (may be null for dgrad)
+  int N, H, W, Cin, Cout;
+  int in_mode;
+  bf16_t* yb;          // bf16 output
+  float* yf;           // fp32 output
+  const float* r1;
+  const float* r2;
+  const float* r3;
+  const bf16_t* aux;   // relu output t (RELUMASK) / CA input u (DG_ACC sums)
+  float* part;         // per-strip channel sums
+  int part_stride;
+  float alpha;
+};
+
+int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st);
+int conv3x3_nstrips(int H, int W);
+
+// weight gradient of a 3x3 conv: slab[s][Cout][9][64] + bias slab[s][Cout]
+struct WgradParams {
+  const bf16_t* x;     // forward input NHWC [N][H][W][64]
+  const bf16_t* dy;    // output grad: plain [N][H][W][Cout] or PS [N][2H][2W][64] (Cout = 256)
+  int N, H, W, Cout;
+  int dy_mode;         // IN_PLAIN / IN_UNSHUF
+  int imgs_per_wg;     // images per workgroup
+  int row_splits;      // H split into this many row groups
+  float* slab;         // [nslab][Cout][9][64]
+  float* bslab;        // [nslab][Cout]
+};
+int wgrad3x3_launch(const WgradParams& p, hipStream_t st);
+int wgrad3x3_nslabs(const WgradParams& p);
+// slab reduction into the torch-layout grad [Cout][64][3][3] (+ bias [Cout]);
+// ps != 0 un-permutes the packed PixelShuffle channel order (c'' = 64q + c -> 4c + q)
+int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, float alpha, float* gw,
+                        float* gb, hipStream_t st);
+
+// small-channel kernels (head / tail), bicubic resampling, loss, CA, Adam, packing
+int head_fwd_launch(const float* lr, const float* w, const float* b, int N, int C, int H, int W, float* x0f,
+                    bf16_t* x0b, hipStream_t st);
+int head_wgrad_launch(const float* lr, const float* g, int N, int C, int H, int W, float* slab, int* nslab,
+                      hipStream_t st);
+int head_wgrad_reduce_launch(const float* slab, int nslab, int C, float* gw, float* gb, hipStream_t st);
+
+int tail_fwd_launch(const bf16_t* x, const float* w, const float* b, int N, int C, int H, int W, float* y,
+                    hipStream_t st);
+// dy is formed on the fly: dy = (y - hr) * scale, scale from loss[2]
+int tail_dgrad_launch(const float* y, const float* hr, const float* loss, const float* w, int N, int C, int H,
+                      int W, bf16_t* dx, hipStream_t st);
+int tail_wgrad_launch(const float* y, const float* hr, const float* loss, const bf16_t* x, int N, int C, int H,
+                      int W, float* slab, int* nslab, hipStream_t st);
+int tail_wgrad_reduce_launch(const float* slab, int nslab, int C, float* gw, float* gb, hipStream_t st);
+
+int downsample_launch(const float* hr, int N, int C, int H, int W, int scale, float* lr, hipStream_t st);
+int upsample_launch(const float* lr, int N, int C, int h, int w, int scale, float* hr, hipStream_t st);
+// loss[0] = sum (y-t)^2 (this rank), loss[1] = element count (global after all-reduce)
+int sqerr_partial_launch(const float* y, const float* t, size_t n, float* partial, int nblk, hipStream_t st);
+int sqerr_finish_launch(const float* partial, int nblk, double count, float* loss, hipStream_t st);
+int loss_finalize_launch(float* loss, hipStream_t st);
+
+// channel attention
+int ca_fwd_launch(const bf16_t* u, const float* part, int nstrips, const float* w1, const float* b1,
+                  const float* w2, const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out,
+                  bf16_t* hb_out, float* rec, hipStream_t st);
+int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
+                     const float* w2, int N, int HW, int C, int R, bf16_t* du, float* brec, hipStream_t st);
+int ca_param_grads_launch(const float* rec, const float* brec, int nblocks, int N, int C, int R,
+                          float* const* gptrs, hipStream_t st);
+int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int C, int R,
+                                  const long long* offs, float* grads, hipStream_t st);
+
+int adam_launch(float* p, const float* g, float* m, float* v, size_t n, float lr, float b1, float b2, float eps,
+                float wd, float step_size, float bc2_sqrt, hipStream_t st);
+
+struct PackEntry {
+  long long w_off;   // offset of the fp32 weight [Cout][Cin][3][3] in the param buffer
+  long long b_off;   // offset of the fp32 bias [Cout]
+  long long f_off;   // offset (elements) of the forward pack in the bf16 pack buffer
+  long long d_off;   // offset of the dgrad pack
+  long long pb_off;  // offset of the packed bias in the fp32 packed-bias buffer
+  int Cout, Cin, ps, pad;
+};
+int pack_launch(const float* params, const PackEntry* dev_entries, int nentries, long long max_elems,
+                bf16_t* packs, float* pbias, hipStream_t st);
+
+int pack_one_launch(const float* w, const float* b, int Cout, int Cin, int ps, bf16_t* fpack, bf16_t* dpack,
+                    float* pbias, hipStream_t st);
+
+int scale_add_launch(float* y, const float* x, float a, size_t n, hipStream_t st);
+
+}  // namespace srmi

@@ -1,0 +1,150 @@
+"""Configuration: the reference's Hydra YAML keys, read with PyYAML.
+
+Mirrors sres/base/util/config.py (ConfigContext, cfg()) closely enough that
+the hot path reads the same keys from the same files:
+
+* model:  config/model/<name>.yaml  -> nfeatures, nlayers, nblocks, cbottleneck,
+          kernel_size, bias, downscale_factors, res_scale, batch_norm, loss_fn
+* task:   config/task/<name>.yaml   -> batch_size, lr, weight_decay, tile_size,
+          input_variables, target_variables, downsample_mode, upsample_mode
+* pipeline.gpu / FMOD_GPU           -> device index (sres/base/gpu.py:6-15)
+
+Parameter resolution follows init_parms (sres/model/common/common.py:9-28):
+common defaults <- model-specific defaults <- kwargs, each overridden by the
+model config when the key is present there.
+Hydra/OmegaConf are not required (not installed on this image); when the code
+runs inside a reference checkout, get_model() uses the reference's own cfg().
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Any, Dict, Iterable, List, Optional
+
+import yaml
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+CONFIG_DIR = os.path.join(os.path.dirname(_HERE), "config")
+
+COMMON_PARMS = dict(nchannels_in=1, nchannels_out=1, nfeatures=64, kernel_size=3, nlayers=16,
+                    downscale_factors=[2, 2], bias=True, batch_norm=False, res_scale=1.0, ups_mode="bicubic")
+MODEL_PARMS = {"rcan": dict(cbottleneck=2, nblocks=20), "edsr": {}}
+
+
+class Section(dict):
+    """dict with attribute access and .get, like an OmegaConf DictConfig."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+    @staticmethod
+    def wrap(d):
+        if isinstance(d, dict):
+            return Section({k: Section.wrap(v) for k, v in d.items()})
+        return d
+
+
+def search_paths() -> List[str]:
+    paths = [CONFIG_DIR]
+    extra = os.environ.get("SRMI_CONFIG_PATH")
+    if extra:
+        paths = extra.split(os.pathsep) + paths
+    return paths
+
+
+def load_group(group: str, name: str) -> Section:
+    for root in search_paths():
+        p = os.path.join(root, group, f"{name}.yaml")
+        if os.path.exists(p):
+            with open(p) as f:
+                return Section.wrap(yaml.safe_load(f) or {})
+    raise FileNotFoundError(f"config {group}/{name}.yaml not found in {search_paths()}")
+
+
+class _Cfg(Section):
+    pass
+
+
+_CURRENT: Optional[_Cfg] = None
+
+
+def cfg() -> _Cfg:
+    if _CURRENT is None:
+        raise RuntimeError("no active srmi ConfigContext")
+    return _CURRENT
+
+
+class ConfigContext:
+    """with ConfigContext('sres', dict(task='SST-tiles-48', model='rcan-10-20-64'), **{'task.lr': 1e-4}):"""
+
+    def __init__(self, cname: str, configuration: Dict[str, str], **overrides):
+        self.cname = cname
+        self.configuration = dict(configuration)
+        self.overrides = overrides
+        self._prev = None
+
+    def load(self) -> _Cfg:
+        c = _Cfg()
+        for group, name in self.configuration.items():
+            try:
+                c[group] = load_group(group, name)
+            except FileNotFoundError:
+                c[group] = Section()
+        c.setdefault("pipeline", Section(gpu=0))
+        c.setdefault("task", Section())
+        c.setdefault("model", Section())
+        for k, v in self.overrides.items():
+            sec, key = k.split(".", 1)
+            c.setdefault(sec, Section())[key] = v
+        if "FMOD_GPU" in os.environ:  # sres/base/util/config.py:79
+            c["pipeline"]["gpu"] = int(os.environ["FMOD_GPU"])
+        if "model" in self.configuration:
+            c["task"]["training_version"] = f"{self.cname}-{self.configuration['model']}"
+        return c
+
+    def __enter__(self):
+        global _CURRENT
+        self._prev = _CURRENT
+        _CURRENT = self.load()
+        return _CURRENT
+
+    def __exit__(self, *exc):
+        global _CURRENT
+        _CURRENT = self._prev
+        return False
+
+
+def model_section_from_env() -> Optional[Any]:
+    """The active model config: the reference's cfg().model when running inside a
+    reference checkout (plugin use), else srmi's own context, else None."""
+    try:
+        from sres.base.util.config import cfg as ref_cfg  # type: ignore
+        return ref_cfg().model
+    except Exception:
+        pass
+    if _CURRENT is not None:
+        return _CURRENT.get("model")
+    return None
+
+
+def init_parms(model: str, custom: Dict[str, Any], model_cfg: Optional[Any] = None) -> Dict[str, Any]:
+    """init_parms of sres/model/common/common.py:22-28."""
+    mc = model_cfg if model_cfg is not None else model_section_from_env()
+    get = (lambda k, d: mc.get(k, d)) if mc is not None else (lambda k, d: d)
+    parms = {k: get(k, v) for k, v in COMMON_PARMS.items()}
+    parms["scale"] = int(math.prod(list(parms["downscale_factors"])))
+    for pd in (MODEL_PARMS.get(model, {}), custom):
+        for k, v in pd.items():
+            parms[k] = get(k, v)
+    return parms
+
+
+def tile_sizes(task) -> tuple:
+    ts = task.get("tile_size", {"x": 48, "y": 48}) if task is not None else {"x": 48, "y": 48}
+    return int(ts["y"]), int(ts["x"])

@@ -1,0 +1,149 @@
+"""Data parallelism over one node: one process per GPU, torch.distributed with
+backend "nccl" (= RCCL over xGMI on ROCm), or "gloo" for the CPU tests.
+
+The reference has no distributed code on its live path; this is
+the MI355X-native addition, designed for exact single-process semantics:
+
+* tiles are sharded contiguously: rank r trains on tiles [r*B, (r+1)*B) of the
+  global batch (independent samples, no batch statistics anywhere in RCAN);
+* the RMSE (sres/controller/stats.py:5-8) is a global-batch quantity:
+  L = sqrt(S / N_global) with S = sum over ranks of the local sums of squares,
+  so ONE scalar all-reduce of S happens before backward and every rank uses
+  dL/dy = (y - t) / (N_global * L) -- averaging per-rank RMSEs would not be
+  the single-process gradient;
+* parameter gradients are then SUMMED over ranks (no 1/world factor: the
+  global count already normalises), bucket by bucket in the order backward
+  finalises them (one bucket per residual group, tail/upsampler first, head
+  last), each bucket launched on a communication stream as soon as its
+  group's HIP event fires, overlapping with the rest of backward.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+
+    @property
+    def enabled(self) -> bool:
+        return self.world > 1
+
+
+def init_from_env(backend: Optional[str] = None) -> DistInfo:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return DistInfo()
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if not dist.is_initialized():
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, rank=rank, world_size=world,
+                                    device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+    return DistInfo(rank, world, local)
+
+
+def shard_range(global_batch: int, info: DistInfo) -> Tuple[int, int]:
+    """Contiguous tile shard of this rank."""
+    if global_batch % info.world:
+        raise ValueError(f"global batch {global_batch} not divisible by world size {info.world}")
+    per = global_batch // info.world
+    return info.rank * per, (info.rank + 1) * per
+
+
+def allreduce_sum_(t: torch.Tensor, info: DistInfo):
+    if info.enabled:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+
+
+def global_rmse_scale(local_sq_sum: torch.Tensor, count_global: float, info: DistInfo):
+    """S -> (L, dL/dy scale); local_sq_sum is a 1-element tensor, reduced in place."""
+    allreduce_sum_(local_sq_sum, info)
+    L = torch.sqrt(local_sq_sum / count_global)
+    return L, 1.0 / (count_global * L)
+
+
+@dataclass
+class Bucket:
+    ranges: List[Tuple[int, int]]   # (offset, numel) in the flat grad buffer
+    event_index: Optional[int]      # backward group event that finalises it (None = end of backward)
+
+
+def grad_buckets(table, arch: str, nlayers: int) -> List[Bucket]:
+    """Partition the flat gradient into buckets in backward-completion order."""
+    def ranges_where(pred):
+        out = []
+        for name, off, n, _ in table:
+            if pred(name):
+                if out and out[-1][0] + out[-1][1] == off:
+                    out[-1] = (out[-1][0], out[-1][1] + n)
+                else:
+                    out.append((off, n))
+        return out
+
+    buckets: List[Bucket] = []
+    tailish = lambda nm: nm.startswith("tail.") or nm.startswith(f"body.{nlayers}.")
+    if arch == "rcan":
+        for k, g in enumerate(range(nlayers - 1, -1, -1)):
+            rg = ranges_where(lambda nm, g=g: nm.startswith(f"body.{g}."))
+            if k == 0:
+                rg = ranges_where(tailish) + rg
+            buckets.append(Bucket(rg, k))
+        buckets.append(Bucket(ranges_where(lambda nm: nm.startswith("head.")), None))
+    else:
+        buckets.append(Bucket(ranges_where(lambda nm: not nm.startswith("head.")), None))
+        buckets.append(Bucket(ranges_where(lambda nm: nm.startswith("head.")), None))
+    return buckets
+
+
+class GradReducer:
+    """Bucketed, event-driven SUM all-reduce of the flat gradient buffer."""
+
+    def __init__(self, table, arch: str, nlayers: int, info: DistInfo, device: torch.device):
+        self.info = info
+        self.buckets = grad_buckets(table, arch, nlayers)
+        self.n_events = max([b.event_index for b in self.buckets if b.event_index is not None], default=-1) + 1
+        self.cuda = device.type == "cuda"
+        self.events = [torch.cuda.Event() for _ in range(max(self.n_events, 0))] if self.cuda else []
+        self.stream = torch.cuda.Stream(device=device) if self.cuda else None
+
+    def covered(self) -> int:
+        return sum(n for b in self.buckets for _, n in b.ranges)
+
+    def reduce(self, grads: torch.Tensor):
+        """Call right after the (asynchronous) backward has been enqueued."""
+        if not self.info.enabled:
+            return
+        if not self.cuda:
+            for b in self.buckets:
+                for off, n in b.ranges:
+                    dist.all_reduce(grads[off:off + n], op=dist.ReduceOp.SUM)
+            return
+        main = torch.cuda.current_stream()
+        works = []
+        with torch.cuda.stream(self.stream):
+            for b in self.buckets:
+                if b.event_index is not None:
+                    self.stream.wait_event(self.events[b.event_index])
+                else:
+                    self.stream.wait_stream(main)
+                for off, n in b.ranges:
+                    works.append(dist.all_reduce(grads[off:off + n], op=dist.ReduceOp.SUM, async_op=True))
+        for w in works:
+            w.wait()
+        main.wait_stream(self.stream)

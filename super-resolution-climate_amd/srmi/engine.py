@@ -1,0 +1,177 @@
+"""Python handle on the native srmi engine (libsrmi.so).
+
+One Engine = one network plan (RCAN or EDSR hyper-parameters), one tile
+geometry, a batch capacity and a device workspace owned by PyTorch's caching
+allocator.  Parameters live in ONE flat fp32 buffer in the reference's
+state_dict order, gradients in another, Adam moments in two more: the whole
+optimizer step is a single fused kernel and the gradient all-reduce works on
+contiguous buckets.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import ModelConfig, ParamInfo, call, ptr, stream_handle
+
+ARCHS = {"rcan": _lib.SRMI_ARCH_RCAN, "edsr": _lib.SRMI_ARCH_EDSR}
+
+
+@dataclass
+class NetSpec:
+    """Hyper-parameters of the plugin (config/model/*.yaml keys)."""
+    arch: str = "rcan"
+    nchannels_in: int = 1
+    nchannels_out: int = 1
+    nfeatures: int = 64
+    nlayers: int = 10
+    nblocks: int = 20
+    cbottleneck: int = 2
+    scale: int = 4
+    res_scale: float = 1.0
+
+    @staticmethod
+    def from_parms(arch: str, parms: Dict) -> "NetSpec":
+        if parms.get("kernel_size", 3) != 3:
+            raise _lib.SrmiError("srmi supports kernel_size 3 only")
+        if parms.get("batch_norm", False):
+            raise _lib.SrmiError("srmi supports batch_norm: False only (the reference configs)")
+        if not parms.get("bias", True):
+            raise _lib.SrmiError("srmi supports bias: True only (the reference configs)")
+        return NetSpec(arch=arch, nchannels_in=int(parms["nchannels_in"]), nchannels_out=int(parms["nchannels_out"]),
+                       nfeatures=int(parms["nfeatures"]), nlayers=int(parms["nlayers"]),
+                       nblocks=int(parms.get("nblocks", 0) or 0), cbottleneck=int(parms.get("cbottleneck", 2) or 2),
+                       scale=int(parms["scale"]), res_scale=float(parms.get("res_scale", 1.0)))
+
+    def cstruct(self, batch: int, lr_h: int, lr_w: int) -> ModelConfig:
+        return ModelConfig(ARCHS[self.arch], self.nchannels_in, self.nchannels_out, self.nfeatures, self.nlayers,
+                           self.nblocks if self.arch == "rcan" else 0, self.cbottleneck if self.arch == "rcan" else 1,
+                           self.scale, self.res_scale, batch, lr_h, lr_w)
+
+
+def param_names(spec: NetSpec) -> List[str]:
+    """state_dict keys of the reference model, in order."""
+    names = ["head.0.weight", "head.0.bias"]
+    if spec.arch == "rcan":
+        for g in range(spec.nlayers):
+            for b in range(spec.nblocks):
+                pre = f"body.{g}.body.{b}.body"
+                names += [f"{pre}.0.weight", f"{pre}.0.bias", f"{pre}.2.weight", f"{pre}.2.bias",
+                          f"{pre}.3.conv_du.0.weight", f"{pre}.3.conv_du.0.bias",
+                          f"{pre}.3.conv_du.2.weight", f"{pre}.3.conv_du.2.bias"]
+            names += [f"body.{g}.body.{spec.nblocks}.weight", f"body.{g}.body.{spec.nblocks}.bias"]
+    else:
+        for i in range(spec.nlayers):
+            names += [f"body.{i}.body.0.weight", f"body.{i}.body.0.bias", f"body.{i}.body.2.weight",
+                      f"body.{i}.body.2.bias"]
+    names += [f"body.{spec.nlayers}.weight", f"body.{spec.nlayers}.bias"]
+    nups = int(round(math.log2(spec.scale)))
+    for k in range(nups):
+        names += [f"tail.0.{2 * k}.weight", f"tail.0.{2 * k}.bias"]
+    names += ["tail.1.weight", "tail.1.bias"]
+    return names
+
+
+def param_table(spec: NetSpec) -> List[Tuple[str, int, int, Tuple[int, ...]]]:
+    cfg = spec.cstruct(1, 48, 48)
+    n = C.c_longlong()
+    nt = C.c_int()
+    call("srmi_param_count", C.byref(cfg), C.byref(n), C.byref(nt))
+    arr = (ParamInfo * nt.value)()
+    call("srmi_param_table", C.byref(cfg), arr, nt.value)
+    names = param_names(spec)
+    if len(names) != nt.value:
+        raise _lib.SrmiError(f"param table mismatch {len(names)} != {nt.value}")
+    return [(names[i], arr[i].offset, arr[i].numel, tuple(arr[i].shape[:arr[i].ndim])) for i in range(nt.value)]
+
+
+class Engine:
+    def __init__(self, spec: NetSpec, batch: int, lr_hw: Tuple[int, int], train: bool = True,
+                 device: Optional[torch.device] = None):
+        self.spec = spec
+        self.batch = int(batch)
+        self.lr_h, self.lr_w = int(lr_hw[0]), int(lr_hw[1])
+        self.train_mode = bool(train)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self._cfg = spec.cstruct(self.batch, self.lr_h, self.lr_w)
+        nbytes = C.c_size_t()
+        call("srmi_workspace_size", C.byref(self._cfg), int(train), C.byref(nbytes))
+        self.workspace = torch.empty(int(nbytes.value) + 256, dtype=torch.uint8, device=self.device)
+        h = C.c_void_p()
+        call("srmi_engine_create", C.byref(self._cfg), ptr(self.workspace), self.workspace.numel(), int(train),
+             C.byref(h))
+        self._h = h
+        self.table = param_table(spec)
+        self.n_params = sum(t[2] for t in self.table)
+        self.hr_h, self.hr_w = self.lr_h * spec.scale, self.lr_w * spec.scale
+        self.loss4 = torch.zeros(4, dtype=torch.float32, device=self.device)
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None):
+                _lib.load().srmi_engine_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ ops
+    def pack(self, params: torch.Tensor, stream=None):
+        call("srmi_pack_weights", self._h, ptr(params), stream_handle(stream))
+
+    def forward(self, params: torch.Tensor, lr: torch.Tensor, out: Optional[torch.Tensor] = None, stream=None):
+        n = lr.shape[0]
+        assert lr.is_contiguous() and lr.dtype == torch.float32 and lr.device == self.device
+        assert tuple(lr.shape[1:]) == (self.spec.nchannels_in, self.lr_h, self.lr_w), lr.shape
+        if n > self.batch:
+            raise _lib.SrmiError(f"batch {n} exceeds engine capacity {self.batch}")
+        if out is None:
+            out = torch.empty((n, self.spec.nchannels_out, self.hr_h, self.hr_w), dtype=torch.float32,
+                              device=self.device)
+        call("srmi_forward", self._h, ptr(params), ptr(lr), ptr(out), n, stream_handle(stream))
+        return out
+
+    def rmse_partial(self, pred: torch.Tensor, target: torch.Tensor, loss4: torch.Tensor, count_global: float,
+                     stream=None):
+        call("srmi_rmse_partial", self._h, ptr(pred), ptr(target), pred.numel(), float(count_global), ptr(loss4),
+             stream_handle(stream))
+
+    @staticmethod
+    def rmse_finalize(loss4: torch.Tensor, stream=None):
+        call("srmi_rmse_finalize", ptr(loss4), stream_handle(stream))
+
+    def backward(self, params: torch.Tensor, lr: torch.Tensor, grads: torch.Tensor, sr=None, hr=None, loss4=None,
+                 dy=None, events: Optional[Sequence] = None, stream=None):
+        evp = None
+        if events is not None:
+            evp = (C.c_void_p * len(events))(*[e.cuda_event if e is not None else None for e in events])
+        call("srmi_backward", self._h, ptr(params), ptr(lr), ptr(sr), ptr(hr), ptr(loss4), ptr(dy), ptr(grads), evp,
+             stream_handle(stream))
+
+
+# ----------------------------------------------------------------- free ops
+def downsample(hr: torch.Tensor, scale: int, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    """bicubic 1/scale (sres/base/util/array.py:72-76), NCHW fp32."""
+    N, Cc, H, W = hr.shape
+    if out is None:
+        out = torch.empty((N, Cc, H // scale, W // scale), dtype=torch.float32, device=hr.device)
+    call("srmi_downsample", ptr(hr), N, Cc, H, W, scale, ptr(out), stream_handle(stream))
+    return out
+
+
+def upsample(lr: torch.Tensor, scale: int, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    """bicubic xscale interp baseline (sres/base/util/array.py:84-87), NCHW fp32."""
+    N, Cc, h, w = lr.shape
+    if out is None:
+        out = torch.empty((N, Cc, h * scale, w * scale), dtype=torch.float32, device=lr.device)
+    call("srmi_upsample", ptr(lr), N, Cc, h, w, scale, ptr(out), stream_handle(stream))
+    return out
+
+
+def adam_step(p, g, m, v, step: int, lr: float, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, stream=None):
+    call("srmi_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), int(step), float(lr), float(betas[0]),
+         float(betas[1]), float(eps), float(weight_decay), stream_handle(stream))

@@ -1,0 +1,217 @@
+"""Model-level parity of the HIP engine against the oracle and the golden vectors
+generated from the reference (tests/golden/make_golden.py).
+
+Tolerances: the engine computes conv operands in bf16 with
+fp32 accumulation and an fp32 residual stream, so element-wise outputs are
+compared by relative L2 (<= 2e-2), the loss within 2e-3 relative (the
+north-star "results within 1e-3 rel" is met for the loss at full size, see
+test_full_rcan_loss_parity), gradients by relative L2 per tensor family.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import rcan_oracle as ro  # noqa: E402
+from srmi.engine import Engine, NetSpec  # noqa: E402
+from srmi.trainer import FusedTrainer  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def dev():
+    assert torch.cuda.is_available()
+    return torch.device("cuda", 0)
+
+
+def rel_l2(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def flat_from_model(model, table):
+    sd = dict(model.named_parameters())
+    flat = torch.empty(sum(t[2] for t in table), dtype=torch.float32)
+    for name, off, n, shape in table:
+        flat[off:off + n] = sd[name].detach().float().reshape(-1)
+    return flat
+
+
+def spec_of(arch, C, nl, nb=0, scale=4, rs=1.0):
+    return NetSpec(arch=arch, nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=nl, nblocks=nb, cbottleneck=2,
+                   scale=scale, res_scale=rs)
+
+
+def oracle_grads(model, hr, scale):
+    model.zero_grad()
+    h = torch.tensor(hr, dtype=torch.float64, requires_grad=True)
+    out = model(ro.downsample(h, scale))
+    loss = ro.l2loss(out, h)
+    loss.backward()
+    return float(loss), out.detach(), {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+
+
+@pytest.mark.parametrize("arch,C,nl,nb,scale,S,B,gname", [
+    ("rcan", 1, 2, 2, 4, 192, 2, "rcan_small_c1_f64.npz"),
+    ("rcan", 2, 2, 2, 4, 192, 2, "rcan_small_c2_f64.npz"),
+    ("edsr", 4, 2, 0, 8, 256, 1, "edsr_small_c4_f64.npz"),
+])
+def test_small_model_step_vs_golden(arch, C, nl, nb, scale, S, B, gname):
+    d = dev()
+    gd = np.load(os.path.join(GOLDEN, gname))
+    kw = dict(nchannels_in=C, nchannels_out=C, nlayers=nl, nfeatures=64)
+    if arch == "rcan":
+        model = ro.RCANOracle(nblocks=nb, cbottleneck=2, **kw)
+    else:
+        model = ro.EDSROracle(downscale_factors=[2, 2, 2], **kw)
+    ro.init_params_numpy(model, int(gd["seed_w"]))
+    model = model.double()
+    hr = ro.synthetic_hr(B, C, S, int(gd["seed_x"]))
+    spec = spec_of(arch, C, nl, nb, scale)
+    tr = FusedTrainer(spec, B, (S // scale, S // scale), lr=float(gd["lr"]), interp_loss=True, device=d,
+                      params=flat_from_model(model, _table(spec)).to(d))
+    # oracle reference gradients (fp64, same weights)
+    l_ref, out_ref, g_ref = oracle_grads(model, hr, scale)
+    assert abs(l_ref - float(gd["loss0"])) < 1e-10  # oracle pinned to the reference
+    hr_d = torch.tensor(hr).to(d)
+    res = tr.step(hr_d)
+    torch.cuda.synchronize()
+    loss0 = float(res["loss"])
+    iloss0 = float(res["interp_loss"])
+    assert abs(loss0 - float(gd["loss0"])) / float(gd["loss0"]) < 2e-3, (loss0, float(gd["loss0"]))
+    assert abs(iloss0 - float(gd["iloss0"])) / float(gd["iloss0"]) < 1e-5
+    # SR output of that forward
+    assert rel_l2(tr.sr[:B].cpu()[:, :, ::4, ::4], gd["out_sub"]) < 2e-2
+    # gradients, per tensor
+    grads = tr.grads.cpu()
+    worst = 0.0
+    for name, off, n, shape in tr.eng.table:
+        r = rel_l2(grads[off:off + n].view(shape), g_ref[name])
+        worst = max(worst, r)
+        assert r < 8e-2, (name, r)
+    gl2 = np.array([float(grads[off:off + n].norm()) for _, off, n, _ in tr.eng.table])
+    np.testing.assert_allclose(gl2, gd["grad_l2"], rtol=8e-2)
+    # second step: loss after one Adam update
+    res = tr.step(hr_d)
+    torch.cuda.synchronize()
+    loss1 = float(res["loss"])
+    assert abs(loss1 - float(gd["loss1"])) / float(gd["loss1"]) < 2e-3, (loss1, float(gd["loss1"]))
+
+
+def _table(spec):
+    from srmi.engine import param_table
+    return param_table(spec)
+
+
+def test_full_rcan_forward_vs_golden():
+    """rcan-10-20-64, 2-var, one tile: output and loss vs the reference (fp64 golden)."""
+    d = dev()
+    gd = np.load(os.path.join(GOLDEN, "rcan_full_c2_f64.npz"))
+    model = ro.RCANOracle(nchannels_in=2, nchannels_out=2, nlayers=10, nblocks=20, nfeatures=64, cbottleneck=2)
+    ro.init_params_numpy(model, int(gd["seed_w"]))
+    spec = spec_of("rcan", 2, 10, 20)
+    table = _table(spec)
+    flat = flat_from_model(model, table).to(d)
+    eng = Engine(spec, 1, (48, 48), train=False, device=d)
+    eng.pack(flat)
+    hr = torch.tensor(ro.synthetic_hr(1, 2, 192, int(gd["seed_x"]))).to(d)
+    from srmi.engine import downsample
+    lr = downsample(hr, 4)
+    out = eng.forward(flat, lr)
+    torch.cuda.synchronize()
+    assert rel_l2(out.cpu()[:, :, ::4, ::4], gd["out_sub"]) < 2e-2
+    loss = float(((out - hr) ** 2).mean().sqrt())
+    assert abs(loss - float(gd["loss0"])) / float(gd["loss0"]) < 1e-3
+
+
+def test_full_rcan_loss_parity_and_grads():
+    """rcan-10-20-64 train step at one tile vs the fp64 golden: loss within 1e-3 rel,
+    gradient norms per tensor within 10 %."""
+    d = dev()
+    gd = np.load(os.path.join(GOLDEN, "rcan_full_c2_f64.npz"))
+    model = ro.RCANOracle(nchannels_in=2, nchannels_out=2, nlayers=10, nblocks=20, nfeatures=64, cbottleneck=2)
+    ro.init_params_numpy(model, int(gd["seed_w"]))
+    spec = spec_of("rcan", 2, 10, 20)
+    table = _table(spec)
+    tr = FusedTrainer(spec, 1, (48, 48), lr=float(gd["lr"]), device=d, params=flat_from_model(model, table).to(d))
+    hr = torch.tensor(ro.synthetic_hr(1, 2, 192, int(gd["seed_x"]))).to(d)
+    res = tr.step(hr)
+    torch.cuda.synchronize()
+    assert abs(float(res["loss"]) - float(gd["loss0"])) / float(gd["loss0"]) < 1e-3
+    grads = tr.grads.cpu()
+    gl2 = np.array([float(grads[off:off + n].norm()) for _, off, n, _ in table])
+    ratio = gl2 / gd["grad_l2"]
+    assert np.all(np.abs(ratio - 1) < 0.1), (ratio.min(), ratio.max())
+
+
+def test_batch_invariance_and_determinism():
+    """Full-size property checks at B=64 (BASELINE config 2): a tile's output does not
+    depend on its batch mates, and a train step is bitwise reproducible."""
+    d = dev()
+    spec = spec_of("rcan", 2, 10, 20)
+    table = _table(spec)
+    from srmi.trainer import default_init_
+    flat = torch.empty(sum(t[2] for t in table), device=d)
+    default_init_(flat, table, seed=3)
+    hr = torch.tensor(ro.synthetic_hr(64, 2, 192, 99)).to(d)
+    from srmi.engine import downsample
+    lr = downsample(hr, 4)
+    e64 = Engine(spec, 64, (48, 48), train=False, device=d)
+    e64.pack(flat)
+    o64 = e64.forward(flat, lr)
+    e2 = Engine(spec, 2, (48, 48), train=False, device=d)
+    e2.pack(flat)
+    o2 = e2.forward(flat, lr[5:7].contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(o64[5:7], o2)
+    del e64, e2
+    losses = []
+    for rep in range(2):
+        tr = FusedTrainer(spec, 64, (48, 48), device=d, params=flat)
+        out = [float(tr.step(hr)["loss"]) for _ in range(3)]
+        losses.append((out, tr.params.clone()))
+        del tr
+    assert losses[0][0] == losses[1][0]
+    assert torch.equal(losses[0][1], losses[1][1])
+    assert all(math.isfinite(x) for x in losses[0][0])
+    assert losses[0][0][2] < losses[0][0][0]   # the loss goes down on a fixed batch
+
+
+def test_plugin_module_reference_style_step():
+    """The drop-in nn.Module: torch.optim.Adam + the reference's l2loss step, against the oracle."""
+    d = dev()
+    from srmi.config import ConfigContext
+    from srmi.model.rcan.network import get_model
+    with ConfigContext("sres", dict(model="rcan-10-20-64", task="SSS_SST-tiles-48"), **{"model.nlayers": 2,
+                                                                                         "model.nblocks": 2}):
+        net = get_model(nchannels_in=2, nchannels_out=2, device=d).to(d)
+    meta = json.load(open(os.path.join(GOLDEN, "keys.json")))
+    oracle = ro.RCANOracle(nchannels_in=2, nchannels_out=2, nlayers=2, nblocks=2)
+    assert [k for k, _ in net.named_parameters()] == [k for k, _ in oracle.named_parameters()]
+    oracle.load_state_dict({k: v.detach().cpu() for k, v in net.state_dict().items()})
+    oracle = oracle.double()
+    net.train()
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    hr = torch.tensor(ro.synthetic_hr(2, 2, 192, 1234)).to(d)
+    from srmi.engine import downsample
+    opt.zero_grad()
+    x = downsample(hr, 4).requires_grad_(True)
+    out = net(x)
+    loss = torch.sqrt(((out - hr) ** 2).mean())
+    loss.backward()
+    l_ref, out_ref, g_ref = oracle_grads(oracle, hr.cpu().numpy(), 4)
+    assert abs(loss.item() - l_ref) / l_ref < 2e-3
+    for name, p in net.named_parameters():
+        assert p.grad is not None
+        assert rel_l2(p.grad, g_ref[name]) < 8e-2, name
+    opt.step()
+    # state_dict round trip through the tolerant loader
+    sd = {k: v.clone() for k, v in net.state_dict().items()}
+    net.load_state_dict(sd)
+    assert len(meta["keys"]["rcan_small_c2"]) == len(sd)
