@@ -55,88 +55,11 @@ __device__ __forceinline__ void load_halo_chunk(char* halo, const bf16_t* __rest
   }
 }
 
-template <int TW, int EPI>
-__global__ void __launch_bounds__(kThreads, 2) conv3x3_kernel(ConvParams p) {
-  using S = ConvSmem<TW>;
-  constexpr int NPT = TW / 16;  // 16-pixel tiles per row
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* halo = smem;
-  char* wbuf = smem + S::HALO_BYTES;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int strips_x = p.W / TW;
-  const int sy = blockIdx.x / strips_x, sx = blockIdx.x - sy * strips_x;
-  const int y0 = sy * kTH, x0 = sx * TW;
-  const int cb = blockIdx.y, n = blockIdx.z;
-  const int nchunks = p.Cin >> 6;
-  const bf16_t* __restrict__ wsrc = p.w;
-
-  f32x4 acc[NPT][4];
-#pragma unroll
-  for (int i = 0; i < NPT; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // lane-constant fragment coordinates
-  const int fr = lane & 15;   // A row (co within tile) / B column (pixel within tile)
-  const int fk = lane >> 4;   // 8-wide k group
-
-  for (int cc = 0; cc < nchunks; ++cc) {
-    if (cc) __syncthreads();
-    load_halo_chunk(halo, p.x, p.in_mode, n, p.H, p.W, p.Cin, cc, y0, x0, TW + 2, S::HALO_PIX);
-    // tap 0 filter slice
-    {
-      const bf16_t* ws = wsrc + ((size_t)(cc * 9 + 0) * p.Cout + cb * 64) * 64;
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        const int i = tid + r * kThreads;
-        const int row = i >> 3, c = i & 7;
-        *reinterpret_cast<uint4*>(wbuf + swz128(row, c)) =
-            *reinterpret_cast<const uint4*>(ws + row * 64 + c * 8);
-      }
-    }
-    __syncthreads();
-#pragma unroll 1
-    for (int tap = 0; tap < 9; ++tap) {
-      uint4 nxt[2];
-      if (tap < 8) {
-        const bf16_t* ws = wsrc + ((size_t)(cc * 9 + tap + 1) * p.Cout + cb * 64) * 64;
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-          const int i = tid + r * kThreads;
-          nxt[r] = *reinterpret_cast<const uint4*>(ws + (i >> 3) * 64 + (i & 7) * 8);
-        }
-      }
-      const char* wb = wbuf + (tap & 1) * S::W_BYTES;
-      const int ky = tap / 3, kx = tap - ky * 3;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int chunk = kk * 4 + fk;
-        bf16x8 a[4];
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) a[ct] = lds_frag(wb, swz128(ct * 16 + fr, chunk));
-#pragma unroll
-        for (int pt = 0; pt < NPT; ++pt) {
-          const int q = (wave + ky) * (TW + 2) + pt * 16 + fr + kx;
-          const bf16x8 b = lds_frag(halo, swz128(q, chunk));
-#pragma unroll
-          for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = mfma16(a[ct], b, acc[pt][ct]);
-        }
-      }
-      if (tap < 8) {
-        char* wn = wbuf + ((tap + 1) & 1) * S::W_BYTES;
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-          const int i = tid + r * kThreads;
-          *reinterpret_cast<uint4*>(wn + swz128(i >> 3, i & 7)) = nxt[r];
-        }
-      }
-      __syncthreads();
-    }
-  }
-
-  // ------------------------------------------------------------------ epilogue
-  const int y = y0 + wave;
+// Fused epilogue shared by both conv kernels.  acc[pt][ct]: lane owns channels
+// ct*16 + 4*(lane>>4) + {0..3} of pixel (y, x0 + pt*16 + (lane&15)).
+template <int NPT, int EPI>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[NPT][4], int n, int cb, int y, int x0,
+                                              int strip, int nstrips, float* red, int fr, int fk, int wave, int tid) {
   const int HW = p.H * p.W;
   constexpr bool kPart1 = (EPI == EPI_POOL_BF16);
   constexpr bool kPart2 = (EPI == EPI_DG_ACC);
@@ -226,8 +149,7 @@ __global__ void __launch_bounds__(kThreads, 2) conv3x3_kernel(ConvParams p) {
 
   if constexpr (kPart1 || kPart2) {
     // reduce over the 16 pixel-lanes, then over the 4 waves via LDS
-    __syncthreads();  // halo no longer needed
-    float* red = reinterpret_cast<float*>(smem);  // [4 waves][2][64]
+    __syncthreads();
     if (!kPart2 || p.part) {
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct)
@@ -244,24 +166,413 @@ __global__ void __launch_bounds__(kThreads, 2) conv3x3_kernel(ConvParams p) {
     }
     __syncthreads();
     if (!kPart2 || p.part) {
-      const int nstrips = gridDim.x;
       if (tid < 64) {
         const float s = red[0 * 128 + tid] + red[1 * 128 + tid] + red[2 * 128 + tid] + red[3 * 128 + tid];
-        p.part[((size_t)n * nstrips + blockIdx.x) * p.part_stride + cb * 64 + tid] = s;
+        p.part[((size_t)n * nstrips + strip) * p.part_stride + cb * 64 + tid] = s;
       } else if (kPart2 && tid < 128) {
         const int c = tid - 64;
         const float s = red[0 * 128 + 64 + c] + red[1 * 128 + 64 + c] + red[2 * 128 + 64 + c] + red[3 * 128 + 64 + c];
-        p.part[((size_t)n * nstrips + blockIdx.x) * p.part_stride + 64 + c] = s;
+        p.part[((size_t)n * nstrips + strip) * p.part_stride + 64 + c] = s;
       }
     }
   }
 }
 
 template <int TW, int EPI>
+__global__ void __launch_bounds__(kThreads, 2) conv3x3_kernel(ConvParams p) {
+  using S = ConvSmem<TW>;
+  constexpr int NPT = TW / 16;  // 16-pixel tiles per row
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* halo = smem;
+  char* wbuf = smem + S::HALO_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int strips_x = p.W / TW;
+  const int sy = blockIdx.x / strips_x, sx = blockIdx.x - sy * strips_x;
+  const int y0 = sy * kTH, x0 = sx * TW;
+  const int cb = blockIdx.y, n = blockIdx.z;
+  const int nchunks = p.Cin >> 6;
+  const bf16_t* __restrict__ wsrc = p.w;
+
+  f32x4 acc[NPT][4];
+#pragma unroll
+  for (int i = 0; i < NPT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // lane-constant fragment coordinates
+  const int fr = lane & 15;   // A row (co within tile) / B column (pixel within tile)
+  const int fk = lane >> 4;   // 8-wide k group
+
+  for (int cc = 0; cc < nchunks; ++cc) {
+    if (cc) __syncthreads();
+    load_halo_chunk(halo, p.x, p.in_mode, n, p.H, p.W, p.Cin, cc, y0, x0, TW + 2, S::HALO_PIX);
+    // tap 0 filter slice
+    {
+      const bf16_t* ws = wsrc + ((size_t)(cc * 9 + 0) * p.Cout + cb * 64) * 64;
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int i = tid + r * kThreads;
+        const int row = i >> 3, c = i & 7;
+        *reinterpret_cast<uint4*>(wbuf + swz128(row, c)) =
+            *reinterpret_cast<const uint4*>(ws + row * 64 + c * 8);
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      uint4 nxt[2];
+      if (tap < 8) {
+        const bf16_t* ws = wsrc + ((size_t)(cc * 9 + tap + 1) * p.Cout + cb * 64) * 64;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const int i = tid + r * kThreads;
+          nxt[r] = *reinterpret_cast<const uint4*>(ws + (i >> 3) * 64 + (i & 7) * 8);
+        }
+      }
+      const char* wb = wbuf + (tap & 1) * S::W_BYTES;
+      const int ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int chunk = kk * 4 + fk;
+        bf16x8 a[4];
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) a[ct] = lds_frag(wb, swz128(ct * 16 + fr, chunk));
+#pragma unroll
+        for (int pt = 0; pt < NPT; ++pt) {
+          const int q = (wave + ky) * (TW + 2) + pt * 16 + fr + kx;
+          const bf16x8 b = lds_frag(halo, swz128(q, chunk));
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = mfma16(a[ct], b, acc[pt][ct]);
+        }
+      }
+      if (tap < 8) {
+        char* wn = wbuf + ((tap + 1) & 1) * S::W_BYTES;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const int i = tid + r * kThreads;
+          *reinterpret_cast<uint4*>(wn + swz128(i >> 3, i & 7)) = nxt[r];
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // ------------------------------------------------------------------ epilogue
+  conv_epilogue<NPT, EPI>(p, acc, n, cb, y0 + wave, x0, blockIdx.x, gridDim.x, reinterpret_cast<float*>(smem), fr, fk,
+                          wave, tid);
+}
+
+// ============================================================================
+// v2 (Cin == 64): persistent runs.  A workgroup owns a vertical run of strips of
+// one image column and one 64-wide output-channel block.  All 9 filter slices
+// ([9][64 co][64 ci] bf16, 72 KiB) stay resident in LDS for the whole run; the
+// input rows live in a ring of 3 groups of 4 rows (group g = rows 4g-3..4g), so
+// strip k reads groups k and k+1 while group k+2 is prefetched into registers
+// (issued before the MFMAs, written to LDS after them: hipcc counts these loads
+// itself).  Halo rows are therefore fetched once per run (1.17x input traffic at
+// 12-row runs instead of 1.5x), with one barrier per strip instead of one per tap.
+template <int TW>
+struct Conv2Smem {
+  static constexpr int ROWB = (TW + 2) * 128;      // one halo row (TW+2 px x 64 ch bf16)
+  static constexpr int GROUPB = 4 * ROWB;
+  static constexpr int WB = 9 * 64 * 128;          // resident filters
+  static constexpr int RING = 3 * GROUPB;
+  static constexpr int RED = 4 * 128 * 4;          // cross-wave channel sums
+  static constexpr int TOTAL = WB + RING + RED;
+  static constexpr int GCH = GROUPB / 16;          // 16-B chunks per group
+  static constexpr int GPT = (GCH + kThreads - 1) / kThreads;
+};
+
+// Epilogue operands that live in global memory are prefetched into registers
+// before the MFMA phase (one wave per SIMD: nothing else would hide their latency).
+template <int NPT, int EPI>
+struct EpiPre {
+  float4 r1[NPT][4];
+  uint2 aux[NPT][4];
+};
+
+template <int NPT, int EPI>
+__device__ __forceinline__ void epi_prefetch(const ConvParams& p, EpiPre<NPT, EPI>& e, int n, int cb, int y, int x0,
+                                             int fr, int fk) {
+  if constexpr (EPI == EPI_RESID || EPI == EPI_DG_ACC || EPI == EPI_DG_RELUMASK) {
+    const size_t HW = (size_t)p.H * p.W;
+#pragma unroll
+    for (int pt = 0; pt < NPT; ++pt) {
+      const size_t pix = (size_t)n * HW + (size_t)y * p.W + x0 + pt * 16 + fr;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const size_t o = pix * p.Cout + cb * 64 + ct * 16 + fk * 4;
+        if constexpr (EPI == EPI_RESID) e.r1[pt][ct] = *reinterpret_cast<const float4*>(p.r1 + o);
+        if constexpr (EPI == EPI_DG_ACC) {
+          e.r1[pt][ct] = p.r1 ? *reinterpret_cast<const float4*>(p.r1 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+          e.aux[pt][ct] = p.part ? *reinterpret_cast<const uint2*>(p.aux + o) : make_uint2(0, 0);
+        }
+        if constexpr (EPI == EPI_DG_RELUMASK) e.aux[pt][ct] = *reinterpret_cast<const uint2*>(p.aux + o);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ float relu_mask(uint32_t bits16, float v) {
+  return (bits16 & 0x7FFFu) && !(bits16 & 0x8000u) ? v : 0.f;
+}
+
+// Fused epilogue of the v2 kernel (same semantics as conv_epilogue).
+template <int NPT, int EPI>
+__device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)[NPT][4], const EpiPre<NPT, EPI>& e,
+                                               const float4 (&bias)[4], int n, int cb, int y, int x0, int strip,
+                                               int nstrips, float* red, int fr, int fk, int wave, int tid) {
+  const size_t HW = (size_t)p.H * p.W;
+  constexpr bool kPart1 = (EPI == EPI_POOL_BF16);
+  constexpr bool kPart2 = (EPI == EPI_DG_ACC);
+  float ps0[4][4], ps1[4][4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ps0[ct][r] = ps1[ct][r] = 0.f;
+#pragma unroll
+  for (int pt = 0; pt < NPT; ++pt) {
+    const int xx = x0 + pt * 16 + fr;
+    const size_t pix = (size_t)n * HW + (size_t)y * p.W + xx;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int col = ct * 16 + fk * 4;
+      const int co = cb * 64 + col;
+      const size_t o = pix * p.Cout + co;
+      f32x4 v = acc[pt][ct];
+      if constexpr (EPI == EPI_RELU_BF16 || EPI == EPI_POOL_BF16 || EPI == EPI_RESID || EPI == EPI_PS_BF16 ||
+                    EPI == EPI_PLAIN_BF16) {
+        v[0] += bias[ct].x; v[1] += bias[ct].y; v[2] += bias[ct].z; v[3] += bias[ct].w;
+      }
+      if constexpr (EPI == EPI_RELU_BF16) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if constexpr (EPI == EPI_RESID) {
+        const float4 rr = e.r1[pt][ct];
+        v[0] = p.alpha * v[0] + rr.x; v[1] = p.alpha * v[1] + rr.y;
+        v[2] = p.alpha * v[2] + rr.z; v[3] = p.alpha * v[3] + rr.w;
+        if (p.yf) *reinterpret_cast<float4*>(p.yf + o) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+      if constexpr (EPI == EPI_DG_RELUMASK) {
+        const uint2 tt = e.aux[pt][ct];
+        v[0] = p.alpha * relu_mask(tt.x & 0xFFFFu, v[0]);
+        v[1] = p.alpha * relu_mask(tt.x >> 16, v[1]);
+        v[2] = p.alpha * relu_mask(tt.y & 0xFFFFu, v[2]);
+        v[3] = p.alpha * relu_mask(tt.y >> 16, v[3]);
+      }
+      if constexpr (EPI == EPI_DG_ACC) {
+        const float4 rr = e.r1[pt][ct];
+        v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
+        if (p.r2) {
+          const float4 q = *reinterpret_cast<const float4*>(p.r2 + o);
+          v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+        }
+        if (p.r3) {
+          const float4 q = *reinterpret_cast<const float4*>(p.r3 + o);
+          v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+        }
+        *reinterpret_cast<float4*>(p.yf + o) = make_float4(v[0], v[1], v[2], v[3]);
+        if (p.part) {
+          const uint2 uu = e.aux[pt][ct];
+          ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
+          ps1[ct][0] += v[0] * bf2f(uu.x & 0xFFFFu);
+          ps1[ct][1] += v[1] * bf2f(uu.x >> 16);
+          ps1[ct][2] += v[2] * bf2f(uu.y & 0xFFFFu);
+          ps1[ct][3] += v[3] * bf2f(uu.y >> 16);
+        }
+      }
+      if constexpr (kPart1) {
+        ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
+      }
+      const uint2 packed = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      if constexpr (EPI == EPI_PS_BF16) {
+        const int oy = 2 * y + (cb >> 1), ox = 2 * xx + (cb & 1);
+        const size_t oo = ((size_t)n * (2 * p.H) + oy) * (size_t)(2 * p.W) + ox;
+        *reinterpret_cast<uint2*>(p.yb + oo * 64 + col) = packed;
+      } else {
+        if (p.yb) *reinterpret_cast<uint2*>(p.yb + o) = packed;
+      }
+    }
+  }
+  if constexpr (kPart1 || kPart2) {
+    const bool on = !kPart2 || p.part;
+    if (on) {
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float s0 = sum16(ps0[ct][r]);
+          float s1 = 0.f;
+          if constexpr (kPart2) s1 = sum16(ps1[ct][r]);
+          if (fr == 0) {
+            red[(wave * 2 + 0) * 64 + ct * 16 + fk * 4 + r] = s0;
+            if constexpr (kPart2) red[(wave * 2 + 1) * 64 + ct * 16 + fk * 4 + r] = s1;
+          }
+        }
+    }
+    __syncthreads();
+    if (on) {
+      if (tid < 64) {
+        const float sum = red[tid] + red[128 + tid] + red[256 + tid] + red[384 + tid];
+        p.part[((size_t)n * nstrips + strip) * p.part_stride + cb * 64 + tid] = sum;
+      } else if (kPart2 && tid < 128) {
+        const int c = tid - 64;
+        const float sum = red[64 + c] + red[192 + c] + red[320 + c] + red[448 + c];
+        p.part[((size_t)n * nstrips + strip) * p.part_stride + 64 + c] = sum;
+      }
+    }
+  }
+}
+
+template <int TW, int EPI>
+__global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int run_len) {
+  using S = Conv2Smem<TW>;
+  constexpr int NPT = TW / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* wl = smem;
+  char* ring = smem + S::WB;
+  float* red = reinterpret_cast<float*>(smem + S::WB + S::RING);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int nsx = p.W / TW, nsy = p.H / kTH;
+  const int runs_per_col = (nsy + run_len - 1) / run_len;
+  int r = blockIdx.x;
+  const int ry = r % runs_per_col;
+  r /= runs_per_col;
+  const int sx = r % nsx;
+  r /= nsx;
+  const int n = r % p.N;
+  const int cb = r / p.N;
+  const int k0 = ry * run_len, k1 = min(nsy, k0 + run_len);
+  const int x0 = sx * TW;
+
+  auto group_load = [&](int gidx, uint4* stg) {
+#pragma unroll
+    for (int j = 0; j < S::GPT; ++j) {
+      const int i = tid + j * kThreads;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (i < S::GCH) {
+        const int q = i >> 3, c = i & 7;
+        const int rr = q / (TW + 2), hx = q - rr * (TW + 2);
+        const int y = 4 * gidx - 3 + rr, xx = x0 - 1 + hx;
+        if (y >= 0 && y < p.H && xx >= 0 && xx < p.W)
+          v = *reinterpret_cast<const uint4*>(p.x + ((size_t)((size_t)n * p.H + y) * p.W + xx) * 64 + c * 8);
+      }
+      stg[j] = v;
+    }
+  };
+  auto group_store = [&](int gidx, const uint4* stg) {
+    const int qbase = (gidx % 3) * 4 * (TW + 2);  // ring-global pixel index (the swizzle depends on it)
+#pragma unroll
+    for (int j = 0; j < S::GPT; ++j) {
+      const int i = tid + j * kThreads;
+      if (i < S::GCH) {
+        const int q = i >> 3, c = i & 7;
+        *reinterpret_cast<uint4*>(ring + swz128(qbase + q, c)) = stg[j];
+      }
+    }
+  };
+
+  // prologue: filters (all taps) + groups k0, k0+1 + bias
+  {
+    const bf16_t* ws = p.w;
+    for (int i = tid; i < 9 * 512; i += kThreads) {
+      const int tap = i >> 9, rem = i & 511, row = rem >> 3, c = rem & 7;
+      *reinterpret_cast<uint4*>(wl + tap * 8192 + swz128(row, c)) =
+          *reinterpret_cast<const uint4*>(ws + ((size_t)tap * p.Cout + cb * 64 + row) * 64 + c * 8);
+    }
+    uint4 stg[S::GPT];
+    group_load(k0, stg);
+    group_store(k0, stg);
+    group_load(k0 + 1, stg);
+    group_store(k0 + 1, stg);
+  }
+  float4 bias[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+    bias[ct] = p.bias ? *reinterpret_cast<const float4*>(p.bias + cb * 64 + ct * 16 + fk * 4)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+  // lane-constant A-fragment byte offsets (tap adds 8192)
+  uint32_t aoff[2][4];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) aoff[kk][ct] = swz128(ct * 16 + fr, kk * 4 + fk);
+  __syncthreads();
+
+#pragma unroll 1
+  for (int k = k0; k < k1; ++k) {
+    const int y = 4 * k + wave;
+    uint4 stg[S::GPT];
+    const bool pf = (k + 1 < k1);
+    if (pf) group_load(k + 2, stg);
+    EpiPre<NPT, EPI> ep;
+    epi_prefetch<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk);
+
+    // B-fragment byte offsets per (ky, kx, kk); +2048 per 16-pixel tile
+    uint32_t boff[3][3][2];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int rr = y + ky - 1 + 3;  // >= 2
+      const int slot = ((rr >> 2) % 3) * 4 + (rr & 3);
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) boff[ky][kx][kk] = swz128(slot * (TW + 2) + fr + kx, kk * 4 + fk);
+    }
+
+    f32x4 acc[NPT][4];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // 18 K-steps (9 taps x 2 halves of 32 ci), fragments double-buffered in
+    // registers: step s+1's ds_reads are in flight while step s's 12 MFMAs run.
+    bf16x8 A[2][4], B[2][NPT];
+    auto load_step = [&](int s, bf16x8 (&a)[4], bf16x8 (&b)[NPT]) {
+      const int tap = s >> 1, kk = s & 1, ky = tap / 3, kx = tap % 3;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) a[ct] = lds_frag(wl, tap * 8192 + aoff[kk][ct]);
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt) b[pt] = lds_frag(ring, boff[ky][kx][kk] + pt * 2048);
+    };
+    load_step(0, A[0], B[0]);
+#pragma unroll
+    for (int s = 0; s < 18; ++s) {
+      if (s + 1 < 18) load_step(s + 1, A[(s + 1) & 1], B[(s + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = mfma16(A[s & 1][ct], B[s & 1][pt], acc[pt][ct]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (pf) group_store(k + 2, stg);
+    conv_epilogue2<NPT, EPI>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx, nsy * nsx, red, fr, fk, wave, tid);
+    __syncthreads();
+  }
+}
+
+template <int TW, int EPI>
 static int launch_tw(const ConvParams& p, hipStream_t st) {
-  dim3 grid((p.H / kTH) * (p.W / TW), p.Cout / 64, p.N);
-  const int smem = ConvSmem<TW>::TOTAL;
-  hipLaunchKernelGGL((conv3x3_kernel<TW, EPI>), grid, dim3(kThreads), smem, st, p);
+  if (p.Cin == 64 && p.in_mode == IN_PLAIN) {
+    // v2: persistent runs; ~1 workgroup per CU (LDS-limited), each a run of strips
+    const int nsy = p.H / kTH;
+    const int units = (p.Cout / 64) * p.N * (p.W / TW);
+    int R = (256 + units / 2) / units;
+    R = R < 1 ? 1 : (R > nsy ? nsy : R);
+    const int run_len = (nsy + R - 1) / R;
+    const int runs = (nsy + run_len - 1) / run_len;
+    dim3 grid(units * runs);
+    hipLaunchKernelGGL((conv64_kernel<TW, EPI>), grid, dim3(kThreads), Conv2Smem<TW>::TOTAL, st, p, run_len);
+  } else {
+    dim3 grid((p.H / kTH) * (p.W / TW), p.Cout / 64, p.N);
+    hipLaunchKernelGGL((conv3x3_kernel<TW, EPI>), grid, dim3(kThreads), ConvSmem<TW>::TOTAL, st, p);
+  }
   SRMI_CHECK_LAUNCH();
   return 0;
 }

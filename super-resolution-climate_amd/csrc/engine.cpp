@@ -153,14 +153,13 @@ struct Carver {
 };
 
 int choose_row_splits(int N, int H, int Cout) {
-  // aim at >= 256 workgroups (one per CU) with >= 4 rows per workgroup
-  const int want = std::max(1, (256 + N * (Cout / 64) - 1) / (N * (Cout / 64)));
+  // wgrad grid = 3 (ky) x N*rs chunks x Cout/64; aim at >= 192 workgroups (one per CU,
+  // 1 WG/CU by LDS) while keeping as few partial slabs (N*rs) as possible
   int best = 1;
   for (int rs = 1; rs <= H / 2; ++rs) {
     if (H % rs || (H / rs) % 2) continue;
-    if (H / rs < 4 && rs > 1) break;
     best = rs;
-    if (rs >= want) break;
+    if (3 * N * rs * (Cout / 64) >= 192) break;
   }
   return best;
 }
@@ -189,6 +188,7 @@ struct srmi_engine {
   size_t slab_floats, bslab_floats;
   float* lpart;
   int lpart_n;
+  float* zeros;  // 256 zero bytes (DMA padding source)
   // packs
   bf16_t* packs;
   float* pbias;
@@ -243,6 +243,7 @@ static size_t carve(srmi_engine* e, char* base) {
   }
   e->lpart_n = 1024;
   e->lpart = cv.take<float>(e->lpart_n);
+  e->zeros = cv.take<float>(64);
   if (e->train) {
     e->GAf = cv.take<float>(m);
     e->GBf = cv.take<float>(m);
@@ -388,6 +389,7 @@ static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const b
   p.row_splits = choose_row_splits(n, H, c.cout);
   p.slab = e->slab;
   p.bslab = e->bslab;
+  p.zeros = e->zeros;
   const size_t ns = (size_t)wgrad3x3_nslabs(p);
   if (ns * c.cout * 576 > e->slab_floats || ns * c.cout > e->bslab_floats) return SRMI_ERR_WORKSPACE;
   int rc = wgrad3x3_launch(p, st);
@@ -413,6 +415,8 @@ static int upload_tables(srmi_engine* e, hipStream_t st) {
                          hipMemcpyHostToDevice, st);
     if (err != hipSuccess) return -(int)err;
   }
+  err = hipMemsetAsync(e->zeros, 0, 256, st);
+  if (err != hipSuccess) return -(int)err;
   // the host vectors must outlive the async copies: keep them in the engine
   e->tables_uploaded = true;
   return 0;
@@ -700,10 +704,14 @@ int srmi_wgrad3x3(const void* x, const void* dy, int N, int H, int W, int Cout, 
   p.imgs_per_wg = 1;
   p.row_splits = row_splits > 0 ? row_splits : choose_row_splits(N, H, Cout);
   const size_t ns = (size_t)wgrad3x3_nslabs(p);
-  const size_t need = ns * Cout * 577 * sizeof(float);
+  const size_t need = ns * Cout * 577 * sizeof(float) + 256;
   if (slab_bytes < need) return SRMI_ERR_WORKSPACE;
   p.slab = slab;
   p.bslab = slab + ns * Cout * 576;
+  float* zeros = slab + ns * Cout * 577;
+  hipError_t er = hipMemsetAsync(zeros, 0, 256, S_(stream));
+  if (er != hipSuccess) return -(int)er;
+  p.zeros = zeros;
   RC(wgrad3x3_launch(p, S_(stream)));
   return wgrad_reduce_launch(p.slab, p.bslab, (int)ns, Cout, ps, alpha, gw, gb, S_(stream));
 }

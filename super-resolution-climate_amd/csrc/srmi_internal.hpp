@@ -52,6 +52,7 @@ struct WgradParams {
   int row_splits;      // H split into this many row groups
   float* slab;         // [nslab][Cout][9][64]
   float* bslab;        // [nslab][Cout]
+  const void* zeros;   // >= 16 zero bytes in global memory (DMA source for padding)
 };
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st);
 int wgrad3x3_nslabs(const WgradParams& p);

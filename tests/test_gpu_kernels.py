@@ -54,7 +54,7 @@ def ps_perm(Cout):
     return torch.tensor([4 * (cp % 64) + cp // 64 for cp in range(Cout)])
 
 
-SHAPES = [(2, 48, 48), (1, 8, 96), (1, 4, 32), (2, 12, 64)]
+SHAPES = [(2, 48, 48), (1, 8, 96), (1, 4, 32), (2, 12, 64), (64, 48, 48), (16, 96, 96), (8, 32, 32)]
 
 
 def conv(x, fp, pb, N, H, W, Cin, Cout, epi, unshuf=0, yb=None, yf=None, r1=None, r2=None, r3=None, aux=None,
@@ -155,7 +155,8 @@ def test_conv_dgrad_unshuffle(N, H, W):
     assert rel_l2(out.float(), ref) < 4e-3
 
 
-@pytest.mark.parametrize("N,H,W,rs", [(2, 48, 48, 0), (2, 48, 48, 1), (1, 8, 96, 0), (1, 4, 32, 0), (3, 12, 64, 2)])
+@pytest.mark.parametrize("N,H,W,rs", [(2, 48, 48, 0), (2, 48, 48, 1), (1, 8, 96, 0), (1, 4, 32, 0), (3, 12, 64, 2),
+                                       (64, 48, 48, 0), (4, 96, 96, 0)])
 def test_wgrad(N, H, W, rs):
     d = dev()
     g = torch.Generator(device="cpu").manual_seed(5)

@@ -1,0 +1,109 @@
+"""Per-kernel microbenchmark at the BASELINE config-2 shapes (B=64, 48x48, 64 ch).
+
+    python tools/kbench.py [--batch 64] [--iters 30]
+
+Times each hot kernel alone with HIP events on its launch stream and prints
+avg us and achieved TFLOP/s (algorithmic) / GB/s.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "super-resolution-climate_amd"), ROOT]
+
+import torch  # noqa: E402
+
+from srmi._lib import call, ptr  # noqa: E402
+
+
+def timeit(fn, iters):
+    st = torch.cuda.current_stream()
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        fn()
+    e1.record(st)
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1000.0 / iters  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--iters", type=int, default=30)
+    args = ap.parse_args()
+    d = torch.device("cuda", 0)
+    N, H, W = args.batch, 48, 48
+    S = lambda: torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.randn(N, H, W, 64, generator=g).to(d).to(torch.bfloat16)
+    dy = torch.randn(N, H, W, 64, generator=g).to(d).to(torch.bfloat16)
+    t = torch.randn(N, H, W, 64, generator=g).clamp_min(0).to(d).to(torch.bfloat16)
+    r1 = torch.randn(N, H, W, 64, generator=g).to(d)
+    yf = torch.empty_like(r1)
+    yb = torch.empty_like(x)
+    w = (torch.randn(64, 64, 3, 3, generator=g) * 0.05).to(d)
+    b = torch.zeros(64, device=d)
+    fp = torch.empty(64 * 64 * 9, dtype=torch.bfloat16, device=d)
+    dp = torch.empty_like(fp)
+    pb = torch.empty(64, device=d)
+    call("srmi_pack_conv", ptr(w), ptr(b), 64, 64, 0, ptr(fp), ptr(dp), ptr(pb), S())
+    ns = call("srmi_conv3x3_nstrips", H, W)
+    part = torch.zeros(N, ns, 128, device=d)
+    flop = 2.0 * N * H * W * 64 * 576
+    res = {}
+
+    def conv(epi, xin, wp, **kw):
+        def f():
+            call("srmi_conv3x3", ptr(xin), ptr(wp), ptr(kw.get("bias")), N, H, W, 64, 64, 0, epi, ptr(kw.get("yb")),
+                 ptr(kw.get("yf")), ptr(kw.get("r1")), None, None, ptr(kw.get("aux")), ptr(kw.get("part")), 1.0, S())
+        return f
+
+    cases = {
+        "fwd_relu": conv(0, x, fp, bias=pb, yb=yb),
+        "fwd_pool": conv(1, x, fp, bias=pb, yb=yb, part=part),
+        "fwd_resid": conv(2, x, fp, bias=pb, yb=yb, yf=yf, r1=r1),
+        "dgrad_relumask": conv(4, dy, dp, yb=yb, aux=t),
+        "dgrad_acc": conv(5, dy, dp, yb=None, yf=yf, r1=yf, aux=t, part=part),
+    }
+    for k, f in cases.items():
+        us = timeit(f, args.iters)
+        res[k] = {"us": round(us, 2), "tflops": round(flop / us / 1e6, 1)}
+    slab = torch.empty(64 << 20, dtype=torch.float32, device=d)
+    gw = torch.empty(64, 64, 3, 3, device=d)
+    gb = torch.empty(64, device=d)
+
+    def wg():
+        call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, 0, ptr(slab), slab.numel() * 4, 0, 1.0, ptr(gw),
+             ptr(gb), S())
+    us = timeit(wg, args.iters)
+    res["wgrad+reduce"] = {"us": round(us, 2), "tflops": round(flop / us / 1e6, 1)}
+    # channel attention elementwise kernels
+    R = 2
+    w1 = torch.randn(32, 64, device=d) * 0.1
+    b1 = torch.zeros(32, device=d)
+    w2 = torch.randn(64, 32, device=d) * 0.1
+    b2 = torch.zeros(64, device=d)
+    rec = torch.zeros(N, 160, device=d)
+    brec = torch.zeros(N, 160, device=d)
+    pool = torch.zeros(N, ns, 64, device=d)
+
+    def caf():
+        call("srmi_ca_forward", ptr(yb), ptr(pool), ns, ptr(w1), ptr(b1), ptr(w2), ptr(b2), N, H * W, 64, R, ptr(r1),
+             ptr(yf), ptr(x), ptr(rec), S())
+
+    def cab():
+        call("srmi_ca_backward", ptr(r1), ptr(part), ns, ptr(rec), ptr(w1), ptr(w2), N, H * W, 64, R, ptr(yb),
+             ptr(brec), S())
+    for k, f, byt in (("ca_fwd", caf, N * H * W * 64 * 12), ("ca_bwd_du", cab, N * H * W * 64 * 6)):
+        us = timeit(f, args.iters)
+        res[k] = {"us": round(us, 2), "GBps": round(byt / us / 1e3, 1)}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
