@@ -114,6 +114,10 @@ int srmi_conv3x3(const void* x, const void* wpack, const float* bias, int N, int
                  int in_unshuffle, int epi, void* yb, float* yf, const float* r1, const float* r2, const float* r3,
                  const void* aux, float* part, float alpha, void* stream);
 int srmi_conv3x3_nstrips(int H, int W);
+/* diagnostic: record s_memtime phase stamps of the Cin=64 conv kernel into buf
+ * (64 x u64 per workgroup); NULL turns it off */
+int srmi_debug_conv_stamps(void* buf);
+int srmi_debug_wgrad_stamps(void* buf);
 /* fp32 torch filter [Cout][Cin][3][3] -> bf16 packs: fwd [Cin/64][9][Cout][64],
  * dgrad [Cout/64][9][Cin][64] (flipped), bias [Cout]; ps != 0 permutes the
  * PixelShuffle channel order (packed c'' = 64q + c <- torch 4c + q)         */

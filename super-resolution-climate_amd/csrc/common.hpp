@@ -70,6 +70,33 @@ __device__ __forceinline__ float sum16(float v) {
   return v;
 }
 
+// LDS-DMA of 16 bytes per lane: LDS[lds_base + 16*lane] <- *src (wave-uniform
+// lds_base).  Issued through inline asm so that hipcc does not treat the in-flight
+// DMA as aliasing every later ds_read (it would drain everything with vmcnt(0));
+// completion is ordered by the caller's own s_waitcnt vmcnt + barrier
+// (cdna_hip_programming.md §5.7: M0 saved/restored inside the statement).
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_base)
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 }  // namespace srmi
 
 #define SRMI_CHECK_LAUNCH()                                  \

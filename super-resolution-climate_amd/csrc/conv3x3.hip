@@ -17,10 +17,23 @@
 // fused epilogues (bias, ReLU, channel-attention pooling, residual add,
 // PixelShuffle scatter, ReLU-mask for dgrad, residual-stream gradient add with
 // the CA reductions).
+#include <stdlib.h>
+
 #include "common.hpp"
 #include "srmi_internal.hpp"
 
 namespace srmi {
+
+// zero bytes in global memory: the LDS-DMA source for padding pixels
+static __device__ uint4 kZeros[4];
+
+static unsigned long long* g_debug_stamps = nullptr;
+void conv3x3_set_debug_stamps(unsigned long long* buf) { g_debug_stamps = buf; }
+
+#define STAMP(i)                                                                     \
+  do {                                                                               \
+    if (p.stamps && tid == 0) p.stamps[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 
 constexpr int kTH = 4;
 constexpr int kThreads = 256;
@@ -426,7 +439,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
   }
 }
 
-template <int TW, int EPI>
+template <int TW, int EPI, int PM>
 __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int run_len) {
   using S = Conv2Smem<TW>;
   constexpr int NPT = TW / 16;
@@ -448,19 +461,30 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
   const int cb = r / p.N;
   const int k0 = ry * run_len, k1 = min(nsy, k0 + run_len);
   const int x0 = sx * TW;
+  STAMP(0);
 
+  // per-lane descriptors of this thread's 16-B chunks of a 4-row group (group
+  // independent): element offset within the group's first row, row, x validity
+  int goff[S::GPT], grow[S::GPT];
+  bool gok[S::GPT];
+#pragma unroll
+  for (int j = 0; j < S::GPT; ++j) {
+    const int i = tid + j * kThreads;
+    const int q = i >> 3, c = i & 7;
+    const int rr = q / (TW + 2), hx = q - rr * (TW + 2);
+    const int xx = x0 - 1 + hx;
+    grow[j] = rr;
+    gok[j] = (i < S::GCH) && xx >= 0 && xx < p.W;
+    goff[j] = (rr * p.W + xx) * 64 + c * 8;
+  }
+  const bf16_t* xn = p.x + (size_t)n * p.H * p.W * 64;
   auto group_load = [&](int gidx, uint4* stg) {
+    const bf16_t* grow0 = xn + (ptrdiff_t)(4 * gidx - 3) * p.W * 64;
 #pragma unroll
     for (int j = 0; j < S::GPT; ++j) {
-      const int i = tid + j * kThreads;
+      const int y = 4 * gidx - 3 + grow[j];
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (i < S::GCH) {
-        const int q = i >> 3, c = i & 7;
-        const int rr = q / (TW + 2), hx = q - rr * (TW + 2);
-        const int y = 4 * gidx - 3 + rr, xx = x0 - 1 + hx;
-        if (y >= 0 && y < p.H && xx >= 0 && xx < p.W)
-          v = *reinterpret_cast<const uint4*>(p.x + ((size_t)((size_t)n * p.H + y) * p.W + xx) * 64 + c * 8);
-      }
+      if (gok[j] && y >= 0 && y < p.H) v = *reinterpret_cast<const uint4*>(grow0 + goff[j]);
       stg[j] = v;
     }
   };
@@ -476,19 +500,65 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
     }
   };
 
-  // prologue: filters (all taps) + groups k0, k0+1 + bias
+  // prologue: filters (all 9 taps, 72 KiB) + input groups k0, k0+1, everything in
+  // flight before the first wait.  PM selects the path: 0 = all LDS-DMA
+  // (global_load_lds_dwordx4, swizzle on the source), 1 = all register staged,
+  // 2 = filters by DMA + input groups register staged.
   {
-    const bf16_t* ws = p.w;
-    for (int i = tid; i < 9 * 512; i += kThreads) {
-      const int tap = i >> 9, rem = i & 511, row = rem >> 3, c = rem & 7;
-      *reinterpret_cast<uint4*>(wl + tap * 8192 + swz128(row, c)) =
-          *reinterpret_cast<const uint4*>(ws + ((size_t)tap * p.Cout + cb * 64 + row) * 64 + c * 8);
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    if constexpr (PM == 0 || PM == 2) {
+      const uint32_t wbase = lds_u32(wl);
+      for (int i = wv; i < 72; i += 4) {
+        const int tap = i >> 3, row = 8 * (i & 7) + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+        glds16(p.w + ((size_t)(tap * p.Cout + cb * 64 + row)) * 64 + c * 8,
+               (uint32_t)__builtin_amdgcn_readfirstlane(wbase + i * 1024));
+      }
     }
-    uint4 stg[S::GPT];
-    group_load(k0, stg);
-    group_store(k0, stg);
-    group_load(k0 + 1, stg);
-    group_store(k0 + 1, stg);
+    if constexpr (PM == 0) {
+      constexpr int NG = S::GROUPB / 1024;
+      static_assert(S::GROUPB % 1024 == 0, "group region must be whole 1 KiB DMA pieces");
+      const uint32_t rbase = lds_u32(ring);
+#pragma unroll
+      for (int gi = 0; gi < 2; ++gi) {
+        const int gidx = k0 + gi;
+        const int qbase = (gidx % 3) * 4 * (TW + 2);
+        for (int i = wv; i < NG; i += 4) {
+          const int q = 8 * i + (lane >> 3);
+          const int Q = qbase + q;
+          const int c = (lane & 7) ^ ((Q >> 1) & 7);
+          const int rr = q / (TW + 2), hx = q - rr * (TW + 2);
+          const int y = 4 * gidx - 3 + rr, xx = x0 - 1 + hx;
+          const void* src = kZeros;
+          if (y >= 0 && y < p.H && xx >= 0 && xx < p.W)
+            src = p.x + ((size_t)((size_t)n * p.H + y) * p.W + xx) * 64 + c * 8;
+          glds16(src, (uint32_t)__builtin_amdgcn_readfirstlane(rbase + (uint32_t)qbase * 128 + i * 1024));
+        }
+      }
+    }
+    if constexpr (PM == 1) {
+      constexpr int WPT = 9 * 512 / kThreads;  // 18 x 16 B per thread
+      uint4 wst[WPT];
+#pragma unroll
+      for (int j = 0; j < WPT; ++j) {
+        const int i = tid + j * kThreads;
+        const int tap = i >> 9, rem = i & 511, row = rem >> 3, c = rem & 7;
+        wst[j] = *reinterpret_cast<const uint4*>(p.w + ((size_t)tap * p.Cout + cb * 64 + row) * 64 + c * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < WPT; ++j) {
+        const int i = tid + j * kThreads;
+        const int tap = i >> 9, rem = i & 511, row = rem >> 3, c = rem & 7;
+        *reinterpret_cast<uint4*>(wl + tap * 8192 + swz128(row, c)) = wst[j];
+      }
+    }
+    if constexpr (PM == 1 || PM == 2) {
+      uint4 g0[S::GPT], g1[S::GPT];
+      group_load(k0, g0);
+      group_load(k0 + 1, g1);
+      group_store(k0, g0);
+      group_store(k0 + 1, g1);
+    }
+    if constexpr (PM == 0 || PM == 2) wait_vm<0>();
   }
   float4 bias[4];
 #pragma unroll
@@ -511,6 +581,8 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
     if (pf) group_load(k + 2, stg);
     EpiPre<NPT, EPI> ep;
     epi_prefetch<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk);
+    const int sj = 2 + 5 * min(k - k0, 11);
+    STAMP(sj);
 
     // B-fragment byte offsets per (ky, kx, kk); +2048 per 16-pixel tile
     uint32_t boff[3][3][2];
@@ -551,9 +623,13 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
         for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = mfma16(A[s & 1][ct], B[s & 1][pt], acc[pt][ct]);
       __builtin_amdgcn_sched_barrier(0);
     }
+    STAMP(sj + 1);
     if (pf) group_store(k + 2, stg);
+    STAMP(sj + 2);
     conv_epilogue2<NPT, EPI>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx, nsy * nsx, red, fr, fk, wave, tid);
+    STAMP(sj + 3);
     __syncthreads();
+    STAMP(sj + 4);
   }
 }
 
@@ -568,7 +644,18 @@ static int launch_tw(const ConvParams& p, hipStream_t st) {
     const int run_len = (nsy + R - 1) / R;
     const int runs = (nsy + run_len - 1) / run_len;
     dim3 grid(units * runs);
-    hipLaunchKernelGGL((conv64_kernel<TW, EPI>), grid, dim3(kThreads), Conv2Smem<TW>::TOTAL, st, p, run_len);
+    ConvParams q = p;
+    q.stamps = g_debug_stamps;
+    static const int pm = [] {
+      const char* e = getenv("SRMI_CONV_PM");
+      return e ? atoi(e) : 2;
+    }();
+    if (pm == 1)
+      hipLaunchKernelGGL((conv64_kernel<TW, EPI, 1>), grid, dim3(kThreads), Conv2Smem<TW>::TOTAL, st, q, run_len);
+    else if (pm == 2)
+      hipLaunchKernelGGL((conv64_kernel<TW, EPI, 2>), grid, dim3(kThreads), Conv2Smem<TW>::TOTAL, st, q, run_len);
+    else
+      hipLaunchKernelGGL((conv64_kernel<TW, EPI, 0>), grid, dim3(kThreads), Conv2Smem<TW>::TOTAL, st, q, run_len);
   } else {
     dim3 grid((p.H / kTH) * (p.W / TW), p.Cout / 64, p.N);
     hipLaunchKernelGGL((conv3x3_kernel<TW, EPI>), grid, dim3(kThreads), ConvSmem<TW>::TOTAL, st, p);

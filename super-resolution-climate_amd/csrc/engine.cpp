@@ -153,13 +153,13 @@ struct Carver {
 };
 
 int choose_row_splits(int N, int H, int Cout) {
-  // wgrad grid = 3 (ky) x N*rs chunks x Cout/64; aim at >= 192 workgroups (one per CU,
-  // 1 WG/CU by LDS) while keeping as few partial slabs (N*rs) as possible
+  // wgrad grid = N*rs chunks x Cout/64 (one workgroup per CU by LDS); aim at >= 192
+  // workgroups while keeping as few partial slabs (N*rs) as possible; rows per chunk % 4 == 0
   int best = 1;
-  for (int rs = 1; rs <= H / 2; ++rs) {
-    if (H % rs || (H / rs) % 2) continue;
+  for (int rs = 1; rs <= H / 4; ++rs) {
+    if (H % rs || (H / rs) % 4) continue;
     best = rs;
-    if (3 * N * rs * (Cout / 64) >= 192) break;
+    if (N * rs * (Cout / 64) >= 192) break;
   }
   return best;
 }
@@ -346,6 +346,7 @@ static int conv_fwd(srmi_engine* e, const ConvRef& c, const bf16_t* x, int n, in
   p.part = part;
   p.part_stride = 64;
   p.alpha = alpha;
+  p.zeros = e->zeros;
   return conv3x3_launch(p, epi, st);
 }
 
@@ -372,6 +373,7 @@ static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n,
   p.part = part;
   p.part_stride = 128;
   p.alpha = alpha;
+  p.zeros = e->zeros;
   return conv3x3_launch(p, epi, st);
 }
 
@@ -685,6 +687,17 @@ int srmi_conv3x3(const void* x, const void* wpack, const float* bias, int N, int
 }
 
 int srmi_conv3x3_nstrips(int H, int W) { return conv3x3_nstrips(H, W); }
+
+// diagnostic only: s_memtime stamps of the conv kernel (64 per workgroup), NULL = off
+int srmi_debug_conv_stamps(void* buf) {
+  conv3x3_set_debug_stamps((unsigned long long*)buf);
+  return 0;
+}
+
+int srmi_debug_wgrad_stamps(void* buf) {
+  wgrad3x3_set_debug_stamps((unsigned long long*)buf);
+  return 0;
+}
 
 int srmi_pack_conv(const float* w, const float* b, int Cout, int Cin, int ps, void* fpack, void* dpack, float* pbias,
                    void* stream) {

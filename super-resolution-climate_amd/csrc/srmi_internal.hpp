@@ -37,8 +37,11 @@ struct ConvParams {
   float* part;         // per-strip channel sums
   int part_stride;
   float alpha;
+  const void* zeros;   // >= 16 zero bytes in global memory (DMA padding source)
+  unsigned long long* stamps;  // diagnostic s_memtime stamps (null in production)
 };
 
+void conv3x3_set_debug_stamps(unsigned long long* buf);
 int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st);
 int conv3x3_nstrips(int H, int W);
 
@@ -53,7 +56,9 @@ struct WgradParams {
   float* slab;         // [nslab][Cout][9][64]
   float* bslab;        // [nslab][Cout]
   const void* zeros;   // >= 16 zero bytes in global memory (DMA source for padding)
+  unsigned long long* stamps;  // diagnostic (null in production)
 };
+void wgrad3x3_set_debug_stamps(unsigned long long* buf);
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st);
 int wgrad3x3_nslabs(const WgradParams& p);
 // slab reduction into the torch-layout grad [Cout][64][3][3] (+ bias [Cout]);

@@ -6,215 +6,225 @@
 //     dW[co][ci][ky][kx] = sum_{n,p} dY[n][p][co] * X[n][p + (ky-1,kx-1)][ci]
 //     db[co]             = sum_{n,p} dY[n][p][co]
 //
-// GEMM view: M = 64 output channels (one co block), N = 3 taps (one kernel row
-// ky) x 64 input channels, K = pixels of one chunk (an image, or a band of rows).
-// Workgroup = 4 waves (one per SIMD), one (chunk, ky, co-block); wave w owns 3 of
-// the 12 16-wide N tiles (48 f32 accumulator VGPRs).  The three ky workgroups of
-// a chunk are launched 1 XCD apart in blockIdx (bid = ky*nchunks + chunk) so the
-// second and third reads of the chunk's dY / X come from the same L2.
-//
-// Data movement: per 2-row stage the dY tile (2 x TW px) and the 2 input rows
-// the stage needs for this ky (2 x TW+2 px, zero-padded) are DMA'd straight
-// into LDS with global_load_lds_dwordx4 (swizzle applied on the SOURCE address,
-// LDS image lane-linear), 4 stages in flight, counted s_waitcnt vmcnt + raw
-// s_barrier -- no VGPR staging.  Both MFMA operands are read K(pixel)-major
-// with ds_read_b64_tr_b16 (v_mfma_f32_16x16x32_bf16).
-// Each workgroup writes one partial slab; wgrad_reduce sums the slabs in a fixed
-// order (deterministic) into the torch-layout gradient.
+// GEMM view: M = 64 output channels (one co block), N = 9 taps x 64 input
+// channels, K = the pixels of one chunk (a band of rows of one image).
+// Workgroup = 4 waves (one per SIMD), one (chunk, co block); wave w owns 9 of the
+// 36 16-wide N tiles -> 144 f32 accumulators per lane.  Per 4-row stage the dY
+// tile (4 x TW px) and the 6 input rows it needs (6 x TW+2 px, zero padded) are
+// register-staged into LDS (issued before the MFMAs of the previous stage,
+// written after them), double buffered.  Both MFMA operands are read
+// K(pixel)-major with ds_read_b64_tr_b16; the LDS row pitches are multiples of 16
+// pixels so the swizzle (swz128t) is invariant across K-steps and every
+// transposed read is a precomputed per-lane offset + an immediate.
+// The bias gradient rides along as one extra MFMA per K-step against a ones
+// fragment.  Each workgroup writes one partial slab; wgrad_reduce sums the slabs
+// in a fixed order (deterministic) into the torch-layout gradient.
 #include "common.hpp"
 #include "srmi_internal.hpp"
 
 namespace srmi {
 
+static unsigned long long* g_wg_stamps = nullptr;
+void wgrad3x3_set_debug_stamps(unsigned long long* buf) { g_wg_stamps = buf; }
+#define WSTAMP(i)                                                                                     \
+  do {                                                                                                \
+    if (p.stamps && tid == 0) p.stamps[(blockIdx.y * gridDim.x + blockIdx.x) * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+
 template <int TW>
-struct Wg2 {
-  static constexpr int DY_PIX = 2 * TW;
-  static constexpr int X_PIX = 2 * (TW + 2);
-  static constexpr int DY_BYTES = DY_PIX * 128;
-  static constexpr int X_BYTES = X_PIX * 128;
-  static constexpr int RAW = DY_BYTES + X_BYTES;
-  static constexpr int NI = ((RAW + 4095) / 4096) * 4;     // 1 KiB DMA instructions per stage (multiple of 4)
-  static constexpr int NIW = NI / 4;                        // per wave
-  static constexpr int STAGE = NI * 1024;
-  static constexpr int NSTG = 4;
-  static constexpr int TOTAL = NSTG * STAGE + 4 * 64 * 4;   // + bias-sum scratch
+struct Wg3 {
+  static constexpr int SR = 4;                      // output rows per stage
+  static constexpr int XP = (TW == 48) ? 64 : 48;   // X row pitch (px), multiple of 16, >= TW + 2
+  static constexpr int DY_BYTES = SR * TW * 128;
+  static constexpr int X_BYTES = (SR + 2) * XP * 128;
+  static constexpr int STAGE = DY_BYTES + X_BYTES;
+  static constexpr int DY_CH = SR * TW * 8;         // 16-B chunks to load
+  static constexpr int X_CH = (SR + 2) * (TW + 2) * 8;
+  static constexpr int PT = (DY_CH + X_CH + 255) / 256;
+  static constexpr int KSTEPS = SR * TW / 32;
+  static constexpr int TOTAL = 2 * STAGE;
 };
-
-// LDS-DMA of 16 bytes per lane: LDS[lds_base + 16*lane] <- *src.  Issued through
-// inline asm so that hipcc does not treat the in-flight DMA as aliasing every later
-// ds_read (it would drain the whole ring with vmcnt(0)); completion is ordered by
-// our own counted s_waitcnt vmcnt + s_barrier (cdna_hip_programming.md §5.7).
-__device__ __forceinline__ void glds16(const void* src, uint32_t lds_base) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(lds_base)
-      : "memory");
-}
-
-__device__ __forceinline__ uint32_t lds_u32(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 template <int TW>
 __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
-  using S = Wg2<TW>;
+  using S = Wg3<TW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nchunks = gridDim.x / 3;
-  const int ky = blockIdx.x / nchunks, chunk = blockIdx.x - ky * nchunks;
-  const int cb = blockIdx.y;
+  const int chunk = blockIdx.x, cb = blockIdx.y;
   const int Hr = p.H / p.row_splits;
   const int n = chunk / p.row_splits, ybase = (chunk % p.row_splits) * Hr;
-  const int nxb = p.W / TW;
-  const int nst = (Hr / 2) * nxb;
+  const int nrp = Hr / S::SR, nxb = p.W / TW;
+  const int nst = nrp * nxb;
+  WSTAMP(0);
 
-  // ---------------------------------------------------------------- DMA issue
-  // stage st -> rows (ybase + 2*(st / nxb)) .. +1, columns x0 .. x0+TW-1
-  auto issue = [&](int st) {
-    const int y0 = ybase + 2 * (st / nxb), x0 = (st % nxb) * TW;
-    const uint32_t base = lds_u32(smem) + (st % S::NSTG) * S::STAGE;
-    const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const bf16_t* dyn = p.dy_mode == IN_PLAIN ? p.dy + (size_t)n * p.H * p.W * p.Cout + cb * 64
+                                             : p.dy + (size_t)n * 4 * p.H * p.W * 64;
+  const bf16_t* xn = p.x + (size_t)n * p.H * p.W * 64;
+
+  // stage st: column block xb = st / nrp, rows y0 .. y0+3 (column-major order)
+  auto load_one = [&](int st, int j) -> uint4 {
+    const int xb = st / nrp, rp = st - xb * nrp;
+    const int y0 = ybase + S::SR * rp, x0 = xb * TW;
+    const int i = tid + 256 * j;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (i < S::DY_CH) {
+      const int q = i >> 3, c = i & 7;
+      const int r = q / TW, xx = x0 + q - r * TW, y = y0 + r;
+      const bf16_t* src;
+      if (p.dy_mode == IN_PLAIN)
+        src = dyn + ((size_t)y * p.W + xx) * p.Cout + c * 8;
+      else
+        src = dyn + ((size_t)(2 * y + (cb >> 1)) * (2 * p.W) + 2 * xx + (cb & 1)) * 64 + c * 8;
+      v = *reinterpret_cast<const uint4*>(src);
+    } else if (i < S::DY_CH + S::X_CH) {
+      const int ii = i - S::DY_CH;
+      const int q = ii >> 3, c = ii & 7;
+      const int r = q / (TW + 2), hx = q - r * (TW + 2);
+      const int y = y0 - 1 + r, xx = x0 - 1 + hx;
+      if (y >= 0 && y < p.H && xx >= 0 && xx < p.W)
+        v = *reinterpret_cast<const uint4*>(xn + ((size_t)y * p.W + xx) * 64 + c * 8);
+    }
+    return v;
+  };
+  auto load_stage = [&](int st, uint4* stg) {
 #pragma unroll
-    for (int j = 0; j < S::NIW; ++j) {
-      const int i = wv + 4 * j;                   // instruction index within the stage (wave-uniform)
-      const int b = i * 1024 + lane * 16;          // destination byte (lane-linear)
-      const void* src = p.zeros;
-      if (b < S::DY_BYTES) {
-        const int q = b >> 7, c = ((b >> 4) & 7) ^ ((((q >> 1) & 1) << 1) | (((q >> 3) & 1) << 2));
-        const int r = q / TW, xx = x0 + q - r * TW, y = y0 + r;
-        if (p.dy_mode == IN_PLAIN)
-          src = p.dy + ((size_t)((size_t)n * p.H + y) * p.W + xx) * p.Cout + cb * 64 + c * 8;
-        else
-          src = p.dy + ((size_t)((size_t)n * 2 * p.H + 2 * y + (cb >> 1)) * (2 * p.W) + 2 * xx + (cb & 1)) * 64 + c * 8;
-      } else if (b < S::DY_BYTES + S::X_BYTES) {
-        const int bb = b - S::DY_BYTES;
-        const int q = bb >> 7, c = ((bb >> 4) & 7) ^ ((((q >> 1) & 1) << 1) | (((q >> 3) & 1) << 2));
+    for (int j = 0; j < S::PT; ++j) stg[j] = load_one(st, j);
+  };
+  auto store_stage = [&](int buf, const uint4* stg) {
+    char* base = smem + buf * S::STAGE;
+#pragma unroll
+    for (int j = 0; j < S::PT; ++j) {
+      const int i = tid + 256 * j;
+      if (i < S::DY_CH) {
+        const int q = i >> 3, c = i & 7;
+        *reinterpret_cast<uint4*>(base + swz128t(q, c)) = stg[j];
+      } else if (i < S::DY_CH + S::X_CH) {
+        const int ii = i - S::DY_CH;
+        const int q = ii >> 3, c = ii & 7;
         const int r = q / (TW + 2), hx = q - r * (TW + 2);
-        const int y = y0 + r + ky - 1, xx = x0 - 1 + hx;
-        if (y >= 0 && y < p.H && xx >= 0 && xx < p.W)
-          src = p.x + ((size_t)((size_t)n * p.H + y) * p.W + xx) * 64 + c * 8;
+        *reinterpret_cast<uint4*>(base + S::DY_BYTES + swz128t(r * S::XP + hx, c)) = stg[j];
       }
-      glds16(src, (uint32_t)__builtin_amdgcn_readfirstlane(base + i * 1024));
     }
   };
 
-  f32x4 acc[4][3];
+  f32x4 acc[4][9];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;
+    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 bacc = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
 
-  // lane coordinates for the transposed reads
+  // transposed-read lane coordinates.  K-step kb covers output rows 2*(kb / nkc)
+  // .. +1 and columns 16*(kb % nkc) .. +15 of the stage; lane group g takes row
+  // g>>1, columns 8*(g&1) + 4*s + q.
   const int g = lane >> 4, li = lane & 15, lq = li >> 2, lp = li & 3;
-  const int prow = g >> 1;
-  const int pcol = 8 * (g & 1) + lq;
+  const int prow = g >> 1, pcol = 8 * (g & 1) + lq;
   const uint32_t half = (lp & 1) * 8;
-  // this wave's 3 N tiles: j = 3*wave + t -> (kx, ci tile)
-  int nkx[3], nit[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const int j = 3 * wave + t;
-    nkx[t] = j >> 2;
-    nit[t] = j & 3;
-  }
-
-  // prologue: NSTG-1 stages in flight
-#pragma unroll
-  for (int s = 0; s < S::NSTG - 1; ++s)
-    if (s < nst) issue(s);
-
-#pragma unroll 1
-  for (int st = 0; st < nst; ++st) {
-    const int ahead = min(nst - 1, st + S::NSTG - 2) - st;   // stages issued after st
-    if (ahead >= 2)
-      wait_vm<2 * S::NIW>();
-    else if (ahead == 1)
-      wait_vm<S::NIW>();
-    else
-      wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");  // keep LDS reads and the next DMA below the barrier
-    if (st + S::NSTG - 1 < nst) issue(st + S::NSTG - 1);
-    const char* dyl = smem + (st % S::NSTG) * S::STAGE;
-    const char* xl = dyl + S::DY_BYTES;
-    // K-steps of 32 pixels; fragments double-buffered in registers so that step
-    // kb+1's transposed reads are in flight while step kb's 12 MFMAs run
-    bf16x8 A[2][4], B[2][3];
-    auto load_step = [&](int kb, bf16x8 (&a)[4], bf16x8 (&b)[3]) {
-      const int px0 = prow * TW + kb * 16 + pcol;
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        const int chunk = 2 * ct + (lp >> 1);
-        a[ct] = cat_tr(lds_tr(dyl, swz128t(px0, chunk) + half), lds_tr(dyl, swz128t(px0 + 4, chunk) + half));
-      }
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const int chunk = 2 * nit[t] + (lp >> 1);
-        const int hq0 = prow * (TW + 2) + kb * 16 + pcol + nkx[t];
-        b[t] = cat_tr(lds_tr(xl, swz128t(hq0, chunk) + half), lds_tr(xl, swz128t(hq0 + 4, chunk) + half));
-      }
-    };
-    load_step(0, A[0], B[0]);
-#pragma unroll
-    for (int kb = 0; kb < TW / 16; ++kb) {
-      if (kb + 1 < TW / 16) load_step(kb + 1, A[(kb + 1) & 1], B[(kb + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-        for (int t = 0; t < 3; ++t) acc[ct][t] = mfma16(A[kb & 1][ct], B[kb & 1][t], acc[ct][t]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (ky == 0) {  // bias gradient: lane = channel, pixels strided over the 4 waves
-      for (int px = wave; px < S::DY_PIX; px += 4) {
-        const bf16_t v = *reinterpret_cast<const bf16_t*>(dyl + swz128t(px, lane >> 3) + (lane & 7) * 2);
-        bsum += bf2f(v);
-      }
-    }
-  }
-
-  // epilogue: partial slab [chunk][Cout][9][64]
-  float* slab = p.slab + (size_t)chunk * p.Cout * 576;
+  uint32_t aoff[4][2], boff[9][2];
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-    for (int t = 0; t < 3; ++t)
+    for (int h = 0; h < 2; ++h) aoff[ct][h] = swz128t(prow * TW + pcol + 4 * h, 2 * ct + (lp >> 1)) + half;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = cb * 64 + ct * 16 + 4 * (lane >> 4) + r;
-        const int ci = nit[t] * 16 + (lane & 15);
-        slab[((size_t)co * 9 + ky * 3 + nkx[t]) * 64 + ci] = acc[ct][t][r];
-      }
-  if (ky == 0) {
-    float* red = reinterpret_cast<float*>(smem + S::NSTG * S::STAGE);
-    red[wave * 64 + lane] = bsum;
-    __syncthreads();
-    if (tid < 64) p.bslab[(size_t)chunk * p.Cout + cb * 64 + tid] = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
+  for (int t = 0; t < 9; ++t) {
+    const int j = 9 * wave + t, tap = j >> 2, it = j & 3, ky = tap / 3, kx = tap % 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      boff[t][h] = S::DY_BYTES + swz128t((prow + ky) * S::XP + pcol + kx + 4 * h, 2 * it + (lp >> 1)) + half;
   }
+  constexpr int NKC = TW / 16;
+
+  {
+    uint4 stg[S::PT];
+    load_stage(0, stg);
+    store_stage(0, stg);
+  }
+  __syncthreads();
+  WSTAMP(1);
+
+  // the next stage's PT loads are spread over the K-steps (LPS per step) so that a
+  // full memory queue stalls the wave between MFMA groups rather than ahead of them
+  constexpr int LPS = (S::PT + S::KSTEPS - 1) / S::KSTEPS;
+#pragma unroll 1
+  for (int st = 0; st < nst; ++st) {
+    uint4 stg[S::PT];
+    const bool pf = st + 1 < nst;
+    const int sj = 2 + 3 * min(st, 19);
+    WSTAMP(sj);
+    const char* sb = smem + (st & 1) * S::STAGE;
+    bf16x8 A[2][4], B[2][9];
+    auto load_step = [&](int kb, bf16x8 (&a)[4], bf16x8 (&b)[9]) {
+      const uint32_t da = (uint32_t)((2 * (kb / NKC) * TW + 16 * (kb % NKC)) * 128);
+      const uint32_t db = (uint32_t)((2 * (kb / NKC) * S::XP + 16 * (kb % NKC)) * 128);
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) a[ct] = cat_tr(lds_tr(sb, aoff[ct][0] + da), lds_tr(sb, aoff[ct][1] + da));
+#pragma unroll
+      for (int t = 0; t < 9; ++t) b[t] = cat_tr(lds_tr(sb, boff[t][0] + db), lds_tr(sb, boff[t][1] + db));
+    };
+    load_step(0, A[0], B[0]);
+#pragma unroll
+    for (int kb = 0; kb < S::KSTEPS; ++kb) {
+      if (pf) {
+#pragma unroll
+        for (int jj = 0; jj < LPS; ++jj)
+          if (kb * LPS + jj < S::PT) stg[kb * LPS + jj] = load_one(st + 1, kb * LPS + jj);
+      }
+      if (kb + 1 < S::KSTEPS) load_step(kb + 1, A[(kb + 1) & 1], B[(kb + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(A[kb & 1][ct], B[kb & 1][t], acc[ct][t]);
+      bf16x8 aw = A[kb & 1][0];
+      if (wave == 1) aw = A[kb & 1][1];
+      if (wave == 2) aw = A[kb & 1][2];
+      if (wave == 3) aw = A[kb & 1][3];
+      bacc = mfma16(aw, ones, bacc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    WSTAMP(sj + 1);
+    if (pf) store_stage((st + 1) & 1, stg);
+    __syncthreads();
+    WSTAMP(sj + 2);
+  }
+
+  // epilogue: partial slab [chunk][9][64 ci][Cout] -- a lane's 4 accumulators are 4
+  // consecutive output channels, so every store is 16 B
+  float* slab = p.slab + (size_t)chunk * p.Cout * 576;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int j = 9 * wave + t, tap = j >> 2, it = j & 3;
+    const int ci = it * 16 + (lane & 15);
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int co = cb * 64 + ct * 16 + 4 * (lane >> 4);
+      *reinterpret_cast<float4*>(slab + ((size_t)tap * 64 + ci) * p.Cout + co) =
+          make_float4(acc[ct][t][0], acc[ct][t][1], acc[ct][t][2], acc[ct][t][3]);
+    }
+  }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      p.bslab[(size_t)chunk * p.Cout + cb * 64 + wave * 16 + 4 * (lane >> 4) + r] = bacc[r];
+  }
+  WSTAMP(63);
 }
 
 int wgrad3x3_nslabs(const WgradParams& p) { return p.N * p.row_splits; }
 
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
-  if (p.Cout % 64 || p.H % p.row_splits || (p.H / p.row_splits) % 2 || !p.zeros) return SRMI_ERR_SHAPE;
+  if (p.Cout % 64 || p.H % p.row_splits || (p.H / p.row_splits) % 4) return SRMI_ERR_SHAPE;
   if (p.dy_mode == IN_UNSHUF && p.Cout != 256) return SRMI_ERR_SHAPE;
-  dim3 grid(3 * wgrad3x3_nslabs(p), p.Cout / 64);
+  dim3 grid(wgrad3x3_nslabs(p), p.Cout / 64);
+  WgradParams q = p;
+  q.stamps = g_wg_stamps;
   if (p.W % 48 == 0) {
-    hipLaunchKernelGGL(wgrad3x3_kernel<48>, grid, dim3(256), Wg2<48>::TOTAL, st, p);
+    hipLaunchKernelGGL(wgrad3x3_kernel<48>, grid, dim3(256), Wg3<48>::TOTAL, st, q);
   } else if (p.W % 32 == 0) {
-    hipLaunchKernelGGL(wgrad3x3_kernel<32>, grid, dim3(256), Wg2<32>::TOTAL, st, p);
+    hipLaunchKernelGGL(wgrad3x3_kernel<32>, grid, dim3(256), Wg3<32>::TOTAL, st, q);
   } else {
     return SRMI_ERR_SHAPE;
   }
@@ -250,7 +260,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   if (q == 0 && (is_w || is_b)) {
     const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
     if (is_w) {
-      const int ci = o & 63, tap = (o >> 6) % 9, cop = o / 576;
+      const int cop = o % Cout, ci = (o / Cout) & 63, tap = o / (Cout * 64);
       const int cot = ps ? (4 * (cop & 63) + (cop >> 6)) : cop;
       gw[((size_t)cot * 64 + ci) * 9 + tap] = alpha * s;
     } else {

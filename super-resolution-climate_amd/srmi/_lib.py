@@ -52,6 +52,8 @@ _SIGS = {
     "srmi_conv3x3": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P,
                       C.c_float, P], C.c_int),
     "srmi_conv3x3_nstrips": ([C.c_int, C.c_int], C.c_int),
+    "srmi_debug_conv_stamps": ([P], C.c_int),
+    "srmi_debug_wgrad_stamps": ([P], C.c_int),
     "srmi_pack_conv": ([P, P, C.c_int, C.c_int, C.c_int, P, P, P, P], C.c_int),
     "srmi_wgrad3x3": ([P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_size_t, C.c_int, C.c_float,
                        P, P, P], C.c_int),

@@ -107,3 +107,81 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def stamps():
+    """Phase timing of the conv kernel (relu epilogue) from s_memtime stamps."""
+    import numpy as np
+    d = torch.device("cuda", 0)
+    N, H, W = 64, 48, 48
+    S = torch.cuda.current_stream().cuda_stream
+    x = torch.randn(N, H, W, 64, device=d).to(torch.bfloat16)
+    w = torch.randn(64, 64, 3, 3, device=d) * 0.05
+    b = torch.zeros(64, device=d)
+    fp = torch.empty(64 * 64 * 9, dtype=torch.bfloat16, device=d)
+    dp = torch.empty_like(fp)
+    pb = torch.empty(64, device=d)
+    call("srmi_pack_conv", ptr(w), ptr(b), 64, 64, 0, ptr(fp), ptr(dp), ptr(pb), S)
+    yb = torch.empty_like(x)
+    buf = torch.zeros(4096 * 64, dtype=torch.int64, device=d)
+    for _ in range(3):
+        call("srmi_conv3x3", ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, 0, ptr(yb), None, None, None, None, None, None,
+             1.0, S)
+    call("srmi_debug_conv_stamps", ptr(buf))
+    call("srmi_conv3x3", ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, 0, ptr(yb), None, None, None, None, None, None,
+         1.0, S)
+    call("srmi_debug_conv_stamps", None)
+    torch.cuda.synchronize()
+    st = buf.view(4096, 64).cpu().numpy()
+    print("raw wg0", st[0, :20].tolist())
+    print("nonzero per column", (st != 0).sum(0)[:20].tolist())
+    st = st[st[:, 0] != 0]
+    base = st[:, 0:1]
+    rel = st - base
+    print("workgroups", len(st), "start spread (cycles)", int(st[:, 0].max() - st[:, 0].min()))
+    names = ["prologue"] + [f"s{j}:{k}" for j in range(3) for k in ("issue", "mfma", "gstore", "epi", "barrier")]
+    prev = np.zeros(len(st))
+    for i, nm in enumerate(names, start=1):
+        if i >= 64 or not np.all(st[:, i]):
+            break
+        cur = rel[:, i]
+        print(f"{nm:12s} median dt {np.median(cur - prev):8.0f}  max {np.max(cur - prev):8.0f}")
+        prev = cur
+
+
+def wstamps():
+    """Phase timing of the wgrad kernel from s_memtime stamps."""
+    import numpy as np
+    d = torch.device("cuda", 0)
+    N, H, W = 64, 48, 48
+    S = torch.cuda.current_stream().cuda_stream
+    x = torch.randn(N, H, W, 64, device=d).to(torch.bfloat16)
+    dy = torch.randn(N, H, W, 64, device=d).to(torch.bfloat16)
+    slab = torch.empty(64 << 20, dtype=torch.float32, device=d)
+    gw = torch.empty(64, 64, 3, 3, device=d)
+    gb = torch.empty(64, device=d)
+    buf = torch.zeros(4096 * 64, dtype=torch.int64, device=d)
+
+    def run():
+        call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, 0, ptr(slab), slab.numel() * 4, 0, 1.0, ptr(gw),
+             ptr(gb), S)
+    for _ in range(3):
+        run()
+    call("srmi_debug_wgrad_stamps", ptr(buf))
+    run()
+    call("srmi_debug_wgrad_stamps", None)
+    torch.cuda.synchronize()
+    st = buf.view(4096, 64).cpu().numpy()
+    st = st[st[:, 0] != 0]
+    rel = st - st[:, 0:1]
+    print("wgrad workgroups", len(st))
+    cols = [i for i in range(1, 64) if np.all(st[:, i] != 0)]
+    prev = np.zeros(len(st))
+    for i in cols:
+        print(f"stamp {i:2d} median dt {np.median(rel[:, i] - prev):8.0f}  max {np.max(rel[:, i] - prev):8.0f}")
+        prev = rel[:, i]
+
+
+if __name__ == "__main__" and os.environ.get("KBENCH_STAMPS"):
+    stamps()
+    wstamps()
