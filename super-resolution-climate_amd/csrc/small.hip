@@ -63,6 +63,47 @@ int head_fwd_launch(const float* lr, const float* w, const float* b, int N, int 
   return 0;
 }
 
+// Deterministic slab reduction shared by the head / tail weight gradients:
+// block = 16 outputs x 16 slab slices (slice q sums slabs q, q+16, ...), then the
+// 16 slice sums are added in a fixed order.  MODE 0: head layout [co][9C+1];
+// MODE 1: tail layout [c][577].
+template <int MODE>
+__global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, int nslab, int per, int C,
+                                                          float* __restrict__ gw, float* __restrict__ gb) {
+  __shared__ float red[16][17];
+  const int oi = threadIdx.x & 15, q = threadIdx.x >> 4;
+  const int o = blockIdx.x * 16 + oi;
+  float s0 = 0.f, s1 = 0.f;
+  if (o < per) {
+    int k = q;
+    for (; k + 16 < nslab; k += 32) {
+      s0 += slab[(size_t)k * per + o];
+      s1 += slab[(size_t)(k + 16) * per + o];
+    }
+    if (k < nslab) s0 += slab[(size_t)k * per + o];
+  }
+  red[q][oi] = s0 + s1;
+  __syncthreads();
+  if (q == 0 && o < per) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += red[i][oi];
+    if (MODE == 0) {
+      const int nj = 9 * C + 1, co = o / nj, j = o % nj;
+      if (j < nj - 1)
+        gw[co * 9 * C + j] = s;
+      else
+        gb[co] = s;
+    } else {
+      const int c = o / 577, j = o % 577;
+      if (j < 576)
+        gw[c * 576 + j] = s;  // [c][ci][tap] == torch [C][64][3][3]
+      else
+        gb[c] = s;
+    }
+  }
+}
+
 // dW[co][c][tap] = sum_p g[p][co] * lr[c][p+off];  db[co] = sum_p g[p][co]
 // one workgroup per (image, 4-row strip); slab [co][9C + 1]
 __global__ void __launch_bounds__(256) head_wgrad_kernel(const float* __restrict__ lr, const float* __restrict__ g,
@@ -114,23 +155,9 @@ int head_wgrad_launch(const float* lr, const float* g, int N, int C, int H, int 
   return 0;
 }
 
-__global__ void head_wgrad_reduce_kernel(const float* __restrict__ slab, int nslab, int C, float* __restrict__ gw,
-                                         float* __restrict__ gb) {
-  const int nj = 9 * C + 1, per = 64 * nj;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= per) return;
-  float s = 0.f;
-  for (int k = 0; k < nslab; ++k) s += slab[(size_t)k * per + idx];
-  const int co = idx / nj, j = idx % nj;
-  if (j < nj - 1)
-    gw[co * 9 * C + j] = s;
-  else
-    gb[co] = s;
-}
-
 int head_wgrad_reduce_launch(const float* slab, int nslab, int C, float* gw, float* gb, hipStream_t st) {
   const int per = 64 * (9 * C + 1);
-  hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((per + 255) / 256), dim3(256), 0, st, slab, nslab, C, gw, gb);
+  hipLaunchKernelGGL(slab_reduce_kernel<0>, dim3((per + 15) / 16), dim3(256), 0, st, slab, nslab, per, C, gw, gb);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
@@ -260,107 +287,103 @@ int tail_dgrad_launch(const float* y, const float* hr, const float* loss, const 
 }
 
 // dW[c][ci][tap] = sum_p dy[c][p] * x[p+off][ci];  db[c] = sum_p dy[c][p]
-// workgroup = (image, 16-row band); slab [C][577]
-constexpr int kTailRows = 16;
-template <int TWT>
+// dy = (y - hr) * loss[2] is formed on the fly (RMSE gradient, stats.py:5-8).
+// Lane = input channel ci; each wave walks whole rows keeping the 3x3 window of
+// x[.][ci] in registers (3 new coalesced 128-B loads per pixel).  dy for 64
+// consecutive pixels is loaded once per row segment with lane = pixel and
+// broadcast with readlane.  Workgroup = (band of kTailRows rows, image); the 4
+// waves' partials are summed in LDS -> slab [n][band][C][577].
+constexpr int kTailRows = 4;
+template <int CC>
 __global__ void __launch_bounds__(256) tail_wgrad_kernel(const float* __restrict__ yv, const float* __restrict__ hr,
                                                         const float* __restrict__ loss, const bf16_t* __restrict__ x,
-                                                        int C, int H, int W, float* __restrict__ slab) {
-  extern __shared__ __attribute__((aligned(16))) char tws[];
-  constexpr int WP = TWT + 2, HP = 6 * WP;
-  char* halo = tws;
-  float* dyl = reinterpret_cast<float*>(tws + HP * 128);  // [C][4][TWT]
-  const int n = blockIdx.y, band = blockIdx.x, tid = threadIdx.x;
-  const int ci = tid & 63, grp = tid >> 6;
+                                                        int H, int W, float* __restrict__ slab) {
+  __shared__ float red[4][CC * 577];
+  const int n = blockIdx.y, band = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float sc = loss ? loss[2] : 1.f;
-  float acc[3][4];
+  float acc[9][CC], bacc[CC];
 #pragma unroll
-  for (int a = 0; a < 3; ++a)
+  for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) acc[a][c] = 0.f;
-  float bacc = 0.f;
-  const int ntx = W / TWT;
-  for (int tile = 0; tile < (kTailRows / 4) * ntx; ++tile) {
-    const int y0 = band * kTailRows + (tile / ntx) * 4, x0 = (tile % ntx) * TWT;
-    __syncthreads();
-    for (int i = tid; i < HP * 8; i += 256) {
-      const int q = i >> 3, c = i & 7;
-      const int hy = q / WP, hx = q - hy * WP;
-      const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (yy >= 0 && yy < H && xx >= 0 && xx < W)
-        v = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + c * 8);
-      *reinterpret_cast<uint4*>(halo + swz128(q, c)) = v;
+    for (int c = 0; c < CC; ++c) acc[t][c] = 0.f;
+#pragma unroll
+  for (int c = 0; c < CC; ++c) bacc[c] = 0.f;
+  const bf16_t* xn = x + (size_t)n * H * W * 64 + lane;
+  auto xat = [&](int yy, int xx) -> float {
+    return (yy >= 0 && yy < H && xx >= 0 && xx < W) ? bf2f(xn[((size_t)yy * W + xx) * 64]) : 0.f;
+  };
+  for (int y = band * kTailRows + wave; y < (band + 1) * kTailRows; y += 4) {
+    float win[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      win[r][0] = 0.f;
+      win[r][1] = xat(y - 1 + r, 0);
     }
-    for (int i = tid; i < C * 4 * TWT; i += 256) {
-      const int c = i / (4 * TWT), r = (i / TWT) % 4, xx = i % TWT;
-      const size_t o = (((size_t)n * C + c) * H + y0 + r) * W + x0 + xx;
-      dyl[i] = hr ? (yv[o] - hr[o]) * sc : yv[o] * sc;
-    }
-    __syncthreads();
-    for (int px = 0; px < 4 * TWT; ++px) {
-      const int r = px / TWT, xx = px - r * TWT;
-      float d[4];
+    for (int x0 = 0; x0 < W; x0 += 64) {
+      float dv[CC];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) d[c] = (c < C) ? dyl[(c * 4 + r) * TWT + xx] : 0.f;
+      for (int c = 0; c < CC; ++c) {
+        const int xx = x0 + lane;
+        float v = 0.f;
+        if (xx < W) {
+          const size_t o = (((size_t)n * CC + c) * H + y) * W + xx;
+          v = hr ? (yv[o] - hr[o]) * sc : yv[o] * sc;
+        }
+        dv[c] = v;
+        bacc[c] += v;
+      }
+      const int nx = min(64, W - x0);
+#pragma unroll 4
+      for (int j = 0; j < nx; ++j) {
+        const int xx = x0 + j;
 #pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const int t = grp + 4 * a;
-        if (t < 9) {
-          const int q = (r + t / 3) * WP + xx + t % 3;
-          const float xv = bf2f(*reinterpret_cast<const bf16_t*>(halo + swz128(q, ci >> 3) + (ci & 7) * 2));
+        for (int r = 0; r < 3; ++r) win[r][2] = xat(y - 1 + r, xx + 1);
 #pragma unroll
-          for (int c = 0; c < 4; ++c) acc[a][c] += d[c] * xv;
+        for (int c = 0; c < CC; ++c) {
+          const float dd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv[c]), j));
+#pragma unroll
+          for (int t = 0; t < 9; ++t) acc[t][c] += dd * win[t / 3][t % 3];
+        }
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          win[r][0] = win[r][1];
+          win[r][1] = win[r][2];
         }
       }
-      if (tid < C) bacc += dyl[(tid * 4 + r) * TWT + xx];
     }
   }
-  float* out = slab + ((size_t)n * gridDim.x + band) * C * 577;
+  // bias: sum the per-lane pixel sums of each wave
 #pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const int t = grp + 4 * a;
-    if (t < 9)
-      for (int c = 0; c < C; ++c) out[c * 577 + ci * 9 + t] = acc[a][c];
+  for (int c = 0; c < CC; ++c) bacc[c] = wave_sum(bacc[c]);
+#pragma unroll
+  for (int c = 0; c < CC; ++c) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) red[wave][c * 577 + lane * 9 + t] = acc[t][c];
+    if (lane == 0) red[wave][c * 577 + 576] = bacc[c];
   }
-  if (tid < C) out[tid * 577 + 576] = bacc;
+  __syncthreads();
+  float* out = slab + ((size_t)n * gridDim.x + band) * CC * 577;
+  for (int i = tid; i < CC * 577; i += 256) out[i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
 }
 
 int tail_wgrad_launch(const float* y, const float* hr, const float* loss, const bf16_t* x, int N, int C, int H,
                       int W, float* slab, int* nslab, hipStream_t st) {
   if (C < 1 || C > 4 || H % kTailRows) return SRMI_ERR_SHAPE;
   const dim3 grid(H / kTailRows, N);
-  if (W % 64 == 0) {
-    const int smem = 6 * 66 * 128 + 4 * 4 * 64 * 4;
-    hipLaunchKernelGGL(tail_wgrad_kernel<64>, grid, dim3(256), smem, st, y, hr, loss, x, C, H, W, slab);
-  } else if (W % 32 == 0) {
-    const int smem = 6 * 34 * 128 + 4 * 4 * 32 * 4;
-    hipLaunchKernelGGL(tail_wgrad_kernel<32>, grid, dim3(256), smem, st, y, hr, loss, x, C, H, W, slab);
-  } else {
-    return SRMI_ERR_SHAPE;
+  switch (C) {
+    case 1: hipLaunchKernelGGL(tail_wgrad_kernel<1>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+    case 2: hipLaunchKernelGGL(tail_wgrad_kernel<2>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+    case 3: hipLaunchKernelGGL(tail_wgrad_kernel<3>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+    default: hipLaunchKernelGGL(tail_wgrad_kernel<4>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
   }
   SRMI_CHECK_LAUNCH();
   *nslab = N * (H / kTailRows);
   return 0;
 }
 
-__global__ void tail_wgrad_reduce_kernel(const float* __restrict__ slab, int nslab, int C, float* __restrict__ gw,
-                                         float* __restrict__ gb) {
-  const int per = C * 577;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= per) return;
-  float s = 0.f;
-  for (int k = 0; k < nslab; ++k) s += slab[(size_t)k * per + idx];
-  const int c = idx / 577, j = idx % 577;
-  if (j < 576)
-    gw[c * 576 + j] = s;  // [c][ci][tap] == torch [C][64][3][3]
-  else
-    gb[c] = s;
-}
-
 int tail_wgrad_reduce_launch(const float* slab, int nslab, int C, float* gw, float* gb, hipStream_t st) {
   const int per = C * 577;
-  hipLaunchKernelGGL(tail_wgrad_reduce_kernel, dim3((per + 255) / 256), dim3(256), 0, st, slab, nslab, C, gw, gb);
+  hipLaunchKernelGGL(slab_reduce_kernel<1>, dim3((per + 15) / 16), dim3(256), 0, st, slab, nslab, per, C, gw, gb);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
@@ -677,44 +700,56 @@ __global__ void __launch_bounds__(256) ca_param_grads_kernel(const float* __rest
                                                              const float* __restrict__ brecs, int N, int C, int CR,
                                                              const long long* __restrict__ offs,
                                                              float* __restrict__ grads) {
+  // blockIdx.y < 2*C*CR/256: one weight gradient per thread; the last y slice
+  // does the biases.  Image sums run in a fixed order (deterministic).
   const int k = blockIdx.x;
   const int rs = 2 * C + CR;
   const float* rec = recs + (size_t)k * N * rs;
   const float* brec = brecs + (size_t)k * N * rs;
-  float* gw1 = grads + offs[k * 5 + 0];
-  float* gb1 = grads + offs[k * 5 + 1];
-  float* gw2 = grads + offs[k * 5 + 2];
-  float* gb2 = grads + offs[k * 5 + 3];
-  float* gbc = grads + offs[k * 5 + 4];
-  for (int o = threadIdx.x; o < 2 * C * CR; o += 256) {
+  const int nw = 2 * C * CR;
+  const int o = blockIdx.y * 256 + threadIdx.x;
+  if ((int)blockIdx.y * 256 < nw) {
+    if (o >= nw) return;
+    float s0 = 0.f, s1 = 0.f;
     if (o < C * CR) {  // dW2[c][j] = sum_n dz2[n][c] * relu(z1[n][j])
       const int c = o / CR, j = o % CR;
-      float s = 0.f;
-      for (int n = 0; n < N; ++n) s += brec[n * rs + c] * fmaxf(rec[n * rs + C + j], 0.f);
-      gw2[o] = s;
+      int n = 0;
+      for (; n + 1 < N; n += 2) {
+        s0 += brec[n * rs + c] * fmaxf(rec[n * rs + C + j], 0.f);
+        s1 += brec[(n + 1) * rs + c] * fmaxf(rec[(n + 1) * rs + C + j], 0.f);
+      }
+      if (n < N) s0 += brec[n * rs + c] * fmaxf(rec[n * rs + C + j], 0.f);
+      grads[offs[k * 5 + 2] + o] = s0 + s1;
     } else {  // dW1[j][c] = sum_n dz1[n][j] * m[n][c]
       const int oo = o - C * CR;
       const int j = oo / C, c = oo % C;
-      float s = 0.f;
-      for (int n = 0; n < N; ++n) s += brec[n * rs + C + j] * rec[n * rs + c];
-      gw1[oo] = s;
+      int n = 0;
+      for (; n + 1 < N; n += 2) {
+        s0 += brec[n * rs + C + j] * rec[n * rs + c];
+        s1 += brec[(n + 1) * rs + C + j] * rec[(n + 1) * rs + c];
+      }
+      if (n < N) s0 += brec[n * rs + C + j] * rec[n * rs + c];
+      grads[offs[k * 5 + 0] + oo] = s0 + s1;
     }
+    return;
   }
-  for (int o = threadIdx.x; o < 2 * C + CR; o += 256) {
+  for (int q = threadIdx.x; q < rs; q += 256) {
     float s = 0.f;
-    for (int n = 0; n < N; ++n) s += brec[n * rs + o];
-    if (o < C)
-      gb2[o] = s;
-    else if (o < C + CR)
-      gb1[o - C] = s;
+    for (int n = 0; n < N; ++n) s += brec[n * rs + q];
+    if (q < C)
+      grads[offs[k * 5 + 3] + q] = s;
+    else if (q < C + CR)
+      grads[offs[k * 5 + 1] + q - C] = s;
     else
-      gbc[o - C - CR] = s;
+      grads[offs[k * 5 + 4] + q - C - CR] = s;
   }
 }
 
 int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int C, int R,
                                   const long long* offs, float* grads, hipStream_t st) {
-  hipLaunchKernelGGL(ca_param_grads_kernel, dim3(nblocks), dim3(256), 0, st, recs, brecs, N, C, C / R, offs, grads);
+  const int CR = C / R;
+  const int ny = (2 * C * CR + 255) / 256 + 1;
+  hipLaunchKernelGGL(ca_param_grads_kernel, dim3(nblocks, ny), dim3(256), 0, st, recs, brecs, N, C, CR, offs, grads);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

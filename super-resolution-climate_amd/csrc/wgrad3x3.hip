@@ -11,8 +11,8 @@
 // Workgroup = 4 waves (one per SIMD), one (chunk, co block); wave w owns 9 of the
 // 36 16-wide N tiles -> 144 f32 accumulators per lane.  Per 4-row stage the dY
 // tile (4 x TW px) and the 6 input rows it needs (6 x TW+2 px, zero padded) are
-// register-staged into LDS (issued before the MFMAs of the previous stage,
-// written after them), double buffered.  Both MFMA operands are read
+// DMA'd into LDS (global_load_lds, issued ahead of the MFMAs of the previous
+// stage), double buffered.  Both MFMA operands are read
 // K(pixel)-major with ds_read_b64_tr_b16; the LDS row pitches are multiples of 16
 // pixels so the swizzle (swz128t) is invariant across K-steps and every
 // transposed read is a precomputed per-lane offset + an immediate.
@@ -24,6 +24,7 @@
 
 namespace srmi {
 
+static __device__ uint4 kZerosW[4];  // zero page for halo lanes of the stage DMA
 static unsigned long long* g_wg_stamps = nullptr;
 void wgrad3x3_set_debug_stamps(unsigned long long* buf) { g_wg_stamps = buf; }
 #define WSTAMP(i)                                                                                     \
@@ -38,9 +39,6 @@ struct Wg3 {
   static constexpr int DY_BYTES = SR * TW * 128;
   static constexpr int X_BYTES = (SR + 2) * XP * 128;
   static constexpr int STAGE = DY_BYTES + X_BYTES;
-  static constexpr int DY_CH = SR * TW * 8;         // 16-B chunks to load
-  static constexpr int X_CH = (SR + 2) * (TW + 2) * 8;
-  static constexpr int PT = (DY_CH + X_CH + 255) / 256;
   static constexpr int KSTEPS = SR * TW / 32;
   static constexpr int TOTAL = 2 * STAGE;
 };
@@ -50,6 +48,7 @@ __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
   using S = Wg3<TW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);  // SGPR copy for the DMA bases
   const int chunk = blockIdx.x, cb = blockIdx.y;
   const int Hr = p.H / p.row_splits;
   const int n = chunk / p.row_splits, ybase = (chunk % p.row_splits) * Hr;
@@ -61,48 +60,39 @@ __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
                                              : p.dy + (size_t)n * 4 * p.H * p.W * 64;
   const bf16_t* xn = p.x + (size_t)n * p.H * p.W * 64;
 
-  // stage st: column block xb = st / nrp, rows y0 .. y0+3 (column-major order)
-  auto load_one = [&](int st, int j) -> uint4 {
+  // Stage fill by LDS-DMA (global_load_lds_dwordx4): one wave instruction moves one
+  // group of 8 pixels x 128 B into a contiguous kilobyte of LDS, so the swizzle is
+  // applied on the source side -- lane (q = lane >> 3, slot = lane & 7) fetches the
+  // logical chunk slot ^ f(q) of its pixel.  Halo / padding lanes read a zero page.
+  // Stage st covers column block xb = st / nrp, rows y0 .. y0+3 (column-major order).
+  constexpr int GD = TW / 8, GX = (TW + 2 + 7) / 8, NDY = S::SR * GD, NG = NDY + (S::SR + 2) * GX;
+  const uint32_t lds0 = lds_u32(smem);
+  const int dq = lane >> 3, ls = lane & 7;
+  auto fsw = [](int q) { return (((q >> 1) & 1) << 1) | (((q >> 3) & 1) << 2); };
+  auto dma_stage = [&](int st, int buf) {
     const int xb = st / nrp, rp = st - xb * nrp;
     const int y0 = ybase + S::SR * rp, x0 = xb * TW;
-    const int i = tid + 256 * j;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (i < S::DY_CH) {
-      const int q = i >> 3, c = i & 7;
-      const int r = q / TW, xx = x0 + q - r * TW, y = y0 + r;
-      const bf16_t* src;
-      if (p.dy_mode == IN_PLAIN)
-        src = dyn + ((size_t)y * p.W + xx) * p.Cout + c * 8;
-      else
-        src = dyn + ((size_t)(2 * y + (cb >> 1)) * (2 * p.W) + 2 * xx + (cb & 1)) * 64 + c * 8;
-      v = *reinterpret_cast<const uint4*>(src);
-    } else if (i < S::DY_CH + S::X_CH) {
-      const int ii = i - S::DY_CH;
-      const int q = ii >> 3, c = ii & 7;
-      const int r = q / (TW + 2), hx = q - r * (TW + 2);
-      const int y = y0 - 1 + r, xx = x0 - 1 + hx;
-      if (y >= 0 && y < p.H && xx >= 0 && xx < p.W)
-        v = *reinterpret_cast<const uint4*>(xn + ((size_t)y * p.W + xx) * 64 + c * 8);
-    }
-    return v;
-  };
-  auto load_stage = [&](int st, uint4* stg) {
+    const uint32_t base = lds0 + buf * S::STAGE;
 #pragma unroll
-    for (int j = 0; j < S::PT; ++j) stg[j] = load_one(st, j);
-  };
-  auto store_stage = [&](int buf, const uint4* stg) {
-    char* base = smem + buf * S::STAGE;
-#pragma unroll
-    for (int j = 0; j < S::PT; ++j) {
-      const int i = tid + 256 * j;
-      if (i < S::DY_CH) {
-        const int q = i >> 3, c = i & 7;
-        *reinterpret_cast<uint4*>(base + swz128t(q, c)) = stg[j];
-      } else if (i < S::DY_CH + S::X_CH) {
-        const int ii = i - S::DY_CH;
-        const int q = ii >> 3, c = ii & 7;
-        const int r = q / (TW + 2), hx = q - r * (TW + 2);
-        *reinterpret_cast<uint4*>(base + S::DY_BYTES + swz128t(r * S::XP + hx, c)) = stg[j];
+    for (int m = 0; m < (NG + 3) / 4; ++m) {
+      const int k = wave_s + 4 * m;
+      if (k < NDY) {
+        const int r = k / GD, px = 8 * (k % GD) + dq;
+        const int c = ls ^ fsw(r * TW + px);
+        const int y = y0 + r, xx = x0 + px;
+        const bf16_t* src;
+        if (p.dy_mode == IN_PLAIN)
+          src = dyn + ((size_t)y * p.W + xx) * p.Cout + c * 8;
+        else
+          src = dyn + ((size_t)(2 * y + (cb >> 1)) * (2 * p.W) + 2 * xx + (cb & 1)) * 64 + c * 8;
+        glds16(src, base + (uint32_t)(r * TW + 8 * (k % GD)) * 128u);
+      } else if (k < NG) {
+        const int kk = k - NDY, r = kk / GX, hx = 8 * (kk % GX) + dq;
+        const int c = ls ^ fsw(r * S::XP + hx);
+        const int y = y0 - 1 + r, xx = x0 - 1 + hx;
+        const bool ok = hx < TW + 2 && y >= 0 && y < p.H && xx >= 0 && xx < p.W;
+        const void* src = ok ? (const void*)(xn + ((size_t)y * p.W + xx) * 64 + c * 8) : (const void*)kZerosW;
+        glds16(src, base + (uint32_t)(S::DY_BYTES + (r * S::XP + 8 * (kk % GX)) * 128));
       }
     }
   };
@@ -137,23 +127,17 @@ __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
   }
   constexpr int NKC = TW / 16;
 
-  {
-    uint4 stg[S::PT];
-    load_stage(0, stg);
-    store_stage(0, stg);
-  }
+  dma_stage(0, 0);
+  wait_vm<0>();
   __syncthreads();
   WSTAMP(1);
 
-  // the next stage's PT loads are spread over the K-steps (LPS per step) so that a
-  // full memory queue stalls the wave between MFMA groups rather than ahead of them
-  constexpr int LPS = (S::PT + S::KSTEPS - 1) / S::KSTEPS;
 #pragma unroll 1
   for (int st = 0; st < nst; ++st) {
-    uint4 stg[S::PT];
     const bool pf = st + 1 < nst;
     const int sj = 2 + 3 * min(st, 19);
     WSTAMP(sj);
+    if (pf) dma_stage(st + 1, (st + 1) & 1);
     const char* sb = smem + (st & 1) * S::STAGE;
     bf16x8 A[2][4], B[2][9];
     auto load_step = [&](int kb, bf16x8 (&a)[4], bf16x8 (&b)[9]) {
@@ -165,13 +149,9 @@ __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
       for (int t = 0; t < 9; ++t) b[t] = cat_tr(lds_tr(sb, boff[t][0] + db), lds_tr(sb, boff[t][1] + db));
     };
     load_step(0, A[0], B[0]);
+    WSTAMP(sj + 1);
 #pragma unroll
     for (int kb = 0; kb < S::KSTEPS; ++kb) {
-      if (pf) {
-#pragma unroll
-        for (int jj = 0; jj < LPS; ++jj)
-          if (kb * LPS + jj < S::PT) stg[kb * LPS + jj] = load_one(st + 1, kb * LPS + jj);
-      }
       if (kb + 1 < S::KSTEPS) load_step(kb + 1, A[(kb + 1) & 1], B[(kb + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -185,10 +165,10 @@ __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
       bacc = mfma16(aw, ones, bacc);
       __builtin_amdgcn_sched_barrier(0);
     }
-    WSTAMP(sj + 1);
-    if (pf) store_stage((st + 1) & 1, stg);
-    __syncthreads();
+    wait_vm<0>();
     WSTAMP(sj + 2);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
 
   // epilogue: partial slab [chunk][9][64 ci][Cout] -- a lane's 4 accumulators are 4

@@ -162,24 +162,25 @@ def wstamps():
     gb = torch.empty(64, device=d)
     buf = torch.zeros(4096 * 64, dtype=torch.int64, device=d)
 
-    def run():
-        call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, 0, ptr(slab), slab.numel() * 4, 0, 1.0, ptr(gw),
-             ptr(gb), S)
-    for _ in range(3):
+    for rs in [int(v) for v in os.environ.get("KBENCH_RS", "0").split(",")]:
+        def run():
+            call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, rs, ptr(slab), slab.numel() * 4, 0, 1.0,
+                 ptr(gw), ptr(gb), S)
+        us = timeit(run, 20)
+        buf.zero_()
+        call("srmi_debug_wgrad_stamps", ptr(buf))
         run()
-    call("srmi_debug_wgrad_stamps", ptr(buf))
-    run()
-    call("srmi_debug_wgrad_stamps", None)
-    torch.cuda.synchronize()
-    st = buf.view(4096, 64).cpu().numpy()
-    st = st[st[:, 0] != 0]
-    rel = st - st[:, 0:1]
-    print("wgrad workgroups", len(st))
-    cols = [i for i in range(1, 64) if np.all(st[:, i] != 0)]
-    prev = np.zeros(len(st))
-    for i in cols:
-        print(f"stamp {i:2d} median dt {np.median(rel[:, i] - prev):8.0f}  max {np.max(rel[:, i] - prev):8.0f}")
-        prev = rel[:, i]
+        call("srmi_debug_wgrad_stamps", None)
+        torch.cuda.synchronize()
+        st = buf.view(4096, 64).cpu().numpy()
+        st = st[st[:, 0] != 0]
+        rel = st - st[:, 0:1]
+        print(f"wgrad rs={rs} workgroups {len(st)} us {us:.2f} (wgrad+reduce)")
+        cols = [i for i in range(1, 64) if np.all(st[:, i] != 0)]
+        prev = np.zeros(len(st))
+        for i in cols:
+            print(f"stamp {i:2d} median dt {np.median(rel[:, i] - prev):8.0f}  max {np.max(rel[:, i] - prev):8.0f}")
+            prev = rel[:, i]
 
 
 if __name__ == "__main__" and os.environ.get("KBENCH_STAMPS"):
