@@ -13,13 +13,15 @@ bf16 filter repack: exactly dual_trainer.py:310-323.
 Inputs are synthetic lnorm'ed N(0,1) tiles already resident in HBM.
 
 Prints ONE JSON line on rank 0 with the roofline of the dominant kernel
-(the 64->64 3x3 conv, measured live with HIP events) and the CPU baseline
+(the 3x3 filter-gradient kernel, measured with HIP events after the timed
+region; the forward conv alongside) and the CPU baseline
 (the oracle, a PyTorch-CPU restatement of the reference step, timed on this
 host's cores on a bounded sample).
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -51,48 +53,78 @@ def parse():
     return ap.parse_args()
 
 
-def conv_roofline(dev, batch):
-    """Average duration of the dominant kernel (64->64 3x3 conv, fused bias+ReLU
-    epilogue, B tiles of 48x48) from HIP events on its launch stream."""
+def _pmc_traffic(kernel_prefix):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary (FETCH_SIZE x2
+    + WRITE_SIZE, gfx950-corrected; tools/pmc_traffic.sh), or None."""
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        for k, v in d.items():
+            if kernel_prefix in k:
+                return {"bytes": v.get("hbm_bytes_per_launch"), "source": os.path.relpath(f, ROOT)}
+    return None
+
+
+def _time_launches(launch, stream, n=50, warm=5):
+    for _ in range(warm):
+        launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(n):
+        launch()
+    e1.record(stream)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
+def rooflines(dev, batch):
+    """Roofline of the dominant kernel (by rocprofv3 time share: the 3x3 filter-
+    gradient MFMA kernel, 23.7 % of a step) plus the forward conv, both at the
+    bench shapes (B tiles of 48x48x64 bf16), average launch duration from HIP events
+    on the launch stream.  Algorithmic bytes = what the op must move at least
+    (inputs once + outputs once); flops = 2 x MACs."""
     from srmi._lib import call, ptr
     g = torch.Generator(device="cpu").manual_seed(0)
-    x = torch.randn(batch, 48, 48, 64, generator=g).to(dev).to(torch.bfloat16)
+    N, H, W = batch, 48, 48
+    st = torch.cuda.current_stream()
+    x = torch.randn(N, H, W, 64, generator=g).to(dev).to(torch.bfloat16)
+    dy = torch.randn(N, H, W, 64, generator=g).to(dev).to(torch.bfloat16)
+    slab = torch.empty(N * 12 * 64 * 577 + 64, dtype=torch.float32, device=dev)
     w = (torch.randn(64, 64, 3, 3, generator=g) * 0.05).to(dev)
     b = torch.zeros(64, device=dev)
     fp = torch.empty(64 * 64 * 9, dtype=torch.bfloat16, device=dev)
     dp = torch.empty_like(fp)
     pb = torch.empty(64, device=dev)
-    st = torch.cuda.current_stream()
     call("srmi_pack_conv", ptr(w), ptr(b), 64, 64, 0, ptr(fp), ptr(dp), ptr(pb), st.cuda_stream)
-    y = torch.empty(batch, 48, 48, 64, dtype=torch.bfloat16, device=dev)
+    y = torch.empty_like(x)
+    flop = CONV64_FLOP_PER_TILE * N
+    act = N * H * W * 64 * 2  # one bf16 activation tensor
 
-    def launch():
-        call("srmi_conv3x3", ptr(x), ptr(fp), ptr(pb), batch, 48, 48, 64, 64, 0, 0, ptr(y), None, None, None, None,
-             None, None, 1.0, st.cuda_stream)
-
-    for _ in range(5):
-        launch()
-    n = 50
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for _ in range(n):
-        launch()
-    e1.record(st)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / n
-    flop = CONV64_FLOP_PER_TILE * batch
-    achieved = flop / (ms * 1e-3) / 1e12
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "conv3x3_pmc.json")
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    return {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-            "kernel": "srmi::conv3x3_kernel<48,EPI_RELU_BF16>", "avg_launch_ms": round(ms, 4),
-            "flop_per_launch": flop}
+    # dominant: filter gradient (partial slabs; the deterministic slab reduction is a separate launch)
+    ms_w = _time_launches(lambda: call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, 0, ptr(slab),
+                                       slab.numel() * 4, 0, 1.0, None, None, st.cuda_stream), st)
+    bytes_w = 2 * act + 64 * 577 * 4          # x + dY read once, dW + db written once
+    t_hbm, t_mfma = bytes_w / (HBM_PEAK_GBS * 1e9), flop / (PEAK_BF16_TFLOPS * 1e12)
+    tr = _pmc_traffic("wgrad3x3_kernel")
+    ach = bytes_w / (ms_w * 1e-3) / 1e9
+    dom = {"bound": "hbm" if t_hbm >= t_mfma else "mfma", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr["bytes"] if tr else None,
+           "kernel": "srmi::wgrad3x3_kernel<48>", "avg_launch_ms": round(ms_w, 4), "bytes_per_launch": bytes_w,
+           "flop_per_launch": flop, "mfma_tflops": round(flop / (ms_w * 1e-3) / 1e12, 1),
+           "mfma_frac": round(flop / (ms_w * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+           "traffic_source": tr["source"] if tr else None}
+    # secondary: forward conv, fused bias + ReLU epilogue
+    ms_c = _time_launches(lambda: call("srmi_conv3x3", ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, 0, ptr(y), None,
+                                       None, None, None, None, None, 1.0, st.cuda_stream), st)
+    trc = _pmc_traffic("conv64_kernel<48, 0")
+    ach_c = flop / (ms_c * 1e-3) / 1e12
+    conv = {"bound": "mfma", "achieved": round(ach_c, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach_c / PEAK_BF16_TFLOPS, 4), "traffic": trc["bytes"] if trc else None,
+            "kernel": "srmi::conv64_kernel<48,RELU>", "avg_launch_ms": round(ms_c, 4), "flop_per_launch": flop,
+            "bytes_per_launch": 2 * act + 64 * 576 * 2}
+    return dom, conv
 
 
 def cpu_baseline(channels, steps):
@@ -169,7 +201,7 @@ def main():
     tiles = B * world * args.steps
     value = tiles / dt
     if info.rank == 0:
-        roof = conv_roofline(dev, B)
+        roof, roof_conv = rooflines(dev, B)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(C, args.cpu_steps)
@@ -184,6 +216,7 @@ def main():
             "model_tflops": round(value * TRAIN_GFLOP_PER_TILE_C2 / 1000.0, 1),
             "loss": round(loss, 6),
             "roofline": roof,
+            "roofline_conv_fwd": roof_conv,
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec), flush=True)

@@ -123,11 +123,18 @@ int srmi_debug_wgrad_stamps(void* buf);
  * PixelShuffle channel order (packed c'' = 64q + c <- torch 4c + q)         */
 int srmi_pack_conv(const float* w, const float* b, int Cout, int Cin, int ps, void* fpack, void* dpack, float* pbias,
                    void* stream);
+/* filter + bias gradient of a 3x3 conv (nn.Conv2d backward, weight half):
+ * x NHWC bf16 [N][H][W][64], dy NHWC bf16 [N][H][W][Cout] (or, dy_unshuffle,
+ * the PixelShuffle output [N][2H][2W][64] with Cout = 256); slab: workspace of
+ * N*rs*Cout*577 floats; gw torch layout [Cout][64][3][3], gb [Cout] (both NULL:
+ * leave the per-chunk partial slabs, skip the reduction) */
 int srmi_wgrad3x3(const void* x, const void* dy, int N, int H, int W, int Cout, int dy_unshuffle, int row_splits,
                   float* slab, size_t slab_bytes, int ps, float alpha, float* gw, float* gb, void* stream);
 int srmi_ca_forward(const void* u, const float* part, int nstrips, const float* w1, const float* b1, const float* w2,
                     const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, void* hb_out,
                     float* rec, void* stream);
+/* brec: N*(2C + C/R) floats (dz2 | dz1 | conv2 bias grad per image) followed by
+ * N*C floats of dm (gradient of the pooled mean) -- N*(3C + C/R) in total */
 int srmi_ca_backward(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
                      const float* w2, int N, int HW, int C, int R, void* du, float* brec, void* stream);
 int srmi_head_forward(const float* lr, const float* w, const float* b, int N, int C, int H, int W, float* x0f,

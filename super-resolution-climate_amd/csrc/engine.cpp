@@ -211,7 +211,7 @@ struct srmi_engine {
   float* recp(int g, int b) const {
     return train ? rec + (size_t)(g * P.cfg.nblocks + (b - 1)) * N * 160 : rec;
   }
-  float* brecp(int g, int b) const { return brec + (size_t)(g * P.cfg.nblocks + (b - 1)) * N * 160; }
+  float* brecp(int g, int b) const { return brec + (size_t)(g * P.cfg.nblocks + (b - 1)) * N * 224; }
 };
 
 static size_t carve(srmi_engine* e, char* base) {
@@ -237,7 +237,7 @@ static size_t carve(srmi_engine* e, char* base) {
   const int nstrips = conv3x3_nstrips(e->h, e->w);
   if (rcan) {
     e->rec = cv.take<float>((size_t)(e->train ? nl * nb : 1) * N * 160);
-    e->brec = e->train ? cv.take<float>((size_t)nl * nb * N * 160) : nullptr;
+    e->brec = e->train ? cv.take<float>((size_t)nl * nb * N * 224) : nullptr;  // [N][160] + dm[N][64]
     e->ppool = cv.take<float>((size_t)N * nstrips * 64);
     e->pacc = cv.take<float>((size_t)N * nstrips * 128);
   }
@@ -721,11 +721,8 @@ int srmi_wgrad3x3(const void* x, const void* dy, int N, int H, int W, int Cout, 
   if (slab_bytes < need) return SRMI_ERR_WORKSPACE;
   p.slab = slab;
   p.bslab = slab + ns * Cout * 576;
-  float* zeros = slab + ns * Cout * 577;
-  hipError_t er = hipMemsetAsync(zeros, 0, 256, S_(stream));
-  if (er != hipSuccess) return -(int)er;
-  p.zeros = zeros;
   RC(wgrad3x3_launch(p, S_(stream)));
+  if (!gw && !gb) return 0;  // partial slabs only (profiling the MFMA kernel alone)
   return wgrad_reduce_launch(p.slab, p.bslab, (int)ns, Cout, ps, alpha, gw, gb, S_(stream));
 }
 

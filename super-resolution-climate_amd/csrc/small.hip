@@ -539,59 +539,82 @@ int loss_finalize_launch(float* loss, hipStream_t st) {
 
 // =============================================================== channel attention
 // rec layout per image: m[C] z1[C/R] s[C]   (C = 64, C/R = 32)
-__device__ void ca_mlp(const float* __restrict__ part, int nstrips, int pstride, int n, int HW,
-                       const float* __restrict__ w1, const float* __restrict__ b1, const float* __restrict__ w2,
-                       const float* __restrict__ b2, int C, int CR, float* sm /* [C] m | [CR] z1 | [C] s */) {
-  const int tid = threadIdx.x;
+// ---------------------------------------------------------------------------
+// Channel attention (CALayer, reference sres/model/rcan/network.py:31-47):
+//   m = avgpool(u); z1 = W1 m + b1; s = sigmoid(W2 relu(z1) + b2); h += s * u
+// The per-image MLP runs once per image in its own tiny kernel (one wave per
+// image) and the elementwise pass streams with no per-block preamble.
+// rec per image: m[C] | z1[CR] | s[C]   (C = 64, CR = C / R)
+__global__ void __launch_bounds__(64) ca_fwd_mlp_kernel(const float* __restrict__ part, int nstrips, int HW,
+                                                        const float* __restrict__ w1, const float* __restrict__ b1,
+                                                        const float* __restrict__ w2, const float* __restrict__ b2,
+                                                        int C, int CR, float* __restrict__ rec) {
+  __shared__ float sm[64 + 32];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  float* r = rec + (size_t)n * (2 * C + CR);
+  float m = 0.f;
   if (tid < C) {
-    float s = 0.f;
-    for (int k = 0; k < nstrips; ++k) s += part[((size_t)n * nstrips + k) * pstride + tid];
-    sm[tid] = s / (float)HW;
+    for (int k = 0; k < nstrips; ++k) m += part[((size_t)n * nstrips + k) * C + tid];
+    m /= (float)HW;
+    sm[tid] = m;
+    r[tid] = m;
   }
   __syncthreads();
   if (tid < CR) {
     float z = b1[tid];
     for (int c = 0; c < C; ++c) z += w1[tid * C + c] * sm[c];
-    sm[C + tid] = z;
+    sm[64 + tid] = z;
+    r[C + tid] = z;
   }
   __syncthreads();
   if (tid < C) {
     float z = b2[tid];
-    for (int j = 0; j < CR; ++j) z += w2[tid * CR + j] * fmaxf(sm[C + j], 0.f);
-    sm[C + CR + tid] = 1.f / (1.f + expf(-z));
+    for (int j = 0; j < CR; ++j) z += w2[tid * CR + j] * fmaxf(sm[64 + j], 0.f);
+    r[C + CR + tid] = 1.f / (1.f + expf(-z));
   }
-  __syncthreads();
 }
 
+// elementwise passes: each thread handles kCaVec groups of 8 channels
+constexpr int kCaVec = 2;
+
 // h_out = u * s + h_in  (fp32 + bf16 copy); grid (chunks, N)
-__global__ void __launch_bounds__(256) ca_fwd_kernel(const bf16_t* __restrict__ u, const float* __restrict__ part,
-                                                     int nstrips, const float* __restrict__ w1,
-                                                     const float* __restrict__ b1, const float* __restrict__ w2,
-                                                     const float* __restrict__ b2, int HW, int C, int CR,
+__global__ void __launch_bounds__(256) ca_fwd_kernel(const bf16_t* __restrict__ u, int HW, int C, int CR,
                                                      const float* __restrict__ h_in, float* __restrict__ h_out,
-                                                     bf16_t* __restrict__ hb_out, float* __restrict__ rec) {
-  __shared__ float sm[64 + 32 + 64];
+                                                     bf16_t* __restrict__ hb_out, const float* __restrict__ rec) {
+  __shared__ float s[64];
   const int n = blockIdx.y;
-  ca_mlp(part, nstrips, C, n, HW, w1, b1, w2, b2, C, CR, sm);
-  if (blockIdx.x == 0 && threadIdx.x < 2 * C + CR) rec[(size_t)n * (2 * C + CR) + threadIdx.x] = sm[threadIdx.x];
-  const float* s = sm + C + CR;
+  if (threadIdx.x < C) s[threadIdx.x] = rec[(size_t)n * (2 * C + CR) + C + CR + threadIdx.x];
+  __syncthreads();
   const size_t base = (size_t)n * HW * C;
   const size_t nv = (size_t)HW * C / 8;
-  for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (size_t)gridDim.x * blockDim.x) {
+  const size_t v0 = ((size_t)blockIdx.x * kCaVec) * blockDim.x + threadIdx.x;
+  uint4 uu[kCaVec];
+  float4 h0[kCaVec], h1[kCaVec];
+#pragma unroll
+  for (int k = 0; k < kCaVec; ++k) {
+    const size_t v = v0 + (size_t)k * blockDim.x;
+    if (v < nv) {
+      const size_t e = base + v * 8;
+      uu[k] = *reinterpret_cast<const uint4*>(u + e);
+      h0[k] = *reinterpret_cast<const float4*>(h_in + e);
+      h1[k] = *reinterpret_cast<const float4*>(h_in + e + 4);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kCaVec; ++k) {
+    const size_t v = v0 + (size_t)k * blockDim.x;
+    if (v >= nv) continue;
     const size_t e = base + v * 8;
     const int c0 = (int)((v * 8) % C);
-    const uint4 uu = *reinterpret_cast<const uint4*>(u + e);
-    const float4 h0 = *reinterpret_cast<const float4*>(h_in + e);
-    const float4 h1 = *reinterpret_cast<const float4*>(h_in + e + 4);
     float o[8];
-    o[0] = bf2f(uu.x & 0xFFFF) * s[c0 + 0] + h0.x;
-    o[1] = bf2f(uu.x >> 16) * s[c0 + 1] + h0.y;
-    o[2] = bf2f(uu.y & 0xFFFF) * s[c0 + 2] + h0.z;
-    o[3] = bf2f(uu.y >> 16) * s[c0 + 3] + h0.w;
-    o[4] = bf2f(uu.z & 0xFFFF) * s[c0 + 4] + h1.x;
-    o[5] = bf2f(uu.z >> 16) * s[c0 + 5] + h1.y;
-    o[6] = bf2f(uu.w & 0xFFFF) * s[c0 + 6] + h1.z;
-    o[7] = bf2f(uu.w >> 16) * s[c0 + 7] + h1.w;
+    o[0] = bf2f(uu[k].x & 0xFFFF) * s[c0 + 0] + h0[k].x;
+    o[1] = bf2f(uu[k].x >> 16) * s[c0 + 1] + h0[k].y;
+    o[2] = bf2f(uu[k].y & 0xFFFF) * s[c0 + 2] + h0[k].z;
+    o[3] = bf2f(uu[k].y >> 16) * s[c0 + 3] + h0[k].w;
+    o[4] = bf2f(uu[k].z & 0xFFFF) * s[c0 + 4] + h1[k].x;
+    o[5] = bf2f(uu[k].z >> 16) * s[c0 + 5] + h1[k].y;
+    o[6] = bf2f(uu[k].w & 0xFFFF) * s[c0 + 6] + h1[k].z;
+    o[7] = bf2f(uu[k].w >> 16) * s[c0 + 7] + h1[k].w;
     *reinterpret_cast<float4*>(h_out + e) = make_float4(o[0], o[1], o[2], o[3]);
     *reinterpret_cast<float4*>(h_out + e + 4) = make_float4(o[4], o[5], o[6], o[7]);
     uint4 ob;
@@ -602,7 +625,7 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const bf16_t* __restrict__ 
 
 static int ca_grid_x(int HW, int C) {
   const int nv = HW * C / 8;
-  int gx = (nv + 255) / 256;
+  int gx = (nv + 256 * kCaVec - 1) / (256 * kCaVec);
   return gx < 1 ? 1 : gx;
 }
 
@@ -610,85 +633,96 @@ int ca_fwd_launch(const bf16_t* u, const float* part, int nstrips, const float* 
                   const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, bf16_t* hb_out,
                   float* rec, hipStream_t st) {
   if (C != 64 || C % R || (HW * C) % 8) return SRMI_ERR_SHAPE;
-  hipLaunchKernelGGL(ca_fwd_kernel, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, u, part, nstrips, w1, b1, w2, b2,
-                     HW, C, C / R, h_in, h_out, hb_out, rec);
+  hipLaunchKernelGGL(ca_fwd_mlp_kernel, dim3(N), dim3(64), 0, st, part, nstrips, HW, w1, b1, w2, b2, C, C / R, rec);
+  hipLaunchKernelGGL(ca_fwd_kernel, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, u, HW, C, C / R, h_in, h_out,
+                     hb_out, rec);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
 
-// CA backward per image + du = g * s + dm / HW  (bf16).  part[n][strip][2C] holds
-// sum_p g (0..C-1) and sum_p g*u (C..2C-1) from the producer of g.
-// brec per image: dz2[C] dz1[CR] dbconv2[C]
-__global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict__ g, const float* __restrict__ part,
-                                                        int nstrips, const float* __restrict__ rec,
-                                                        const float* __restrict__ w1, const float* __restrict__ w2,
-                                                        int HW, int C, int CR, bf16_t* __restrict__ du,
+// CA backward per image.  part[n][strip][2C] holds sum_p g (0..C-1) and
+// sum_p g*u (C..2C-1) from the producer of g.
+// brec per image: dz2[C] dz1[CR] dbconv2[C]; followed (after all N images) by
+// dm[N][C] = W1^T dz1 (the gradient of the pooled mean).
+__global__ void __launch_bounds__(64) ca_bwd_mlp_kernel(const float* __restrict__ part, int nstrips,
+                                                        const float* __restrict__ rec, const float* __restrict__ w1,
+                                                        const float* __restrict__ w2, int N, int C, int CR,
                                                         float* __restrict__ brec) {
-  __shared__ float sm[64 * 4 + 32 * 2];
-  const int n = blockIdx.y, tid = threadIdx.x;
+  __shared__ float dz2[64], dz1[32];
+  const int n = blockIdx.x, tid = threadIdx.x;
   const float* r = rec + (size_t)n * (2 * C + CR);
-  float* G = sm;            // [C]
-  float* dsv = sm + C;      // [C]
-  float* dz2 = sm + 2 * C;  // [C]
-  float* dm = sm + 3 * C;   // [C]
-  float* dz1 = sm + 4 * C;  // [CR]
+  float* br = brec + (size_t)n * (2 * C + CR);
+  float G = 0.f;
   if (tid < C) {
-    float a = 0.f, b = 0.f;
+    float b = 0.f;
     for (int k = 0; k < nstrips; ++k) {
       const float* pp = part + ((size_t)n * nstrips + k) * (2 * C);
-      a += pp[tid];
+      G += pp[tid];
       b += pp[C + tid];
     }
-    G[tid] = a;
-    dsv[tid] = b;
     const float s = r[C + CR + tid];
     dz2[tid] = b * s * (1.f - s);
+    br[tid] = dz2[tid];
   }
   __syncthreads();
   if (tid < CR) {
     float a = 0.f;
     for (int c = 0; c < C; ++c) a += w2[c * CR + tid] * dz2[c];
     dz1[tid] = (r[C + tid] > 0.f) ? a : 0.f;
+    br[C + tid] = dz1[tid];
   }
   __syncthreads();
   if (tid < C) {
     float a = 0.f;
     for (int j = 0; j < CR; ++j) a += w1[j * C + tid] * dz1[j];
-    dm[tid] = a;
+    br[C + CR + tid] = r[C + CR + tid] * G + a;  // conv2 bias grad: sum_p du
+    brec[(size_t)N * (2 * C + CR) + (size_t)n * C + tid] = a;
+  }
+}
+
+// du = g * s + dm / HW  (bf16)
+__global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict__ g, const float* __restrict__ rec,
+                                                        const float* __restrict__ brec, int N, int HW, int C, int CR,
+                                                        bf16_t* __restrict__ du) {
+  __shared__ float s[64], dmh[64];
+  const int n = blockIdx.y, tid = threadIdx.x;
+  if (tid < C) {
+    s[tid] = rec[(size_t)n * (2 * C + CR) + C + CR + tid];
+    dmh[tid] = brec[(size_t)N * (2 * C + CR) + (size_t)n * C + tid] * (1.f / (float)HW);
   }
   __syncthreads();
-  if (blockIdx.x == 0) {
-    float* br = brec + (size_t)n * (2 * C + CR);
-    if (tid < C) {
-      br[tid] = dz2[tid];
-      br[C + CR + tid] = r[C + CR + tid] * G[tid] + dm[tid];
-    } else if (tid < C + CR) {
-      br[tid] = dz1[tid - C];
-    }
-  }
-  const float* s = r + C + CR;
-  const float inv = 1.f / (float)HW;
   const size_t base = (size_t)n * HW * C;
   const size_t nv = (size_t)HW * C / 8;
-  for (size_t v = (size_t)blockIdx.x * blockDim.x + tid; v < nv; v += (size_t)gridDim.x * blockDim.x) {
-    const size_t e = base + v * 8;
+  const size_t v0 = ((size_t)blockIdx.x * kCaVec) * blockDim.x + tid;
+  float4 g0[kCaVec], g1[kCaVec];
+#pragma unroll
+  for (int k = 0; k < kCaVec; ++k) {
+    const size_t v = v0 + (size_t)k * blockDim.x;
+    if (v < nv) {
+      g0[k] = *reinterpret_cast<const float4*>(g + base + v * 8);
+      g1[k] = *reinterpret_cast<const float4*>(g + base + v * 8 + 4);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kCaVec; ++k) {
+    const size_t v = v0 + (size_t)k * blockDim.x;
+    if (v >= nv) continue;
     const int c0 = (int)((v * 8) % C);
-    const float4 g0 = *reinterpret_cast<const float4*>(g + e);
-    const float4 g1 = *reinterpret_cast<const float4*>(g + e + 4);
     uint4 ob;
-    ob.x = pack2(g0.x * s[c0 + 0] + dm[c0 + 0] * inv, g0.y * s[c0 + 1] + dm[c0 + 1] * inv);
-    ob.y = pack2(g0.z * s[c0 + 2] + dm[c0 + 2] * inv, g0.w * s[c0 + 3] + dm[c0 + 3] * inv);
-    ob.z = pack2(g1.x * s[c0 + 4] + dm[c0 + 4] * inv, g1.y * s[c0 + 5] + dm[c0 + 5] * inv);
-    ob.w = pack2(g1.z * s[c0 + 6] + dm[c0 + 6] * inv, g1.w * s[c0 + 7] + dm[c0 + 7] * inv);
-    *reinterpret_cast<uint4*>(du + e) = ob;
+    ob.x = pack2(g0[k].x * s[c0 + 0] + dmh[c0 + 0], g0[k].y * s[c0 + 1] + dmh[c0 + 1]);
+    ob.y = pack2(g0[k].z * s[c0 + 2] + dmh[c0 + 2], g0[k].w * s[c0 + 3] + dmh[c0 + 3]);
+    ob.z = pack2(g1[k].x * s[c0 + 4] + dmh[c0 + 4], g1[k].y * s[c0 + 5] + dmh[c0 + 5]);
+    ob.w = pack2(g1[k].z * s[c0 + 6] + dmh[c0 + 6], g1[k].w * s[c0 + 7] + dmh[c0 + 7]);
+    *reinterpret_cast<uint4*>(du + base + v * 8) = ob;
   }
 }
 
 int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
                      const float* w2, int N, int HW, int C, int R, bf16_t* du, float* brec, hipStream_t st) {
   if (C != 64 || C % R || (HW * C) % 8) return SRMI_ERR_SHAPE;
-  hipLaunchKernelGGL(ca_bwd_du_kernel, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, g, part, nstrips, rec, w1, w2,
-                     HW, C, C / R, du, brec);
+  hipLaunchKernelGGL(ca_bwd_mlp_kernel, dim3(N), dim3(64), 0, st, part, nstrips, rec, w1, w2, N, C, C / R, brec);
+  hipLaunchKernelGGL(ca_bwd_du_kernel, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, g, rec, brec, N, HW, C, C / R,
+                     du);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
@@ -705,7 +739,7 @@ __global__ void __launch_bounds__(256) ca_param_grads_kernel(const float* __rest
   const int k = blockIdx.x;
   const int rs = 2 * C + CR;
   const float* rec = recs + (size_t)k * N * rs;
-  const float* brec = brecs + (size_t)k * N * rs;
+  const float* brec = brecs + (size_t)k * N * (rs + C);  // [N][rs] then dm[N][C]
   const int nw = 2 * C * CR;
   const int o = blockIdx.y * 256 + threadIdx.x;
   if ((int)blockIdx.y * 256 < nw) {

@@ -57,6 +57,7 @@ struct WgradParams {
   float* bslab;        // [nslab][Cout]
   const void* zeros;   // >= 16 zero bytes in global memory (DMA source for padding)
   unsigned long long* stamps;  // diagnostic (null in production)
+  int dbg;             // debug: bit0 skip MFMA, bit1 skip DMA, bit2 nt loads
 };
 void wgrad3x3_set_debug_stamps(unsigned long long* buf);
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st);

@@ -19,6 +19,8 @@
 // The bias gradient rides along as one extra MFMA per K-step against a ones
 // fragment.  Each workgroup writes one partial slab; wgrad_reduce sums the slabs
 // in a fixed order (deterministic) into the torch-layout gradient.
+#include <cstdlib>
+
 #include "common.hpp"
 #include "srmi_internal.hpp"
 
@@ -69,32 +71,38 @@ __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
   const uint32_t lds0 = lds_u32(smem);
   const int dq = lane >> 3, ls = lane & 7;
   auto fsw = [](int q) { return (((q >> 1) & 1) << 1) | (((q >> 3) & 1) << 2); };
-  auto dma_stage = [&](int st, int buf) {
+  // DMA group m (0 .. NGW-1) of this wave for stage st into buffer buf
+  constexpr int NGW = (NG + 3) / 4;
+  auto dma_group = [&](int st, int buf, int m) {
+    if (p.dbg & 2) return;
     const int xb = st / nrp, rp = st - xb * nrp;
     const int y0 = ybase + S::SR * rp, x0 = xb * TW;
     const uint32_t base = lds0 + buf * S::STAGE;
-#pragma unroll
-    for (int m = 0; m < (NG + 3) / 4; ++m) {
-      const int k = wave_s + 4 * m;
-      if (k < NDY) {
-        const int r = k / GD, px = 8 * (k % GD) + dq;
-        const int c = ls ^ fsw(r * TW + px);
-        const int y = y0 + r, xx = x0 + px;
-        const bf16_t* src;
-        if (p.dy_mode == IN_PLAIN)
-          src = dyn + ((size_t)y * p.W + xx) * p.Cout + c * 8;
-        else
-          src = dyn + ((size_t)(2 * y + (cb >> 1)) * (2 * p.W) + 2 * xx + (cb & 1)) * 64 + c * 8;
-        glds16(src, base + (uint32_t)(r * TW + 8 * (k % GD)) * 128u);
-      } else if (k < NG) {
-        const int kk = k - NDY, r = kk / GX, hx = 8 * (kk % GX) + dq;
-        const int c = ls ^ fsw(r * S::XP + hx);
-        const int y = y0 - 1 + r, xx = x0 - 1 + hx;
-        const bool ok = hx < TW + 2 && y >= 0 && y < p.H && xx >= 0 && xx < p.W;
-        const void* src = ok ? (const void*)(xn + ((size_t)y * p.W + xx) * 64 + c * 8) : (const void*)kZerosW;
-        glds16(src, base + (uint32_t)(S::DY_BYTES + (r * S::XP + 8 * (kk % GX)) * 128));
-      }
+    const int k = wave_s + 4 * m;
+    if (k < NDY) {
+      const int r = k / GD, px = 8 * (k % GD) + dq;
+      const int c = ls ^ fsw(r * TW + px);
+      const int y = y0 + r, xx = x0 + px;
+      const bf16_t* src;
+      if (p.dy_mode == IN_PLAIN)
+        src = dyn + ((size_t)y * p.W + xx) * p.Cout + c * 8;
+      else
+        src = dyn + ((size_t)(2 * y + (cb >> 1)) * (2 * p.W) + 2 * xx + (cb & 1)) * 64 + c * 8;
+      if (p.dbg & 4) glds16_nt(src, base + (uint32_t)(r * TW + 8 * (k % GD)) * 128u);
+      else glds16(src, base + (uint32_t)(r * TW + 8 * (k % GD)) * 128u);
+    } else if (k < NG) {
+      const int kk = k - NDY, r = kk / GX, hx = 8 * (kk % GX) + dq;
+      const int c = ls ^ fsw(r * S::XP + hx);
+      const int y = y0 - 1 + r, xx = x0 - 1 + hx;
+      const bool ok = hx < TW + 2 && y >= 0 && y < p.H && xx >= 0 && xx < p.W;
+      const void* src = ok ? (const void*)(xn + ((size_t)y * p.W + xx) * 64 + c * 8) : (const void*)kZerosW;
+      if (p.dbg & 4) glds16_nt(src, base + (uint32_t)(S::DY_BYTES + (r * S::XP + 8 * (kk % GX)) * 128));
+      else glds16(src, base + (uint32_t)(S::DY_BYTES + (r * S::XP + 8 * (kk % GX)) * 128));
     }
+  };
+  auto dma_stage = [&](int st, int buf) {
+#pragma unroll
+    for (int m = 0; m < NGW; ++m) dma_group(st, buf, m);
   };
 
   f32x4 acc[4][9];
@@ -126,6 +134,7 @@ __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
       boff[t][h] = S::DY_BYTES + swz128t((prow + ky) * S::XP + pcol + kx + 4 * h, 2 * it + (lp >> 1)) + half;
   }
   constexpr int NKC = TW / 16;
+  constexpr int DPS = (NGW + S::KSTEPS - 1) / S::KSTEPS;
 
   dma_stage(0, 0);
   wait_vm<0>();
@@ -137,7 +146,6 @@ __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
     const bool pf = st + 1 < nst;
     const int sj = 2 + 3 * min(st, 19);
     WSTAMP(sj);
-    if (pf) dma_stage(st + 1, (st + 1) & 1);
     const char* sb = smem + (st & 1) * S::STAGE;
     bf16x8 A[2][4], B[2][9];
     auto load_step = [&](int kb, bf16x8 (&a)[4], bf16x8 (&b)[9]) {
@@ -152,8 +160,16 @@ __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
     WSTAMP(sj + 1);
 #pragma unroll
     for (int kb = 0; kb < S::KSTEPS; ++kb) {
+      // the next stage's DMA, spread over the K-steps (DPS groups per step) so the
+      // wave stalls on a full memory queue between MFMA groups, not ahead of them
+      if (pf) {
+#pragma unroll
+        for (int i = 0; i < DPS; ++i)
+          if (kb * DPS + i < NGW) dma_group(st + 1, (st + 1) & 1, kb * DPS + i);
+      }
       if (kb + 1 < S::KSTEPS) load_step(kb + 1, A[(kb + 1) & 1], B[(kb + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
+      if (p.dbg & 1) continue;
 #pragma unroll
       for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -193,6 +209,185 @@ __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
   WSTAMP(63);
 }
 
+// ---------------------------------------------------------------------------
+// v4 for W == 48 (the 64->64 convs of every RCAB / group tail / body, and the
+// first upsampler conv via IN_UNSHUF): row-pair granularity with rings.
+//   * K-step = 2 output rows x 16 columns; a row pair = 3 K-steps.
+//   * dY rows live in an RD-slot ring (6 KiB each), input rows in an RX-slot ring
+//     (pitch 64 px, 8 KiB each): every input row is fetched once per chunk (v3
+//     fetched 6 rows per 4), i.e. 26 DMA groups (26 KiB) per row pair.
+//   * PF row pairs are in flight; the DMA for pair j+PF is spread over pair j's
+//     K-steps and completion is tracked with a counted vmcnt (no vmcnt(0)
+//     sawtooth), then one barrier per pair.
+// Slot reuse: pair j+PF writes the dY slots and input rows last read by pair j-1,
+// which every wave finished before the barrier that ended pair j-1.
+namespace v4 {
+constexpr int TW = 48, XP = 64, PF = 3, RD = 2 * (PF + 1), RX = 2 * PF + 4;
+constexpr int DSLOT = TW * 128, XSLOT = XP * 128;
+constexpr int DY_RING = RD * DSLOT, LDS = DY_RING + RX * XSLOT;  // 48 + 80 KiB
+constexpr int GD = TW / 8, GX = 7;                               // 8-px groups per row
+constexpr int NGP = 2 * GD + 2 * GX;                             // groups per pair (26)
+}  // namespace v4
+
+__global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
+  using namespace v4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const int chunk = blockIdx.x, cb = blockIdx.y;
+  const int Hr = p.H / p.row_splits;
+  const int n = chunk / p.row_splits, ybase = (chunk % p.row_splits) * Hr;
+  const int np = Hr / 2;
+  const int H = p.H, Cout = p.Cout;
+  const bool plain = p.dy_mode == IN_PLAIN;
+  WSTAMP(0);
+  const bf16_t* dyn = plain ? p.dy + (size_t)n * H * TW * Cout + cb * 64 : p.dy + (size_t)n * 4 * H * TW * 64;
+  const bf16_t* xn = p.x + (size_t)n * H * TW * 64;
+  const uint32_t lds0 = lds_u32(smem);
+  const int dq = lane >> 3, ls = lane & 7;
+  // source chunk of this lane inside its pixel: the swizzle bits of q = 8g + dq
+  // are bit 1 of dq and bit 0 of g (row and slot bases are multiples of 16 px)
+  const int cl0 = ls ^ (((dq >> 1) & 1) << 1);   // g even
+  const int cl1 = cl0 ^ 4;                         // g odd
+
+  // one DMA group: k < 2*GD -> dY row 2P + k / GD; else input row 2P + 1 + rr
+  // (pre = true: input rows -1 and 0 of the chunk, k < 2*GX)
+  auto dma = [&](int P, int k, bool pre) __attribute__((always_inline)) {
+    if (!pre && k < 2 * GD) {
+      const int rr = k / GD, g = k - rr * GD;
+      const int r = 2 * P + rr, y = ybase + r, xx = 8 * g + dq;
+      const int c = (g & 1) ? cl1 : cl0;
+      const bf16_t* src = plain
+                              ? dyn + ((size_t)y * TW + xx) * Cout + c * 8
+                              : dyn + ((size_t)(2 * y + (cb >> 1)) * (2 * TW) + 2 * xx + (cb & 1)) * 64 + c * 8;
+      glds16(src, lds0 + (uint32_t)((r % RD) * DSLOT + g * 1024));
+    } else {
+      const int kk = pre ? k : k - 2 * GD, rr = kk / GX, g = kk - rr * GX;
+      const int r = pre ? rr - 1 : 2 * P + 1 + rr;  // chunk-relative input row
+      const int y = ybase + r, hx = 8 * g + dq, xx = hx - 1;
+      const bool ok = hx < TW + 2 && y >= 0 && y < H && xx >= 0 && xx < TW;
+      const int c = (g & 1) ? cl1 : cl0;
+      const void* src = ok ? (const void*)(xn + ((size_t)y * TW + xx) * 64 + c * 8) : (const void*)kZerosW;
+      glds16(src, lds0 + (uint32_t)(DY_RING + ((r + 1) % RX) * XSLOT + g * 1024));
+    }
+  };
+  // groups of pair P owned by this wave: k = wave + 4m, m < 7 (waves 0,1) / 6 (2,3)
+  auto dma_pair_part = [&](int P, int m0, int m1) __attribute__((always_inline)) {
+#pragma unroll
+    for (int m = m0; m < m1; ++m)
+      if (wave_s + 4 * m < NGP) dma(P, wave_s + 4 * m, false);
+  };
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 bacc = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+
+  // transposed-read lane coordinates (see v3); row parts are added per pair
+  const int g4 = lane >> 4, li = lane & 15, lq = li >> 2, lp = li & 3;
+  const int prow = g4 >> 1, pcol = 8 * (g4 & 1) + lq;
+  const uint32_t half = (lp & 1) * 8;
+  uint32_t acol[4][2], bcol[9][2];
+  int bky[9];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) acol[ct][h] = swz128t(pcol + 4 * h, 2 * ct + (lp >> 1)) + half;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int j = 9 * wave + t, tap = j >> 2, it = j & 3, kx = tap % 3;
+    bky[t] = tap / 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) bcol[t][h] = DY_RING + swz128t(pcol + kx + 4 * h, 2 * it + (lp >> 1)) + half;
+  }
+
+  // prologue: input rows -1, 0 and pairs 0 .. PF-1
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+    if (wave_s + 4 * m < 2 * GX) dma(0, wave_s + 4 * m, true);
+  for (int P = 0; P < PF && P < np; ++P) dma_pair_part(P, 0, 7);
+  // wait for pair 0 (+ the pre rows): allow the later prologue pairs to stay in flight
+  {
+    const int later = min(PF, np) - 1;
+    if (wave_s < 2) {
+      if (later >= 2) wait_vm<14>(); else if (later == 1) wait_vm<7>(); else wait_vm<0>();
+    } else {
+      if (later >= 2) wait_vm<12>(); else if (later == 1) wait_vm<6>(); else wait_vm<0>();
+    }
+  }
+  __syncthreads();
+  WSTAMP(1);
+
+#pragma unroll 1
+  for (int j = 0; j < np; ++j) {
+    WSTAMP(2 + min(j, 59));
+    const bool pf = j + PF < np;
+    const uint32_t ra = (uint32_t)(((2 * j + prow) % RD) * DSLOT);
+    uint32_t rb[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) rb[t] = (uint32_t)(((2 * j + prow + bky[t]) % RX) * XSLOT);
+    bf16x8 A[2][4], B[2][9];
+    auto load_step = [&](int kc, bf16x8 (&a)[4], bf16x8 (&b)[9]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+        a[ct] = cat_tr(lds_tr(smem, ra + acol[ct][0] + kc * 2048), lds_tr(smem, ra + acol[ct][1] + kc * 2048));
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+        b[t] = cat_tr(lds_tr(smem, rb[t] + bcol[t][0] + kc * 2048), lds_tr(smem, rb[t] + bcol[t][1] + kc * 2048));
+    };
+    load_step(0, A[0], B[0]);
+#pragma unroll
+    for (int kc = 0; kc < 3; ++kc) {
+      if (pf) dma_pair_part(j + PF, kc == 0 ? 0 : (kc == 1 ? 3 : 5), kc == 0 ? 3 : (kc == 1 ? 5 : 7));
+      if (kc + 1 < 3) load_step(kc + 1, A[(kc + 1) & 1], B[(kc + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(A[kc & 1][ct], B[kc & 1][t], acc[ct][t]);
+      bf16x8 aw = A[kc & 1][0];
+      if (wave == 1) aw = A[kc & 1][1];
+      if (wave == 2) aw = A[kc & 1][2];
+      if (wave == 3) aw = A[kc & 1][3];
+      bacc = mfma16(aw, ones, bacc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // pair j+1 must have landed; pairs j+2 .. min(j+PF, np-1) may stay in flight
+    const int later = min(j + PF, np - 1) - (j + 1);
+    if (wave_s < 2) {
+      if (later >= 2) wait_vm<14>(); else if (later == 1) wait_vm<7>(); else wait_vm<0>();
+    } else {
+      if (later >= 2) wait_vm<12>(); else if (later == 1) wait_vm<6>(); else wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  float* slab = p.slab + (size_t)chunk * Cout * 576;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int j = 9 * wave + t, tap = j >> 2, it = j & 3;
+    const int ci = it * 16 + (lane & 15);
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int co = cb * 64 + ct * 16 + 4 * (lane >> 4);
+      *reinterpret_cast<float4*>(slab + ((size_t)tap * 64 + ci) * Cout + co) =
+          make_float4(acc[ct][t][0], acc[ct][t][1], acc[ct][t][2], acc[ct][t][3]);
+    }
+  }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      p.bslab[(size_t)chunk * Cout + cb * 64 + wave * 16 + 4 * (lane >> 4) + r] = bacc[r];
+  }
+  WSTAMP(63);
+}
+
 int wgrad3x3_nslabs(const WgradParams& p) { return p.N * p.row_splits; }
 
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
@@ -201,7 +396,13 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
   dim3 grid(wgrad3x3_nslabs(p), p.Cout / 64);
   WgradParams q = p;
   q.stamps = g_wg_stamps;
-  if (p.W % 48 == 0) {
+  static const int dbg = getenv("SRMI_WGRAD_DBG") ? atoi(getenv("SRMI_WGRAD_DBG")) : 0;
+  q.dbg = dbg;
+  // v4 (row-pair rings) is opt-in until it beats v3 (tools/kbench.py)
+  static const bool use_v4 = getenv("SRMI_WGRAD_V4") && atoi(getenv("SRMI_WGRAD_V4"));
+  if (use_v4 && p.W == 48 && (p.H / p.row_splits) % 2 == 0) {
+    hipLaunchKernelGGL(wgrad48_kernel, grid, dim3(256), v4::LDS, st, q);
+  } else if (p.W % 48 == 0) {
     hipLaunchKernelGGL(wgrad3x3_kernel<48>, grid, dim3(256), Wg3<48>::TOTAL, st, q);
   } else if (p.W % 32 == 0) {
     hipLaunchKernelGGL(wgrad3x3_kernel<32>, grid, dim3(256), Wg3<32>::TOTAL, st, q);

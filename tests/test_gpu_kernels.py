@@ -156,7 +156,8 @@ def test_conv_dgrad_unshuffle(N, H, W):
 
 
 @pytest.mark.parametrize("N,H,W,rs", [(2, 48, 48, 0), (2, 48, 48, 1), (1, 8, 96, 0), (1, 4, 32, 0), (3, 12, 64, 3),
-                                       (64, 48, 48, 0), (4, 96, 96, 0)])
+                                       (64, 48, 48, 0), (4, 96, 96, 0), (3, 12, 48, 3), (2, 48, 48, 12), (1, 8, 48, 2),
+                                       (2, 24, 48, 2)])
 def test_wgrad(N, H, W, rs):
     d = dev()
     g = torch.Generator(device="cpu").manual_seed(5)
@@ -224,12 +225,12 @@ def test_channel_attention_fwd_bwd():
     bpart[:, 0, :Cc] = gy.sum((1, 2))
     bpart[:, 0, Cc:] = (gy * u.float()).sum((1, 2))
     du = torch.empty(N, H, W, Cc, dtype=torch.bfloat16, device=d)
-    brec = torch.empty(N, 160, device=d)
+    brec = torch.empty(N * 224, device=d)  # [N][160] then dm[N][64]
     call("srmi_ca_backward", ptr(gy), ptr(bpart), ns, ptr(rec), ptr(w1), ptr(w2), N, H * W, Cc, R, ptr(du), ptr(brec),
          S())
     assert rel_l2(du.float(), U.grad) < 4e-3
     # conv2-bias grad path: sum_p du = s*G + dm
-    np.testing.assert_allclose(brec[:, 96:].double().cpu().numpy(), U.grad.sum((1, 2)).numpy(), rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(brec[:N * 160].view(N, 160)[:, 96:].double().cpu().numpy(), U.grad.sum((1, 2)).numpy(), rtol=1e-4, atol=1e-3)
 
 
 def test_downsample_upsample_match_reference():

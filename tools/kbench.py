@@ -89,7 +89,7 @@ def main():
     w2 = torch.randn(64, 32, device=d) * 0.1
     b2 = torch.zeros(64, device=d)
     rec = torch.zeros(N, 160, device=d)
-    brec = torch.zeros(N, 160, device=d)
+    brec = torch.zeros(N * 224, device=d)
     pool = torch.zeros(N, ns, 64, device=d)
 
     def caf():
