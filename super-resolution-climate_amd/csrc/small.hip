@@ -545,32 +545,56 @@ int loss_finalize_launch(float* loss, hipStream_t st) {
 // The per-image MLP runs once per image in its own tiny kernel (one wave per
 // image) and the elementwise pass streams with no per-block preamble.
 // rec per image: m[C] | z1[CR] | s[C]   (C = 64, CR = C / R)
-__global__ void __launch_bounds__(64) ca_fwd_mlp_kernel(const float* __restrict__ part, int nstrips, int HW,
-                                                        const float* __restrict__ w1, const float* __restrict__ b1,
-                                                        const float* __restrict__ w2, const float* __restrict__ b2,
-                                                        int C, int CR, float* __restrict__ rec) {
-  __shared__ float sm[64 + 32];
+// Per-image MLP, one 256-thread block per image: the weights are staged in LDS
+// with coalesced loads and every dot product is split over 8 (4) lanes and
+// finished with a fixed-order butterfly, so no thread walks a long dependent chain.
+__global__ void __launch_bounds__(256) ca_fwd_mlp_kernel(const float* __restrict__ part, int nstrips, int HW,
+                                                         const float* __restrict__ w1, const float* __restrict__ b1,
+                                                         const float* __restrict__ w2, const float* __restrict__ b2,
+                                                         int C, int CR, float* __restrict__ rec) {
+  __shared__ float W1[32 * 64], W2[64 * 32], red[4][64], m[64], z1[32];
   const int n = blockIdx.x, tid = threadIdx.x;
+  for (int i = tid; i < CR * C; i += 256) {
+    W1[i] = w1[i];
+    W2[i] = w2[i];
+  }
+  {
+    const int c = tid & 63, q = tid >> 6;
+    float a = 0.f;
+    for (int k = q; k < nstrips; k += 4) a += part[((size_t)n * nstrips + k) * C + c];
+    red[q][c] = a;
+  }
+  __syncthreads();
   float* r = rec + (size_t)n * (2 * C + CR);
-  float m = 0.f;
   if (tid < C) {
-    for (int k = 0; k < nstrips; ++k) m += part[((size_t)n * nstrips + k) * C + tid];
-    m /= (float)HW;
-    sm[tid] = m;
-    r[tid] = m;
+    const float v = (red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]) / (float)HW;
+    m[tid] = v;
+    r[tid] = v;
   }
   __syncthreads();
-  if (tid < CR) {
-    float z = b1[tid];
-    for (int c = 0; c < C; ++c) z += w1[tid * C + c] * sm[c];
-    sm[64 + tid] = z;
-    r[C + tid] = z;
+  {  // z1[j] = b1[j] + sum_c W1[j][c] m[c]: lane group of 8 per j (CR = 32)
+    const int j = tid >> 3, pp = tid & 7;
+    float a = 0.f;
+    if (j < CR)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a += W1[j * C + pp * 8 + i] * m[pp * 8 + i];
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    a += __shfl_xor(a, 4, 64);
+    if (j < CR && pp == 0) {
+      z1[j] = a + b1[j];
+      r[C + j] = a + b1[j];
+    }
   }
   __syncthreads();
-  if (tid < C) {
-    float z = b2[tid];
-    for (int j = 0; j < CR; ++j) z += w2[tid * CR + j] * fmaxf(sm[64 + j], 0.f);
-    r[C + CR + tid] = 1.f / (1.f + expf(-z));
+  {  // s[c] = sigmoid(b2[c] + sum_j W2[c][j] relu(z1[j])): 4 lanes per c
+    const int c = tid >> 2, pp = tid & 3;
+    float a = 0.f;
+    const int per = CR / 4;
+    for (int i = 0; i < per; ++i) a += W2[c * CR + pp * per + i] * fmaxf(z1[pp * per + i], 0.f);
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    if (pp == 0) r[C + CR + c] = 1.f / (1.f + expf(-(a + b2[c])));
   }
 }
 
@@ -632,8 +656,8 @@ static int ca_grid_x(int HW, int C) {
 int ca_fwd_launch(const bf16_t* u, const float* part, int nstrips, const float* w1, const float* b1, const float* w2,
                   const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, bf16_t* hb_out,
                   float* rec, hipStream_t st) {
-  if (C != 64 || C % R || (HW * C) % 8) return SRMI_ERR_SHAPE;
-  hipLaunchKernelGGL(ca_fwd_mlp_kernel, dim3(N), dim3(64), 0, st, part, nstrips, HW, w1, b1, w2, b2, C, C / R, rec);
+  if (C != 64 || C % R || (C / R) > 32 || (C / R) % 4 || (HW * C) % 8) return SRMI_ERR_SHAPE;
+  hipLaunchKernelGGL(ca_fwd_mlp_kernel, dim3(N), dim3(256), 0, st, part, nstrips, HW, w1, b1, w2, b2, C, C / R, rec);
   hipLaunchKernelGGL(ca_fwd_kernel, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, u, HW, C, C / R, h_in, h_out,
                      hb_out, rec);
   SRMI_CHECK_LAUNCH();
@@ -644,40 +668,62 @@ int ca_fwd_launch(const bf16_t* u, const float* part, int nstrips, const float* 
 // sum_p g*u (C..2C-1) from the producer of g.
 // brec per image: dz2[C] dz1[CR] dbconv2[C]; followed (after all N images) by
 // dm[N][C] = W1^T dz1 (the gradient of the pooled mean).
-__global__ void __launch_bounds__(64) ca_bwd_mlp_kernel(const float* __restrict__ part, int nstrips,
-                                                        const float* __restrict__ rec, const float* __restrict__ w1,
-                                                        const float* __restrict__ w2, int N, int C, int CR,
-                                                        float* __restrict__ brec) {
-  __shared__ float dz2[64], dz1[32];
+__global__ void __launch_bounds__(256) ca_bwd_mlp_kernel(const float* __restrict__ part, int nstrips,
+                                                         const float* __restrict__ rec, const float* __restrict__ w1,
+                                                         const float* __restrict__ w2, int N, int C, int CR,
+                                                         float* __restrict__ brec) {
+  __shared__ float W1[32 * 64], W2[64 * 32], red[4][128], dz2[64], dz1[32];
   const int n = blockIdx.x, tid = threadIdx.x;
   const float* r = rec + (size_t)n * (2 * C + CR);
   float* br = brec + (size_t)n * (2 * C + CR);
+  for (int i = tid; i < CR * C; i += 256) {
+    W1[i] = w1[i];
+    W2[i] = w2[i];
+  }
+  {  // G[c] = sum_p g, ds[c] = sum_p g*u  (part[n][strip][2C])
+    const int c2 = tid & 127, q = tid >> 7;
+    float a = 0.f;
+    for (int k = q; k < nstrips; k += 2) a += part[((size_t)n * nstrips + k) * (2 * C) + c2];
+    red[q][c2] = a;
+  }
+  __syncthreads();
   float G = 0.f;
   if (tid < C) {
-    float b = 0.f;
-    for (int k = 0; k < nstrips; ++k) {
-      const float* pp = part + ((size_t)n * nstrips + k) * (2 * C);
-      G += pp[tid];
-      b += pp[C + tid];
-    }
+    G = red[0][tid] + red[1][tid];
+    const float ds = red[0][C + tid] + red[1][C + tid];
     const float s = r[C + CR + tid];
-    dz2[tid] = b * s * (1.f - s);
+    dz2[tid] = ds * s * (1.f - s);
     br[tid] = dz2[tid];
   }
   __syncthreads();
-  if (tid < CR) {
+  {  // dz1[j] = relu'(z1[j]) sum_c W2[c][j] dz2[c]: 8 lanes per j
+    const int j = tid >> 3, pp = tid & 7;
     float a = 0.f;
-    for (int c = 0; c < C; ++c) a += w2[c * CR + tid] * dz2[c];
-    dz1[tid] = (r[C + tid] > 0.f) ? a : 0.f;
-    br[C + tid] = dz1[tid];
+    if (j < CR)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a += W2[(pp * 8 + i) * CR + j] * dz2[pp * 8 + i];
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    a += __shfl_xor(a, 4, 64);
+    if (j < CR && pp == 0) {
+      const float v = (r[C + j] > 0.f) ? a : 0.f;
+      dz1[j] = v;
+      br[C + j] = v;
+    }
   }
   __syncthreads();
-  if (tid < C) {
+  {  // dm[c] = sum_j W1[j][c] dz1[j]: 4 lanes per c
+    const int c = tid >> 2, pp = tid & 3;
+    const int per = CR / 4;
     float a = 0.f;
-    for (int j = 0; j < CR; ++j) a += w1[j * C + tid] * dz1[j];
-    br[C + CR + tid] = r[C + CR + tid] * G + a;  // conv2 bias grad: sum_p du
-    brec[(size_t)N * (2 * C + CR) + (size_t)n * C + tid] = a;
+    for (int i = 0; i < per; ++i) a += W1[(pp * per + i) * C + c] * dz1[pp * per + i];
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    if (pp == 0) brec[(size_t)N * (2 * C + CR) + (size_t)n * C + c] = a;
+    if (pp == 0) red[2][c] = a;
   }
+  __syncthreads();
+  if (tid < C) br[C + CR + tid] = r[C + CR + tid] * G + red[2][tid];  // conv2 bias grad: sum_p du
 }
 
 // du = g * s + dm / HW  (bf16)
@@ -719,8 +765,8 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
 
 int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
                      const float* w2, int N, int HW, int C, int R, bf16_t* du, float* brec, hipStream_t st) {
-  if (C != 64 || C % R || (HW * C) % 8) return SRMI_ERR_SHAPE;
-  hipLaunchKernelGGL(ca_bwd_mlp_kernel, dim3(N), dim3(64), 0, st, part, nstrips, rec, w1, w2, N, C, C / R, brec);
+  if (C != 64 || C % R || (C / R) > 32 || (C / R) % 4 || (HW * C) % 8) return SRMI_ERR_SHAPE;
+  hipLaunchKernelGGL(ca_bwd_mlp_kernel, dim3(N), dim3(256), 0, st, part, nstrips, rec, w1, w2, N, C, C / R, brec);
   hipLaunchKernelGGL(ca_bwd_du_kernel, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, g, rec, brec, N, HW, C, C / R,
                      du);
   SRMI_CHECK_LAUNCH();

@@ -414,49 +414,79 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
 }
 
 // -------------------------------------------------------------------- reduce
-// one block = 64 consecutive outputs x 4 slab lanes; fixed summation order
+// block = 64 output quads (256 consecutive outputs, float4 loads) x 4 slab phases;
+// phase q sums slabs q, q+4, ... with 4 independent accumulators, then the
+// 4 x 4 partials are added in a fixed order (deterministic).  The bias slab
+// ([nslab][Cout]) is handled by the last block(s) the same way.
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab,
                                                            const float* __restrict__ bslab, int nslab, int Cout,
                                                            int ps, float alpha, float* __restrict__ gw,
                                                            float* __restrict__ gb) {
-  __shared__ float red[4][64];
+  __shared__ float4 red[4][64];
   const int per = Cout * 576;
-  const int o = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int q = threadIdx.x >> 6;
-  const bool is_w = o < per;
-  const bool is_b = !is_w && gb && o < per + Cout;
-  float s0 = 0.f, s1 = 0.f;
+  const int nwb = per / 256;  // weight blocks (per % 256 == 0 since Cout % 64 == 0)
+  const int qd = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const bool is_w = (int)blockIdx.x < nwb;
+  const float* src;
+  int stride, o4, valid;
   if (is_w) {
-    int k = q;
-    for (; k + 4 < nslab; k += 8) {
-      s0 += slab[(size_t)k * per + o];
-      s1 += slab[(size_t)(k + 4) * per + o];
-    }
-    if (k < nslab) s0 += slab[(size_t)k * per + o];
-  } else if (is_b) {
-    for (int k = q; k < nslab; k += 4) s0 += bslab[(size_t)k * Cout + (o - per)];
+    if (!gw) return;
+    o4 = blockIdx.x * 256 + qd * 4;
+    src = slab + o4;
+    stride = per;
+    valid = 1;
+  } else {
+    if (!gb) return;
+    o4 = (blockIdx.x - nwb) * 256 + qd * 4;
+    src = bslab + o4;
+    stride = Cout;
+    valid = o4 < Cout;
   }
-  red[q][threadIdx.x & 63] = s0 + s1;
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0, a3 = a0;
+  if (valid) {
+    int k = ph;
+    for (; k + 12 < nslab; k += 16) {
+      const float4 v0 = *reinterpret_cast<const float4*>(src + (size_t)k * stride);
+      const float4 v1 = *reinterpret_cast<const float4*>(src + (size_t)(k + 4) * stride);
+      const float4 v2 = *reinterpret_cast<const float4*>(src + (size_t)(k + 8) * stride);
+      const float4 v3 = *reinterpret_cast<const float4*>(src + (size_t)(k + 12) * stride);
+      a0.x += v0.x; a0.y += v0.y; a0.z += v0.z; a0.w += v0.w;
+      a1.x += v1.x; a1.y += v1.y; a1.z += v1.z; a1.w += v1.w;
+      a2.x += v2.x; a2.y += v2.y; a2.z += v2.z; a2.w += v2.w;
+      a3.x += v3.x; a3.y += v3.y; a3.z += v3.z; a3.w += v3.w;
+    }
+    for (; k < nslab; k += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(src + (size_t)k * stride);
+      a0.x += v.x; a0.y += v.y; a0.z += v.z; a0.w += v.w;
+    }
+  }
+  red[ph][qd] = make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
+                            (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w));
   __syncthreads();
-  if (q == 0 && (is_w || is_b)) {
-    const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+  if (ph != 0 || !valid) return;
+  const float4 r0 = red[0][qd], r1 = red[1][qd], r2 = red[2][qd], r3 = red[3][qd];
+  const float s4[4] = {((r0.x + r1.x) + r2.x) + r3.x, ((r0.y + r1.y) + r2.y) + r3.y, ((r0.z + r1.z) + r2.z) + r3.z,
+                       ((r0.w + r1.w) + r2.w) + r3.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int o = o4 + e;
     if (is_w) {
       const int cop = o % Cout, ci = (o / Cout) & 63, tap = o / (Cout * 64);
       const int cot = ps ? (4 * (cop & 63) + (cop >> 6)) : cop;
-      gw[((size_t)cot * 64 + ci) * 9 + tap] = alpha * s;
-    } else {
-      const int cop = o - per;
-      const int cot = ps ? (4 * (cop & 63) + (cop >> 6)) : cop;
-      gb[cot] = alpha * s;
+      gw[((size_t)cot * 64 + ci) * 9 + tap] = alpha * s4[e];
+    } else if (o < Cout) {
+      const int cot = ps ? (4 * (o & 63) + (o >> 6)) : o;
+      gb[cot] = alpha * s4[e];
     }
   }
 }
 
 int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, float alpha, float* gw,
                         float* gb, hipStream_t st) {
-  const int total = Cout * 576 + Cout;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 63) / 64), dim3(256), 0, st, slab, bslab, nslab, Cout, ps,
-                     alpha, gw, gb);
+  if (Cout % 64) return SRMI_ERR_SHAPE;
+  const int blocks = Cout * 576 / 256 + (Cout + 255) / 256;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, bslab, nslab, Cout, ps, alpha, gw,
+                     gb);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
