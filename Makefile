@@ -24,10 +24,28 @@ $(OBJDIR)/%.o: $(SRC)/%.cpp $(HDRS)
 $(OUT): $(OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(OBJS) -o $@
 
+# diagnostic build with s_memtime phase stamps (tools/kbench.py KBENCH_STAMPS=1)
+STAMPOBJDIR := build/obj_stamps
+STAMPOUT := $(PKG)/srmi/libsrmi_stamps.so
+STAMPOBJS := $(patsubst $(SRC)/%.hip,$(STAMPOBJDIR)/%.o,$(HIPSRC)) $(patsubst $(SRC)/%.cpp,$(STAMPOBJDIR)/%.o,$(CPPSRC))
+
+$(STAMPOBJDIR)/%.o: $(SRC)/%.hip $(HDRS)
+	@mkdir -p $(STAMPOBJDIR)
+	$(HIPCC) $(CXXFLAGS) -DSRMI_STAMPS -c $< -o $@
+
+$(STAMPOBJDIR)/%.o: $(SRC)/%.cpp $(HDRS)
+	@mkdir -p $(STAMPOBJDIR)
+	$(HIPCC) $(CXXFLAGS) -DSRMI_STAMPS -c $< -o $@
+
+$(STAMPOUT): $(STAMPOBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(STAMPOBJS) -o $@
+
+stamps: $(STAMPOUT)
+
 oracle:
 	@true
 
 clean:
-	rm -rf build $(OUT)
+	rm -rf build $(OUT) $(STAMPOUT)
 
-.PHONY: all clean oracle
+.PHONY: all clean oracle stamps

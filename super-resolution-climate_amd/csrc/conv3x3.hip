@@ -25,15 +25,23 @@
 namespace srmi {
 
 // zero bytes in global memory: the LDS-DMA source for padding pixels
-static __device__ uint4 kZeros[4];
+static __device__ uint4 kZeros[64];  // 1 KiB zero page (padding source, absent bias)
 
 static unsigned long long* g_debug_stamps = nullptr;
 void conv3x3_set_debug_stamps(unsigned long long* buf) { g_debug_stamps = buf; }
 
+// Phase stamps exist only in the diagnostic build (make stamps): even a disabled
+// stamp store makes the compiler drain vmcnt where its data registers are reused.
+#ifdef SRMI_STAMPS
 #define STAMP(i)                                                                     \
   do {                                                                               \
     if (p.stamps && tid == 0) p.stamps[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
 
 constexpr int kTH = 4;
 constexpr int kThreads = 256;
@@ -75,7 +83,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[
                                               int strip, int nstrips, float* red, int fr, int fk, int wave, int tid) {
   const int HW = p.H * p.W;
   constexpr bool kPart1 = (EPI == EPI_POOL_BF16);
-  constexpr bool kPart2 = (EPI == EPI_DG_ACC);
+  constexpr bool kPart2 = (EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_CA);
   float ps0[4][4], ps1[4][4];  // per (ct, r) partial sums over this lane's pixels
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
@@ -308,7 +316,7 @@ struct EpiPre {
 template <int NPT, int EPI>
 __device__ __forceinline__ void epi_prefetch(const ConvParams& p, EpiPre<NPT, EPI>& e, int n, int cb, int y, int x0,
                                              int fr, int fk) {
-  if constexpr (EPI == EPI_RESID || EPI == EPI_DG_ACC || EPI == EPI_DG_RELUMASK) {
+  if constexpr (EPI == EPI_RESID || EPI == EPI_DG_ACC || EPI == EPI_DG_RELUMASK || EPI == EPI_DG_ACC_CA) {
     const size_t HW = (size_t)p.H * p.W;
 #pragma unroll
     for (int pt = 0; pt < NPT; ++pt) {
@@ -322,6 +330,10 @@ __device__ __forceinline__ void epi_prefetch(const ConvParams& p, EpiPre<NPT, EP
           e.aux[pt][ct] = p.part ? *reinterpret_cast<const uint2*>(p.aux + o) : make_uint2(0, 0);
         }
         if constexpr (EPI == EPI_DG_RELUMASK) e.aux[pt][ct] = *reinterpret_cast<const uint2*>(p.aux + o);
+        if constexpr (EPI == EPI_DG_ACC_CA) {
+          e.r1[pt][ct] = *reinterpret_cast<const float4*>(p.r1 + o);
+          e.aux[pt][ct] = *reinterpret_cast<const uint2*>(p.aux + o);
+        }
       }
     }
   }
@@ -338,7 +350,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
                                                int nstrips, float* red, int fr, int fk, int wave, int tid) {
   const size_t HW = (size_t)p.H * p.W;
   constexpr bool kPart1 = (EPI == EPI_POOL_BF16);
-  constexpr bool kPart2 = (EPI == EPI_DG_ACC);
+  constexpr bool kPart2 = (EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_CA);
   float ps0[4][4], ps1[4][4];
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
@@ -396,6 +408,18 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
           ps1[ct][3] += v[3] * bf2f(uu.y >> 16);
         }
       }
+      if constexpr (EPI == EPI_DG_ACC_CA) {
+        const float4 rr = e.r1[pt][ct];
+        v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
+        *reinterpret_cast<float4*>(p.yf + o) = make_float4(v[0], v[1], v[2], v[3]);
+        const uint2 uu = e.aux[pt][ct];
+        ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
+        ps1[ct][0] += v[0] * bf2f(uu.x & 0xFFFFu);
+        ps1[ct][1] += v[1] * bf2f(uu.x >> 16);
+        ps1[ct][2] += v[2] * bf2f(uu.y & 0xFFFFu);
+        ps1[ct][3] += v[3] * bf2f(uu.y >> 16);
+        continue;  // no bf16 copy
+      }
       if constexpr (kPart1) {
         ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
       }
@@ -410,7 +434,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
     }
   }
   if constexpr (kPart1 || kPart2) {
-    const bool on = !kPart2 || p.part;
+    const bool on = EPI != EPI_DG_ACC || p.part;
     if (on) {
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct)
@@ -425,7 +449,9 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
           }
         }
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // red[] writes visible; global stores may stay in flight
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     if (on) {
       if (tid < 64) {
         const float sum = red[tid] + red[128 + tid] + red[256 + tid] + red[384 + tid];
@@ -463,108 +489,46 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
   const int x0 = sx * TW;
   STAMP(0);
 
-  // per-lane descriptors of this thread's 16-B chunks of a 4-row group (group
-  // independent): element offset within the group's first row, row, x validity
-  int goff[S::GPT], grow[S::GPT];
-  bool gok[S::GPT];
-#pragma unroll
-  for (int j = 0; j < S::GPT; ++j) {
-    const int i = tid + j * kThreads;
-    const int q = i >> 3, c = i & 7;
-    const int rr = q / (TW + 2), hx = q - rr * (TW + 2);
-    const int xx = x0 - 1 + hx;
-    grow[j] = rr;
-    gok[j] = (i < S::GCH) && xx >= 0 && xx < p.W;
-    goff[j] = (rr * p.W + xx) * 64 + c * 8;
-  }
   const bf16_t* xn = p.x + (size_t)n * p.H * p.W * 64;
-  auto group_load = [&](int gidx, uint4* stg) {
-    const bf16_t* grow0 = xn + (ptrdiff_t)(4 * gidx - 3) * p.W * 64;
-#pragma unroll
-    for (int j = 0; j < S::GPT; ++j) {
-      const int y = 4 * gidx - 3 + grow[j];
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (gok[j] && y >= 0 && y < p.H) v = *reinterpret_cast<const uint4*>(grow0 + goff[j]);
-      stg[j] = v;
-    }
-  };
-  auto group_store = [&](int gidx, const uint4* stg) {
-    const int qbase = (gidx % 3) * 4 * (TW + 2);  // ring-global pixel index (the swizzle depends on it)
-#pragma unroll
-    for (int j = 0; j < S::GPT; ++j) {
-      const int i = tid + j * kThreads;
-      if (i < S::GCH) {
-        const int q = i >> 3, c = i & 7;
-        *reinterpret_cast<uint4*>(ring + swz128(qbase + q, c)) = stg[j];
-      }
+
+  // LDS-DMA of one 4-row input group into its ring slot: one wave instruction per
+  // 8 pixels (1 KiB), swizzle applied on the source side, halo lanes read the zero
+  // page.  No registers hold in-flight data, so no compiler-inserted vmcnt waits.
+  const int wv_s = __builtin_amdgcn_readfirstlane(wave);
+  const uint32_t rbase = lds_u32(ring);
+  auto group_dma = [&](int gidx) __attribute__((always_inline)) {
+    constexpr int NG = S::GROUPB / 1024;
+    const int qbase = (gidx % 3) * 4 * (TW + 2);
+    for (int i = wv_s; i < NG; i += 4) {
+      const int q = 8 * i + (lane >> 3);
+      const int Q = qbase + q;
+      const int c = (lane & 7) ^ ((Q >> 1) & 7);
+      const int rr = q / (TW + 2), hx = q - rr * (TW + 2);
+      const int y = 4 * gidx - 3 + rr, xx = x0 - 1 + hx;
+      const bool ok = y >= 0 && y < p.H && xx >= 0 && xx < p.W;
+      const void* src = ok ? (const void*)(xn + ((size_t)y * p.W + xx) * 64 + c * 8) : (const void*)kZeros;
+      glds16(src, rbase + (uint32_t)qbase * 128u + (uint32_t)i * 1024u);
     }
   };
 
-  // prologue: filters (all 9 taps, 72 KiB) + input groups k0, k0+1, everything in
-  // flight before the first wait.  PM selects the path: 0 = all LDS-DMA
-  // (global_load_lds_dwordx4, swizzle on the source), 1 = all register staged,
-  // 2 = filters by DMA + input groups register staged.
+  // prologue: filters (all 9 taps, 72 KiB) and input groups k0, k0+1, all by LDS-DMA
+  // (swizzle on the source side), everything in flight before the one wait.
   {
-    const int wv = __builtin_amdgcn_readfirstlane(wave);
-    if constexpr (PM == 0 || PM == 2) {
-      const uint32_t wbase = lds_u32(wl);
-      for (int i = wv; i < 72; i += 4) {
-        const int tap = i >> 3, row = 8 * (i & 7) + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
-        glds16(p.w + ((size_t)(tap * p.Cout + cb * 64 + row)) * 64 + c * 8,
-               (uint32_t)__builtin_amdgcn_readfirstlane(wbase + i * 1024));
-      }
+    const uint32_t wbase = lds_u32(wl);
+    for (int i = wv_s; i < 72; i += 4) {
+      const int tap = i >> 3, row = 8 * (i & 7) + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+      glds16(p.w + ((size_t)(tap * p.Cout + cb * 64 + row)) * 64 + c * 8, wbase + (uint32_t)i * 1024u);
     }
-    if constexpr (PM == 0) {
-      constexpr int NG = S::GROUPB / 1024;
-      static_assert(S::GROUPB % 1024 == 0, "group region must be whole 1 KiB DMA pieces");
-      const uint32_t rbase = lds_u32(ring);
-#pragma unroll
-      for (int gi = 0; gi < 2; ++gi) {
-        const int gidx = k0 + gi;
-        const int qbase = (gidx % 3) * 4 * (TW + 2);
-        for (int i = wv; i < NG; i += 4) {
-          const int q = 8 * i + (lane >> 3);
-          const int Q = qbase + q;
-          const int c = (lane & 7) ^ ((Q >> 1) & 7);
-          const int rr = q / (TW + 2), hx = q - rr * (TW + 2);
-          const int y = 4 * gidx - 3 + rr, xx = x0 - 1 + hx;
-          const void* src = kZeros;
-          if (y >= 0 && y < p.H && xx >= 0 && xx < p.W)
-            src = p.x + ((size_t)((size_t)n * p.H + y) * p.W + xx) * 64 + c * 8;
-          glds16(src, (uint32_t)__builtin_amdgcn_readfirstlane(rbase + (uint32_t)qbase * 128 + i * 1024));
-        }
-      }
-    }
-    if constexpr (PM == 1) {
-      constexpr int WPT = 9 * 512 / kThreads;  // 18 x 16 B per thread
-      uint4 wst[WPT];
-#pragma unroll
-      for (int j = 0; j < WPT; ++j) {
-        const int i = tid + j * kThreads;
-        const int tap = i >> 9, rem = i & 511, row = rem >> 3, c = rem & 7;
-        wst[j] = *reinterpret_cast<const uint4*>(p.w + ((size_t)tap * p.Cout + cb * 64 + row) * 64 + c * 8);
-      }
-#pragma unroll
-      for (int j = 0; j < WPT; ++j) {
-        const int i = tid + j * kThreads;
-        const int tap = i >> 9, rem = i & 511, row = rem >> 3, c = rem & 7;
-        *reinterpret_cast<uint4*>(wl + tap * 8192 + swz128(row, c)) = wst[j];
-      }
-    }
-    if constexpr (PM == 1 || PM == 2) {
-      uint4 g0[S::GPT], g1[S::GPT];
-      group_load(k0, g0);
-      group_load(k0 + 1, g1);
-      group_store(k0, g0);
-      group_store(k0 + 1, g1);
-    }
-    if constexpr (PM == 0 || PM == 2) wait_vm<0>();
+    group_dma(k0);
+    group_dma(k0 + 1);  // strip k0 reads groups k0 and k0+1
+    wait_vm<0>();
   }
   float4 bias[4];
+  {
+    const float* bp = p.bias ? p.bias : reinterpret_cast<const float*>(kZeros);  // pointer select, no branch
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct)
-    bias[ct] = p.bias ? *reinterpret_cast<const float4*>(p.bias + cb * 64 + ct * 16 + fk * 4)
-                      : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int ct = 0; ct < 4; ++ct) bias[ct] = *reinterpret_cast<const float4*>(bp + cb * 64 + ct * 16 + fk * 4);
+  }
   // lane-constant A-fragment byte offsets (tap adds 8192)
   uint32_t aoff[2][4];
 #pragma unroll
@@ -576,12 +540,13 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
 #pragma unroll 1
   for (int k = k0; k < k1; ++k) {
     const int y = 4 * k + wave;
-    uint4 stg[S::GPT];
     const bool pf = (k + 1 < k1);
-    if (pf) group_load(k + 2, stg);
+    // group k+2 -> ring slot (k+2)%3, which held group k-1 (last read by strip k-1,
+    // released by the barrier that ended it)
+    if (pf) group_dma(k + 2);
     EpiPre<NPT, EPI> ep;
     epi_prefetch<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk);
-    const int sj = 2 + 5 * min(k - k0, 11);
+    [[maybe_unused]] const int sj = 2 + 5 * min(k - k0, 11);
     STAMP(sj);
 
     // B-fragment byte offsets per (ky, kx, kk); +2048 per 16-pixel tile
@@ -605,7 +570,7 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
     // 18 K-steps (9 taps x 2 halves of 32 ci), fragments double-buffered in
     // registers: step s+1's ds_reads are in flight while step s's 12 MFMAs run.
     bf16x8 A[2][4], B[2][NPT];
-    auto load_step = [&](int s, bf16x8 (&a)[4], bf16x8 (&b)[NPT]) {
+    auto load_step = [&](int s, bf16x8 (&a)[4], bf16x8 (&b)[NPT]) __attribute__((always_inline)) {
       const int tap = s >> 1, kk = s & 1, ky = tap / 3, kx = tap % 3;
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) a[ct] = lds_frag(wl, tap * 8192 + aoff[kk][ct]);
@@ -623,12 +588,18 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
         for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = mfma16(A[s & 1][ct], B[s & 1][pt], acc[pt][ct]);
       __builtin_amdgcn_sched_barrier(0);
     }
+    // group k+2's DMA, the epilogue operands and the previous strip's stores had the
+    // whole MFMA phase to land: drain them here, before the epilogue (the barrier at
+    // the end of the strip then publishes group k+2 to every wave)
+    wait_vm<0>();
     STAMP(sj + 1);
-    if (pf) group_store(k + 2, stg);
     STAMP(sj + 2);
     conv_epilogue2<NPT, EPI>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx, nsy * nsx, red, fr, fk, wave, tid);
     STAMP(sj + 3);
-    __syncthreads();
+    // LDS-only barrier: this strip's global stores stay in flight into the next strip
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     STAMP(sj + 4);
   }
 }
@@ -646,19 +617,12 @@ static int launch_tw(const ConvParams& p, hipStream_t st) {
     dim3 grid(units * runs);
     ConvParams q = p;
     q.stamps = g_debug_stamps;
-    static const int pm = [] {
-      const char* e = getenv("SRMI_CONV_PM");
-      return e ? atoi(e) : 2;
-    }();
-    if (pm == 1)
-      hipLaunchKernelGGL((conv64_kernel<TW, EPI, 1>), grid, dim3(kThreads), Conv2Smem<TW>::TOTAL, st, q, run_len);
-    else if (pm == 2)
-      hipLaunchKernelGGL((conv64_kernel<TW, EPI, 2>), grid, dim3(kThreads), Conv2Smem<TW>::TOTAL, st, q, run_len);
-    else
-      hipLaunchKernelGGL((conv64_kernel<TW, EPI, 0>), grid, dim3(kThreads), Conv2Smem<TW>::TOTAL, st, q, run_len);
+    // prologue mode 2 (filters by LDS-DMA, input groups register-staged) measured fastest
+    hipLaunchKernelGGL((conv64_kernel<TW, EPI, 2>), grid, dim3(kThreads), Conv2Smem<TW>::TOTAL, st, q, run_len);
   } else {
+    constexpr int E1 = EPI == EPI_DG_ACC_CA ? EPI_DG_ACC : EPI;  // v1 handles the general form
     dim3 grid((p.H / kTH) * (p.W / TW), p.Cout / 64, p.N);
-    hipLaunchKernelGGL((conv3x3_kernel<TW, EPI>), grid, dim3(kThreads), ConvSmem<TW>::TOTAL, st, p);
+    hipLaunchKernelGGL((conv3x3_kernel<TW, E1>), grid, dim3(kThreads), ConvSmem<TW>::TOTAL, st, p);
   }
   SRMI_CHECK_LAUNCH();
   return 0;
@@ -689,6 +653,9 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
     case EPI_DG_RELUMASK: return launch_epi<EPI_DG_RELUMASK>(p, st);
     case EPI_DG_ACC: return launch_epi<EPI_DG_ACC>(p, st);
     case EPI_PLAIN_BF16: return launch_epi<EPI_PLAIN_BF16>(p, st);
+    case EPI_DG_ACC_CA:
+      if (!p.r1 || !p.aux || !p.part || p.yb || p.r2 || p.r3 || !p.yf) return SRMI_ERR_ARG;
+      return launch_epi<EPI_DG_ACC_CA>(p, st);
     default: return SRMI_ERR_ARG;
   }
 }

@@ -374,6 +374,8 @@ static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n,
   p.part_stride = 128;
   p.alpha = alpha;
   p.zeros = e->zeros;
+  if (epi == EPI_DG_ACC && r1 && aux && part && !yb && !r2 && !r3 && yf && c.cout == 64 && !c.ps)
+    epi = EPI_DG_ACC_CA;  // the hot RCAB case: specialised epilogue without runtime operand checks
   return conv3x3_launch(p, epi, st);
 }
 

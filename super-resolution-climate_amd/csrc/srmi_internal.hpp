@@ -20,6 +20,8 @@ enum Epi {
   EPI_DG_RELUMASK = 4, // dz = acc * (aux > 0)                      -> bf16
   EPI_DG_ACC = 5,      // g = acc + r1 + r2 + r3 (+ sums of g, g*aux) -> fp32 + bf16
   EPI_PLAIN_BF16 = 6,  // y = acc (+ b)                              -> bf16
+  EPI_DG_ACC_CA = 7,   // g = acc + r1, sums of g and g*aux; r1/aux/part non-null, no yb/r2/r3
+                       // (the hot RCAB case of EPI_DG_ACC, specialised: no runtime operand checks)
 };
 
 struct ConvParams {

@@ -29,10 +29,16 @@ namespace srmi {
 static __device__ uint4 kZerosW[4];  // zero page for halo lanes of the stage DMA
 static unsigned long long* g_wg_stamps = nullptr;
 void wgrad3x3_set_debug_stamps(unsigned long long* buf) { g_wg_stamps = buf; }
+#ifdef SRMI_STAMPS
 #define WSTAMP(i)                                                                                     \
   do {                                                                                                \
     if (p.stamps && tid == 0) p.stamps[(blockIdx.y * gridDim.x + blockIdx.x) * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+#else
+#define WSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
 
 template <int TW>
 struct Wg3 {
@@ -144,7 +150,7 @@ __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
 #pragma unroll 1
   for (int st = 0; st < nst; ++st) {
     const bool pf = st + 1 < nst;
-    const int sj = 2 + 3 * min(st, 19);
+    [[maybe_unused]] const int sj = 2 + 3 * min(st, 19);
     WSTAMP(sj);
     const char* sb = smem + (st & 1) * S::STAGE;
     bf16x8 A[2][4], B[2][9];
@@ -306,66 +312,94 @@ __global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
     for (int h = 0; h < 2; ++h) bcol[t][h] = DY_RING + swz128t(pcol + kx + 4 * h, 2 * it + (lp >> 1)) + half;
   }
 
-  // prologue: input rows -1, 0 and pairs 0 .. PF-1
+  // slot offsets: dY row r -> slot r & (RD-1); input row r -> slot (r + 1) % RX.
+  // Per pair the lane's A row is 2j + prow, its B rows 2j + prow + ky (ky of tap t).
+  int boffr[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) boffr[t] = prow + bky[t];  // 0..3
+  auto slots = [&](int j, uint32_t& ra, uint32_t (&rb)[9]) __attribute__((always_inline)) {
+    ra = (uint32_t)(((2 * j + prow) & (RD - 1)) * DSLOT);
+    int sb = (2 * j) % RX;  // uniform
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      int sl = sb + boffr[t];
+      sl = sl >= RX ? sl - RX : sl;
+      rb[t] = (uint32_t)(sl * XSLOT);
+    }
+  };
+  auto load_step = [&](uint32_t ra, const uint32_t (&rb)[9], int kc, bf16x8 (&a)[4], bf16x8 (&b)[9])
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+      a[ct] = cat_tr(lds_tr(smem, ra + acol[ct][0] + kc * 2048), lds_tr(smem, ra + acol[ct][1] + kc * 2048));
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      b[t] = cat_tr(lds_tr(smem, rb[t] + bcol[t][0] + kc * 2048), lds_tr(smem, rb[t] + bcol[t][1] + kc * 2048));
+  };
+  // vmcnt helper: this wave owns 7 (waves 0,1) or 6 (waves 2,3) groups of a pair
+  auto wait_groups = [&](int full_pairs, int extra) __attribute__((always_inline)) {
+    const int n = full_pairs * (wave_s < 2 ? 7 : 6) + extra;
+    if (n >= 14) wait_vm<14>();
+    else if (n == 13) wait_vm<13>();
+    else if (n == 12) wait_vm<12>();
+    else if (n == 11) wait_vm<11>();
+    else if (n == 7) wait_vm<7>();
+    else if (n == 6) wait_vm<6>();
+    else if (n == 5) wait_vm<5>();
+    else wait_vm<0>();
+  };
+
+  // prologue: input rows -1, 0 and pairs 0 .. PF-1; wait for the rows and pair 0
 #pragma unroll
   for (int m = 0; m < 4; ++m)
     if (wave_s + 4 * m < 2 * GX) dma(0, wave_s + 4 * m, true);
   for (int P = 0; P < PF && P < np; ++P) dma_pair_part(P, 0, 7);
-  // wait for pair 0 (+ the pre rows): allow the later prologue pairs to stay in flight
-  {
-    const int later = min(PF, np) - 1;
-    if (wave_s < 2) {
-      if (later >= 2) wait_vm<14>(); else if (later == 1) wait_vm<7>(); else wait_vm<0>();
-    } else {
-      if (later >= 2) wait_vm<12>(); else if (later == 1) wait_vm<6>(); else wait_vm<0>();
-    }
-  }
+  wait_groups(min(PF, np) - 1, 0);
   __syncthreads();
   WSTAMP(1);
+
+  bf16x8 A[3][4], B[3][9];
+  uint32_t ra, rb[9];
+  slots(0, ra, rb);
+  load_step(ra, rb, 0, A[0], B[0]);
 
 #pragma unroll 1
   for (int j = 0; j < np; ++j) {
     WSTAMP(2 + min(j, 59));
     const bool pf = j + PF < np;
-    const uint32_t ra = (uint32_t)(((2 * j + prow) % RD) * DSLOT);
-    uint32_t rb[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) rb[t] = (uint32_t)(((2 * j + prow + bky[t]) % RX) * XSLOT);
-    bf16x8 A[2][4], B[2][9];
-    auto load_step = [&](int kc, bf16x8 (&a)[4], bf16x8 (&b)[9]) __attribute__((always_inline)) {
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
-        a[ct] = cat_tr(lds_tr(smem, ra + acol[ct][0] + kc * 2048), lds_tr(smem, ra + acol[ct][1] + kc * 2048));
-#pragma unroll
-      for (int t = 0; t < 9; ++t)
-        b[t] = cat_tr(lds_tr(smem, rb[t] + bcol[t][0] + kc * 2048), lds_tr(smem, rb[t] + bcol[t][1] + kc * 2048));
-    };
-    load_step(0, A[0], B[0]);
+    const bool more = j + 1 < np;
+    uint32_t ran, rbn[9];
+    slots(j + 1, ran, rbn);
 #pragma unroll
     for (int kc = 0; kc < 3; ++kc) {
+      // the DMA for pair j+PF, spread over the K-steps (m 0-2 | 3-4 | 5-6)
       if (pf) dma_pair_part(j + PF, kc == 0 ? 0 : (kc == 1 ? 3 : 5), kc == 0 ? 3 : (kc == 1 ? 5 : 7));
-      if (kc + 1 < 3) load_step(kc + 1, A[(kc + 1) & 1], B[(kc + 1) & 1]);
+      if (kc < 2) load_step(ra, rb, kc + 1, A[kc + 1], B[kc + 1]);
+      else if (more) load_step(ran, rbn, 0, A[0], B[0]);  // next pair's first K-step
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int t = 0; t < 9; ++t)
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(A[kc & 1][ct], B[kc & 1][t], acc[ct][t]);
-      bf16x8 aw = A[kc & 1][0];
-      if (wave == 1) aw = A[kc & 1][1];
-      if (wave == 2) aw = A[kc & 1][2];
-      if (wave == 3) aw = A[kc & 1][3];
+        for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(A[kc][ct], B[kc][t], acc[ct][t]);
+      bf16x8 aw = A[kc][0];
+      if (wave == 1) aw = A[kc][1];
+      if (wave == 2) aw = A[kc][2];
+      if (wave == 3) aw = A[kc][3];
       bacc = mfma16(aw, ones, bacc);
       __builtin_amdgcn_sched_barrier(0);
+      if (kc == 1) {
+        // pair j+1 must have landed before K-step 2 reads its first fragments.  In
+        // flight may stay: pair j+2 (whole) and the 5 groups of pair j+PF issued above.
+        if (j + 2 < np) wait_groups(1, pf ? 5 : 0);
+        else wait_groups(0, 0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
     }
-    // pair j+1 must have landed; pairs j+2 .. min(j+PF, np-1) may stay in flight
-    const int later = min(j + PF, np - 1) - (j + 1);
-    if (wave_s < 2) {
-      if (later >= 2) wait_vm<14>(); else if (later == 1) wait_vm<7>(); else wait_vm<0>();
-    } else {
-      if (later >= 2) wait_vm<12>(); else if (later == 1) wait_vm<6>(); else wait_vm<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    ra = ran;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) rb[t] = rbn[t];
   }
 
   float* slab = p.slab + (size_t)chunk * Cout * 576;

@@ -11,7 +11,7 @@ import os
 from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsrmi.so")
+LIB_PATH = os.environ.get("SRMI_LIB") or os.path.join(_HERE, "libsrmi.so")  # SRMI_LIB: diagnostic build
 
 SRMI_ARCH_RCAN = 0
 SRMI_ARCH_EDSR = 1

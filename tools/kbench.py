@@ -12,6 +12,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "super-resolution-climate_amd"), ROOT]
+if os.environ.get("KBENCH_STAMPS"):  # phase stamps live only in the diagnostic build (make stamps)
+    os.environ.setdefault("SRMI_LIB", os.path.join(ROOT, "super-resolution-climate_amd", "srmi", "libsrmi_stamps.so"))
 
 import torch  # noqa: E402
 
@@ -110,12 +112,14 @@ if __name__ == "__main__":
 
 
 def stamps():
-    """Phase timing of the conv kernel (relu epilogue) from s_memtime stamps."""
+    """Phase timing of the Cin=64 conv kernel from s_memtime stamps (KBENCH_EPI: epilogues)."""
     import numpy as np
     d = torch.device("cuda", 0)
     N, H, W = 64, 48, 48
     S = torch.cuda.current_stream().cuda_stream
     x = torch.randn(N, H, W, 64, device=d).to(torch.bfloat16)
+    t = torch.randn(N, H, W, 64, device=d).clamp_min(0).to(torch.bfloat16)
+    r1 = torch.randn(N, H, W, 64, device=d)
     w = torch.randn(64, 64, 3, 3, device=d) * 0.05
     b = torch.zeros(64, device=d)
     fp = torch.empty(64 * 64 * 9, dtype=torch.bfloat16, device=d)
@@ -123,30 +127,35 @@ def stamps():
     pb = torch.empty(64, device=d)
     call("srmi_pack_conv", ptr(w), ptr(b), 64, 64, 0, ptr(fp), ptr(dp), ptr(pb), S)
     yb = torch.empty_like(x)
+    ns = call("srmi_conv3x3_nstrips", H, W)
+    part = torch.zeros(N, ns, 128, device=d)
     buf = torch.zeros(4096 * 64, dtype=torch.int64, device=d)
-    for _ in range(3):
-        call("srmi_conv3x3", ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, 0, ptr(yb), None, None, None, None, None, None,
-             1.0, S)
-    call("srmi_debug_conv_stamps", ptr(buf))
-    call("srmi_conv3x3", ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, 0, ptr(yb), None, None, None, None, None, None,
-         1.0, S)
-    call("srmi_debug_conv_stamps", None)
-    torch.cuda.synchronize()
-    st = buf.view(4096, 64).cpu().numpy()
-    print("raw wg0", st[0, :20].tolist())
-    print("nonzero per column", (st != 0).sum(0)[:20].tolist())
-    st = st[st[:, 0] != 0]
-    base = st[:, 0:1]
-    rel = st - base
-    print("workgroups", len(st), "start spread (cycles)", int(st[:, 0].max() - st[:, 0].min()))
-    names = ["prologue"] + [f"s{j}:{k}" for j in range(3) for k in ("issue", "mfma", "gstore", "epi", "barrier")]
-    prev = np.zeros(len(st))
-    for i, nm in enumerate(names, start=1):
-        if i >= 64 or not np.all(st[:, i]):
-            break
-        cur = rel[:, i]
-        print(f"{nm:12s} median dt {np.median(cur - prev):8.0f}  max {np.max(cur - prev):8.0f}")
-        prev = cur
+    for epi in [int(v) for v in os.environ.get("KBENCH_EPI", "0").split(",")]:
+        if epi == 5:
+            args = (ptr(x), ptr(dp), None, N, H, W, 64, 64, 0, 5, None, ptr(r1), ptr(r1), None, None, ptr(t), ptr(part))
+        elif epi == 1:
+            args = (ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, 1, ptr(yb), None, None, None, None, None, ptr(part))
+        else:
+            args = (ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, epi, ptr(yb), None, None, None, None, None, None)
+        for _ in range(3):
+            call("srmi_conv3x3", *args, 1.0, S)
+        buf.zero_()
+        call("srmi_debug_conv_stamps", ptr(buf))
+        call("srmi_conv3x3", *args, 1.0, S)
+        call("srmi_debug_conv_stamps", None)
+        torch.cuda.synchronize()
+        st = buf.view(4096, 64).cpu().numpy()
+        st = st[st[:, 0] != 0]
+        rel = st - st[:, 0:1]
+        print(f"conv epi={epi} workgroups", len(st), "start spread (cycles)", int(st[:, 0].max() - st[:, 0].min()))
+        names = ["prologue"] + [f"s{j}:{k}" for j in range(3) for k in ("issue", "mfma", "gstore", "epi", "barrier")]
+        prev = np.zeros(len(st))
+        for i, nm in enumerate(names, start=1):
+            if i >= 64 or not np.all(st[:, i]):
+                break
+            cur = rel[:, i]
+            print(f"{nm:12s} median dt {np.median(cur - prev):8.0f}  max {np.max(cur - prev):8.0f}")
+            prev = cur
 
 
 def wstamps():
