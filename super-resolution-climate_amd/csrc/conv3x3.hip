@@ -523,6 +523,7 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
     group_dma(k0 + 1);  // strip k0 reads groups k0 and k0+1
     wait_vm<0>();
   }
+  STAMP(1);
   float4 bias[4];
   {
     const float* bp = p.bias ? p.bias : reinterpret_cast<const float*>(kZeros);  // pointer select, no branch
@@ -643,6 +644,27 @@ int conv3x3_tw(const ConvParams& p) {
 
 int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
   if (p.Cin % 64 || p.Cout % 64 || p.N <= 0 || p.H % kTH) return SRMI_ERR_SHAPE;
+  // operands each epilogue dereferences unconditionally: refuse, never fault
+  if (!p.x || !p.w) return SRMI_ERR_ARG;
+  switch (epi) {
+    case EPI_PS_BF16:
+      if (!p.yb) return SRMI_ERR_ARG;
+      break;
+    case EPI_POOL_BF16:
+      if (!p.part) return SRMI_ERR_ARG;
+      break;
+    case EPI_RESID:
+      if (!p.r1) return SRMI_ERR_ARG;
+      break;
+    case EPI_DG_RELUMASK:
+      if (!p.aux) return SRMI_ERR_ARG;
+      break;
+    case EPI_DG_ACC:
+      if (!p.yf || (p.part && !p.aux)) return SRMI_ERR_ARG;
+      break;
+    default:
+      break;
+  }
   if (epi == EPI_PS_BF16 && p.Cout != 256) return SRMI_ERR_SHAPE;
   if (p.in_mode == IN_UNSHUF && p.Cin != 256) return SRMI_ERR_SHAPE;
   switch (epi) {

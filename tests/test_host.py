@@ -182,3 +182,18 @@ def test_data_parallel_semantics_gloo_world2():
     for rank, L, g in res:
         assert abs(L - float(loss)) < 1e-12
         np.testing.assert_allclose(g, ref, rtol=1e-9, atol=1e-12)
+
+
+def test_conv_abi_rejects_missing_operands():
+    """Op-level convs refuse (SRMI_ERR_ARG) instead of dereferencing a NULL operand.
+    The checks run before any launch, so this needs no GPU."""
+    import ctypes as C
+    from srmi import _lib
+    lib = _lib.load()
+    dummy = C.c_void_p(16)  # never dereferenced: every case below fails validation first
+    # epi 4 (dgrad * relu mask) without the mask, epi 2 (residual) without r1,
+    # epi 1 (pool) without the partial-sum buffer, epi 3 (pixel shuffle) without yb
+    for epi in (4, 2, 1, 3):
+        args = [dummy, dummy, None, 1, 4, 48, 64, 256 if epi == 3 else 64, 0, epi, None, None, None, None, None,
+                None, None, 1.0, None]
+        assert lib.srmi_conv3x3(*args) == -10001, (epi, "expected SRMI_ERR_ARG")

@@ -135,6 +135,10 @@ def stamps():
             args = (ptr(x), ptr(dp), None, N, H, W, 64, 64, 0, 5, None, ptr(r1), ptr(r1), None, None, ptr(t), ptr(part))
         elif epi == 1:
             args = (ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, 1, ptr(yb), None, None, None, None, None, ptr(part))
+        elif epi == 4:
+            args = (ptr(x), ptr(dp), None, N, H, W, 64, 64, 0, 4, ptr(yb), None, None, None, None, ptr(t), None)
+        elif epi == 2:
+            args = (ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, 2, ptr(yb), ptr(r1), ptr(r1), None, None, None, None)
         else:
             args = (ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, epi, ptr(yb), None, None, None, None, None, None)
         for _ in range(3):
