@@ -235,11 +235,13 @@ constexpr int GD = TW / 8, GX = 7;                               // 8-px groups 
 constexpr int NGP = 2 * GD + 2 * GX;                             // groups per pair (26)
 }  // namespace v4
 
-__global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
+// The body is instantiated once per wave (WV = wave index): the wave's DMA groups,
+// taps and tile rotation are compile-time constants (no SGPR pressure, no branches).
+template <int WV>
+__device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
   using namespace v4;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const int tid = threadIdx.x, lane = tid & 63;
+  constexpr int wave = WV, wave_s = WV;
   const int chunk = blockIdx.x, cb = blockIdx.y;
   const int Hr = p.H / p.row_splits;
   const int n = chunk / p.row_splits, ybase = (chunk % p.row_splits) * Hr;
@@ -277,11 +279,48 @@ __global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
       glds16(src, lds0 + (uint32_t)(DY_RING + ((r + 1) % RX) * XSLOT + g * 1024));
     }
   };
-  // groups of pair P owned by this wave: k = wave + 4m, m < 7 (waves 0,1) / 6 (2,3)
-  auto dma_pair_part = [&](int P, int m0, int m1) __attribute__((always_inline)) {
+  // Pair DMA with precomputed per-lane offsets: group m of this wave is k = wave + 4m
+  // (m < 7: waves 0,1 own 7 groups of a pair, waves 2,3 own 6).  Everything that
+  // does not change from pair to pair -- the lane's pixel, chunk and x validity --
+  // is computed once; per pair only a uniform base pointer and one add remain.
+  int loff[7];
+  uint32_t okx = 0;
 #pragma unroll
-    for (int m = m0; m < m1; ++m)
-      if (wave_s + 4 * m < NGP) dma(P, wave_s + 4 * m, false);
+  for (int m = 0; m < 7; ++m) {
+    const int k = wave_s + 4 * m;
+    loff[m] = 0;
+    if (k < 2 * GD) {
+      const int rr = k / GD, g = k - rr * GD, xx = 8 * g + dq;
+      const int c = (g & 1) ? cl1 : cl0;
+      loff[m] = plain ? (rr * TW + xx) * Cout + c * 8 : (2 * rr * (2 * TW) + 2 * xx) * 64 + c * 8;
+    } else if (k < NGP) {
+      const int kk = k - 2 * GD, rr = kk / GX, g = kk - rr * GX, hx = 8 * g + dq, xx = hx - 1;
+      const int c = (g & 1) ? cl1 : cl0;
+      const bool ok = hx < TW + 2 && xx >= 0 && xx < TW;
+      okx |= ok ? (1u << m) : 0u;
+      loff[m] = (rr * TW + (ok ? xx : 0)) * 64 + c * 8;
+    }
+  }
+  auto dma_pair_part = [&](int P, int m0, int m1) __attribute__((always_inline)) {
+    const bf16_t* dyb = plain ? dyn + (size_t)(ybase + 2 * P) * TW * Cout
+                              : dyn + ((size_t)(2 * (ybase + 2 * P) + (cb >> 1)) * (2 * TW) + (cb & 1)) * 64;
+    const bf16_t* xb = xn + (ptrdiff_t)(ybase + 2 * P + 1) * TW * 64;
+    const bool yv0 = ybase + 2 * P + 1 < H, yv1 = ybase + 2 * P + 2 < H;
+#pragma unroll
+    for (int m = m0; m < m1; ++m) {
+      const int k = wave_s + 4 * m;
+      if (k < 2 * GD) {
+        const int rr = k / GD, g = k - rr * GD;
+        glds16(dyb + loff[m], lds0 + (uint32_t)(((2 * P + rr) & (RD - 1)) * DSLOT + g * 1024));
+      } else if (k < NGP) {
+        const int kk = k - 2 * GD, rr = kk / GX, g = kk - rr * GX;
+        const bool ok = ((okx >> m) & 1u) && (rr ? yv1 : yv0);
+        const void* src = ok ? (const void*)(xb + loff[m]) : (const void*)kZerosW;
+        int slot = 2 * P + 2 + rr;  // input row 2P+1+rr -> slot (row + 1) % RX
+        slot = slot % RX;
+        glds16(src, lds0 + (uint32_t)(DY_RING + slot * XSLOT + g * 1024));
+      }
+    }
   };
 
   f32x4 acc[4][9];
@@ -303,7 +342,7 @@ __global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) acol[ct][h] = swz128t(pcol + 4 * h, 2 * ct + (lp >> 1)) + half;
+    for (int h = 0; h < 2; ++h) acol[ct][h] = swz128t(pcol + 4 * h, 2 * ((ct + wave) & 3) + (lp >> 1)) + half;
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
     const int j = 9 * wave + t, tap = j >> 2, it = j & 3, kx = tap % 3;
@@ -358,48 +397,50 @@ __global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
   __syncthreads();
   WSTAMP(1);
 
-  bf16x8 A[3][4], B[3][9];
+  // fragments double-buffered across K-steps; a pair has 3 K-steps, so the pair loop
+  // is unrolled by two (np is even) to keep the buffer parity compile-time
+  bf16x8 A[2][4], B[2][9];
   uint32_t ra, rb[9];
   slots(0, ra, rb);
   load_step(ra, rb, 0, A[0], B[0]);
 
 #pragma unroll 1
-  for (int j = 0; j < np; ++j) {
-    WSTAMP(2 + min(j, 59));
-    const bool pf = j + PF < np;
-    const bool more = j + 1 < np;
-    uint32_t ran, rbn[9];
-    slots(j + 1, ran, rbn);
+  for (int j0 = 0; j0 < np; j0 += 2) {
 #pragma unroll
-    for (int kc = 0; kc < 3; ++kc) {
-      // the DMA for pair j+PF, spread over the K-steps (m 0-2 | 3-4 | 5-6)
-      if (pf) dma_pair_part(j + PF, kc == 0 ? 0 : (kc == 1 ? 3 : 5), kc == 0 ? 3 : (kc == 1 ? 5 : 7));
-      if (kc < 2) load_step(ra, rb, kc + 1, A[kc + 1], B[kc + 1]);
-      else if (more) load_step(ran, rbn, 0, A[0], B[0]);  // next pair's first K-step
-      __builtin_amdgcn_sched_barrier(0);
+    for (int q = 0; q < 2; ++q) {
+      const int j = j0 + q;
+      WSTAMP(2 + min(j, 59));
+      const bool pf = j + PF < np;
+      const bool more = j + 1 < np;
+      uint32_t ran, rbn[9];
+      slots(j + 1, ran, rbn);
 #pragma unroll
-      for (int t = 0; t < 9; ++t)
+      for (int kc = 0; kc < 3; ++kc) {
+        const int cur = (3 * q + kc) & 1, nxt = cur ^ 1;
+        if (pf) dma_pair_part(j + PF, kc == 0 ? 0 : (kc == 1 ? 3 : 5), kc == 0 ? 3 : (kc == 1 ? 5 : 7));
+        if (kc < 2) load_step(ra, rb, kc + 1, A[nxt], B[nxt]);
+        else if (more) load_step(ran, rbn, 0, A[nxt], B[nxt]);  // next pair's first K-step
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(A[kc][ct], B[kc][t], acc[ct][t]);
-      bf16x8 aw = A[kc][0];
-      if (wave == 1) aw = A[kc][1];
-      if (wave == 2) aw = A[kc][2];
-      if (wave == 3) aw = A[kc][3];
-      bacc = mfma16(aw, ones, bacc);
-      __builtin_amdgcn_sched_barrier(0);
-      if (kc == 1) {
-        // pair j+1 must have landed before K-step 2 reads its first fragments.  In
-        // flight may stay: pair j+2 (whole) and the 5 groups of pair j+PF issued above.
-        if (j + 2 < np) wait_groups(1, pf ? 5 : 0);
-        else wait_groups(0, 0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(A[cur][ct], B[cur][t], acc[ct][t]);
+        bacc = mfma16(A[cur][0], ones, bacc);  // slot 0 = this wave's own co tile
+        __builtin_amdgcn_sched_barrier(0);
+        if (kc == 1) {
+          // pair j+1 must have landed before K-step 2 reads its first fragments.  In
+          // flight may stay: pair j+2 (whole) and the 5 groups of pair j+PF issued above.
+          if (j + 2 < np) wait_groups(1, pf ? 5 : 0);
+          else wait_groups(0, 0);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+        }
       }
-    }
-    ra = ran;
+      ra = ran;
 #pragma unroll
-    for (int t = 0; t < 9; ++t) rb[t] = rbn[t];
+      for (int t = 0; t < 9; ++t) rb[t] = rbn[t];
+    }
   }
 
   float* slab = p.slab + (size_t)chunk * Cout * 576;
@@ -409,7 +450,7 @@ __global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
     const int ci = it * 16 + (lane & 15);
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {
-      const int co = cb * 64 + ct * 16 + 4 * (lane >> 4);
+      const int co = cb * 64 + ((ct + wave) & 3) * 16 + 4 * (lane >> 4);  // slot ct = co tile (ct + wave) & 3
       *reinterpret_cast<float4*>(slab + ((size_t)tap * 64 + ci) * Cout + co) =
           make_float4(acc[ct][t][0], acc[ct][t][1], acc[ct][t][2], acc[ct][t][3]);
     }
@@ -422,6 +463,16 @@ __global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
   WSTAMP(63);
 }
 
+__global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+    case 0: wgrad48_body<0>(p, smem); break;
+    case 1: wgrad48_body<1>(p, smem); break;
+    case 2: wgrad48_body<2>(p, smem); break;
+    default: wgrad48_body<3>(p, smem); break;
+  }
+}
+
 int wgrad3x3_nslabs(const WgradParams& p) { return p.N * p.row_splits; }
 
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
@@ -432,8 +483,8 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
   q.stamps = g_wg_stamps;
   static const int dbg = getenv("SRMI_WGRAD_DBG") ? atoi(getenv("SRMI_WGRAD_DBG")) : 0;
   q.dbg = dbg;
-  // v4 (row-pair rings) is opt-in until it beats v3 (tools/kbench.py)
-  static const bool use_v4 = getenv("SRMI_WGRAD_V4") && atoi(getenv("SRMI_WGRAD_V4"));
+  // v4 (row-pair rings, per-wave specialised) for W == 48; SRMI_WGRAD_V3=1 forces v3
+  static const bool use_v4 = !(getenv("SRMI_WGRAD_V3") && atoi(getenv("SRMI_WGRAD_V3")));
   if (use_v4 && p.W == 48 && (p.H / p.row_splits) % 2 == 0) {
     hipLaunchKernelGGL(wgrad48_kernel, grid, dim3(256), v4::LDS, st, q);
   } else if (p.W % 48 == 0) {
