@@ -81,7 +81,7 @@ def _time_launches(launch, stream, n=50, warm=5):
 
 def rooflines(dev, batch):
     """Roofline of the dominant kernel (by rocprofv3 time share: the 3x3 filter-
-    gradient MFMA kernel, 23.7 % of a step) plus the forward conv, both at the
+    gradient MFMA kernel, ~24 % of a step) plus the forward conv, both at the
     bench shapes (B tiles of 48x48x64 bf16), average launch duration from HIP events
     on the launch stream.  Algorithmic bytes = what the op must move at least
     (inputs once + outputs once); flops = 2 x MACs."""
@@ -107,11 +107,11 @@ def rooflines(dev, batch):
                                        slab.numel() * 4, 0, 1.0, None, None, st.cuda_stream), st)
     bytes_w = 2 * act + 64 * 577 * 4          # x + dY read once, dW + db written once
     t_hbm, t_mfma = bytes_w / (HBM_PEAK_GBS * 1e9), flop / (PEAK_BF16_TFLOPS * 1e12)
-    tr = _pmc_traffic("wgrad3x3_kernel")
+    tr = _pmc_traffic("wgrad48_kernel")
     ach = bytes_w / (ms_w * 1e-3) / 1e9
     dom = {"bound": "hbm" if t_hbm >= t_mfma else "mfma", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr["bytes"] if tr else None,
-           "kernel": "srmi::wgrad3x3_kernel<48>", "avg_launch_ms": round(ms_w, 4), "bytes_per_launch": bytes_w,
+           "kernel": "srmi::wgrad48_kernel", "avg_launch_ms": round(ms_w, 4), "bytes_per_launch": bytes_w,
            "flop_per_launch": flop, "mfma_tflops": round(flop / (ms_w * 1e-3) / 1e12, 1),
            "mfma_frac": round(flop / (ms_w * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
            "traffic_source": tr["source"] if tr else None}

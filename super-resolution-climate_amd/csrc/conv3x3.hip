@@ -339,6 +339,28 @@ __device__ __forceinline__ void epi_prefetch(const ConvParams& p, EpiPre<NPT, EP
   }
 }
 
+// one (pt, ct) element of epi_prefetch (e = pt * 4 + ct), for interleaving
+template <int NPT, int EPI>
+__device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT, EPI>& e, int n, int cb, int y,
+                                                 int x0, int fr, int fk, int idx) {
+  if constexpr (EPI == EPI_RESID || EPI == EPI_DG_ACC || EPI == EPI_DG_RELUMASK || EPI == EPI_DG_ACC_CA) {
+    const int pt = idx >> 2, ct = idx & 3;
+    const size_t HW = (size_t)p.H * p.W;
+    const size_t pix = (size_t)n * HW + (size_t)y * p.W + x0 + pt * 16 + fr;
+    const size_t o = pix * p.Cout + cb * 64 + ct * 16 + fk * 4;
+    if constexpr (EPI == EPI_RESID) e.r1[pt][ct] = *reinterpret_cast<const float4*>(p.r1 + o);
+    if constexpr (EPI == EPI_DG_ACC) {
+      e.r1[pt][ct] = p.r1 ? *reinterpret_cast<const float4*>(p.r1 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+      e.aux[pt][ct] = p.part ? *reinterpret_cast<const uint2*>(p.aux + o) : make_uint2(0, 0);
+    }
+    if constexpr (EPI == EPI_DG_RELUMASK) e.aux[pt][ct] = *reinterpret_cast<const uint2*>(p.aux + o);
+    if constexpr (EPI == EPI_DG_ACC_CA) {
+      e.r1[pt][ct] = *reinterpret_cast<const float4*>(p.r1 + o);
+      e.aux[pt][ct] = *reinterpret_cast<const uint2*>(p.aux + o);
+    }
+  }
+}
+
 __device__ __forceinline__ float relu_mask(uint32_t bits16, float v) {
   return (bits16 & 0x7FFFu) && !(bits16 & 0x8000u) ? v : 0.f;
 }
@@ -496,10 +518,9 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
   // page.  No registers hold in-flight data, so no compiler-inserted vmcnt waits.
   const int wv_s = __builtin_amdgcn_readfirstlane(wave);
   const uint32_t rbase = lds_u32(ring);
-  auto group_dma = [&](int gidx) __attribute__((always_inline)) {
-    constexpr int NG = S::GROUPB / 1024;
+  auto group_dma_one = [&](int gidx, int i) __attribute__((always_inline)) {
     const int qbase = (gidx % 3) * 4 * (TW + 2);
-    for (int i = wv_s; i < NG; i += 4) {
+    {
       const int q = 8 * i + (lane >> 3);
       const int Q = qbase + q;
       const int c = (lane & 7) ^ ((Q >> 1) & 7);
@@ -509,6 +530,11 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
       const void* src = ok ? (const void*)(xn + ((size_t)y * p.W + xx) * 64 + c * 8) : (const void*)kZeros;
       glds16(src, rbase + (uint32_t)qbase * 128u + (uint32_t)i * 1024u);
     }
+  };
+  constexpr int NGRP = S::GROUPB / 1024;         // 1 KiB DMA pieces per group
+  constexpr int NGW = (NGRP + 3) / 4;            // pieces per wave (upper bound)
+  auto group_dma = [&](int gidx) __attribute__((always_inline)) {
+    for (int i = wv_s; i < NGRP; i += 4) group_dma_one(gidx, i);
   };
 
   // prologue: filters (all 9 taps, 72 KiB) and input groups k0, k0+1, all by LDS-DMA
@@ -544,9 +570,7 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
     const bool pf = (k + 1 < k1);
     // group k+2 -> ring slot (k+2)%3, which held group k-1 (last read by strip k-1,
     // released by the barrier that ended it)
-    if (pf) group_dma(k + 2);
     EpiPre<NPT, EPI> ep;
-    epi_prefetch<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk);
     [[maybe_unused]] const int sj = 2 + 5 * min(k - k0, 11);
     STAMP(sj);
 
@@ -581,6 +605,10 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
     load_step(0, A[0], B[0]);
 #pragma unroll
     for (int s = 0; s < 18; ++s) {
+      // group k+2's DMA pieces and the epilogue operands are issued one or two per
+      // K-step, so a full memory queue stalls the wave between MFMA groups only
+      if (s < NGW && pf && wv_s + 4 * s < NGRP) group_dma_one(k + 2, wv_s + 4 * s);
+      if (s >= 2 && s - 2 < NPT * 4) epi_prefetch_one<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk, s - 2);
       if (s + 1 < 18) load_step(s + 1, A[(s + 1) & 1], B[(s + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
