@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-interp-loss", action="store_true")
+    ap.add_argument("--no-inference", action="store_true", help="skip the C5 tiled-region inference line")
+    ap.add_argument("--infer-region", type=int, default=4096, help="C5 HR region side (BASELINE: 4096)")
+    ap.add_argument("--infer-iters", type=int, default=5)
     return ap.parse_args()
 
 
@@ -127,6 +130,43 @@ def rooflines(dev, batch):
     return dom, conv
 
 
+def inference_bench(dev, side, iters):
+    """BASELINE config 5: RCAN inference over a full region, 1 variable, HR side x side
+    cut floor-wise into 192x192 tiles (4096 -> 21 x 21 = 441 tiles, 4032^2 HR produced),
+    per region: tiling + lnorm, bicubic 1/4, rcan-10-20-64 forward (bf16 MFMA), bicubic
+    x4 baseline, both RMSEs, de-normalised mosaics of input/target/interp/model --
+    captured once as a HIP graph and replayed (dual_trainer.process_image semantics).
+    MPix/s counts produced HR pixels."""
+    from oracle import rcan_oracle as ro  # synthetic region generator only
+    from srmi.engine import NetSpec
+    from srmi.inference import TiledInference
+    from srmi.trainer import default_init_
+    spec = NetSpec(arch="rcan", nchannels_in=1, nchannels_out=1, nfeatures=64, nlayers=10, nblocks=20,
+                   cbottleneck=2, scale=4)
+    from srmi.engine import param_table
+    table = param_table(spec)
+    params = torch.empty(sum(t[2] for t in table), dtype=torch.float32, device=dev)
+    default_init_(params, table, 0)
+    region = torch.tensor(ro.synthetic_hr(1, 1, side, 99)[0]).to(dev)
+    ti = TiledInference(spec, params, tuple(region.shape), (192, 192), device=dev, graph=True)
+    ti.process_region(region)  # builds + captures the graph
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        ti.replay()
+    e1.record(st)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    mpix = ti.n * 192 * 192 / 1e6
+    return {"metric": "inference MPix/sec (HR pixels produced)", "value": round(mpix / (ms * 1e-3), 2),
+            "unit": "MPix/s", "ms_per_region": round(ms, 3), "tiles": ti.n, "hr_mpix_per_region": round(mpix, 3),
+            "model_tflops": round(ti.n * 73.26e9 / (ms * 1e-3) / 1e12, 1), "dtype": "bf16", "data": "synthetic",
+            "config": {"workload": f"rcan-10-20-64 tiled inference, 1 var, {side}x{side} HR region, 192^2 tiles "
+                                   "(floor), graph-replayed", "graph": True}}
+
+
 def cpu_baseline(channels, steps):
     """Oracle (PyTorch-CPU restatement of the reference step) on this host's cores."""
     from oracle import rcan_oracle as ro
@@ -202,6 +242,9 @@ def main():
     value = tiles / dt
     if info.rank == 0:
         roof, roof_conv = rooflines(dev, B)
+        infer = None
+        if not args.no_inference and world == 1:
+            infer = inference_bench(dev, args.infer_region, args.infer_iters)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(C, args.cpu_steps)
@@ -218,6 +261,7 @@ def main():
             "roofline": roof,
             "roofline_conv_fwd": roof_conv,
             "cpu_baseline": cpu,
+            "inference": infer,
         }
         print(json.dumps(rec), flush=True)
     if info.enabled:

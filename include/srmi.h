@@ -21,6 +21,10 @@
  *   srmi_conv3x3* / srmi_wgrad*  -> nn.Conv2d of default_conv
  *                                   sres/model/common/cnn.py:8-9 (op level)
  *   srmi_ca_*                    -> CALayer sres/model/rcan/network.py:31-47
+ *   srmi_region_to_tiles         -> get_tiles + 'lnorm' norm
+ *                                   sres/base/source/swot/raw.py:216-233, :169-181
+ *   srmi_tiles_to_region         -> denorm + assemble_images
+ *                                   sres/controller/dual_trainer.py:67-77, :482-512
  */
 #ifndef SRMI_H
 #define SRMI_H
@@ -141,6 +145,19 @@ int srmi_head_forward(const float* lr, const float* w, const float* b, int N, in
                       void* x0b, void* stream);
 int srmi_tail_forward(const void* x, const float* w, const float* b, int N, int C, int H, int W, float* y,
                       void* stream);
+
+/* ---- tiled-region inference data path --------------------------------- */
+/* region [C][H][W] fp32 -> floor grid gy = H/ty, gx = W/tx; tiles
+ * [gy*gx][C][ty][tx] normalised per tile and channel ((x - mean) / std over the
+ * tile, ddof 0); mean/std [gy*gx][C]; bad[gy*gx] (optional) = 1 where the tile
+ * holds a non-finite value (the reference drops those tiles) */
+int srmi_region_to_tiles(const float* region, int C, int H, int W, int ty, int tx, float* tiles, float* mean,
+                         float* std, int* bad, void* stream);
+/* tiles [n][C][ty][tx] -> out [C][gy*ty][gx*tx]: x * std + mean (mean == NULL:
+ * no denorm); inv[gy*gx] = tile index of each grid cell or -1 (NaN cell);
+ * inv == NULL: tile i is cell i */
+int srmi_tiles_to_region(const float* tiles, const float* mean, const float* std, const int* inv, int C, int ty,
+                         int tx, int gy, int gx, float* out, void* stream);
 
 #ifdef __cplusplus
 }

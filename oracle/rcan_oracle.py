@@ -19,6 +19,11 @@ from the imported reference (``tests/golden/make_golden.py``):
 * l2loss (RMSE) ........ sres/controller/stats.py:5-8
 * train step ........... sres/controller/dual_trainer.py:310-323, :557-571
 * Adam ................. torch.optim.Adam defaults used at dual_trainer.py:126
+* tiled inference ...... get_tiles + lnorm (sres/base/source/swot/raw.py:216-233,
+                         :169-181), denorm + assemble_images + process_image
+                         (dual_trainer.py:67-77, :482-512, :396-480); pinned by
+                         restatement only (the reference wraps them in xarray,
+                         which is not installed)
 
 State-dict keys are identical to the reference model's.
 """
@@ -275,3 +280,57 @@ def train_step(model: nn.Module, opt: AdamOracle, hr: torch.Tensor, scale: int,
     loss.backward()
     opt.step()
     return float(loss), iloss, out.detach()
+
+
+# --------------------------------------------------------------------------
+# Tiled-region inference data path.  The reference's own
+# functions wrap numpy in xarray (not installed here), so these restate them:
+# parity for this row is pinned by restatement, not by golden vectors.
+
+def region_to_tiles(region: np.ndarray, ty: int, tx: int):
+    """get_tiles (sres/base/source/swot/raw.py:216-233) for C == 1 plus the 'lnorm'
+    branch of norm() (raw.py:169-181).  region [C, H, W] -> (tiles [n, C, ty, tx]
+    normalised, mean [n, C], std [n, C], tile_ids [n]); tiles whose mean is not
+    finite are dropped, as the reference's mask does."""
+    C, H, W = region.shape
+    gy, gx = H // ty, W // tx
+    reg = region[:, :gy * ty, :gx * tx]
+    t = reg.reshape(C, gy, ty, gx, tx).swapaxes(2, 3).reshape(C, gy * gx, ty, tx).swapaxes(0, 1)
+    keep = np.isfinite(t.mean(axis=(1, 2, 3)))
+    ids = np.nonzero(keep)[0]
+    t = t[keep]
+    mean = t.mean(axis=(2, 3))
+    std = t.std(axis=(2, 3))  # xarray .std(): ddof 0
+    tiles = (t - mean[:, :, None, None]) / std[:, :, None, None]
+    return tiles, mean, std, ids, (gy, gx)
+
+
+def assemble(tiles: np.ndarray, mean: Optional[np.ndarray], std: Optional[np.ndarray], ids: np.ndarray,
+             grid: Tuple[int, int]) -> np.ndarray:
+    """denorm (dual_trainer.py:67-77) + assemble_images (dual_trainer.py:482-512):
+    tile id -> cell (id // gx, id % gx), missing cells NaN.  -> [C, gy*ty, gx*tx]"""
+    n, C, ty, tx = tiles.shape
+    gy, gx = grid
+    x = tiles if mean is None else tiles * std[:, :, None, None] + mean[:, :, None, None]
+    out = np.full((C, gy * ty, gx * tx), np.nan, dtype=x.dtype)
+    for i, tid in enumerate(ids):
+        y0, x0 = (tid // gx) * ty, (tid % gx) * tx
+        out[:, y0:y0 + ty, x0:x0 + tx] = x[i]
+    return out
+
+
+def process_region(model, region: np.ndarray, ty: int, tx: int, scale: int):
+    """process_image (dual_trainer.py:396-480) on one region, all tiles in one batch.
+    Returns (images dict, losses dict) with the reference's image types."""
+    tiles, mean, std, ids, grid = region_to_tiles(region, ty, tx)
+    dt = torch.float64 if tiles.dtype == np.float64 else torch.float32
+    target = torch.tensor(tiles, dtype=dt)
+    lr = downsample(target, scale)
+    with torch.no_grad():
+        sr = model(lr)
+    interp = upsample(lr, scale)
+    losses = {"model": float(l2loss(sr, target)), "interpolated": float(l2loss(interp, target))}
+    images = {"input": assemble(lr.numpy(), mean, std, ids, grid), "target": assemble(tiles, mean, std, ids, grid),
+              "interpolated": assemble(interp.numpy(), mean, std, ids, grid),
+              "model": assemble(sr.numpy(), mean, std, ids, grid)}
+    return images, losses

@@ -750,4 +750,16 @@ int srmi_tail_forward(const void* x, const float* w, const float* b, int N, int 
   return tail_fwd_launch((const bf16_t*)x, w, b, N, C, H, W, y, S_(stream));
 }
 
+int srmi_region_to_tiles(const float* region, int C, int H, int W, int ty, int tx, float* tiles, float* mean,
+                         float* std, int* bad, void* stream) {
+  if (!region || !tiles || !mean || !std) return SRMI_ERR_ARG;
+  return region_to_tiles_launch(region, C, H, W, ty, tx, tiles, mean, std, bad, S_(stream));
+}
+
+int srmi_tiles_to_region(const float* tiles, const float* mean, const float* std, const int* inv, int C, int ty,
+                         int tx, int gy, int gx, float* out, void* stream) {
+  if (!tiles || !out || (mean && !std)) return SRMI_ERR_ARG;
+  return tiles_to_region_launch(tiles, mean, std, inv, C, ty, tx, gy, gx, out, S_(stream));
+}
+
 }  // extern "C"

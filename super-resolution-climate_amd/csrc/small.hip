@@ -333,7 +333,7 @@ __global__ void __launch_bounds__(256) tail_wgrad_kernel(const float* __restrict
         bacc[c] += v;
       }
       const int nx = min(64, W - x0);
-#pragma unroll 2
+
       for (int j = 0; j < nx; ++j) {
         const int xx = x0 + j;
 #pragma unroll

@@ -122,4 +122,10 @@ int pack_one_launch(const float* w, const float* b, int Cout, int Cin, int ps, b
 
 int scale_add_launch(float* y, const float* x, float a, size_t n, hipStream_t st);
 
+// tiled-region data path (tiles.hip)
+int region_to_tiles_launch(const float* region, int C, int H, int W, int ty, int tx, float* tiles, float* mean,
+                           float* stdv, int* bad, hipStream_t st);
+int tiles_to_region_launch(const float* tiles, const float* mean, const float* stdv, const int* inv, int C, int ty,
+                           int tx, int gy, int gx, float* out, hipStream_t st);
+
 }  // namespace srmi

@@ -61,6 +61,8 @@ _SIGS = {
     "srmi_ca_backward": ([P, P, C.c_int, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P], C.c_int),
     "srmi_head_forward": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P], C.c_int),
     "srmi_tail_forward": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),
+    "srmi_region_to_tiles": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P], C.c_int),
+    "srmi_tiles_to_region": ([P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),
 }
 EXPORTED = tuple(_SIGS)
 

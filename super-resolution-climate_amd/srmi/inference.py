@@ -1,0 +1,153 @@
+"""Tiled-region inference: drop-in for ModelTrainer.process_image + assemble_images.
+
+Reference (sres/controller/dual_trainer.py:396-512, sres/base/source/swot/raw.py:169-233):
+a region [C, H, W] is cut floor-wise into a gy x gx grid of HR tiles (tile id =
+y * gx + x), tiles holding a non-finite value are dropped, every tile/channel is
+'lnorm'-normalised (mean/std over the tile, ddof 0), the LR input is the bicubic
+1/s of the tile (apply_network, :557-571), the model output and the bicubic
+interpolation baseline (upsample) are scored with RMSE against the tile, and each
+image type (input, target, interpolated, model) is de-normalised and mosaicked
+back into the grid (NaN where a tile was dropped).
+
+Every step runs in srmi's HIP kernels (region_to_tiles, downsample, the RCAN/EDSR
+inference engine, upsample, RMSE, tiles_to_region) on one stream; the whole
+per-region sequence is captured once in a HIP graph (torch.cuda.CUDAGraph drives
+hipGraph capture of the ctypes launches on the capture stream) and replayed per
+region, so a region costs one graph launch.
+
+Differences from the reference, by design: losses are the RMSE over all kept
+tiles of the region (the reference averages per-batch RMSEs of task.batch_size
+tiles); for C > 1 channel c of tile t is region channel c at tile t (the
+reference's channel-major flattening packs neighbouring tiles of one variable into
+the channel axis, SURVEY.md §8f row 3 -- identical for the 1-variable C5 case).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from ._lib import call, ptr, stream_handle
+from .engine import Engine, NetSpec, downsample, upsample
+
+
+class TiledInference:
+    def __init__(self, spec: NetSpec, params: torch.Tensor, region_chw: Tuple[int, int, int],
+                 tile_hr: Tuple[int, int] = (192, 192), device: Optional[torch.device] = None, graph: bool = True):
+        self.spec = spec
+        self.device = device or params.device
+        C, H, W = region_chw
+        if C != spec.nchannels_in or spec.nchannels_in != spec.nchannels_out:
+            raise ValueError("region channels must equal the model's input/output channels")
+        ty, tx = tile_hr
+        s = spec.scale
+        if ty % s or tx % s:
+            raise ValueError(f"tile {tile_hr} not divisible by the model scale {s}")
+        self.C, self.H, self.W, self.ty, self.tx, self.s = C, H, W, ty, tx, s
+        self.gy, self.gx = H // ty, W // tx
+        n = self.gy * self.gx
+        if n < 1:
+            raise ValueError("region smaller than one tile")
+        self.n = n
+        self.params = params
+        d = self.device
+        f32 = dict(dtype=torch.float32, device=d)
+        self.region = torch.empty((C, H, W), **f32)
+        self.tiles = torch.empty((n, C, ty, tx), **f32)
+        self.mean = torch.empty((n, C), **f32)
+        self.std = torch.empty((n, C), **f32)
+        self.bad = torch.zeros(n, dtype=torch.int32, device=d)
+        self.lr = torch.empty((n, C, ty // s, tx // s), **f32)
+        self.sr = torch.empty((n, C, ty, tx), **f32)
+        self.interp = torch.empty((n, C, ty, tx), **f32)
+        self.loss_m = torch.zeros(4, **f32)
+        self.loss_i = torch.zeros(4, **f32)
+        hr_shape = (C, self.gy * ty, self.gx * tx)
+        self.images = {
+            "input": torch.empty((C, self.gy * ty // s, self.gx * tx // s), **f32),
+            "target": torch.empty(hr_shape, **f32),
+            "interpolated": torch.empty(hr_shape, **f32),
+            "model": torch.empty(hr_shape, **f32),
+        }
+        self.eng = Engine(spec, n, (ty // s, tx // s), train=False, device=d)
+        self.eng.pack(params)
+        self._graph = None
+        self._use_graph = graph and self.device.type == "cuda"
+
+    # ---------------------------------------------------------------- pieces
+    def _tile(self):
+        st = stream_handle()
+        call("srmi_region_to_tiles", ptr(self.region), self.C, self.H, self.W, self.ty, self.tx, ptr(self.tiles),
+             ptr(self.mean), ptr(self.std), ptr(self.bad), st)
+
+    def _model_and_mosaic(self, tiles, lr, sr, interp, mean, std, inv, nt):
+        st = stream_handle()
+        downsample(tiles, self.s, out=lr)
+        self.eng.forward(self.params, lr, out=sr)
+        upsample(lr, self.s, out=interp)
+        count = float(tiles.numel())
+        for pred, l4 in ((sr, self.loss_m), (interp, self.loss_i)):
+            self.eng.rmse_partial(pred, tiles, l4, count)
+            Engine.rmse_finalize(l4)
+        C, gy, gx, s = self.C, self.gy, self.gx, self.s
+        for name, src, ty, tx in (("input", lr, self.ty // s, self.tx // s), ("target", tiles, self.ty, self.tx),
+                                  ("interpolated", interp, self.ty, self.tx), ("model", sr, self.ty, self.tx)):
+            call("srmi_tiles_to_region", ptr(src), ptr(mean), ptr(std), ptr(inv), C, ty, tx, gy, gx,
+                 ptr(self.images[name]), st)
+
+    def _all_tiles(self):
+        self._model_and_mosaic(self.tiles, self.lr, self.sr, self.interp, self.mean, self.std, None, self.n)
+
+    # ------------------------------------------------------------------- API
+    def process_region(self, region: torch.Tensor) -> Tuple[Dict[str, torch.Tensor], Dict[str, torch.Tensor]]:
+        """region [C, H, W] fp32 (device) -> (images, losses); images are device tensors
+        (input [C, gy*ty/s, gx*tx/s], target/interpolated/model [C, gy*ty, gx*tx]),
+        losses {'model', 'interpolated'} 1-element device tensors (RMSE)."""
+        if tuple(region.shape) != (self.C, self.H, self.W):
+            raise ValueError(f"region shape {tuple(region.shape)} != {(self.C, self.H, self.W)}")
+        self.region.copy_(region)
+        self._tile()
+        if bool(self.bad.any()):  # rare: drop non-finite tiles (reference get_tiles mask)
+            self._run_compacted()
+        elif self._use_graph:
+            if self._graph is None:
+                self._capture()
+            self._graph.replay()
+        else:
+            self._all_tiles()
+        return self.images, {"model": self.loss_m[3:4], "interpolated": self.loss_i[3:4]}
+
+    def replay(self):
+        """Re-run the captured per-region graph on the current region buffer (bench)."""
+        if self._graph is None:
+            self._capture()
+        self._graph.replay()
+
+    def _capture(self):
+        self._all_tiles()  # warm-up outside capture (uploads engine tables)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                self._tile()
+                self._all_tiles()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self._graph = g
+
+    def _run_compacted(self):
+        keep = torch.nonzero(self.bad == 0).flatten()
+        nt = int(keep.numel())
+        inv = torch.full((self.n,), -1, dtype=torch.int32, device=self.device)
+        if nt == 0:
+            for img in self.images.values():
+                img.fill_(float("nan"))
+            self.loss_m.fill_(float("nan"))
+            self.loss_i.fill_(float("nan"))
+            return
+        inv[keep] = torch.arange(nt, dtype=torch.int32, device=self.device)
+        tiles = self.tiles.index_select(0, keep).contiguous()
+        mean = self.mean.index_select(0, keep).contiguous()
+        std = self.std.index_select(0, keep).contiguous()
+        self._model_and_mosaic(tiles, self.lr[:nt], self.sr[:nt], self.interp[:nt], mean, std, inv, nt)

@@ -1,0 +1,112 @@
+"""Tiled-region inference on the HIP path (srmi.inference.TiledInference, the
+srmi_region_to_tiles / srmi_tiles_to_region kernels) against the oracle's
+restatement of process_image + assemble_images (parity pinned by restatement:
+the reference's own functions need xarray, which is absent)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import rcan_oracle as ro  # noqa: E402
+from srmi._lib import call, ptr  # noqa: E402
+from srmi.engine import NetSpec, param_table  # noqa: E402
+from srmi.inference import TiledInference  # noqa: E402
+
+
+def dev():
+    assert torch.cuda.is_available()
+    return torch.device("cuda", 0)
+
+
+def rel_l2(a, b):
+    a = torch.as_tensor(np.asarray(a, dtype=np.float64))
+    b = torch.as_tensor(np.asarray(b, dtype=np.float64))
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def test_region_tiles_kernels():
+    d = dev()
+    rng = np.random.RandomState(4)
+    region = (rng.randn(2, 3 * 40 + 7, 2 * 56 + 3) * 3 + 1).astype(np.float32)
+    C, H, W = region.shape
+    ty, tx = 40, 56
+    n = (H // ty) * (W // tx)
+    rg = torch.tensor(region, device=d)
+    tiles = torch.empty(n, C, ty, tx, device=d)
+    mean = torch.empty(n, C, device=d)
+    std = torch.empty(n, C, device=d)
+    bad = torch.empty(n, dtype=torch.int32, device=d)
+    st = torch.cuda.current_stream().cuda_stream
+    call("srmi_region_to_tiles", ptr(rg), C, H, W, ty, tx, ptr(tiles), ptr(mean), ptr(std), ptr(bad), st)
+    ref_t, ref_m, ref_s, ids, grid = ro.region_to_tiles(region.astype(np.float64), ty, tx)
+    assert list(ids) == list(range(n)) and int(bad.sum()) == 0
+    np.testing.assert_allclose(mean.cpu().numpy(), ref_m, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(std.cpu().numpy(), ref_s, rtol=1e-5)
+    np.testing.assert_allclose(tiles.cpu().numpy(), ref_t, atol=2e-5)
+    out = torch.empty(C, grid[0] * ty, grid[1] * tx, device=d)
+    call("srmi_tiles_to_region", ptr(tiles), ptr(mean), ptr(std), None, C, ty, tx, grid[0], grid[1], ptr(out), st)
+    np.testing.assert_allclose(out.cpu().numpy(), region[:, :grid[0] * ty, :grid[1] * tx], rtol=1e-5, atol=1e-4)
+    # a NaN marks its tile bad; an inverse map with -1 leaves that cell NaN
+    region2 = region.copy()
+    region2[1, ty + 3, 5] = np.nan
+    call("srmi_region_to_tiles", ptr(torch.tensor(region2, device=d)), C, H, W, ty, tx, ptr(tiles), ptr(mean),
+         ptr(std), ptr(bad), st)
+    assert bad.cpu().tolist() == [0, 0, 1, 0, 0, 0]
+    inv = torch.tensor([0, 1, -1, 2, 3, 4], dtype=torch.int32, device=d)
+    call("srmi_tiles_to_region", ptr(tiles), None, None, ptr(inv), C, ty, tx, grid[0], grid[1], ptr(out), st)
+    o = out.cpu().numpy()
+    assert np.isnan(o[:, ty:2 * ty, 0:tx]).all() and np.isfinite(o[:, :ty]).all()
+
+
+def _small_rcan():
+    spec = NetSpec(arch="rcan", nchannels_in=1, nchannels_out=1, nfeatures=64, nlayers=1, nblocks=2, cbottleneck=2,
+                   scale=4)
+    model = ro.RCANOracle(nchannels_in=1, nchannels_out=1, nlayers=1, nblocks=2).double()
+    ro.init_params_numpy(model, 11)
+    table = param_table(spec)
+    sd = dict(model.named_parameters())
+    flat = torch.empty(sum(t[2] for t in table), dtype=torch.float32)
+    for name, off, n, shape in table:
+        flat[off:off + n] = sd[name].detach().float().reshape(-1)
+    return spec, model, flat
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_tiled_inference_matches_oracle(graph):
+    d = dev()
+    spec, model, flat = _small_rcan()
+    rng = np.random.RandomState(7)
+    # smooth-ish field so the bicubic baseline is meaningful; ragged edge cropped
+    base = rng.randn(1, 2 * 192 + 17, 3 * 192 + 9)
+    region = (base + np.roll(base, 1, 1) + np.roll(base, 1, 2)).astype(np.float32)
+    ti = TiledInference(spec, flat.to(d), region.shape, (192, 192), device=d, graph=graph)
+    images, losses = ti.process_region(torch.tensor(region, device=d))
+    ref_img, ref_loss = ro.process_region(model, region.astype(np.float64), 192, 192, 4)
+    for k in ("input", "target", "interpolated"):
+        assert rel_l2(images[k].cpu().numpy(), ref_img[k]) < 1e-5, k
+    assert rel_l2(images["model"].cpu().numpy(), ref_img["model"]) < 2e-2
+    assert abs(float(losses["interpolated"]) - ref_loss["interpolated"]) < 1e-5 * ref_loss["interpolated"] + 1e-7
+    assert abs(float(losses["model"]) - ref_loss["model"]) < 2e-3 * ref_loss["model"]
+    # a second region through the same (captured) pipeline
+    region2 = (region[:, ::-1, :].copy() * 0.5 + 2.0).astype(np.float32)
+    images2, losses2 = ti.process_region(torch.tensor(region2, device=d))
+    ref_img2, ref_loss2 = ro.process_region(model, region2.astype(np.float64), 192, 192, 4)
+    assert rel_l2(images2["target"].cpu().numpy(), ref_img2["target"]) < 1e-5
+    assert rel_l2(images2["model"].cpu().numpy(), ref_img2["model"]) < 2e-2
+
+
+def test_tiled_inference_drops_nonfinite_tiles():
+    d = dev()
+    spec, model, flat = _small_rcan()
+    rng = np.random.RandomState(8)
+    region = rng.randn(1, 2 * 192, 2 * 192).astype(np.float32)
+    region[0, 200, 10] = np.nan  # tile (1, 0) -> id 2
+    ti = TiledInference(spec, flat.to(d), region.shape, (192, 192), device=d, graph=True)
+    images, losses = ti.process_region(torch.tensor(region, device=d))
+    ref_img, ref_loss = ro.process_region(model, region.astype(np.float64), 192, 192, 4)
+    m = images["model"].cpu().numpy()
+    assert np.isnan(m[0, 192:, :192]).all() and np.isnan(ref_img["model"][0, 192:, :192]).all()
+    keep = np.isfinite(ref_img["model"])
+    assert rel_l2(m[keep], ref_img["model"][keep]) < 2e-2
+    assert abs(float(losses["model"]) - ref_loss["model"]) < 2e-3 * ref_loss["model"]
