@@ -33,9 +33,12 @@ void conv3x3_set_debug_stamps(unsigned long long* buf) { g_debug_stamps = buf; }
 // Phase stamps exist only in the diagnostic build (make stamps): even a disabled
 // stamp store makes the compiler drain vmcnt where its data registers are reused.
 #ifdef SRMI_STAMPS
-#define STAMP(i)                                                                     \
-  do {                                                                               \
-    if (p.stamps && tid == 0) p.stamps[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
+#define STAMP(i)                                                                                   \
+  do {                                                                                             \
+    if (p.stamps && tid == 0) {                                                                    \
+      p.stamps[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memtime();                              \
+      if ((i) == 0 || (i) == 61) p.stamps[blockIdx.x * 64 + 62 + ((i) == 61)] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                                              \
   } while (0)
 #else
 #define STAMP(i) \
@@ -631,6 +634,7 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
     asm volatile("" ::: "memory");
     STAMP(sj + 4);
   }
+  STAMP(61);
 }
 
 template <int TW, int EPI>

@@ -186,6 +186,12 @@ struct srmi_engine {
   bf16_t* dPS[3];
   float *slab, *bslab;
   size_t slab_floats, bslab_floats;
+  // side stream for the RCAB filter gradients (overlapped with the dgrad chain)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_du[2] = {}, ev_dz[2] = {}, ev_w2[2] = {}, ev_w1[2] = {}, ev_grp = nullptr, ev_side = nullptr;
+  bf16_t *DUr[2] = {}, *DZr[2] = {};  // double-buffered RCAB gradients (ring of 2 blocks)
+  float *slab_s = nullptr, *bslab_s = nullptr;
+  size_t slab_s_floats = 0, bslab_s_floats = 0;
   float* lpart;
   int lpart_n;
   float* zeros;  // 256 zero bytes (DMA padding source)
@@ -252,6 +258,10 @@ static size_t carve(srmi_engine* e, char* base) {
     e->GBb = cv.take<bf16_t>(m);
     e->DU = cv.take<bf16_t>(m);
     e->DZ = cv.take<bf16_t>(m);
+    e->DUr[0] = e->DU;
+    e->DZr[0] = e->DZ;
+    e->DUr[1] = rcan ? cv.take<bf16_t>(m) : e->DU;
+    e->DZr[1] = rcan ? cv.take<bf16_t>(m) : e->DZ;
     e->dRESb = cv.take<bf16_t>(m);
     for (int k = 0; k < 3; ++k) e->dPS[k] = nullptr;
     for (int k = 0; k < P.nups; ++k) e->dPS[k] = cv.take<bf16_t>(m << (2 * (k + 1)));
@@ -273,6 +283,13 @@ static size_t carve(srmi_engine* e, char* base) {
     e->bslab_floats = bf;
     e->slab = cv.take<float>(sf);
     e->bslab = cv.take<float>(bf);
+    if (rcan) {  // the side stream's own slabs (64-channel RCAB convs only)
+      const size_t ns = (size_t)N * choose_row_splits(N, e->h, 64);
+      e->slab_s_floats = ns * 64 * 576;
+      e->bslab_s_floats = ns * 64;
+      e->slab_s = cv.take<float>(e->slab_s_floats);
+      e->bslab_s = cv.take<float>(e->bslab_s_floats);
+    }
   }
   e->packs = cv.take<bf16_t>(P.pack_elems);
   e->pbias = cv.take<float>(P.pbias_elems);
@@ -380,7 +397,7 @@ static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n,
 }
 
 static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const bf16_t* dy, int n, int H, int W,
-                      float* grads, bool with_bias, float alpha, hipStream_t st) {
+                      float* grads, bool with_bias, float alpha, hipStream_t st, bool side = false) {
   WgradParams p{};
   p.x = x;
   p.dy = dy;
@@ -391,14 +408,15 @@ static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const b
   p.dy_mode = c.ps ? IN_UNSHUF : IN_PLAIN;
   p.imgs_per_wg = 1;
   p.row_splits = choose_row_splits(n, H, c.cout);
-  p.slab = e->slab;
-  p.bslab = e->bslab;
+  p.slab = side ? e->slab_s : e->slab;
+  p.bslab = side ? e->bslab_s : e->bslab;
   p.zeros = e->zeros;
   const size_t ns = (size_t)wgrad3x3_nslabs(p);
-  if (ns * c.cout * 576 > e->slab_floats || ns * c.cout > e->bslab_floats) return SRMI_ERR_WORKSPACE;
+  const size_t cap = side ? e->slab_s_floats : e->slab_floats, bcap = side ? e->bslab_s_floats : e->bslab_floats;
+  if (ns * c.cout * 576 > cap || ns * c.cout > bcap) return SRMI_ERR_WORKSPACE;
   int rc = wgrad3x3_launch(p, st);
   if (rc) return rc;
-  return wgrad_reduce_launch(e->slab, e->bslab, (int)ns, c.cout, c.ps, alpha, grads + c.w,
+  return wgrad_reduce_launch(p.slab, p.bslab, (int)ns, c.cout, c.ps, alpha, grads + c.w,
                              with_bias ? grads + c.b : nullptr, st);
 }
 
@@ -406,6 +424,11 @@ static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const b
   do {                     \
     int _rc = (x);         \
     if (_rc) return _rc;   \
+  } while (0)
+#define HC(x)                                  \
+  do {                                         \
+    const hipError_t _he = (x);                \
+    if (_he != hipSuccess) return -(int)_he;   \
   } while (0)
 
 static int upload_tables(srmi_engine* e, hipStream_t st) {
@@ -508,6 +531,7 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
     RC(conv_wgrad(e, P.body_tail, e->hb(nl, 0), e->dRESb, n, h, w, grads, true, 1.f, st));
     RC(conv_dgrad(e, P.body_tail, e->dRESb, n, h, w, EPI_DG_ACC, gRb, gRf, nullptr, nullptr, nullptr, nullptr, nullptr,
                   1.f, st));
+    int it = 0;  // RCAB counter (buffer ring parity)
     for (int g = nl - 1; g >= 0; --g) {
       const ConvRef& gt = P.group_tail[g];
       RC(conv_wgrad(e, gt, e->hb(g, nb), gRb, n, h, w, grads, true, 1.f, st));
@@ -515,14 +539,30 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
                     1.f, st));
       for (int b = nb; b >= 1; --b) {
         const RCABRef& r = P.groups[g][b - 1];
-        RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, e->DU,
+        // The two filter gradients of this RCAB run on the side stream, overlapped with
+        // the dgrad chain; DU/DZ alternate between two buffers, and a buffer is only
+        // rewritten after the side stream has finished the wgrad that read it.
+        const int q = it & 1;
+        const bool reuse = it >= 2;
+        ++it;
+        bf16_t* du = e->DUr[q];
+        bf16_t* dz = e->DZr[q];
+        if (reuse) HC(hipStreamWaitEvent(st, e->ev_w2[q], 0));
+        RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
                             e->brecp(g, b), st));
-        RC(conv_wgrad(e, r.c2, e->Tm(g, b), e->DU, n, h, w, grads, false, 1.f, st));
-        RC(conv_dgrad(e, r.c2, e->DU, n, h, w, EPI_DG_RELUMASK, e->DZ, nullptr, nullptr, nullptr, nullptr, e->Tm(g, b),
+        HC(hipEventRecord(e->ev_du[q], st));
+        HC(hipStreamWaitEvent(e->side, e->ev_du[q], 0));
+        RC(conv_wgrad(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, e->side, true));
+        HC(hipEventRecord(e->ev_w2[q], e->side));
+        if (reuse) HC(hipStreamWaitEvent(st, e->ev_w1[q], 0));
+        RC(conv_dgrad(e, r.c2, du, n, h, w, EPI_DG_RELUMASK, dz, nullptr, nullptr, nullptr, nullptr, e->Tm(g, b),
                       nullptr, 1.f, st));
-        RC(conv_wgrad(e, r.c1, e->hb(g, b - 1), e->DZ, n, h, w, grads, true, 1.f, st));
+        HC(hipEventRecord(e->ev_dz[q], st));
+        HC(hipStreamWaitEvent(e->side, e->ev_dz[q], 0));
+        RC(conv_wgrad(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, e->side, true));
+        HC(hipEventRecord(e->ev_w1[q], e->side));
         const bool last = (b == 1);
-        RC(conv_dgrad(e, r.c1, e->DZ, n, h, w, EPI_DG_ACC, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
+        RC(conv_dgrad(e, r.c1, dz, n, h, w, EPI_DG_ACC, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
                       (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
                       last ? nullptr : e->pacc, 1.f, st));
       }
@@ -531,8 +571,11 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
       std::swap(gRf, ghf);
       std::swap(gRb, ghb);
       if (group_events && group_events[g]) {
-        hipError_t er = hipEventRecord(reinterpret_cast<hipEvent_t>(group_events[g]), st);
-        if (er != hipSuccess) return -(int)er;
+        // the group's gradients are final once main (CA grads, dgrad chain) and the
+        // side stream (filter gradients) are both past it
+        HC(hipEventRecord(e->ev_grp, st));
+        HC(hipStreamWaitEvent(e->side, e->ev_grp, 0));
+        HC(hipEventRecord(reinterpret_cast<hipEvent_t>(group_events[g]), e->side));
       }
     }
   } else {
@@ -551,6 +594,10 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
       std::swap(gRf, ghf);
       std::swap(gRb, ghb);
     }
+  }
+  if (P.cfg.arch == SRMI_ARCH_RCAN) {  // every side-stream filter gradient is in grads
+    HC(hipEventRecord(e->ev_side, e->side));
+    HC(hipStreamWaitEvent(st, e->ev_side, 0));
   }
   // head: only the weight gradient (the input gradient is never read)
   RC(head_wgrad_launch(lr, gRf, n, e->C, h, w, e->slab, &nsl, st));
@@ -606,11 +653,26 @@ int srmi_engine_create(const srmi_model_config* cfg, void* workspace, size_t ws_
     return SRMI_ERR_WORKSPACE;
   }
   carve(e, base);
+  if (train && e->P.cfg.arch == SRMI_ARCH_RCAN) {
+    HC(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
+    hipEvent_t* evs[] = {&e->ev_du[0], &e->ev_du[1], &e->ev_dz[0], &e->ev_dz[1], &e->ev_w2[0],
+                         &e->ev_w2[1], &e->ev_w1[0], &e->ev_w1[1], &e->ev_grp, &e->ev_side};
+    for (hipEvent_t* ev : evs) HC(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+  }
   *out = e;
   return 0;
 }
 
 int srmi_engine_destroy(srmi_engine* e) {
+  if (!e) return 0;
+  hipEvent_t evs[] = {e->ev_du[0], e->ev_du[1], e->ev_dz[0], e->ev_dz[1], e->ev_w2[0],
+                      e->ev_w2[1], e->ev_w1[0], e->ev_w1[1], e->ev_grp, e->ev_side};
+  for (hipEvent_t ev : evs)
+    if (ev) (void)hipEventDestroy(ev);
+  if (e->side) {
+    (void)hipStreamSynchronize(e->side);
+    (void)hipStreamDestroy(e->side);
+  }
   delete e;
   return 0;
 }

@@ -151,7 +151,12 @@ def stamps():
         st = buf.view(4096, 64).cpu().numpy()
         st = st[st[:, 0] != 0]
         rel = st - st[:, 0:1]
-        print(f"conv epi={epi} workgroups", len(st), "start spread (cycles)", int(st[:, 0].max() - st[:, 0].min()))
+        rt = st[:, 62:64].astype(np.float64)  # s_memrealtime (100 MHz) at start / end
+        clk = np.median((st[:, 61] - st[:, 0]) / np.maximum(rt[:, 1] - rt[:, 0], 1)) * 100.0
+        span_us = (rt[:, 1] - rt[:, 0]) / 100.0
+        print(f"conv epi={epi} workgroups {len(st)} clock {clk:.0f} MHz  WG span median {np.median(span_us):.2f} us "
+              f"max {span_us.max():.2f} us; WG start spread {(rt[:, 0].max() - rt[:, 0].min()) / 100.0:.2f} us, "
+              f"first start -> last end {(rt[:, 1].max() - rt[:, 0].min()) / 100.0:.2f} us")
         names = ["prologue"] + [f"s{j}:{k}" for j in range(3) for k in ("issue", "mfma", "gstore", "epi", "barrier")]
         prev = np.zeros(len(st))
         for i, nm in enumerate(names, start=1):
