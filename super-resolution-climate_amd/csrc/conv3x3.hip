@@ -35,7 +35,7 @@ void conv3x3_set_debug_stamps(unsigned long long* buf) { g_debug_stamps = buf; }
 #ifdef SRMI_STAMPS
 #define STAMP(i)                                                                                   \
   do {                                                                                             \
-    if (p.stamps && threadIdx.x == 0) {                                                            \
+    if (p.stamps && tid == 0) {                                                                    \
       p.stamps[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memtime();                              \
       if ((i) == 0 || (i) == 61) p.stamps[blockIdx.x * 64 + 62 + ((i) == 61)] = __builtin_amdgcn_s_memrealtime(); \
     }                                                                                              \
@@ -491,11 +491,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
 }
 
 template <int TW, int EPI, int PM>
-// 512 threads: waves 0-3 (one per SIMD) do the MFMAs and epilogues, waves 4-7 are
-// loaders that only issue the LDS-DMA of the next input row group, so a full
-// memory queue stalls a loader, never an MFMA wave.  Both kinds pass the same
-// barriers (prologue, the POOL/ACC epilogue's reduction, end of strip).
-__global__ void __launch_bounds__(2 * kThreads, 1) conv64_kernel(ConvParams p, int run_len) {
+__global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int run_len) {
   using S = Conv2Smem<TW>;
   constexpr int NPT = TW / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -503,8 +499,7 @@ __global__ void __launch_bounds__(2 * kThreads, 1) conv64_kernel(ConvParams p, i
   char* ring = smem + S::WB;
   float* red = reinterpret_cast<float*>(smem + S::WB + S::RING);
 
-  const int tid = threadIdx.x & (kThreads - 1), lane = tid & 63, wave = tid >> 6;
-  const bool loader = threadIdx.x >= kThreads;  // wave-uniform
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fk = lane >> 4;
   const int nsx = p.W / TW, nsy = p.H / kTH;
   const int runs_per_col = (nsy + run_len - 1) / run_len;
@@ -545,9 +540,9 @@ __global__ void __launch_bounds__(2 * kThreads, 1) conv64_kernel(ConvParams p, i
     for (int i = wv_s; i < NGRP; i += 4) group_dma_one(gidx, i);
   };
 
-  // prologue (loaders): filters (all 9 taps, 72 KiB) and input groups k0, k0+1, all
-  // by LDS-DMA (swizzle on the source side), everything in flight before the one wait.
-  if (loader) {
+  // prologue: filters (all 9 taps, 72 KiB) and input groups k0, k0+1, all by LDS-DMA
+  // (swizzle on the source side), everything in flight before the one wait.
+  {
     const uint32_t wbase = lds_u32(wl);
     for (int i = wv_s; i < 72; i += 4) {
       const int tap = i >> 3, row = 8 * (i & 7) + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
@@ -559,86 +554,81 @@ __global__ void __launch_bounds__(2 * kThreads, 1) conv64_kernel(ConvParams p, i
   }
   STAMP(1);
   float4 bias[4];
-  uint32_t aoff[2][4];  // lane-constant A-fragment byte offsets (tap adds 8192)
-  if (!loader) {
+  {
     const float* bp = p.bias ? p.bias : reinterpret_cast<const float*>(kZeros);  // pointer select, no branch
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) bias[ct] = *reinterpret_cast<const float4*>(bp + cb * 64 + ct * 16 + fk * 4);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) aoff[kk][ct] = swz128(ct * 16 + fr, kk * 4 + fk);
   }
+  // lane-constant A-fragment byte offsets (tap adds 8192)
+  uint32_t aoff[2][4];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) aoff[kk][ct] = swz128(ct * 16 + fr, kk * 4 + fk);
   __syncthreads();
 
-  constexpr bool kEpiBarrier = (EPI == EPI_POOL_BF16 || EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_CA);
 #pragma unroll 1
   for (int k = k0; k < k1; ++k) {
+    const int y = 4 * k + wave;
     const bool pf = (k + 1 < k1);
+    // group k+2 -> ring slot (k+2)%3, which held group k-1 (last read by strip k-1,
+    // released by the barrier that ended it)
+    EpiPre<NPT, EPI> ep;
     [[maybe_unused]] const int sj = 2 + 5 * min(k - k0, 11);
-    if (loader) {
-      // group k+2 -> ring slot (k+2)%3, which held group k-1 (last read by strip k-1,
-      // released by the barrier that ended it); landed before the end-of-strip barrier
-      if (pf) group_dma(k + 2);
-      wait_vm<0>();
-      if constexpr (kEpiBarrier) {  // the epilogue's channel-sum reduction barrier
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-      }
-    } else {
-      const int y = 4 * k + wave;
-      EpiPre<NPT, EPI> ep;
-      STAMP(sj);
+    STAMP(sj);
 
-      // B-fragment byte offsets per (ky, kx, kk); +2048 per 16-pixel tile
-      uint32_t boff[3][3][2];
+    // B-fragment byte offsets per (ky, kx, kk); +2048 per 16-pixel tile
+    uint32_t boff[3][3][2];
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {
-        const int rr = y + ky - 1 + 3;  // >= 2
-        const int slot = ((rr >> 2) % 3) * 4 + (rr & 3);
+    for (int ky = 0; ky < 3; ++ky) {
+      const int rr = y + ky - 1 + 3;  // >= 2
+      const int slot = ((rr >> 2) % 3) * 4 + (rr & 3);
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx)
+      for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-          for (int kk = 0; kk < 2; ++kk) boff[ky][kx][kk] = swz128(slot * (TW + 2) + fr + kx, kk * 4 + fk);
-      }
-
-      f32x4 acc[NPT][4];
-#pragma unroll
-      for (int i = 0; i < NPT; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-      // 18 K-steps (9 taps x 2 halves of 32 ci), fragments double-buffered in
-      // registers: step s+1's ds_reads are in flight while step s's 12 MFMAs run.
-      bf16x8 A[2][4], B[2][NPT];
-      auto load_step = [&](int s, bf16x8 (&a)[4], bf16x8 (&b)[NPT]) __attribute__((always_inline)) {
-        const int tap = s >> 1, kk = s & 1, ky = tap / 3, kx = tap % 3;
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) a[ct] = lds_frag(wl, tap * 8192 + aoff[kk][ct]);
-#pragma unroll
-        for (int pt = 0; pt < NPT; ++pt) b[pt] = lds_frag(ring, boff[ky][kx][kk] + pt * 2048);
-      };
-      load_step(0, A[0], B[0]);
-#pragma unroll
-      for (int s = 0; s < 18; ++s) {
-        // epilogue operands issued one per K-step from step 2 on
-        if (s >= 2 && s - 2 < NPT * 4) epi_prefetch_one<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk, s - 2);
-        if (s + 1 < 18) load_step(s + 1, A[(s + 1) & 1], B[(s + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int pt = 0; pt < NPT; ++pt)
-#pragma unroll
-          for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = mfma16(A[s & 1][ct], B[s & 1][pt], acc[pt][ct]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      wait_vm<0>();  // epilogue operands (and the previous strip's stores)
-      STAMP(sj + 1);
-      STAMP(sj + 2);
-      conv_epilogue2<NPT, EPI>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx, nsy * nsx, red, fr, fk, wave, tid);
-      STAMP(sj + 3);
+        for (int kk = 0; kk < 2; ++kk) boff[ky][kx][kk] = swz128(slot * (TW + 2) + fr + kx, kk * 4 + fk);
     }
-    // LDS-only barrier: the MFMA waves' global stores stay in flight into the next strip
+
+    f32x4 acc[NPT][4];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // 18 K-steps (9 taps x 2 halves of 32 ci), fragments double-buffered in
+    // registers: step s+1's ds_reads are in flight while step s's 12 MFMAs run.
+    bf16x8 A[2][4], B[2][NPT];
+    auto load_step = [&](int s, bf16x8 (&a)[4], bf16x8 (&b)[NPT]) __attribute__((always_inline)) {
+      const int tap = s >> 1, kk = s & 1, ky = tap / 3, kx = tap % 3;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) a[ct] = lds_frag(wl, tap * 8192 + aoff[kk][ct]);
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt) b[pt] = lds_frag(ring, boff[ky][kx][kk] + pt * 2048);
+    };
+    load_step(0, A[0], B[0]);
+#pragma unroll
+    for (int s = 0; s < 18; ++s) {
+      // group k+2's DMA pieces and the epilogue operands are issued one or two per
+      // K-step, so a full memory queue stalls the wave between MFMA groups only
+      if (s < NGW && pf && wv_s + 4 * s < NGRP) group_dma_one(k + 2, wv_s + 4 * s);
+      if (s >= 2 && s - 2 < NPT * 4) epi_prefetch_one<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk, s - 2);
+      if (s + 1 < 18) load_step(s + 1, A[(s + 1) & 1], B[(s + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = mfma16(A[s & 1][ct], B[s & 1][pt], acc[pt][ct]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // group k+2's DMA, the epilogue operands and the previous strip's stores had the
+    // whole MFMA phase to land: drain them here, before the epilogue (the barrier at
+    // the end of the strip then publishes group k+2 to every wave)
+    wait_vm<0>();
+    STAMP(sj + 1);
+    STAMP(sj + 2);
+    conv_epilogue2<NPT, EPI>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx, nsy * nsx, red, fr, fk, wave, tid);
+    STAMP(sj + 3);
+    // LDS-only barrier: this strip's global stores stay in flight into the next strip
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -661,7 +651,7 @@ static int launch_tw(const ConvParams& p, hipStream_t st) {
     ConvParams q = p;
     q.stamps = g_debug_stamps;
     // prologue mode 2 (filters by LDS-DMA, input groups register-staged) measured fastest
-    hipLaunchKernelGGL((conv64_kernel<TW, EPI, 2>), grid, dim3(2 * kThreads), Conv2Smem<TW>::TOTAL, st, q, run_len);
+    hipLaunchKernelGGL((conv64_kernel<TW, EPI, 2>), grid, dim3(kThreads), Conv2Smem<TW>::TOTAL, st, q, run_len);
   } else {
     constexpr int E1 = EPI == EPI_DG_ACC_CA ? EPI_DG_ACC : EPI;  // v1 handles the general form
     dim3 grid((p.H / kTH) * (p.W / TW), p.Cout / 64, p.N);
