@@ -56,6 +56,8 @@ typedef struct srmi_model_config {
   float res_scale;   /* EDSR model.res_scale                                */
   int batch;         /* max tiles per call (workspace capacity)             */
   int lr_h, lr_w;    /* LR tile size, e.g. 48 x 48                          */
+  int cu_budget;     /* CUs one launch should fill (0 = the whole GPU); two
+                        engines on two streams each take half the chip     */
 } srmi_model_config;
 
 typedef struct srmi_param_info {
@@ -109,6 +111,9 @@ int srmi_upsample(const float* lr, int N, int C, int h, int w, int scale, float*
 /* Adam on flat buffers, step counted from 1 */
 int srmi_adam_step(float* p, const float* g, float* m, float* v, size_t n, int step, float lr, float beta1,
                    float beta2, float eps, float weight_decay, void* stream);
+
+/* y += a * x (flat fp32; sums micro-batch gradients) */
+int srmi_axpy(float* y, const float* x, float a, size_t n, void* stream);
 
 /* ---- op-level entry points (kernel parity tests, custom graphs) ---------- */
 /* forward conv: x NHWC bf16 [N][H][W][Cin], packed filters (srmi_pack_conv),

@@ -643,7 +643,8 @@ static int launch_tw(const ConvParams& p, hipStream_t st) {
     // v2: persistent runs; ~1 workgroup per CU (LDS-limited), each a run of strips
     const int nsy = p.H / kTH;
     const int units = (p.Cout / 64) * p.N * (p.W / TW);
-    int R = (256 + units / 2) / units;
+    const int cus = p.cu_budget > 0 ? p.cu_budget : 256;
+    int R = (cus + units / 2) / units;
     R = R < 1 ? 1 : (R > nsy ? nsy : R);
     const int run_len = (nsy + R - 1) / R;
     const int runs = (nsy + run_len - 1) / run_len;

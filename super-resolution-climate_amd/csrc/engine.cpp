@@ -152,14 +152,16 @@ struct Carver {
   }
 };
 
-int choose_row_splits(int N, int H, int Cout) {
-  // wgrad grid = N*rs chunks x Cout/64 (one workgroup per CU by LDS); aim at >= 192
-  // workgroups while keeping as few partial slabs (N*rs) as possible; rows per chunk % 4 == 0
+int choose_row_splits(int N, int H, int Cout, int cu_budget = 0) {
+  // wgrad grid = N*rs chunks x Cout/64 (one workgroup per CU by LDS); aim at >= 3/4
+  // of the CU budget while keeping as few partial slabs (N*rs) as possible; rows per
+  // chunk % 4 == 0
+  const int target = 3 * (cu_budget > 0 ? cu_budget : 256) / 4;
   int best = 1;
   for (int rs = 1; rs <= H / 4; ++rs) {
     if (H % rs || (H / rs) % 4) continue;
     best = rs;
-    if (N * rs * (Cout / 64) >= 192) break;
+    if (N * rs * (Cout / 64) >= target) break;
   }
   return best;
 }
@@ -170,6 +172,7 @@ struct srmi_engine {
   Plan P;
   int train = 0;
   int N = 0, h = 0, w = 0, C = 0, Co = 0, S = 0;
+  int cu_budget = 0;  // CUs one launch aims to fill (0 = all)
   size_t mapn = 0;  // elements of one [N][h][w][64] map
   // forward state
   float *X0f, *Rf, *Hf;
@@ -268,7 +271,7 @@ static size_t carve(srmi_engine* e, char* base) {
     // slab: max over all wgrads
     size_t sf = 0, bf = 0;
     auto upd = [&](int H, int W, int Cout) {
-      const int rs = choose_row_splits(N, H, Cout);
+      const int rs = choose_row_splits(N, H, Cout, e->cu_budget);
       const size_t ns = (size_t)N * rs;
       sf = std::max(sf, ns * Cout * 576);
       bf = std::max(bf, ns * Cout);
@@ -284,7 +287,7 @@ static size_t carve(srmi_engine* e, char* base) {
     e->slab = cv.take<float>(sf);
     e->bslab = cv.take<float>(bf);
     if (rcan) {  // the side stream's own slabs (64-channel RCAB convs only)
-      const size_t ns = (size_t)N * choose_row_splits(N, e->h, 64);
+      const size_t ns = (size_t)N * choose_row_splits(N, e->h, 64, e->cu_budget);
       e->slab_s_floats = ns * 64 * 576;
       e->bslab_s_floats = ns * 64;
       e->slab_s = cv.take<float>(e->slab_s_floats);
@@ -308,6 +311,7 @@ static int init_engine(srmi_engine* e, const srmi_model_config* cfg, int train) 
   e->C = cfg->nchannels_in;
   e->Co = cfg->nchannels_out;
   e->S = cfg->scale;
+  e->cu_budget = cfg->cu_budget > 0 ? cfg->cu_budget : 0;
   e->mapn = (size_t)e->N * e->h * e->w * 64;
   if (e->h % 4 || (e->w % 32 && e->w % 48)) return SRMI_ERR_SHAPE;
   const int Hs = e->h * e->S;
@@ -364,6 +368,7 @@ static int conv_fwd(srmi_engine* e, const ConvRef& c, const bf16_t* x, int n, in
   p.part_stride = 64;
   p.alpha = alpha;
   p.zeros = e->zeros;
+  p.cu_budget = e->cu_budget;
   return conv3x3_launch(p, epi, st);
 }
 
@@ -391,6 +396,7 @@ static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n,
   p.part_stride = 128;
   p.alpha = alpha;
   p.zeros = e->zeros;
+  p.cu_budget = e->cu_budget;
   if (epi == EPI_DG_ACC && r1 && aux && part && !yb && !r2 && !r3 && yf && c.cout == 64 && !c.ps)
     epi = EPI_DG_ACC_CA;  // the hot RCAB case: specialised epilogue without runtime operand checks
   return conv3x3_launch(p, epi, st);
@@ -407,7 +413,7 @@ static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const b
   p.Cout = c.cout;
   p.dy_mode = c.ps ? IN_UNSHUF : IN_PLAIN;
   p.imgs_per_wg = 1;
-  p.row_splits = choose_row_splits(n, H, c.cout);
+  p.row_splits = choose_row_splits(n, H, c.cout, e->cu_budget);
   p.slab = side ? e->slab_s : e->slab;
   p.bslab = side ? e->bslab_s : e->bslab;
   p.zeros = e->zeros;
@@ -822,6 +828,11 @@ int srmi_tiles_to_region(const float* tiles, const float* mean, const float* std
                          int tx, int gy, int gx, float* out, void* stream) {
   if (!tiles || !out || (mean && !std)) return SRMI_ERR_ARG;
   return tiles_to_region_launch(tiles, mean, std, inv, C, ty, tx, gy, gx, out, S_(stream));
+}
+
+int srmi_axpy(float* y, const float* x, float a, size_t n, void* stream) {
+  if (!y || !x) return SRMI_ERR_ARG;
+  return scale_add_launch(y, x, a, n, S_(stream));
 }
 
 }  // extern "C"

@@ -41,6 +41,7 @@ struct ConvParams {
   float alpha;
   const void* zeros;   // >= 16 zero bytes in global memory (DMA padding source)
   unsigned long long* stamps;  // diagnostic s_memtime stamps (null in production)
+  int cu_budget;               // CUs a launch should fill (0 = all 256)
 };
 
 void conv3x3_set_debug_stamps(unsigned long long* buf);

@@ -24,7 +24,7 @@ class ModelConfig(C.Structure):
     _fields_ = [("arch", C.c_int), ("nchannels_in", C.c_int), ("nchannels_out", C.c_int),
                 ("nfeatures", C.c_int), ("nlayers", C.c_int), ("nblocks", C.c_int), ("reduction", C.c_int),
                 ("scale", C.c_int), ("res_scale", C.c_float), ("batch", C.c_int), ("lr_h", C.c_int),
-                ("lr_w", C.c_int)]
+                ("lr_w", C.c_int), ("cu_budget", C.c_int)]
 
 
 class ParamInfo(C.Structure):
@@ -61,6 +61,7 @@ _SIGS = {
     "srmi_ca_backward": ([P, P, C.c_int, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P], C.c_int),
     "srmi_head_forward": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P], C.c_int),
     "srmi_tail_forward": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),
+    "srmi_axpy": ([P, P, C.c_float, C.c_size_t, P], C.c_int),
     "srmi_region_to_tiles": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P], C.c_int),
     "srmi_tiles_to_region": ([P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),
 }

@@ -125,8 +125,10 @@ class GradReducer:
     def covered(self) -> int:
         return sum(n for b in self.buckets for _, n in b.ranges)
 
-    def reduce(self, grads: torch.Tensor):
-        """Call right after the (asynchronous) backward has been enqueued."""
+    def reduce(self, grads: torch.Tensor, events_recorded: bool = True):
+        """Call right after the (asynchronous) backward has been enqueued.  With
+        events_recorded False (the backward did not record the group events, e.g.
+        summed micro-batch gradients) every bucket waits for the current stream."""
         if not self.info.enabled:
             return
         if not self.cuda:
@@ -138,7 +140,7 @@ class GradReducer:
         works = []
         with torch.cuda.stream(self.stream):
             for b in self.buckets:
-                if b.event_index is not None:
+                if b.event_index is not None and events_recorded:
                     self.stream.wait_event(self.events[b.event_index])
                 else:
                     self.stream.wait_stream(main)

@@ -48,10 +48,10 @@ class NetSpec:
                        nblocks=int(parms.get("nblocks", 0) or 0), cbottleneck=int(parms.get("cbottleneck", 2) or 2),
                        scale=int(parms["scale"]), res_scale=float(parms.get("res_scale", 1.0)))
 
-    def cstruct(self, batch: int, lr_h: int, lr_w: int) -> ModelConfig:
+    def cstruct(self, batch: int, lr_h: int, lr_w: int, cu_budget: int = 0) -> ModelConfig:
         return ModelConfig(ARCHS[self.arch], self.nchannels_in, self.nchannels_out, self.nfeatures, self.nlayers,
                            self.nblocks if self.arch == "rcan" else 0, self.cbottleneck if self.arch == "rcan" else 1,
-                           self.scale, self.res_scale, batch, lr_h, lr_w)
+                           self.scale, self.res_scale, batch, lr_h, lr_w, int(cu_budget))
 
 
 def param_names(spec: NetSpec) -> List[str]:
@@ -92,13 +92,13 @@ def param_table(spec: NetSpec) -> List[Tuple[str, int, int, Tuple[int, ...]]]:
 
 class Engine:
     def __init__(self, spec: NetSpec, batch: int, lr_hw: Tuple[int, int], train: bool = True,
-                 device: Optional[torch.device] = None):
+                 device: Optional[torch.device] = None, cu_budget: int = 0):
         self.spec = spec
         self.batch = int(batch)
         self.lr_h, self.lr_w = int(lr_hw[0]), int(lr_hw[1])
         self.train_mode = bool(train)
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self._cfg = spec.cstruct(self.batch, self.lr_h, self.lr_w)
+        self._cfg = spec.cstruct(self.batch, self.lr_h, self.lr_w, cu_budget)
         nbytes = C.c_size_t()
         call("srmi_workspace_size", C.byref(self._cfg), int(train), C.byref(nbytes))
         self.workspace = torch.empty(int(nbytes.value) + 256, dtype=torch.uint8, device=self.device)
@@ -170,6 +170,13 @@ def upsample(lr: torch.Tensor, scale: int, out: Optional[torch.Tensor] = None, s
         out = torch.empty((N, Cc, h * scale, w * scale), dtype=torch.float32, device=lr.device)
     call("srmi_upsample", ptr(lr), N, Cc, h, w, scale, ptr(out), stream_handle(stream))
     return out
+
+
+def axpy(y: torch.Tensor, x: torch.Tensor, a: float = 1.0, stream=None):
+    """y += a * x on flat fp32 device buffers (HIP kernel)."""
+    assert y.numel() == x.numel() and y.dtype == x.dtype == torch.float32
+    call("srmi_axpy", ptr(y), ptr(x), float(a), y.numel(), stream_handle(stream))
+    return y
 
 
 def adam_step(p, g, m, v, step: int, lr: float, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, stream=None):

@@ -20,7 +20,15 @@ from typing import Dict, Optional
 import torch
 
 from .dist import DistInfo, GradReducer, allreduce_sum_
-from .engine import Engine, NetSpec, adam_step, downsample, upsample
+from .engine import Engine, NetSpec, adam_step, axpy, downsample, upsample
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
 
 
 def default_init_(flat: torch.Tensor, table, seed: int = 0) -> None:
@@ -36,15 +44,36 @@ def default_init_(flat: torch.Tensor, table, seed: int = 0) -> None:
 
 
 class FusedTrainer:
+    """One training step = dual_trainer.py:310-323 on the native engine.
+
+    micro > 1 splits the batch into `micro` equal micro-batches, each with its own
+    engine (workspace, filter packs, side stream) on its own HIP stream, launches
+    sized for 1/micro of the chip (cu_budget).  RCAN/EDSR have no coupling between
+    tiles except the loss scale and the gradient sum, so the step is exact: the
+    micro-batches' squared-error partials are added before the RMSE is finalised
+    (one global L, as with data parallelism) and their gradients are summed before
+    the all-reduce / Adam.  The two streams overlap each layer's launch ramp and
+    drain with the other micro-batch's work.
+    """
+
     def __init__(self, spec: NetSpec, batch: int, lr_hw=(48, 48), lr: float = 1e-4, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.0, interp_loss: bool = True,
                  info: Optional[DistInfo] = None, device: Optional[torch.device] = None, seed: int = 0,
-                 params: Optional[torch.Tensor] = None):
+                 params: Optional[torch.Tensor] = None, micro: Optional[int] = None):
         self.info = info or DistInfo()
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.spec = spec
         self.batch = batch
-        self.eng = Engine(spec, batch, lr_hw, train=True, device=self.device)
+        if micro is None:
+            micro = 2 if (batch % 2 == 0 and batch >= 16) else 1
+        if batch % micro:
+            raise ValueError(f"batch {batch} not divisible into {micro} micro-batches")
+        self.micro = micro
+        self.mb = batch // micro
+        budget = 256 // micro if micro > 1 else 0
+        self.engines = [Engine(spec, self.mb, lr_hw, train=True, device=self.device, cu_budget=budget)
+                        for _ in range(micro)]
+        self.eng = self.engines[0]
         n = self.eng.n_params
         self.params = torch.empty(n, dtype=torch.float32, device=self.device)
         if params is not None:
@@ -54,6 +83,8 @@ class FusedTrainer:
         if self.info.enabled:  # identical replicas (rank 0's weights)
             torch.distributed.broadcast(self.params, 0)
         self.grads = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.mgrads = [self.grads] + [torch.zeros(n, dtype=torch.float32, device=self.device)
+                                      for _ in range(micro - 1)]
         self.m = torch.zeros_like(self.grads)
         self.v = torch.zeros_like(self.grads)
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
@@ -65,33 +96,80 @@ class FusedTrainer:
         self.up = torch.empty_like(self.sr) if interp_loss else None
         self.loss4 = torch.zeros(4, dtype=torch.float32, device=self.device)
         self.iloss4 = torch.zeros(4, dtype=torch.float32, device=self.device)
+        self.mloss4 = [torch.zeros(4, dtype=torch.float32, device=self.device) for _ in range(micro)]
+        self.miloss4 = [torch.zeros(4, dtype=torch.float32, device=self.device) for _ in range(micro)]
+        self.streams = [None] + [torch.cuda.Stream(device=self.device) for _ in range(micro - 1)]
         self.reducer = GradReducer(self.eng.table, spec.arch, spec.nlayers, self.info, self.device)
-        self.eng.pack(self.params)
+        for e in self.engines:
+            e.pack(self.params)
+
+    def _ctx(self, k):
+        st = self.streams[k]
+        return torch.cuda.stream(st) if st is not None else _Null()
 
     def step(self, hr: torch.Tensor) -> Dict[str, torch.Tensor]:
         """hr: this rank's HR tiles [b, C, H, W] fp32 on the device (already normalised)."""
         b = hr.shape[0]
-        s = self.spec.scale
-        lr_in = self.lrbuf[:b]
-        sr = self.sr[:b]
-        downsample(hr, s, out=lr_in)
-        self.eng.forward(self.params, lr_in, out=sr)
+        if b != self.batch:
+            raise ValueError(f"batch {b} != trainer batch {self.batch}")
+        s, mb = self.spec.scale, self.mb
+        main = torch.cuda.current_stream(self.device)
         count = float(hr.numel()) * self.info.world
-        self.eng.rmse_partial(sr, hr, self.loss4, count)
+        for st in self.streams[1:]:
+            st.wait_stream(main)
+        # forward + squared-error partials per micro-batch
+        for k, eng in enumerate(self.engines):
+            sl = slice(k * mb, (k + 1) * mb)
+            with self._ctx(k):
+                downsample(hr[sl], s, out=self.lrbuf[sl])
+                eng.forward(self.params, self.lrbuf[sl], out=self.sr[sl])
+                eng.rmse_partial(self.sr[sl], hr[sl], self.mloss4[k], count)
+                if self.interp_loss:
+                    up = upsample(self.lrbuf[sl], s, out=self.up[sl])
+                    eng.rmse_partial(hr[sl], up, self.miloss4[k], count)
+        for st in self.streams[1:]:
+            main.wait_stream(st)
+        self._combine(self.loss4, self.mloss4)
         allreduce_sum_(self.loss4[0:1], self.info)
         Engine.rmse_finalize(self.loss4)
         if self.interp_loss:
-            up = upsample(lr_in, s, out=self.up[:b])
-            self.eng.rmse_partial(hr, up, self.iloss4, count)
+            self._combine(self.iloss4, self.miloss4)
             allreduce_sum_(self.iloss4[0:1], self.info)
             Engine.rmse_finalize(self.iloss4)
-        ev = self.reducer.events if self.info.enabled and self.reducer.cuda else None
-        self.eng.backward(self.params, lr_in, self.grads, sr=sr, hr=hr, loss4=self.loss4, events=ev)
-        self.reducer.reduce(self.grads)
+        for st in self.streams[1:]:
+            st.wait_stream(main)
+        # backward per micro-batch with the global loss scale
+        ev = self.reducer.events if (self.info.enabled and self.reducer.cuda and self.micro == 1) else None
+        for k, eng in enumerate(self.engines):
+            sl = slice(k * mb, (k + 1) * mb)
+            with self._ctx(k):
+                eng.backward(self.params, self.lrbuf[sl], self.mgrads[k], sr=self.sr[sl], hr=hr[sl],
+                             loss4=self.loss4, events=ev)
+        for st in self.streams[1:]:
+            main.wait_stream(st)
+        for g in self.mgrads[1:]:
+            axpy(self.grads, g, 1.0)  # exact gradient of the whole batch
+        self.reducer.reduce(self.grads, events_recorded=ev is not None)
         self.t += 1
         adam_step(self.params, self.grads, self.m, self.v, self.t, self.lr, self.betas, self.eps, self.wd)
-        self.eng.pack(self.params)
+        for k, eng in enumerate(self.engines):
+            if k:
+                self.streams[k].wait_stream(main)
+            with self._ctx(k):
+                eng.pack(self.params)
+        for st in self.streams[1:]:
+            main.wait_stream(st)
         return {"loss": self.loss4[3:4], "interp_loss": self.iloss4[3:4]}
+
+    @staticmethod
+    def _combine(dst, parts):
+        """loss4 of the whole batch from the micro-batches' partials (sum of squares, count)."""
+        if len(parts) == 1:
+            dst.copy_(parts[0])
+            return
+        dst.copy_(parts[0])
+        for q in parts[1:]:
+            dst[0:1].add_(q[0:1])
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
         """Reference-format model state_dict (CPU copies)."""

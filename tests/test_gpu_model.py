@@ -221,3 +221,27 @@ def test_plugin_module_reference_style_step():
     sd = {k: v.clone() for k, v in net.state_dict().items()}
     net.load_state_dict(sd)
     assert len(meta["keys"]["rcan_small_c2"]) == len(sd)
+
+
+def test_micro_batch_step_matches_single_engine():
+    """FusedTrainer(micro=2) -- two half-batch engines on two streams -- computes the
+    same step as one engine: the loss partials and gradients are summed exactly (up
+    to fp32 summation order)."""
+    d = dev()
+    spec = spec_of("rcan", 2, 2, 3)
+    table = _table(spec)
+    from srmi.trainer import default_init_
+    flat = torch.empty(sum(t[2] for t in table), device=d)
+    default_init_(flat, table, seed=5)
+    hr = torch.tensor(ro.synthetic_hr(16, 2, 192, 17)).to(d)
+    res = []
+    for micro in (1, 2):
+        tr = FusedTrainer(spec, 16, (48, 48), device=d, params=flat, micro=micro)
+        out = tr.step(hr)
+        res.append((float(out["loss"]), float(out["interp_loss"]), tr.grads.clone(), tr.params.clone()))
+        del tr
+    (l1, i1, g1, p1), (l2, i2, g2, p2) = res
+    assert abs(l1 - l2) <= 1e-6 * abs(l1)
+    assert abs(i1 - i2) <= 1e-6 * abs(i1)
+    assert rel_l2(g2, g1) < 1e-5
+    assert rel_l2(p2 - flat, p1 - flat) < 1e-4
