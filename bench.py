@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-interp-loss", action="store_true")
     ap.add_argument("--no-inference", action="store_true", help="skip the C5 tiled-region inference line")
+    ap.add_argument("--micro", type=int, default=None, help="micro-batches per step (default: trainer's choice)")
     ap.add_argument("--infer-region", type=int, default=4096, help="C5 HR region side (BASELINE: 4096)")
     ap.add_argument("--infer-iters", type=int, default=5)
     return ap.parse_args()
@@ -216,7 +217,8 @@ def main():
     C, B = args.channels, args.batch
     spec = NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=10, nblocks=20,
                    cbottleneck=2, scale=4)
-    tr = FusedTrainer(spec, B, (48, 48), lr=1e-4, interp_loss=not args.no_interp_loss, info=info, device=dev, seed=0)
+    tr = FusedTrainer(spec, B, (48, 48), lr=1e-4, interp_loss=not args.no_interp_loss, info=info, device=dev, seed=0,
+                      micro=args.micro)
     hr = torch.tensor(ro.synthetic_hr(B, C, 192, 1234 + info.rank)).to(dev)
 
     for _ in range(args.warmup):
