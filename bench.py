@@ -57,6 +57,17 @@ def parse():
     return ap.parse_args()
 
 
+def synthetic_hr(batch, nchan, size, seed):
+    """Synthetic HR tiles ~ N(0,1) from RandomState(seed), normalised per tile and
+    channel to mean 0 / std 1 (ddof 0) -- the statistics of the reference's 'lnorm'
+    tiles (sres/base/source/swot/raw.py:177-181).  Same stream as
+    the tests' generator, so bench inputs equal the parity-test inputs."""
+    import numpy as np
+    x = np.random.RandomState(seed).standard_normal((batch, nchan, size, size))
+    x = (x - x.mean(axis=(2, 3), keepdims=True)) / x.std(axis=(2, 3), keepdims=True)
+    return x.astype(np.float32)
+
+
 def _pmc_traffic(kernel_prefix):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary (FETCH_SIZE x2
     + WRITE_SIZE, gfx950-corrected; tools/pmc_traffic.sh), or None."""
@@ -138,7 +149,6 @@ def inference_bench(dev, side, iters):
     x4 baseline, both RMSEs, de-normalised mosaics of input/target/interp/model --
     captured once as a HIP graph and replayed (dual_trainer.process_image semantics).
     MPix/s counts produced HR pixels."""
-    from oracle import rcan_oracle as ro  # synthetic region generator only
     from srmi.engine import NetSpec
     from srmi.inference import TiledInference
     from srmi.trainer import default_init_
@@ -148,7 +158,7 @@ def inference_bench(dev, side, iters):
     table = param_table(spec)
     params = torch.empty(sum(t[2] for t in table), dtype=torch.float32, device=dev)
     default_init_(params, table, 0)
-    region = torch.tensor(ro.synthetic_hr(1, 1, side, 99)[0]).to(dev)
+    region = torch.tensor(synthetic_hr(1, 1, side, 99)[0]).to(dev)
     ti = TiledInference(spec, params, tuple(region.shape), (192, 192), device=dev, graph=True)
     ti.process_region(region)  # builds + captures the graph
     torch.cuda.synchronize()
@@ -206,7 +216,6 @@ def main():
     from srmi.dist import init_from_env
     from srmi.engine import NetSpec
     from srmi.trainer import FusedTrainer
-    from oracle import rcan_oracle as ro  # synthetic inputs only (same generator as the tests)
 
     info = init_from_env()
     world = info.world
@@ -219,7 +228,7 @@ def main():
                    cbottleneck=2, scale=4)
     tr = FusedTrainer(spec, B, (48, 48), lr=1e-4, interp_loss=not args.no_interp_loss, info=info, device=dev, seed=0,
                       micro=args.micro)
-    hr = torch.tensor(ro.synthetic_hr(B, C, 192, 1234 + info.rank)).to(dev)
+    hr = torch.tensor(synthetic_hr(B, C, 192, 1234 + info.rank)).to(dev)
 
     for _ in range(args.warmup):
         tr.step(hr)
