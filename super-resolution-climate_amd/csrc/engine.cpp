@@ -173,6 +173,12 @@ struct srmi_engine {
   int train = 0;
   int N = 0, h = 0, w = 0, C = 0, Co = 0, S = 0;
   int cu_budget = 0;  // CUs one launch aims to fill (0 = all)
+  // backward partition of the chip (RCAN train engines): the dgrad chain runs on
+  // `bmain` (bwd_budget CUs), the RCAB filter gradients on `side` (side_cus CUs,
+  // side_rs row chunks per image).  0 = unpartitioned defaults.
+  int bwd_budget = 0, side_cus = 0, side_rs = 0;
+  hipStream_t bmain = nullptr;
+  hipEvent_t ev_bin = nullptr, ev_bout = nullptr;
   size_t mapn = 0;  // elements of one [N][h][w][64] map
   // forward state
   float *X0f, *Rf, *Hf;
@@ -222,6 +228,13 @@ struct srmi_engine {
   }
   float* brecp(int g, int b) const { return brec + (size_t)(g * P.cfg.nblocks + (b - 1)) * N * 224; }
 };
+
+// row chunks per image of the side-stream (RCAB) filter gradients
+static int side_row_splits(const srmi_engine* e) {
+  const int rs = e->side_rs;
+  if (rs > 0 && e->h % rs == 0 && (e->h / rs) % 4 == 0) return rs;
+  return choose_row_splits(e->N, e->h, 64, e->side_cus > 0 ? e->side_cus : e->cu_budget);
+}
 
 static size_t carve(srmi_engine* e, char* base) {
   Carver cv;
@@ -287,7 +300,7 @@ static size_t carve(srmi_engine* e, char* base) {
     e->slab = cv.take<float>(sf);
     e->bslab = cv.take<float>(bf);
     if (rcan) {  // the side stream's own slabs (64-channel RCAB convs only)
-      const size_t ns = (size_t)N * choose_row_splits(N, e->h, 64, e->cu_budget);
+      const size_t ns = (size_t)N * side_row_splits(e);
       e->slab_s_floats = ns * 64 * 576;
       e->bslab_s_floats = ns * 64;
       e->slab_s = cv.take<float>(e->slab_s_floats);
@@ -312,6 +325,10 @@ static int init_engine(srmi_engine* e, const srmi_model_config* cfg, int train) 
   e->Co = cfg->nchannels_out;
   e->S = cfg->scale;
   e->cu_budget = cfg->cu_budget > 0 ? cfg->cu_budget : 0;
+  auto envi = [](const char* k) { const char* v = getenv(k); return v ? atoi(v) : 0; };
+  e->side_cus = std::max(0, std::min(255, envi("SRMI_SIDE_CUS")));
+  e->side_rs = std::max(0, envi("SRMI_SIDE_RS"));
+  e->bwd_budget = e->side_cus > 0 ? 256 - e->side_cus : std::max(0, envi("SRMI_BWD_BUDGET"));
   e->mapn = (size_t)e->N * e->h * e->w * 64;
   if (e->h % 4 || (e->w % 32 && e->w % 48)) return SRMI_ERR_SHAPE;
   const int Hs = e->h * e->S;
@@ -396,7 +413,7 @@ static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n,
   p.part_stride = 128;
   p.alpha = alpha;
   p.zeros = e->zeros;
-  p.cu_budget = e->cu_budget;
+  p.cu_budget = e->bwd_budget > 0 ? e->bwd_budget : e->cu_budget;
   if (epi == EPI_DG_ACC && r1 && aux && part && !yb && !r2 && !r3 && yf && c.cout == 64 && !c.ps)
     epi = EPI_DG_ACC_CA;  // the hot RCAB case: specialised epilogue without runtime operand checks
   return conv3x3_launch(p, epi, st);
@@ -413,7 +430,7 @@ static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const b
   p.Cout = c.cout;
   p.dy_mode = c.ps ? IN_UNSHUF : IN_PLAIN;
   p.imgs_per_wg = 1;
-  p.row_splits = choose_row_splits(n, H, c.cout, e->cu_budget);
+  p.row_splits = side ? side_row_splits(e) : choose_row_splits(n, H, c.cout, e->cu_budget);
   p.slab = side ? e->slab_s : e->slab;
   p.bslab = side ? e->bslab_s : e->bslab;
   p.zeros = e->zeros;
@@ -422,7 +439,7 @@ static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const b
   if (ns * c.cout * 576 > cap || ns * c.cout > bcap) return SRMI_ERR_WORKSPACE;
   int rc = wgrad3x3_launch(p, st);
   if (rc) return rc;
-  return wgrad_reduce_launch(p.slab, p.bslab, (int)ns, c.cout, c.ps, alpha, grads + c.w,
+  return wgrad_reduce_launch(p.slab, p.bslab, (int)ns, c.cout, c.ps, wgrad3x3_slab_layout(p), alpha, grads + c.w,
                              with_bias ? grads + c.b : nullptr, st);
 }
 
@@ -659,8 +676,23 @@ int srmi_engine_create(const srmi_model_config* cfg, void* workspace, size_t ws_
     return SRMI_ERR_WORKSPACE;
   }
   carve(e, base);
+  if (train && e->P.cfg.arch == SRMI_ARCH_RCAN && e->side_cus > 0) {
+    // spatial partition: side_cus CUs spread evenly over the mask for the filter
+    // gradients, the rest for the dgrad chain
+    uint32_t ms[8] = {}, mm[8] = {};
+    const int nc = 256, k = e->side_cus;
+    for (int i = 0; i < k; ++i) {
+      const int cu = (int)(((long long)i * nc) / k);
+      ms[cu >> 5] |= 1u << (cu & 31);
+    }
+    for (int w = 0; w < 8; ++w) mm[w] = ~ms[w];
+    HC(hipExtStreamCreateWithCUMask(&e->side, 8, ms));
+    HC(hipExtStreamCreateWithCUMask(&e->bmain, 8, mm));
+    HC(hipEventCreateWithFlags(&e->ev_bin, hipEventDisableTiming));
+    HC(hipEventCreateWithFlags(&e->ev_bout, hipEventDisableTiming));
+  }
   if (train && e->P.cfg.arch == SRMI_ARCH_RCAN) {
-    HC(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
+    if (!e->side) HC(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
     hipEvent_t* evs[] = {&e->ev_du[0], &e->ev_du[1], &e->ev_dz[0], &e->ev_dz[1], &e->ev_w2[0],
                          &e->ev_w2[1], &e->ev_w1[0], &e->ev_w1[1], &e->ev_grp, &e->ev_side};
     for (hipEvent_t* ev : evs) HC(hipEventCreateWithFlags(ev, hipEventDisableTiming));
@@ -675,6 +707,12 @@ int srmi_engine_destroy(srmi_engine* e) {
                       e->ev_w2[1], e->ev_w1[0], e->ev_w1[1], e->ev_grp, e->ev_side};
   for (hipEvent_t ev : evs)
     if (ev) (void)hipEventDestroy(ev);
+  if (e->ev_bin) (void)hipEventDestroy(e->ev_bin);
+  if (e->ev_bout) (void)hipEventDestroy(e->ev_bout);
+  if (e->bmain) {
+    (void)hipStreamSynchronize(e->bmain);
+    (void)hipStreamDestroy(e->bmain);
+  }
   if (e->side) {
     (void)hipStreamSynchronize(e->side);
     (void)hipStreamDestroy(e->side);
@@ -700,7 +738,15 @@ int srmi_backward(srmi_engine* e, const float* params, const float* lr, const fl
                   const float* loss4, const float* dy, float* grads, void** group_events, void* stream) {
   if (!e || !e->train || !params || !lr || !grads || e->last_n < 1) return SRMI_ERR_ARG;
   if (!dy && (!sr || !hr || !loss4)) return SRMI_ERR_ARG;
-  return backward_impl(e, params, lr, sr, hr, loss4, dy, grads, group_events, S_(stream));
+  if (!e->bmain) return backward_impl(e, params, lr, sr, hr, loss4, dy, grads, group_events, S_(stream));
+  // partitioned backward: the dgrad chain runs on the CU-masked stream, joined to
+  // the caller's stream on both sides
+  HC(hipEventRecord(e->ev_bin, S_(stream)));
+  HC(hipStreamWaitEvent(e->bmain, e->ev_bin, 0));
+  RC(backward_impl(e, params, lr, sr, hr, loss4, dy, grads, group_events, e->bmain));
+  HC(hipEventRecord(e->ev_bout, e->bmain));
+  HC(hipStreamWaitEvent(S_(stream), e->ev_bout, 0));
+  return 0;
 }
 
 int srmi_rmse_partial(srmi_engine* e, const float* pred, const float* target, size_t n, double count_global,
@@ -793,7 +839,7 @@ int srmi_wgrad3x3(const void* x, const void* dy, int N, int H, int W, int Cout, 
   p.bslab = slab + ns * Cout * 576;
   RC(wgrad3x3_launch(p, S_(stream)));
   if (!gw && !gb) return 0;  // partial slabs only (profiling the MFMA kernel alone)
-  return wgrad_reduce_launch(p.slab, p.bslab, (int)ns, Cout, ps, alpha, gw, gb, S_(stream));
+  return wgrad_reduce_launch(p.slab, p.bslab, (int)ns, Cout, ps, wgrad3x3_slab_layout(p), alpha, gw, gb, S_(stream));
 }
 
 int srmi_ca_forward(const void* u, const float* part, int nstrips, const float* w1, const float* b1, const float* w2,

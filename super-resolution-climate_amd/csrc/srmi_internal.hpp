@@ -65,10 +65,13 @@ struct WgradParams {
 void wgrad3x3_set_debug_stamps(unsigned long long* buf);
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st);
 int wgrad3x3_nslabs(const WgradParams& p);
+// order of the partial slabs the launch writes: 0 = [tap][ci][Cout], 1 = wgrad48's
+// MFMA-native [Cout/64][wave][9][4][lane][4]
+int wgrad3x3_slab_layout(const WgradParams& p);
 // slab reduction into the torch-layout grad [Cout][64][3][3] (+ bias [Cout]);
 // ps != 0 un-permutes the packed PixelShuffle channel order (c'' = 64q + c -> 4c + q)
-int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, float alpha, float* gw,
-                        float* gb, hipStream_t st);
+int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, int layout, float alpha,
+                        float* gw, float* gb, hipStream_t st);
 
 // small-channel kernels (head / tail), bicubic resampling, loss, CA, Adam, packing
 int head_fwd_launch(const float* lr, const float* w, const float* b, int N, int C, int H, int W, float* x0f,

@@ -443,18 +443,15 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
     }
   }
 
-  float* slab = p.slab + (size_t)chunk * Cout * 576;
+  // partial slab in the MFMA-native order (slab layout 1): every store instruction
+  // writes 1 KiB contiguous; wgrad_reduce_kernel maps it back to (co, ci, tap)
+  float* slab = p.slab + (size_t)chunk * Cout * 576 + (size_t)cb * (64 * 576) + (size_t)wave * (9 * 4 * 256);
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int j = 9 * wave + t, tap = j >> 2, it = j & 3;
-    const int ci = it * 16 + (lane & 15);
+  for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      const int co = cb * 64 + ((ct + wave) & 3) * 16 + 4 * (lane >> 4);  // slot ct = co tile (ct + wave) & 3
-      *reinterpret_cast<float4*>(slab + ((size_t)tap * 64 + ci) * Cout + co) =
+    for (int ct = 0; ct < 4; ++ct)
+      *reinterpret_cast<float4*>(slab + ((t * 4 + ct) * 64 + lane) * 4) =
           make_float4(acc[ct][t][0], acc[ct][t][1], acc[ct][t][2], acc[ct][t][3]);
-    }
-  }
   if ((lane & 15) == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -475,6 +472,14 @@ __global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
 
 int wgrad3x3_nslabs(const WgradParams& p) { return p.N * p.row_splits; }
 
+static bool use_wgrad48(const WgradParams& p) {
+  // v4 (row-pair rings, per-wave specialised) for W == 48; SRMI_WGRAD_V3=1 forces v3
+  static const bool use_v4 = !(getenv("SRMI_WGRAD_V3") && atoi(getenv("SRMI_WGRAD_V3")));
+  return use_v4 && p.W == 48 && p.row_splits > 0 && (p.H / p.row_splits) % 2 == 0;
+}
+
+int wgrad3x3_slab_layout(const WgradParams& p) { return use_wgrad48(p) ? 1 : 0; }
+
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
   if (p.Cout % 64 || p.H % p.row_splits || (p.H / p.row_splits) % 4) return SRMI_ERR_SHAPE;
   if (p.dy_mode == IN_UNSHUF && p.Cout != 256) return SRMI_ERR_SHAPE;
@@ -483,9 +488,7 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
   q.stamps = g_wg_stamps;
   static const int dbg = getenv("SRMI_WGRAD_DBG") ? atoi(getenv("SRMI_WGRAD_DBG")) : 0;
   q.dbg = dbg;
-  // v4 (row-pair rings, per-wave specialised) for W == 48; SRMI_WGRAD_V3=1 forces v3
-  static const bool use_v4 = !(getenv("SRMI_WGRAD_V3") && atoi(getenv("SRMI_WGRAD_V3")));
-  if (use_v4 && p.W == 48 && (p.H / p.row_splits) % 2 == 0) {
+  if (use_wgrad48(p)) {
     hipLaunchKernelGGL(wgrad48_kernel, grid, dim3(256), v4::LDS, st, q);
   } else if (p.W % 48 == 0) {
     hipLaunchKernelGGL(wgrad3x3_kernel<48>, grid, dim3(256), Wg3<48>::TOTAL, st, q);
@@ -499,15 +502,17 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
 }
 
 // -------------------------------------------------------------------- reduce
-// block = 64 output quads (256 consecutive outputs, float4 loads) x 4 slab phases;
-// phase q sums slabs q, q+4, ... with 4 independent accumulators, then the
-// 4 x 4 partials are added in a fixed order (deterministic).  The bias slab
-// ([nslab][Cout]) is handled by the last block(s) the same way.
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab,
-                                                           const float* __restrict__ bslab, int nslab, int Cout,
-                                                           int ps, float alpha, float* __restrict__ gw,
-                                                           float* __restrict__ gb) {
-  __shared__ float4 red[4][64];
+// block = 64 output quads (256 consecutive outputs, float4 loads) x 8 slab phases
+// (512 threads); phase q sums slabs q, q+8, ... with 4 independent accumulators
+// and 8 loads in flight per thread (the reduction is latency-, not bandwidth-
+// limited at ~200 slabs), then the 8 x 4 partials are added in a fixed order
+// (deterministic).  The bias slab ([nslab][Cout]) is handled by the last block(s).
+constexpr int kRedPh = 8;
+__global__ void __launch_bounds__(64 * kRedPh) wgrad_reduce_kernel(const float* __restrict__ slab,
+                                                                   const float* __restrict__ bslab, int nslab,
+                                                                   int Cout, int ps, int layout, float alpha,
+                                                                   float* __restrict__ gw, float* __restrict__ gb) {
+  __shared__ float4 red[kRedPh][64];
   const int per = Cout * 576;
   const int nwb = per / 256;  // weight blocks (per % 256 == 0 since Cout % 64 == 0)
   const int qd = threadIdx.x & 63, ph = threadIdx.x >> 6;
@@ -527,36 +532,55 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     stride = Cout;
     valid = o4 < Cout;
   }
-  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0, a3 = a0;
+  float4 a[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (valid) {
     int k = ph;
-    for (; k + 12 < nslab; k += 16) {
-      const float4 v0 = *reinterpret_cast<const float4*>(src + (size_t)k * stride);
-      const float4 v1 = *reinterpret_cast<const float4*>(src + (size_t)(k + 4) * stride);
-      const float4 v2 = *reinterpret_cast<const float4*>(src + (size_t)(k + 8) * stride);
-      const float4 v3 = *reinterpret_cast<const float4*>(src + (size_t)(k + 12) * stride);
-      a0.x += v0.x; a0.y += v0.y; a0.z += v0.z; a0.w += v0.w;
-      a1.x += v1.x; a1.y += v1.y; a1.z += v1.z; a1.w += v1.w;
-      a2.x += v2.x; a2.y += v2.y; a2.z += v2.z; a2.w += v2.w;
-      a3.x += v3.x; a3.y += v3.y; a3.z += v3.z; a3.w += v3.w;
+    constexpr int U = 8;  // loads in flight
+    for (; k + (U - 1) * kRedPh < nslab; k += U * kRedPh) {
+      float4 v[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) v[j] = *reinterpret_cast<const float4*>(src + (size_t)(k + j * kRedPh) * stride);
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        float4& t = a[j & 3];
+        t.x += v[j].x; t.y += v[j].y; t.z += v[j].z; t.w += v[j].w;
+      }
     }
-    for (; k < nslab; k += 4) {
+    for (; k < nslab; k += kRedPh) {
       const float4 v = *reinterpret_cast<const float4*>(src + (size_t)k * stride);
-      a0.x += v.x; a0.y += v.y; a0.z += v.z; a0.w += v.w;
+      a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
     }
   }
-  red[ph][qd] = make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
-                            (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w));
+  red[ph][qd] = make_float4((a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y),
+                            (a[0].z + a[1].z) + (a[2].z + a[3].z), (a[0].w + a[1].w) + (a[2].w + a[3].w));
   __syncthreads();
   if (ph != 0 || !valid) return;
-  const float4 r0 = red[0][qd], r1 = red[1][qd], r2 = red[2][qd], r3 = red[3][qd];
-  const float s4[4] = {((r0.x + r1.x) + r2.x) + r3.x, ((r0.y + r1.y) + r2.y) + r3.y, ((r0.z + r1.z) + r2.z) + r3.z,
-                       ((r0.w + r1.w) + r2.w) + r3.w};
+  float4 r = red[0][qd];
+#pragma unroll
+  for (int q = 1; q < kRedPh; ++q) {
+    const float4 t = red[q][qd];
+    r.x += t.x; r.y += t.y; r.z += t.z; r.w += t.w;
+  }
+  const float s4[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int o = o4 + e;
     if (is_w) {
-      const int cop = o % Cout, ci = (o / Cout) & 63, tap = o / (Cout * 64);
+      int cop, ci, tap;
+      if (layout == 1) {  // wgrad48 native order [cb][wave][t][ct][lane][4]
+        const int cb = o / (64 * 576), l = o - cb * (64 * 576);
+        const int r = l & 3, lane = (l >> 2) & 63, ct = (l >> 8) & 3, wt = l >> 10;
+        const int wave = wt / 9, j = wt;  // j = 9 * wave + t
+        tap = j >> 2;
+        ci = (j & 3) * 16 + (lane & 15);
+        cop = cb * 64 + ((ct + wave) & 3) * 16 + 4 * (lane >> 4) + r;
+      } else {  // [tap][ci][Cout]
+        cop = o % Cout;
+        ci = (o / Cout) & 63;
+        tap = o / (Cout * 64);
+      }
       const int cot = ps ? (4 * (cop & 63) + (cop >> 6)) : cop;
       gw[((size_t)cot * 64 + ci) * 9 + tap] = alpha * s4[e];
     } else if (o < Cout) {
@@ -566,12 +590,12 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
-int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, float alpha, float* gw,
-                        float* gb, hipStream_t st) {
+int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, int layout, float alpha,
+                        float* gw, float* gb, hipStream_t st) {
   if (Cout % 64) return SRMI_ERR_SHAPE;
   const int blocks = Cout * 576 / 256 + (Cout + 255) / 256;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, slab, bslab, nslab, Cout, ps, alpha, gw,
-                     gb);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(64 * kRedPh), 0, st, slab, bslab, nslab, Cout, ps, layout,
+                     alpha, gw, gb);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

@@ -71,6 +71,7 @@ def main():
         "fwd_resid": conv(2, x, fp, bias=pb, yb=yb, yf=yf, r1=r1),
         "dgrad_relumask": conv(4, dy, dp, yb=yb, aux=t),
         "dgrad_acc": conv(5, dy, dp, yb=None, yf=yf, r1=yf, aux=t, part=part),
+        "dgrad_acc_ca": conv(7, dy, dp, yb=None, yf=yf, r1=yf, aux=t, part=part),
     }
     for k, f in cases.items():
         us = timeit(f, args.iters)
@@ -84,6 +85,11 @@ def main():
              ptr(gb), S())
     us = timeit(wg, args.iters)
     res["wgrad+reduce"] = {"us": round(us, 2), "tflops": round(flop / us / 1e6, 1)}
+
+    def wg_only():
+        call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, 0, ptr(slab), slab.numel() * 4, 0, 1.0, None, None, S())
+    us = timeit(wg_only, args.iters)
+    res["wgrad"] = {"us": round(us, 2), "tflops": round(flop / us / 1e6, 1)}
     # channel attention elementwise kernels
     R = 2
     w1 = torch.randn(32, 64, device=d) * 0.1
