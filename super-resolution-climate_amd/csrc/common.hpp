@@ -81,6 +81,17 @@ __device__ __forceinline__ float sum16(float v) {
 // DMA as aliasing every later ds_read (it would drain everything with vmcnt(0));
 // completion is ordered by the caller's own s_waitcnt vmcnt + barrier
 // (cdna_hip_programming.md §5.7: M0 saved/restored inside the statement).
+// A pointer (e.g. the address of a __device__ zero page) pinned in SGPRs once.
+// Without this the compiler re-loads a global's address from the GOT (s_load)
+// after every asm volatile with a "memory" clobber (glds16), and the
+// s_waitcnt lgkmcnt(0) for that scalar load also drains every LDS read in flight.
+__device__ __forceinline__ const void* uniform_ptr(const void* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ void glds16(const void* src, uint32_t lds_base) {
   uint32_t keep;
   asm volatile(

@@ -490,6 +490,11 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
   }
 }
 
+#ifndef SRMI_CONV_FRAGBUF
+#define SRMI_CONV_FRAGBUF 2
+#endif
+constexpr int kFragBuf = SRMI_CONV_FRAGBUF;  // register buffers of A/B fragments (K-steps)
+
 template <int TW, int EPI, int PM>
 __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int run_len) {
   using S = Conv2Smem<TW>;
@@ -521,23 +526,37 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
   // page.  No registers hold in-flight data, so no compiler-inserted vmcnt waits.
   const int wv_s = __builtin_amdgcn_readfirstlane(wave);
   const uint32_t rbase = lds_u32(ring);
-  auto group_dma_one = [&](int gidx, int i) __attribute__((always_inline)) {
-    const int qbase = (gidx % 3) * 4 * (TW + 2);
-    {
-      const int q = 8 * i + (lane >> 3);
-      const int Q = qbase + q;
-      const int c = (lane & 7) ^ ((Q >> 1) & 7);
-      const int rr = q / (TW + 2), hx = q - rr * (TW + 2);
-      const int y = 4 * gidx - 3 + rr, xx = x0 - 1 + hx;
-      const bool ok = y >= 0 && y < p.H && xx >= 0 && xx < p.W;
-      const void* src = ok ? (const void*)(xn + ((size_t)y * p.W + xx) * 64 + c * 8) : (const void*)kZeros;
-      glds16(src, rbase + (uint32_t)qbase * 128u + (uint32_t)i * 1024u);
-    }
-  };
+  const void* const zpage = uniform_ptr(kZeros);
   constexpr int NGRP = S::GROUPB / 1024;         // 1 KiB DMA pieces per group
   constexpr int NGW = (NGRP + 3) / 4;            // pieces per wave (upper bound)
+  // Per-lane parts of the DMA source, computed once: piece i = wv_s + 4m covers ring
+  // pixels q = 8i + lane/8, i.e. row rr and halo column hx of the group; the chunk
+  // swizzle of ring slot 1 differs from slots 0 and 2 by bit 2 (200 px per slot).
+  int loff[NGW], lrr[NGW];
+  uint32_t okx = 0;
+#pragma unroll
+  for (int m = 0; m < NGW; ++m) {
+    const int i = wv_s + 4 * m;
+    const int q = 8 * i + (lane >> 3);
+    const int c = (lane & 7) ^ ((q >> 1) & 7);
+    const int rr = q / (TW + 2), hx = q - rr * (TW + 2);
+    const int xx = x0 - 1 + hx;
+    okx |= (i < NGRP && xx >= 0 && xx < p.W) ? (1u << m) : 0u;
+    loff[m] = ((rr * p.W + hx - 1) * 64 + c * 8) * (int)sizeof(bf16_t);
+    lrr[m] = rr;
+  }
+  auto group_dma_one = [&](int gidx, int m) __attribute__((always_inline)) {
+    const int slot = gidx % 3, y0 = 4 * gidx - 3;
+    const char* base = reinterpret_cast<const char*>(xn + ((ptrdiff_t)y0 * p.W + x0) * 64);
+    const int o = loff[m] ^ (slot == 1 ? 64 : 0);  // chunk c ^ 4 (8 bf16 = 16 B per chunk)
+    const bool ok = ((okx >> m) & 1u) && y0 + lrr[m] >= 0 && y0 + lrr[m] < p.H;
+    const void* src = ok ? (const void*)(base + o) : zpage;
+    glds16(src, rbase + (uint32_t)(slot * 4 * (TW + 2)) * 128u + (uint32_t)(wv_s + 4 * m) * 1024u);
+  };
   auto group_dma = [&](int gidx) __attribute__((always_inline)) {
-    for (int i = wv_s; i < NGRP; i += 4) group_dma_one(gidx, i);
+#pragma unroll
+    for (int m = 0; m < NGW; ++m)
+      if (wv_s + 4 * m < NGRP) group_dma_one(gidx, m);
   };
 
   // prologue: filters (all 9 taps, 72 KiB) and input groups k0, k0+1, all by LDS-DMA
@@ -595,9 +614,9 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // 18 K-steps (9 taps x 2 halves of 32 ci), fragments double-buffered in
-    // registers: step s+1's ds_reads are in flight while step s's 12 MFMAs run.
-    bf16x8 A[2][4], B[2][NPT];
+    // 18 K-steps (9 taps x 2 halves of 32 ci), fragments triple-buffered in
+    // registers: steps s+1 and s+2's ds_reads are in flight while step s's MFMAs run.
+    bf16x8 A[kFragBuf][4], B[kFragBuf][NPT];
     auto load_step = [&](int s, bf16x8 (&a)[4], bf16x8 (&b)[NPT]) __attribute__((always_inline)) {
       const int tap = s >> 1, kk = s & 1, ky = tap / 3, kx = tap % 3;
 #pragma unroll
@@ -605,19 +624,28 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
 #pragma unroll
       for (int pt = 0; pt < NPT; ++pt) b[pt] = lds_frag(ring, boff[ky][kx][kk] + pt * 2048);
     };
-    load_step(0, A[0], B[0]);
+    constexpr int LA = kFragBuf - 1;  // K-steps of LDS reads in flight ahead of the MFMAs
+#pragma unroll
+    for (int s = 0; s < LA; ++s) load_step(s, A[s], B[s]);
 #pragma unroll
     for (int s = 0; s < 18; ++s) {
       // group k+2's DMA pieces and the epilogue operands are issued one or two per
       // K-step, so a full memory queue stalls the wave between MFMA groups only
-      if (s < NGW && pf && wv_s + 4 * s < NGRP) group_dma_one(k + 2, wv_s + 4 * s);
-      if (s >= 2 && s - 2 < NPT * 4) epi_prefetch_one<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk, s - 2);
-      if (s + 1 < 18) load_step(s + 1, A[(s + 1) & 1], B[(s + 1) & 1]);
+#ifndef SRMI_CONV_DBG
+#define SRMI_CONV_DBG 0
+#endif
+      // SRMI_CONV_DBG (diagnostic builds only, wrong results): bit0 no DMA in the K loop,
+      // bit1 no fragment reads after the first, bit2 no epilogue prefetch
+      if (!(SRMI_CONV_DBG & 1) && s < NGW && pf && wv_s + 4 * s < NGRP) group_dma_one(k + 2, s);
+      if (!(SRMI_CONV_DBG & 4) && s >= 2 && s - 2 < NPT * 4)
+        epi_prefetch_one<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk, s - 2);
+      if (!(SRMI_CONV_DBG & 2) && s + LA < 18) load_step(s + LA, A[(s + LA) % kFragBuf], B[(s + LA) % kFragBuf]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int pt = 0; pt < NPT; ++pt)
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = mfma16(A[s & 1][ct], B[s & 1][pt], acc[pt][ct]);
+        for (int ct = 0; ct < 4; ++ct)
+          acc[pt][ct] = mfma16(A[s % kFragBuf][ct], B[s % kFragBuf][pt], acc[pt][ct]);
       __builtin_amdgcn_sched_barrier(0);
     }
     // group k+2's DMA, the epilogue operands and the previous strip's stores had the

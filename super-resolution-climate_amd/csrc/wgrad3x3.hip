@@ -252,6 +252,7 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
   const bf16_t* dyn = plain ? p.dy + (size_t)n * H * TW * Cout + cb * 64 : p.dy + (size_t)n * 4 * H * TW * 64;
   const bf16_t* xn = p.x + (size_t)n * H * TW * 64;
   const uint32_t lds0 = lds_u32(smem);
+  const void* const zpage = uniform_ptr(kZerosW);
   const int dq = lane >> 3, ls = lane & 7;
   // source chunk of this lane inside its pixel: the swizzle bits of q = 8g + dq
   // are bit 1 of dq and bit 0 of g (row and slot bases are multiples of 16 px)
@@ -275,7 +276,7 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
       const int y = ybase + r, hx = 8 * g + dq, xx = hx - 1;
       const bool ok = hx < TW + 2 && y >= 0 && y < H && xx >= 0 && xx < TW;
       const int c = (g & 1) ? cl1 : cl0;
-      const void* src = ok ? (const void*)(xn + ((size_t)y * TW + xx) * 64 + c * 8) : (const void*)kZerosW;
+      const void* src = ok ? (const void*)(xn + ((size_t)y * TW + xx) * 64 + c * 8) : zpage;
       glds16(src, lds0 + (uint32_t)(DY_RING + ((r + 1) % RX) * XSLOT + g * 1024));
     }
   };
@@ -315,7 +316,7 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
       } else if (k < NGP) {
         const int kk = k - 2 * GD, rr = kk / GX, g = kk - rr * GX;
         const bool ok = ((okx >> m) & 1u) && (rr ? yv1 : yv0);
-        const void* src = ok ? (const void*)(xb + loff[m]) : (const void*)kZerosW;
+        const void* src = ok ? (const void*)(xb + loff[m]) : zpage;
         int slot = 2 * P + 2 + rr;  // input row 2P+1+rr -> slot (row + 1) % RX
         slot = slot % RX;
         glds16(src, lds0 + (uint32_t)(DY_RING + slot * XSLOT + g * 1024));
