@@ -493,7 +493,10 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
 #ifndef SRMI_CONV_FRAGBUF
 #define SRMI_CONV_FRAGBUF 2
 #endif
-constexpr int kFragBuf = SRMI_CONV_FRAGBUF;  // register buffers of A/B fragments (K-steps)
+constexpr int kFragBuf = SRMI_CONV_FRAGBUF;
+#ifndef SRMI_CONV_ILV
+#define SRMI_CONV_ILV 1
+#endif  // register buffers of A/B fragments (K-steps)
 
 template <int TW, int EPI, int PM>
 __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int run_len) {
@@ -639,13 +642,26 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
       if (!(SRMI_CONV_DBG & 1) && s < NGW && pf && wv_s + 4 * s < NGRP) group_dma_one(k + 2, s);
       if (!(SRMI_CONV_DBG & 4) && s >= 2 && s - 2 < NPT * 4)
         epi_prefetch_one<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk, s - 2);
-      if (!(SRMI_CONV_DBG & 2) && s + LA < 18) load_step(s + LA, A[(s + LA) % kFragBuf], B[(s + LA) % kFragBuf]);
       __builtin_amdgcn_sched_barrier(0);
+      const bool ld = !(SRMI_CONV_DBG & 2) && s + LA < 18;
+      if (ld) load_step(s + LA, A[(s + LA) % kFragBuf], B[(s + LA) % kFragBuf]);
 #pragma unroll
       for (int pt = 0; pt < NPT; ++pt)
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct)
           acc[pt][ct] = mfma16(A[s % kFragBuf][ct], B[s % kFragBuf][pt], acc[pt][ct]);
+#if SRMI_CONV_ILV
+      // one fragment read issued behind each MFMA: the reads' issue time hides under
+      // the MFMA pipe instead of stalling it between K-steps
+      if (ld) {
+#pragma unroll
+        for (int j = 0; j < 4 + NPT; ++j) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4 * NPT - (4 + NPT), 0);
+      }
+#endif
       __builtin_amdgcn_sched_barrier(0);
     }
     // group k+2's DMA, the epilogue operands and the previous strip's stores had the
