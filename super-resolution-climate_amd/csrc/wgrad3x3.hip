@@ -235,6 +235,10 @@ constexpr int GD = TW / 8, GX = 7;                               // 8-px groups 
 constexpr int NGP = 2 * GD + 2 * GX;                             // groups per pair (26)
 }  // namespace v4
 
+#ifndef SRMI_WGRAD_ILV
+#define SRMI_WGRAD_ILV 1
+#endif
+
 // The body is instantiated once per wave (WV = wave index): the wave's DMA groups,
 // taps and tile rotation are compile-time constants (no SGPR pressure, no branches).
 template <int WV>
@@ -419,14 +423,26 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
       for (int kc = 0; kc < 3; ++kc) {
         const int cur = (3 * q + kc) & 1, nxt = cur ^ 1;
         if (pf) dma_pair_part(j + PF, kc == 0 ? 0 : (kc == 1 ? 3 : 5), kc == 0 ? 3 : (kc == 1 ? 5 : 7));
+        __builtin_amdgcn_sched_barrier(0);
+        const bool ld = kc < 2 || more;
         if (kc < 2) load_step(ra, rb, kc + 1, A[nxt], B[nxt]);
         else if (more) load_step(ran, rbn, 0, A[nxt], B[nxt]);  // next pair's first K-step
-        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int t = 0; t < 9; ++t)
 #pragma unroll
           for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(A[cur][ct], B[cur][t], acc[ct][t]);
         bacc = mfma16(A[cur][0], ones, bacc);  // slot 0 = this wave's own co tile
+#if SRMI_WGRAD_ILV
+        // the next K-step's 26 transposed reads issued behind the MFMAs, one per MFMA
+        if (ld) {
+#pragma unroll
+          for (int i = 0; i < 26; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 11, 0);
+        }
+#endif
         __builtin_amdgcn_sched_barrier(0);
         if (kc == 1) {
           // pair j+1 must have landed before K-step 2 reads its first fragments.  In
