@@ -23,6 +23,8 @@
  *   srmi_ca_*                    -> CALayer sres/model/rcan/network.py:31-47
  *   srmi_region_to_tiles         -> get_tiles + 'lnorm' norm
  *                                   sres/base/source/swot/raw.py:216-233, :169-181
+ *   srmi_batch_prep              -> norm 'lnorm' (swot/raw.py:169-181) + xyflip
+ *                                   sres/base/source/batch.py:37-49 + downsample
  *   srmi_tiles_to_region         -> denorm + assemble_images
  *                                   sres/controller/dual_trainer.py:67-77, :482-512
  */
@@ -163,6 +165,16 @@ int srmi_region_to_tiles(const float* region, int C, int H, int W, int ty, int t
  * inv == NULL: tile i is cell i */
 int srmi_tiles_to_region(const float* tiles, const float* mean, const float* std, const int* inv, int C, int ty,
                          int tx, int gy, int gx, float* out, void* stream);
+
+/* ---- training batch preparation ------------------ */
+/* raw [B][C][T][T] fp32 tiles (select_batch, sres/base/source/swot/raw.py:160-166)
+ * -> hr [B][C][T][T] = xyflip(lnorm(raw)) (norm 'lnorm' raw.py:169-181: per tile
+ * and channel (x - mean) / std, ddof 0; xyflip sres/base/source/batch.py:37-49
+ * with the drawn flip_index 0..7), lr [B][C][T/scale][T/scale] = downsample(hr)
+ * (array.py:72-76; NULL: skipped), mean/std [B][C] (norm's ncstats attrs; NULL:
+ * skipped).  T even. */
+int srmi_batch_prep(const float* raw, int B, int C, int T, int flip_index, int scale, float* hr, float* lr,
+                    float* mean, float* std, void* stream);
 
 #ifdef __cplusplus
 }

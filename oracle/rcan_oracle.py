@@ -19,6 +19,8 @@ from the imported reference (``tests/golden/make_golden.py``):
 * l2loss (RMSE) ........ sres/controller/stats.py:5-8
 * train step ........... sres/controller/dual_trainer.py:310-323, :557-571
 * Adam ................. torch.optim.Adam defaults used at dual_trainer.py:126
+* batch preparation .... norm lnorm + xyflip (swot/raw.py:160-181,
+                         sres/base/source/batch.py:33-49)
 * tiled inference ...... get_tiles + lnorm (sres/base/source/swot/raw.py:216-233,
                          :169-181), denorm + assemble_images + process_image
                          (dual_trainer.py:67-77, :482-512, :396-480); pinned by
@@ -334,3 +336,35 @@ def process_region(model, region: np.ndarray, ty: int, tx: int, scale: int):
               "interpolated": assemble(interp.numpy(), mean, std, ids, grid),
               "model": assemble(sr.numpy(), mean, std, ids, grid)}
     return images, losses
+
+
+# --------------------------------------------------------------------------
+# Training batch preparation: 'lnorm' of select_batch ->
+# norm (sres/base/source/swot/raw.py:160-181), then xyflip
+# (sres/base/source/batch.py:33-49, applied by load_batch :301), then the
+# apply_network input downsample (array.py:72-76).  xyflip is pinned by golden
+# vectors from the imported reference (tests/golden/make_golden_batch.py);
+# lnorm by restatement (xarray's mean/std over (x, y): skipna, ddof 0).
+
+def xyflip(x: np.ndarray, flip_index: int) -> np.ndarray:
+    """batch.py:37-49 for a given flip_index (the reference draws it with
+    random.randint(0, 7) when task.xyflip is set, else 0): bit 0 flips x
+    (axis -1), bit 1 flips y (axis -2), bit 2 swaps the two axes
+    (flip_xarray_axis, batch.py:33-35), in that order."""
+    if flip_index % 2 == 1:
+        x = np.flip(x, axis=-1)
+    if (flip_index // 2) % 2 == 1:
+        x = np.flip(x, axis=-2)
+    if flip_index // 4 == 1:
+        x = np.swapaxes(x, -1, -2)
+    return np.ascontiguousarray(x)
+
+
+def prep_batch(raw: np.ndarray, flip_index: int, scale: int):
+    """raw tiles [B, C, T, T] -> (hr = xyflip(lnorm(raw)), lr = downsample(hr),
+    mean [B, C], std [B, C]) -- the tensors the reference's train loop hands to
+    apply_network (dual_trainer.py:557-571), plus norm()'s ncstats attrs."""
+    mean = raw.mean(axis=(2, 3))
+    std = raw.std(axis=(2, 3))
+    hr = xyflip((raw - mean[:, :, None, None]) / std[:, :, None, None], flip_index)
+    return hr, downsample_explicit(hr, scale), mean, std

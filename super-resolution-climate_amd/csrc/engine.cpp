@@ -864,6 +864,11 @@ int srmi_tail_forward(const void* x, const float* w, const float* b, int N, int 
   return tail_fwd_launch((const bf16_t*)x, w, b, N, C, H, W, y, S_(stream));
 }
 
+int srmi_batch_prep(const float* raw, int B, int C, int T, int flip_index, int scale, float* hr, float* lr,
+                    float* mean, float* std, void* stream) {
+  return batch_prep_launch(raw, B, C, T, flip_index, scale, hr, lr, mean, std, S_(stream));
+}
+
 int srmi_region_to_tiles(const float* region, int C, int H, int W, int ty, int tx, float* tiles, float* mean,
                          float* std, int* bad, void* stream) {
   if (!region || !tiles || !mean || !std) return SRMI_ERR_ARG;

@@ -131,5 +131,7 @@ int region_to_tiles_launch(const float* region, int C, int H, int W, int ty, int
                            float* stdv, int* bad, hipStream_t st);
 int tiles_to_region_launch(const float* tiles, const float* mean, const float* stdv, const int* inv, int C, int ty,
                            int tx, int gy, int gx, float* out, hipStream_t st);
+int batch_prep_launch(const float* raw, int B, int C, int T, int flip, int scale, float* hr, float* lr, float* mean,
+                      float* stdv, hipStream_t st);
 
 }  // namespace srmi

@@ -110,6 +110,16 @@ def main():
     for k, f, byt in (("ca_fwd", caf, N * H * W * 64 * 12), ("ca_bwd_du", cab, N * H * W * 64 * 6)):
         us = timeit(f, args.iters)
         res[k] = {"us": round(us, 2), "GBps": round(byt / us / 1e3, 1)}
+    # batch preparation (lnorm + xyflip + downsample) of the C2 HR batch: 1 read + 1.06 writes
+    Cb, T = 2, 4 * H
+    raw = torch.randn(N, Cb, T, T, device=d) + 280.0
+    hrb, lrb = torch.empty_like(raw), torch.empty(N, Cb, H, W, device=d)
+    mb, sb = torch.empty(N, Cb, device=d), torch.empty(N, Cb, device=d)
+
+    def prep():
+        call("srmi_batch_prep", ptr(raw), N, Cb, T, 5, 4, ptr(hrb), ptr(lrb), ptr(mb), ptr(sb), S())
+    us = timeit(prep, args.iters)
+    res["batch_prep"] = {"us": round(us, 2), "GBps": round(raw.numel() * 4 * (2 + 1 / 16) / us / 1e3, 1)}
     print(json.dumps(res, indent=1))
 
 
