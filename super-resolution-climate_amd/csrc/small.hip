@@ -538,92 +538,111 @@ int loss_finalize_launch(float* loss, hipStream_t st) {
 }
 
 // =============================================================== channel attention
-// rec layout per image: m[C] z1[C/R] s[C]   (C = 64, C/R = 32)
-// ---------------------------------------------------------------------------
 // Channel attention (CALayer, reference sres/model/rcan/network.py:31-47):
 //   m = avgpool(u); z1 = W1 m + b1; s = sigmoid(W2 relu(z1) + b2); h += s * u
-// The per-image MLP runs once per image in its own tiny kernel (one wave per
-// image) and the elementwise pass streams with no per-block preamble.
-// rec per image: m[C] | z1[CR] | s[C]   (C = 64, CR = C / R)
-// Per-image MLP, one 256-thread block per image: the weights are staged in LDS
-// with coalesced loads and every dot product is split over 8 (4) lanes and
-// finished with a fixed-order butterfly, so no thread walks a long dependent chain.
-__global__ void __launch_bounds__(256) ca_fwd_mlp_kernel(const float* __restrict__ part, int nstrips, int HW,
-                                                         const float* __restrict__ w1, const float* __restrict__ b1,
-                                                         const float* __restrict__ w2, const float* __restrict__ b2,
-                                                         int C, int CR, float* __restrict__ rec) {
-  __shared__ float W1[32 * 64], W2[64 * 32], red[4][64], m[64], z1[32];
-  const int n = blockIdx.x, tid = threadIdx.x;
-  for (int i = tid; i < CR * C; i += 256) {
-    W1[i] = w1[i];
-    W2[i] = w2[i];
-  }
-  {
-    const int c = tid & 63, q = tid >> 6;
-    float a = 0.f;
-    for (int k = q; k < nstrips; k += 4) a += part[((size_t)n * nstrips + k) * C + c];
-    red[q][c] = a;
-  }
-  __syncthreads();
-  float* r = rec + (size_t)n * (2 * C + CR);
-  if (tid < C) {
-    const float v = (red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]) / (float)HW;
-    m[tid] = v;
-    r[tid] = v;
-  }
-  __syncthreads();
-  {  // z1[j] = b1[j] + sum_c W1[j][c] m[c]: lane group of 8 per j (CR = 32)
-    const int j = tid >> 3, pp = tid & 7;
-    float a = 0.f;
-    if (j < CR)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) a += W1[j * C + pp * 8 + i] * m[pp * 8 + i];
-    a += __shfl_xor(a, 1, 64);
-    a += __shfl_xor(a, 2, 64);
-    a += __shfl_xor(a, 4, 64);
-    if (j < CR && pp == 0) {
-      z1[j] = a + b1[j];
-      r[C + j] = a + b1[j];
-    }
-  }
-  __syncthreads();
-  {  // s[c] = sigmoid(b2[c] + sum_j W2[c][j] relu(z1[j])): 4 lanes per c
-    const int c = tid >> 2, pp = tid & 3;
-    float a = 0.f;
-    const int per = CR / 4;
-    for (int i = 0; i < per; ++i) a += W2[c * CR + pp * per + i] * fmaxf(z1[pp * per + i], 0.f);
-    a += __shfl_xor(a, 1, 64);
-    a += __shfl_xor(a, 2, 64);
-    if (pp == 0) r[C + CR + c] = 1.f / (1.f + expf(-(a + b2[c])));
-  }
+// rec per image: m[C] | z1[CR] | s[C]   (C = 64, CR = C / R <= 32)
+//
+// One launch per direction: every block of the elementwise pass first issues its
+// own stream loads, then recomputes the image's tiny MLP (4 K MACs) from the
+// producer's per-strip pool partials while those loads are in flight -- no
+// separate per-image MLP launch and no launch-to-launch bubble on the critical
+// chain.  Weights are read straight into registers (L2 hits); every dot product
+// is split over 8 (4) lanes and finished with a fixed-order butterfly; the pool
+// partials are summed in a fixed order, so all blocks of an image agree bit for
+// bit and block 0 of the image writes the record the backward pass reads.
+
+// workgroup barrier that orders LDS only: global loads stay in flight across it
+// (__syncthreads' release fence would drain vmcnt)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 }
 
-// elementwise passes: each thread handles kCaVec groups of 8 channels
-constexpr int kCaVec = 2;
+// elementwise passes: each thread handles kCaVec groups of 8 channels (4: the
+// per-block MLP is amortised over 2x the data of the former 2; 18 blocks per
+// 48x48 image, every block resident at once; ca_fwd 22.6 -> 20.0 us, ca_bwd
+// 15.1 -> 13.7 us against the former separate MLP launches)
+#ifndef SRMI_CA_VEC
+#define SRMI_CA_VEC 4
+#endif
+constexpr int kCaVec = SRMI_CA_VEC;
 
 // h_out = u * s + h_in  (fp32 + bf16 copy); grid (chunks, N)
-__global__ void __launch_bounds__(256) ca_fwd_kernel(const bf16_t* __restrict__ u, int HW, int C, int CR,
+__global__ void __launch_bounds__(256) ca_fwd_kernel(const bf16_t* __restrict__ u, const float* __restrict__ part,
+                                                     int nstrips, int HW, const float* __restrict__ w1,
+                                                     const float* __restrict__ b1, const float* __restrict__ w2,
+                                                     const float* __restrict__ b2, int C, int CR,
                                                      const float* __restrict__ h_in, float* __restrict__ h_out,
-                                                     bf16_t* __restrict__ hb_out, const float* __restrict__ rec) {
-  __shared__ float s[64];
-  const int n = blockIdx.y;
-  if (threadIdx.x < C) s[threadIdx.x] = rec[(size_t)n * (2 * C + CR) + C + CR + threadIdx.x];
-  __syncthreads();
+                                                     bf16_t* __restrict__ hb_out, float* __restrict__ rec) {
+  __shared__ float red[4][64], m[64], z1[32], s[64];
+  const int n = blockIdx.y, tid = threadIdx.x;
+  // 1. the MLP operands (L2 hits), issued first so that waiting for them does not
+  //    wait for the stream loads behind them (vmcnt retires in order): W1 row
+  //    slice (z1 lane group j, 8 lanes), W2 row slice (s lane group c, 4 lanes),
+  //    biases, the pool partials.
+  const int j = tid >> 3, pj = tid & 7;
+  const int c4 = tid >> 2, p4 = tid & 3, per = CR / 4;
+  // (unconditional loads at clamped indices -- no divergent branches, so the
+  //  compiler's vmcnt accounting stays exact across the stream loads below)
+  float pa = 0.f;
+  for (int k = tid >> 6; k < nstrips; k += 4) pa += part[((size_t)n * nstrips + k) * C + (tid & 63)];
+  const int jc = min(j, CR - 1);
+  float wa[8], wb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) wa[i] = w1[jc * C + pj * 8 + i];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) wb[i] = w2[c4 * CR + p4 * per + min(i, per - 1)];
+  const float bj = b1[jc];
+  const float bc = b2[c4];
+  __builtin_amdgcn_sched_barrier(0);
+  // 2. this thread's stream loads (independent of s), in flight during the MLP
   const size_t base = (size_t)n * HW * C;
   const size_t nv = (size_t)HW * C / 8;
-  const size_t v0 = ((size_t)blockIdx.x * kCaVec) * blockDim.x + threadIdx.x;
+  const size_t v0 = ((size_t)blockIdx.x * kCaVec) * blockDim.x + tid;
   uint4 uu[kCaVec];
   float4 h0[kCaVec], h1[kCaVec];
 #pragma unroll
-  for (int k = 0; k < kCaVec; ++k) {
-    const size_t v = v0 + (size_t)k * blockDim.x;
-    if (v < nv) {
-      const size_t e = base + v * 8;
-      uu[k] = *reinterpret_cast<const uint4*>(u + e);
-      h0[k] = *reinterpret_cast<const float4*>(h_in + e);
-      h1[k] = *reinterpret_cast<const float4*>(h_in + e + 4);
-    }
+  for (int k = 0; k < kCaVec; ++k) {  // clamped, unconditional (tail lanes store nothing)
+    const size_t e = base + min(v0 + (size_t)k * blockDim.x, nv - 1) * 8;
+    uu[k] = *reinterpret_cast<const uint4*>(u + e);
+    h0[k] = *reinterpret_cast<const float4*>(h_in + e);
+    h1[k] = *reinterpret_cast<const float4*>(h_in + e + 4);
   }
+  __builtin_amdgcn_sched_barrier(0);
+  // 3. the MLP (LDS-only barriers: the stream loads stay in flight)
+  red[tid >> 6][tid & 63] = pa;
+  lds_barrier();
+  if (tid < C) m[tid] = (red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]) / (float)HW;
+  lds_barrier();
+  {  // z1[j] = b1[j] + sum_c W1[j][c] m[c]
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a += wa[i] * m[pj * 8 + i];
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    a += __shfl_xor(a, 4, 64);
+    if (j < CR && pj == 0) z1[j] = a + bj;
+  }
+  lds_barrier();
+  {  // s[c] = sigmoid(b2[c] + sum_j W2[c][j] relu(z1[j]))
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (i < per) a += wb[i] * fmaxf(z1[p4 * per + i], 0.f);
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    if (p4 == 0) s[c4] = 1.f / (1.f + expf(-(a + bc)));
+  }
+  lds_barrier();
+  if (blockIdx.x == 0) {
+    float* r = rec + (size_t)n * (2 * C + CR);
+    if (tid < C) {
+      r[tid] = m[tid];
+      r[C + CR + tid] = s[tid];
+    }
+    if (tid < CR) r[C + tid] = z1[tid];
+  }
+  // 4. elementwise
 #pragma unroll
   for (int k = 0; k < kCaVec; ++k) {
     const size_t v = v0 + (size_t)k * blockDim.x;
@@ -657,108 +676,103 @@ int ca_fwd_launch(const bf16_t* u, const float* part, int nstrips, const float* 
                   const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, bf16_t* hb_out,
                   float* rec, hipStream_t st) {
   if (C != 64 || C % R || (C / R) > 32 || (C / R) % 4 || (HW * C) % 8) return SRMI_ERR_SHAPE;
-  hipLaunchKernelGGL(ca_fwd_mlp_kernel, dim3(N), dim3(256), 0, st, part, nstrips, HW, w1, b1, w2, b2, C, C / R, rec);
-  hipLaunchKernelGGL(ca_fwd_kernel, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, u, HW, C, C / R, h_in, h_out,
-                     hb_out, rec);
+  hipLaunchKernelGGL(ca_fwd_kernel, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, u, part, nstrips, HW, w1, b1, w2,
+                     b2, C, C / R, h_in, h_out, hb_out, rec);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
 
-// CA backward per image.  part[n][strip][2C] holds sum_p g (0..C-1) and
-// sum_p g*u (C..2C-1) from the producer of g.
+// CA backward.  part[n][strip][2C] holds sum_p g (0..C-1) and sum_p g*u
+// (C..2C-1) from the producer of g.  Every block recomputes the image's MLP
+// backward while its g loads are in flight; block 0 of the image writes
 // brec per image: dz2[C] dz1[CR] dbconv2[C]; followed (after all N images) by
 // dm[N][C] = W1^T dz1 (the gradient of the pooled mean).
-__global__ void __launch_bounds__(256) ca_bwd_mlp_kernel(const float* __restrict__ part, int nstrips,
-                                                         const float* __restrict__ rec, const float* __restrict__ w1,
-                                                         const float* __restrict__ w2, int N, int C, int CR,
-                                                         float* __restrict__ brec) {
-  __shared__ float W1[32 * 64], W2[64 * 32], red[4][128], dz2[64], dz1[32];
-  const int n = blockIdx.x, tid = threadIdx.x;
-  const float* r = rec + (size_t)n * (2 * C + CR);
-  float* br = brec + (size_t)n * (2 * C + CR);
-  for (int i = tid; i < CR * C; i += 256) {
-    W1[i] = w1[i];
-    W2[i] = w2[i];
-  }
-  {  // G[c] = sum_p g, ds[c] = sum_p g*u  (part[n][strip][2C])
-    const int c2 = tid & 127, q = tid >> 7;
-    float a = 0.f;
-    for (int k = q; k < nstrips; k += 2) a += part[((size_t)n * nstrips + k) * (2 * C) + c2];
-    red[q][c2] = a;
-  }
-  __syncthreads();
-  float G = 0.f;
-  if (tid < C) {
-    G = red[0][tid] + red[1][tid];
-    const float ds = red[0][C + tid] + red[1][C + tid];
-    const float s = r[C + CR + tid];
-    dz2[tid] = ds * s * (1.f - s);
-    br[tid] = dz2[tid];
-  }
-  __syncthreads();
-  {  // dz1[j] = relu'(z1[j]) sum_c W2[c][j] dz2[c]: 8 lanes per j
-    const int j = tid >> 3, pp = tid & 7;
-    float a = 0.f;
-    if (j < CR)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) a += W2[(pp * 8 + i) * CR + j] * dz2[pp * 8 + i];
-    a += __shfl_xor(a, 1, 64);
-    a += __shfl_xor(a, 2, 64);
-    a += __shfl_xor(a, 4, 64);
-    if (j < CR && pp == 0) {
-      const float v = (r[C + j] > 0.f) ? a : 0.f;
-      dz1[j] = v;
-      br[C + j] = v;
-    }
-  }
-  __syncthreads();
-  {  // dm[c] = sum_j W1[j][c] dz1[j]: 4 lanes per c
-    const int c = tid >> 2, pp = tid & 3;
-    const int per = CR / 4;
-    float a = 0.f;
-    for (int i = 0; i < per; ++i) a += W1[(pp * per + i) * C + c] * dz1[pp * per + i];
-    a += __shfl_xor(a, 1, 64);
-    a += __shfl_xor(a, 2, 64);
-    if (pp == 0) brec[(size_t)N * (2 * C + CR) + (size_t)n * C + c] = a;
-    if (pp == 0) red[2][c] = a;
-  }
-  __syncthreads();
-  if (tid < C) br[C + CR + tid] = r[C + CR + tid] * G + red[2][tid];  // conv2 bias grad: sum_p du
-}
-
 // du = g * s + dm / HW  (bf16)
-__global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict__ g, const float* __restrict__ rec,
-                                                        const float* __restrict__ brec, int N, int HW, int C, int CR,
-                                                        bf16_t* __restrict__ du) {
-  __shared__ float s[64], dmh[64];
+__global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict__ g, const float* __restrict__ part,
+                                                        int nstrips, const float* __restrict__ rec,
+                                                        const float* __restrict__ w1, const float* __restrict__ w2,
+                                                        int N, int HW, int C, int CR, bf16_t* __restrict__ du,
+                                                        float* __restrict__ brec) {
+  __shared__ float red[2][128], s[64], dz2[64], dz1[32], dm[64];
   const int n = blockIdx.y, tid = threadIdx.x;
-  if (tid < C) {
-    s[tid] = rec[(size_t)n * (2 * C + CR) + C + CR + tid];
-    dmh[tid] = brec[(size_t)N * (2 * C + CR) + (size_t)n * C + tid] * (1.f / (float)HW);
-  }
-  __syncthreads();
+  const float* r = rec + (size_t)n * (2 * C + CR);
+  const int j = tid >> 3, pj = tid & 7;
+  const int c4 = tid >> 2, p4 = tid & 3, per = CR / 4;
+  float pa = 0.f;  // G[c] = sum_p g, ds[c] = sum_p g*u (MLP operands first, see ca_fwd_kernel)
+  for (int k = tid >> 7; k < nstrips; k += 2) pa += part[((size_t)n * nstrips + k) * (2 * C) + (tid & 127)];
+  const int jc = min(j, CR - 1);
+  float wa[8], wb[8];  // W2 column slice (dz1 lane group j), W1 column slice (dm lane group c)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) wa[i] = w2[(pj * 8 + i) * CR + jc];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) wb[i] = w1[(p4 * per + min(i, per - 1)) * C + c4];
+  const float zj = r[C + jc];
+  const float svl = r[C + CR + (tid & 63)];
+  __builtin_amdgcn_sched_barrier(0);
   const size_t base = (size_t)n * HW * C;
   const size_t nv = (size_t)HW * C / 8;
   const size_t v0 = ((size_t)blockIdx.x * kCaVec) * blockDim.x + tid;
   float4 g0[kCaVec], g1[kCaVec];
 #pragma unroll
-  for (int k = 0; k < kCaVec; ++k) {
-    const size_t v = v0 + (size_t)k * blockDim.x;
-    if (v < nv) {
-      g0[k] = *reinterpret_cast<const float4*>(g + base + v * 8);
-      g1[k] = *reinterpret_cast<const float4*>(g + base + v * 8 + 4);
+  for (int k = 0; k < kCaVec; ++k) {  // clamped, unconditional (tail lanes store nothing)
+    const size_t e = base + min(v0 + (size_t)k * blockDim.x, nv - 1) * 8;
+    g0[k] = *reinterpret_cast<const float4*>(g + e);
+    g1[k] = *reinterpret_cast<const float4*>(g + e + 4);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  red[tid >> 7][tid & 127] = pa;
+  s[tid & 63] = svl;  // (unconditional: the load cannot sink past the stream loads)
+  lds_barrier();
+  float G = 0.f, sv = 0.f;
+  if (tid < C) {
+    G = red[0][tid] + red[1][tid];
+    const float ds = red[0][C + tid] + red[1][C + tid];
+    sv = s[tid];
+    dz2[tid] = ds * sv * (1.f - sv);
+  }
+  lds_barrier();
+  {  // dz1[j] = relu'(z1[j]) sum_c W2[c][j] dz2[c]
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a += wa[i] * dz2[pj * 8 + i];
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    a += __shfl_xor(a, 4, 64);
+    if (j < CR && pj == 0) dz1[j] = (zj > 0.f) ? a : 0.f;
+  }
+  lds_barrier();
+  {  // dm[c] = sum_j W1[j][c] dz1[j]
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (i < per) a += wb[i] * dz1[p4 * per + i];
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    if (p4 == 0) dm[c4] = a;
+  }
+  lds_barrier();
+  if (blockIdx.x == 0) {
+    float* br = brec + (size_t)n * (2 * C + CR);
+    if (tid < C) {
+      br[tid] = dz2[tid];
+      brec[(size_t)N * (2 * C + CR) + (size_t)n * C + tid] = dm[tid];
+      br[C + CR + tid] = sv * G + dm[tid];  // conv2 bias grad: sum_p du
     }
+    if (tid < CR) br[C + tid] = dz1[tid];
   }
 #pragma unroll
   for (int k = 0; k < kCaVec; ++k) {
     const size_t v = v0 + (size_t)k * blockDim.x;
     if (v >= nv) continue;
     const int c0 = (int)((v * 8) % C);
+    float dmh[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dmh[i] = dm[c0 + i] * (1.f / (float)HW);
     uint4 ob;
-    ob.x = pack2(g0[k].x * s[c0 + 0] + dmh[c0 + 0], g0[k].y * s[c0 + 1] + dmh[c0 + 1]);
-    ob.y = pack2(g0[k].z * s[c0 + 2] + dmh[c0 + 2], g0[k].w * s[c0 + 3] + dmh[c0 + 3]);
-    ob.z = pack2(g1[k].x * s[c0 + 4] + dmh[c0 + 4], g1[k].y * s[c0 + 5] + dmh[c0 + 5]);
-    ob.w = pack2(g1[k].z * s[c0 + 6] + dmh[c0 + 6], g1[k].w * s[c0 + 7] + dmh[c0 + 7]);
+    ob.x = pack2(g0[k].x * s[c0 + 0] + dmh[0], g0[k].y * s[c0 + 1] + dmh[1]);
+    ob.y = pack2(g0[k].z * s[c0 + 2] + dmh[2], g0[k].w * s[c0 + 3] + dmh[3]);
+    ob.z = pack2(g1[k].x * s[c0 + 4] + dmh[4], g1[k].y * s[c0 + 5] + dmh[5]);
+    ob.w = pack2(g1[k].z * s[c0 + 6] + dmh[6], g1[k].w * s[c0 + 7] + dmh[7]);
     *reinterpret_cast<uint4*>(du + base + v * 8) = ob;
   }
 }
@@ -766,9 +780,8 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
 int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
                      const float* w2, int N, int HW, int C, int R, bf16_t* du, float* brec, hipStream_t st) {
   if (C != 64 || C % R || (C / R) > 32 || (C / R) % 4 || (HW * C) % 8) return SRMI_ERR_SHAPE;
-  hipLaunchKernelGGL(ca_bwd_mlp_kernel, dim3(N), dim3(256), 0, st, part, nstrips, rec, w1, w2, N, C, C / R, brec);
-  hipLaunchKernelGGL(ca_bwd_du_kernel, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, g, rec, brec, N, HW, C, C / R,
-                     du);
+  hipLaunchKernelGGL(ca_bwd_du_kernel, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, g, part, nstrips, rec, w1, w2, N,
+                     HW, C, C / R, du, brec);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

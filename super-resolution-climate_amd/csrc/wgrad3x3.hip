@@ -519,32 +519,33 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
 }
 
 // -------------------------------------------------------------------- reduce
-// block = 64 output quads (256 consecutive outputs, float4 loads) x 8 slab phases
-// (512 threads); phase q sums slabs q, q+8, ... with 4 independent accumulators
-// and 8 loads in flight per thread (the reduction is latency-, not bandwidth-
-// limited at ~200 slabs), then the 8 x 4 partials are added in a fixed order
-// (deterministic).  The bias slab ([nslab][Cout]) is handled by the last block(s).
-constexpr int kRedPh = 8;
-__global__ void __launch_bounds__(64 * kRedPh) wgrad_reduce_kernel(const float* __restrict__ slab,
-                                                                   const float* __restrict__ bslab, int nslab,
-                                                                   int Cout, int ps, int layout, float alpha,
-                                                                   float* __restrict__ gw, float* __restrict__ gb) {
-  __shared__ float4 red[kRedPh][64];
+// block = kRedQ output quads (4*kRedQ consecutive outputs, float4 loads) x kRedPh
+// slab phases (512 threads); phase q sums slabs q, q+kRedPh, ... with 4
+// independent accumulators (4 loads in flight), then the kRedPh x 4 partials are
+// combined in a fixed 2-level order (deterministic).  64 outputs per block -> 576
+// blocks for a 64->64 conv (the former 256-output blocks left 112 CUs idle).
+// The bias slab ([nslab][Cout]) is handled by the last block(s).
+constexpr int kRedQ = 16, kRedPh = 32;
+__global__ void __launch_bounds__(kRedQ * kRedPh) wgrad_reduce_kernel(const float* __restrict__ slab,
+                                                                      const float* __restrict__ bslab, int nslab,
+                                                                      int Cout, int ps, int layout, float alpha,
+                                                                      float* __restrict__ gw, float* __restrict__ gb) {
+  __shared__ float4 red[kRedPh][kRedQ], red2[4][kRedQ];
   const int per = Cout * 576;
-  const int nwb = per / 256;  // weight blocks (per % 256 == 0 since Cout % 64 == 0)
-  const int qd = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int nwb = per / (4 * kRedQ);  // weight blocks (per % 64 == 0 since Cout % 64 == 0)
+  const int qd = threadIdx.x % kRedQ, ph = threadIdx.x / kRedQ;
   const bool is_w = (int)blockIdx.x < nwb;
   const float* src;
   int stride, o4, valid;
   if (is_w) {
     if (!gw) return;
-    o4 = blockIdx.x * 256 + qd * 4;
+    o4 = blockIdx.x * (4 * kRedQ) + qd * 4;
     src = slab + o4;
     stride = per;
     valid = 1;
   } else {
     if (!gb) return;
-    o4 = (blockIdx.x - nwb) * 256 + qd * 4;
+    o4 = (blockIdx.x - nwb) * (4 * kRedQ) + qd * 4;
     src = bslab + o4;
     stride = Cout;
     valid = o4 < Cout;
@@ -553,31 +554,43 @@ __global__ void __launch_bounds__(64 * kRedPh) wgrad_reduce_kernel(const float* 
 #pragma unroll
   for (int j = 0; j < 4; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (valid) {
-    int k = ph;
-    constexpr int U = 8;  // loads in flight
-    for (; k + (U - 1) * kRedPh < nslab; k += U * kRedPh) {
+    // phase ph sums slabs ph, ph + kRedPh, ... -- U loads in flight per round,
+    // clamped + zeroed past the end (adding 0.f is exact; no divergent branch)
+    constexpr int U = 4;
+    for (int k = ph; k < nslab; k += U * kRedPh) {
       float4 v[U];
 #pragma unroll
-      for (int j = 0; j < U; ++j) v[j] = *reinterpret_cast<const float4*>(src + (size_t)(k + j * kRedPh) * stride);
+      for (int j = 0; j < U; ++j) {
+        const int sl = k + j * kRedPh;
+        v[j] = *reinterpret_cast<const float4*>(src + (size_t)min(sl, nslab - 1) * stride);
+        if (sl >= nslab) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
 #pragma unroll
       for (int j = 0; j < U; ++j) {
-        float4& t = a[j & 3];
-        t.x += v[j].x; t.y += v[j].y; t.z += v[j].z; t.w += v[j].w;
+        a[j].x += v[j].x; a[j].y += v[j].y; a[j].z += v[j].z; a[j].w += v[j].w;
       }
-    }
-    for (; k < nslab; k += kRedPh) {
-      const float4 v = *reinterpret_cast<const float4*>(src + (size_t)k * stride);
-      a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
     }
   }
   red[ph][qd] = make_float4((a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y),
                             (a[0].z + a[1].z) + (a[2].z + a[3].z), (a[0].w + a[1].w) + (a[2].w + a[3].w));
   __syncthreads();
-  if (ph != 0 || !valid) return;
-  float4 r = red[0][qd];
+  // fixed-order 2-level combine of the kRedPh phase partials
+  constexpr int L1 = 4, PER = kRedPh / L1;
+  if (ph < L1) {
+    float4 r = red[ph][qd];
 #pragma unroll
-  for (int q = 1; q < kRedPh; ++q) {
-    const float4 t = red[q][qd];
+    for (int q = 1; q < PER; ++q) {
+      const float4 t = red[ph + q * L1][qd];
+      r.x += t.x; r.y += t.y; r.z += t.z; r.w += t.w;
+    }
+    red2[ph][qd] = r;
+  }
+  __syncthreads();
+  if (ph != 0 || !valid) return;
+  float4 r = red2[0][qd];
+#pragma unroll
+  for (int q = 1; q < L1; ++q) {
+    const float4 t = red2[q][qd];
     r.x += t.x; r.y += t.y; r.z += t.z; r.w += t.w;
   }
   const float s4[4] = {r.x, r.y, r.z, r.w};
@@ -610,8 +623,8 @@ __global__ void __launch_bounds__(64 * kRedPh) wgrad_reduce_kernel(const float* 
 int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, int layout, float alpha,
                         float* gw, float* gb, hipStream_t st) {
   if (Cout % 64) return SRMI_ERR_SHAPE;
-  const int blocks = Cout * 576 / 256 + (Cout + 255) / 256;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(64 * kRedPh), 0, st, slab, bslab, nslab, Cout, ps, layout,
+  const int blocks = Cout * 576 / (4 * kRedQ) + (Cout + 4 * kRedQ - 1) / (4 * kRedQ);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(kRedQ * kRedPh), 0, st, slab, bslab, nslab, Cout, ps, layout,
                      alpha, gw, gb);
   SRMI_CHECK_LAUNCH();
   return 0;
