@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=64, help="tiles per GPU")
     ap.add_argument("--channels", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=12, help="timed CPU oracle steps (~1 s each at B=4)")
     ap.add_argument("--no-interp-loss", action="store_true")
     ap.add_argument("--no-inference", action="store_true", help="skip the C5 tiled-region inference line")
     ap.add_argument("--micro", type=int, default=None, help="micro-batches per step (default: trainer's choice)")
