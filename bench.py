@@ -37,6 +37,7 @@ METRIC = "training tiles/sec (48→192, bf16) at 1/2/4/8 MI355X; inference MPix/
 PEAK_BF16_TFLOPS = 2516.6          # 256 CU x 2.4 GHz x 4096 FLOP/clk (MI355X_MICROARCH.md, dense)
 HBM_PEAK_GBS = 8000.0
 TRAIN_GFLOP_PER_TILE_C2 = 219.9    # 6 x conv MACs per tile
+EDSR_TRAIN_GFLOP_PER_TILE = 27.4   # C4 EDSR x8 4-var, 6 x 4.57 G MAC
 CONV64_FLOP_PER_TILE = 2 * 64 * 576 * 48 * 48   # one 64->64 3x3 conv at 48x48 (84.93 M MAC)
 
 
@@ -51,6 +52,8 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=12, help="timed CPU oracle steps (~1 s each at B=4)")
     ap.add_argument("--no-interp-loss", action="store_true")
     ap.add_argument("--no-inference", action="store_true", help="skip the C5 tiled-region inference line")
+    ap.add_argument("--no-edsr", action="store_true", help="skip the C4 EDSR x8 line")
+    ap.add_argument("--edsr-batch", type=int, default=64)
     ap.add_argument("--micro", type=int, default=None, help="micro-batches per step (default: trainer's choice)")
     ap.add_argument("--infer-region", type=int, default=4096, help="C5 HR region side (BASELINE: 4096)")
     ap.add_argument("--infer-iters", type=int, default=5)
@@ -178,6 +181,32 @@ def inference_bench(dev, side, iters):
                                    "(floor), graph-replayed", "graph": True}}
 
 
+def edsr_bench(dev, batch, steps, warmup):
+    """BASELINE config 4: EDSR-style x8 (16 ResBlocks, 64 features, 3 x [conv 64->256 +
+    PixelShuffle 2]), 4-variable tiles 32x32 -> 256x256, full train step (down8, fwd,
+    RMSE + interp RMSE, bwd, Adam) on this GPU.  Operands bf16 / fp32 accumulate
+    (BASELINE names fp32; the engine's one compute type is stated in `dtype`)."""
+    from srmi.engine import NetSpec
+    from srmi.trainer import FusedTrainer
+    spec = NetSpec(arch="edsr", nchannels_in=4, nchannels_out=4, nfeatures=64, nlayers=16, scale=8)
+    tr = FusedTrainer(spec, batch, (32, 32), lr=1e-4, device=dev, seed=0)
+    hr = torch.tensor(synthetic_hr(batch, 4, 256, 4321)).to(dev)
+    for _ in range(warmup):
+        tr.step(hr)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.step(hr)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    v = batch * steps / dt
+    return {"metric": "EDSR x8 training tiles/sec (32->256, 4-var)", "value": round(v, 2), "unit": "tiles/s",
+            "ms_per_step": round(1000 * dt / steps, 3), "steps": steps, "warmup": warmup, "dtype": "bf16",
+            "data": "synthetic", "model_tflops": round(v * EDSR_TRAIN_GFLOP_PER_TILE / 1000.0, 1),
+            "config": {"workload": "edsr-16-64 x8 train step (down8 + fwd + RMSE + interp RMSE + bwd + Adam), "
+                                   "4-var 32x32->256x256 tiles", "batch": batch}}
+
+
 def cpu_baseline(channels, steps):
     """Oracle (PyTorch-CPU restatement of the reference step) on this host's cores."""
     from oracle import rcan_oracle as ro
@@ -256,6 +285,9 @@ def main():
         infer = None
         if not args.no_inference and world == 1:
             infer = inference_bench(dev, args.infer_region, args.infer_iters)
+        edsr = None
+        if not args.no_edsr and world == 1:
+            edsr = edsr_bench(dev, args.edsr_batch, 5, 2)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(C, args.cpu_steps)
@@ -273,6 +305,7 @@ def main():
             "roofline_conv_fwd": roof_conv,
             "cpu_baseline": cpu,
             "inference": infer,
+            "edsr_x8": edsr,
         }
         print(json.dumps(rec), flush=True)
     if info.enabled:

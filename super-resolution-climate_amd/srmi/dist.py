@@ -125,26 +125,45 @@ class GradReducer:
     def covered(self) -> int:
         return sum(n for b in self.buckets for _, n in b.ranges)
 
-    def reduce(self, grads: torch.Tensor, events_recorded: bool = True):
+    def new_events(self) -> List:
+        """One more set of group events (one set per micro-batch engine)."""
+        return [torch.cuda.Event() for _ in range(max(self.n_events, 0))] if self.cuda else []
+
+    def reduce(self, grads: torch.Tensor, events_recorded: bool = True, extra: Sequence[torch.Tensor] = (),
+               extra_events: Sequence[Sequence] = ()):
         """Call right after the (asynchronous) backward has been enqueued.  With
-        events_recorded False (the backward did not record the group events, e.g.
-        summed micro-batch gradients) every bucket waits for the current stream."""
+        events_recorded False (the backward did not record the group events) every
+        bucket waits for the current stream.
+
+        extra: gradients of further micro-batch engines (same layout); bucket by
+        bucket they are added into `grads` on the communication stream right
+        before that bucket's all-reduce, once every engine's group event for it
+        (self.events, then extra_events[k]) has fired -- so with micro-batches the
+        all-reduce still overlaps the rest of backward.  The caller must not add
+        them itself."""
         if not self.info.enabled:
             return
         if not self.cuda:
             for b in self.buckets:
                 for off, n in b.ranges:
+                    for x in extra:
+                        grads[off:off + n].add_(x[off:off + n])
                     dist.all_reduce(grads[off:off + n], op=dist.ReduceOp.SUM)
             return
+        from .engine import axpy
         main = torch.cuda.current_stream()
         works = []
         with torch.cuda.stream(self.stream):
             for b in self.buckets:
                 if b.event_index is not None and events_recorded:
                     self.stream.wait_event(self.events[b.event_index])
+                    for evs in extra_events:
+                        self.stream.wait_event(evs[b.event_index])
                 else:
                     self.stream.wait_stream(main)
                 for off, n in b.ranges:
+                    for x in extra:
+                        axpy(grads[off:off + n], x[off:off + n], 1.0, stream=self.stream)
                     works.append(dist.all_reduce(grads[off:off + n], op=dist.ReduceOp.SUM, async_op=True))
         for w in works:
             w.wait()

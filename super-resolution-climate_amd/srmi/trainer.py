@@ -100,6 +100,8 @@ class FusedTrainer:
         self.miloss4 = [torch.zeros(4, dtype=torch.float32, device=self.device) for _ in range(micro)]
         self.streams = [None] + [torch.cuda.Stream(device=self.device) for _ in range(micro - 1)]
         self.reducer = GradReducer(self.eng.table, spec.arch, spec.nlayers, self.info, self.device)
+        # group events of engines 1.. (engine 0 records into reducer.events)
+        self.xevents = [self.reducer.new_events() for _ in range(micro - 1)]
         for e in self.engines:
             e.pack(self.params)
 
@@ -138,18 +140,25 @@ class FusedTrainer:
             Engine.rmse_finalize(self.iloss4)
         for st in self.streams[1:]:
             st.wait_stream(main)
-        # backward per micro-batch with the global loss scale
-        ev = self.reducer.events if (self.info.enabled and self.reducer.cuda and self.micro == 1) else None
+        # backward per micro-batch with the global loss scale.  Data parallel: every
+        # engine records its residual-group events; the reducer adds the engines'
+        # gradients bucket by bucket on its stream and all-reduces each bucket as
+        # soon as all engines are past it (overlapped with the rest of backward).
+        dp = self.info.enabled and self.reducer.cuda
+        evs = [self.reducer.events] + self.xevents if dp else [None] * self.micro
         for k, eng in enumerate(self.engines):
             sl = slice(k * mb, (k + 1) * mb)
             with self._ctx(k):
                 eng.backward(self.params, self.lrbuf[sl], self.mgrads[k], sr=self.sr[sl], hr=hr[sl],
-                             loss4=self.loss4, events=ev)
+                             loss4=self.loss4, events=evs[k])
         for st in self.streams[1:]:
             main.wait_stream(st)
-        for g in self.mgrads[1:]:
-            axpy(self.grads, g, 1.0)  # exact gradient of the whole batch
-        self.reducer.reduce(self.grads, events_recorded=ev is not None)
+        if dp:
+            self.reducer.reduce(self.grads, events_recorded=True, extra=self.mgrads[1:], extra_events=self.xevents)
+        else:
+            for g in self.mgrads[1:]:
+                axpy(self.grads, g, 1.0)  # exact gradient of the whole batch
+            self.reducer.reduce(self.grads, events_recorded=False)
         self.t += 1
         adam_step(self.params, self.grads, self.m, self.v, self.t, self.lr, self.betas, self.eps, self.wd)
         for k, eng in enumerate(self.engines):

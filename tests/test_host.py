@@ -127,7 +127,7 @@ def test_grad_buckets_partition_every_parameter_once():
     assert [x.event_index for x in b] == [0, 1, 2, None]
 
 
-def _dp_rank(rank, world, port, q):
+def _dp_rank(rank, world, port, q, micro=1):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import sys
@@ -151,22 +151,31 @@ def _dp_rank(rank, world, port, q):
     count = float(hr_all.numel())
     L, scale = global_rmse_scale(S, count, info)
     dy = (out - hr).detach() * scale          # dL/dy with the GLOBAL count and L
-    out.backward(dy)
     sd = dict(model.named_parameters())
-    grads = torch.cat([sd[n].grad.reshape(-1) for n, _, _, _ in table])
-    GradReducer(table, "rcan", 1, info, torch.device("cpu")).reduce(grads)
+    mg = []
+    per = hr.shape[0] // micro
+    for k in range(micro):  # micro-batch engines: separate gradients, summed by the reducer
+        model.zero_grad()
+        o = model(ro.downsample(hr[k * per:(k + 1) * per], 4))
+        o.backward(dy[k * per:(k + 1) * per])
+        mg.append(torch.cat([sd[n].grad.reshape(-1) for n, _, _, _ in table]))
+    GradReducer(table, "rcan", 1, info, torch.device("cpu")).reduce(mg[0], extra=mg[1:])
+    grads = mg[0]
     q.put((rank, float(L), grads.numpy()))
     dist.destroy_process_group()
 
 
-def test_data_parallel_semantics_gloo_world2():
-    """2 ranks x 2 tiles == 1 process x 4 tiles: global RMSE and summed grads."""
+@pytest.mark.parametrize("micro", [1, 2])
+def test_data_parallel_semantics_gloo_world2(micro):
+    """2 ranks x 2 tiles == 1 process x 4 tiles: global RMSE and summed grads
+    (micro=2: each rank's 2 tiles as 2 micro-batch gradients, summed per bucket
+    by the reducer before its all-reduce)."""
     import multiprocessing as mp
     import random
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29500 + random.randint(0, 2000)
-    ps = [ctx.Process(target=_dp_rank, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_dp_rank, args=(r, 2, port, q, micro)) for r in range(2)]
     for p in ps:
         p.start()
     res = sorted([q.get(timeout=300) for _ in ps], key=lambda t: t[0])

@@ -7,7 +7,7 @@ shift
 cd $R; mkdir -p gpurun_out
 rm -f gpurun_out/ab_new_*.log gpurun_out/ab_old_*.log
 for i in 1 2 3; do
-  timeout -k 10 300 python bench.py --no-cpu-baseline --no-inference --steps 20 --warmup 3 "$@" > gpurun_out/ab_new_$i.log 2>&1 || exit 1
-  SRMI_LIB=$ALT timeout -k 10 300 python bench.py --no-cpu-baseline --no-inference --steps 20 --warmup 3 "$@" > gpurun_out/ab_old_$i.log 2>&1 || exit 2
+  timeout -k 10 300 python bench.py --no-cpu-baseline --no-inference --no-edsr --steps 20 --warmup 3 "$@" > gpurun_out/ab_new_$i.log 2>&1 || exit 1
+  SRMI_LIB=$ALT timeout -k 10 300 python bench.py --no-cpu-baseline --no-inference --no-edsr --steps 20 --warmup 3 "$@" > gpurun_out/ab_old_$i.log 2>&1 || exit 2
 done
 grep -o '"value": [0-9.]*' gpurun_out/ab_*.log
