@@ -25,6 +25,8 @@
  *                                   sres/base/source/swot/raw.py:216-233, :169-181
  *   srmi_batch_prep              -> norm 'lnorm' (swot/raw.py:169-181) + xyflip
  *                                   sres/base/source/batch.py:37-49 + downsample
+ *   srmi_llc_*, srmi_tiles_*     -> SWOTRawDataLoader.load_file + get_tiles
+ *                                   sres/base/source/swot/raw.py:133-145, :216-233
  *   srmi_tiles_to_region         -> denorm + assemble_images
  *                                   sres/controller/dual_trainer.py:67-77, :482-512
  */
@@ -175,6 +177,28 @@ int srmi_tiles_to_region(const float* tiles, const float* mean, const float* std
  * skipped).  T even. */
 int srmi_batch_prep(const float* raw, int B, int C, int T, int flip_index, int scale, float* hr, float* lr,
                     float* mean, float* std, void* stream);
+
+/* ---- on-disk LLC4320 source -> tiles --------------- */
+/* Replaces SWOTRawDataLoader.load_file (sres/base/source/swot/raw.py:133-145):
+ * template_be = the raw bytes of the '>f4' mask template (13 nx^2 words, 0 =
+ * land), data_be = the raw bytes of a '>f4' wet-value file.  The index map of
+ * the ROI [y0, y0+ys) x [x0, x0+xs) of the east | west.T[::-1] image (mds2d,
+ * swot/util.py:3-7; subset_roi raw.py:38-45) is built once per template:
+ * idx_map[ys*xs] = wet-value index or -1; *n_wet (device) = wet cell count.
+ * workspace: srmi_llc_index_map_workspace bytes (n_template int32 ranks + scan). */
+int srmi_llc_index_map_workspace(long long n_template, size_t* bytes);
+int srmi_llc_index_map(const void* template_be, long long n_template, int nx, int y0, int ys, int x0, int xs,
+                       int* idx_map, long long* n_wet, void* workspace, size_t workspace_bytes, void* stream);
+/* out[p] = decoded data[idx_map[p]], NaN for land: one time slice of one variable */
+int srmi_llc_gather(const void* data_be, long long n_values, const int* idx_map, long long npix, float* out,
+                    void* stream);
+/* get_tiles (raw.py:216-233): bad[c*gy*gx + t] = 1 where tile t of channel c of
+ * region [C][H][W] holds a non-finite value (floor grid gy = H/ty, gx = W/tx) */
+int srmi_tiles_nonfinite(const float* region, int C, int H, int W, int ty, int tx, int* bad, void* stream);
+/* out[m] (ty x tx plane m of the [n/C][C][ty][tx] result) = tile plane src[m]
+ * (= c*gy*gx + t of the channel-major flattening) */
+int srmi_tiles_gather(const float* region, int C, int H, int W, int ty, int tx, const int* src, int nslots,
+                      float* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -21,6 +21,8 @@ from the imported reference (``tests/golden/make_golden.py``):
 * Adam ................. torch.optim.Adam defaults used at dual_trainer.py:126
 * batch preparation .... norm lnorm + xyflip (swot/raw.py:160-181,
                          sres/base/source/batch.py:33-49)
+* on-disk LLC source ... load_file + mds2d + subset_roi + get_tiles
+                         (swot/raw.py:133-145, :38-45, :216-233; swot/util.py:3-7)
 * tiled inference ...... get_tiles + lnorm (sres/base/source/swot/raw.py:216-233,
                          :169-181), denorm + assemble_images + process_image
                          (dual_trainer.py:67-77, :482-512, :396-480); pinned by
@@ -368,3 +370,55 @@ def prep_batch(raw: np.ndarray, flip_index: int, scale: int):
     std = raw.std(axis=(2, 3))
     hr = xyflip((raw - mean[:, :, None, None]) / std[:, :, None, None], flip_index)
     return hr, downsample_explicit(hr, scale), mean, std
+
+
+# --------------------------------------------------------------------------
+# On-disk source -> tiles, pinned by digests of the
+# reference's own load_file / get_tiles outputs (tests/golden/make_golden_llc.py).
+
+def mds2d(d: np.ndarray, nx: int = 4320):
+    """util.py:3-7 rearrange (mds2d with one array): LLC faces 1-6 -> east
+    [3nx, 2nx], faces 8-13 -> west [2nx, 3nx] (face 7, the Arctic, unused)."""
+    east = np.concatenate([d[:nx * nx * 3].reshape(3 * nx, nx), d[nx * nx * 3:nx * nx * 6].reshape(3 * nx, nx)], axis=1)
+    west = d[nx * nx * 7:].reshape(nx * 2, nx * 3)
+    return east, west
+
+
+def llc_load_file(template: np.ndarray, wet_values: np.ndarray, roi: Optional[Dict] = None,
+                  nx: int = 4320) -> np.ndarray:
+    """SWOTRawDataLoader.load_file (sres/base/source/swot/raw.py:133-145) on
+    already-decoded arrays: wet cells (template != 0) take the file's values in
+    order, land is NaN; east | west.T[::-1] assembled to [1, 3nx, 4nx]; then
+    subset_roi (raw.py:38-45)."""
+    full = template.astype(np.float32).copy()
+    mask = full != 0
+    if int(mask.sum()) != len(wet_values):
+        raise ValueError(f"{len(wet_values)} values for {int(mask.sum())} wet cells")
+    full[mask] = wet_values
+    full[~mask] = np.nan
+    east, west = mds2d(full, nx)
+    res = np.concatenate([east, west.T[::-1, :]], axis=1)[None]
+    if roi:
+        x0, xs = roi.get("x0", 0), roi.get("xs", res.shape[-1])
+        y0, ys = roi.get("y0", 0), roi.get("ys", res.shape[-2])
+        res = res[..., y0:y0 + ys, x0:x0 + xs]
+    return res
+
+
+def get_tiles(var_data: Sequence[np.ndarray], ty: int, tx: int):
+    """SWOTRawDataLoader.get_tiles (raw.py:216-233) with the default TileGrid
+    (origin 0, tile_grid -1 -> floor grid, sres/data/tiles.py:112-135): tiles
+    flattened channel-major, tiles whose mean is not finite dropped, the rest
+    reshaped to [n // C, C, ty, tx] -- with C > 1 this packs consecutive kept
+    tiles of the SAME variable into the channel axis (the reference's quirk,
+    reproduced).  -> (tiles, tile_ids (first n // C kept flat ids), (gy, gx))."""
+    raw = np.concatenate(var_data, axis=0)
+    C, H, W = raw.shape
+    gy, gx = H // ty, W // tx
+    region = raw[..., :gy * ty, :gx * tx]
+    t = region.reshape(C, gy, ty, gx, tx).swapaxes(2, 3).reshape(C * gy * gx, ty, tx)
+    msk = np.isfinite(t.mean(axis=-1).mean(axis=-1))
+    kept = t[msk]
+    ids = np.flatnonzero(msk)
+    res = kept.reshape(kept.shape[0] // C, C, ty, tx)
+    return res, ids[:res.shape[0]], (gy, gx)

@@ -864,6 +864,31 @@ int srmi_tail_forward(const void* x, const float* w, const float* b, int N, int 
   return tail_fwd_launch((const bf16_t*)x, w, b, N, C, H, W, y, S_(stream));
 }
 
+int srmi_llc_index_map_workspace(long long n_template, size_t* bytes) {
+  if (!bytes) return SRMI_ERR_ARG;
+  return llc_index_map_workspace(n_template, bytes);
+}
+
+int srmi_llc_index_map(const void* template_be, long long n_template, int nx, int y0, int ys, int x0, int xs,
+                       int* idx_map, long long* n_wet, void* workspace, size_t workspace_bytes, void* stream) {
+  return llc_index_map_launch(static_cast<const uint32_t*>(template_be), n_template, nx, y0, ys, x0, xs, idx_map,
+                              n_wet, workspace, workspace_bytes, S_(stream));
+}
+
+int srmi_llc_gather(const void* data_be, long long n_values, const int* idx_map, long long npix, float* out,
+                    void* stream) {
+  return llc_gather_launch(static_cast<const uint32_t*>(data_be), n_values, idx_map, npix, out, S_(stream));
+}
+
+int srmi_tiles_nonfinite(const float* region, int C, int H, int W, int ty, int tx, int* bad, void* stream) {
+  return tiles_nonfinite_launch(region, C, H, W, ty, tx, bad, S_(stream));
+}
+
+int srmi_tiles_gather(const float* region, int C, int H, int W, int ty, int tx, const int* src, int nslots,
+                      float* out, void* stream) {
+  return tiles_gather_launch(region, C, H, W, ty, tx, src, nslots, out, S_(stream));
+}
+
 int srmi_batch_prep(const float* raw, int B, int C, int T, int flip_index, int scale, float* hr, float* lr,
                     float* mean, float* std, void* stream) {
   return batch_prep_launch(raw, B, C, T, flip_index, scale, hr, lr, mean, std, S_(stream));

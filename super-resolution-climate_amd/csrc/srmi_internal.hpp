@@ -131,6 +131,14 @@ int region_to_tiles_launch(const float* region, int C, int H, int W, int ty, int
                            float* stdv, int* bad, hipStream_t st);
 int tiles_to_region_launch(const float* tiles, const float* mean, const float* stdv, const int* inv, int C, int ty,
                            int tx, int gy, int gx, float* out, hipStream_t st);
+int llc_index_map_workspace(long long n, size_t* bytes);
+int llc_index_map_launch(const uint32_t* tmpl, long long n, int nx, int y0, int ys, int x0, int xs, int* idx,
+                         long long* n_wet, void* ws, size_t ws_bytes, hipStream_t st);
+int llc_gather_launch(const uint32_t* data, long long nvals, const int* idx, long long np, float* out,
+                      hipStream_t st);
+int tiles_nonfinite_launch(const float* region, int C, int H, int W, int ty, int tx, int* bad, hipStream_t st);
+int tiles_gather_launch(const float* region, int C, int H, int W, int ty, int tx, const int* src, int nslots,
+                        float* out, hipStream_t st);
 int batch_prep_launch(const float* raw, int B, int C, int T, int flip, int scale, float* hr, float* lr, float* mean,
                       float* stdv, hipStream_t st);
 

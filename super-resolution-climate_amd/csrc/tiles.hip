@@ -11,6 +11,10 @@
 // (sres/base/source/batch.py:37-49, applied by load_batch :301) and the
 // apply_network input downsample (array.py:72-76) -- one pass over HBM.
 //
+// llc_* replace SWOTRawDataLoader.load_file (swot/raw.py:133-145, mds2d
+// swot/util.py:3-7, subset_roi raw.py:38-45) and tiles_nonfinite/tiles_gather
+// the tiling of get_tiles (raw.py:216-233) -- SURVEY.md §8f row 3, see below.
+//
 // tiles_to_region replaces denorm (dual_trainer.py:67-77: x * std + mean) fused
 // with assemble_images (dual_trainer.py:482-512: tile id -> grid cell
 // (tid / gx, tid % gx), cells without a tile are NaN).
@@ -236,6 +240,213 @@ int batch_prep_launch(const float* raw, int B, int C, int T, int flip, int scale
     hipLaunchKernelGGL(batch_prep_kernel<false>, dim3(C, B), dim3(kPrepThreads), 0, st, raw, C, T, flip, scale, hr,
                        lr, mean, stdv);
   }
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------ LLC4320 source
+// The reference expands a '>f4' wet-value file through a '>f4' mask template
+// (13 nx^2 cells, 0 = land) on the host, then cuts the east | flipped-west
+// image and the ROI.  Device version: the template -> ROI index map is built
+// ONCE (the template is static): per-cell wet flags, a 3-kernel exclusive scan
+// (block counts, one-block scan of the counts, block-local ranks), then each ROI
+// pixel looks up the rank of its LLC cell.  Every time slice is then ONE
+// gather: out[p] = bswap(data[idx[p]]) or NaN -- HBM-bound byte work.
+constexpr int kScanThreads = 1024, kScanPer = 16, kScanBlk = kScanThreads * kScanPer;
+
+__device__ __forceinline__ bool llc_wet(uint32_t be_word) {
+  // file bytes are big-endian float32; "template != 0" (+-0 are land, NaN is wet)
+  return (__builtin_bswap32(be_word) & 0x7fffffffu) != 0u;
+}
+
+__global__ void __launch_bounds__(kScanThreads) llc_count_kernel(const uint32_t* __restrict__ tmpl, long long n,
+                                                                 int* __restrict__ blkcnt) {
+  __shared__ int red[kScanThreads / 64];
+  const long long base = (long long)blockIdx.x * kScanBlk + (long long)threadIdx.x * kScanPer;
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) c += (base + k < n) && llc_wet(tmpl[base + k]);
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int i = 0; i < kScanThreads / 64; ++i) t += red[i];
+    blkcnt[blockIdx.x] = t;
+  }
+}
+
+// one block: blkoff[b] = sum_{i<b} blkcnt[i]; *total = sum
+__global__ void __launch_bounds__(kScanThreads) llc_scan_counts_kernel(const int* __restrict__ blkcnt, int nb,
+                                                                       long long* __restrict__ blkoff,
+                                                                       long long* __restrict__ total) {
+  __shared__ long long wsum[kScanThreads / 64];
+  const int per = (nb + kScanThreads - 1) / kScanThreads;
+  const int b0 = threadIdx.x * per;
+  long long s = 0;
+  for (int i = 0; i < per; ++i)
+    if (b0 + i < nb) s += blkcnt[b0 + i];
+  // exclusive scan of s over the block: wave inclusive scan + wave offsets
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  long long inc = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  long long woff = 0;
+  for (int i = 0; i < w; ++i) woff += wsum[i];
+  long long run = woff + inc - s;
+  for (int i = 0; i < per; ++i)
+    if (b0 + i < nb) {
+      blkoff[b0 + i] = run;
+      run += blkcnt[b0 + i];
+    }
+  if (threadIdx.x == kScanThreads - 1) *total = run;
+}
+
+// rank[i] = number of wet cells before i (wet i), -1 for land
+__global__ void __launch_bounds__(kScanThreads) llc_rank_kernel(const uint32_t* __restrict__ tmpl, long long n,
+                                                                const long long* __restrict__ blkoff,
+                                                                int* __restrict__ rank) {
+  __shared__ int wsum[kScanThreads / 64];
+  const long long base = (long long)blockIdx.x * kScanBlk + (long long)threadIdx.x * kScanPer;
+  uint32_t bits = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) bits |= (uint32_t)((base + k < n) && llc_wet(tmpl[base + k])) << k;
+  const int c = __builtin_popcount(bits);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int inc = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int woff = 0;
+  for (int i = 0; i < w; ++i) woff += wsum[i];
+  long long r = blkoff[blockIdx.x] + woff + inc - c;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    if (base + k < n) {
+      const bool wet = (bits >> k) & 1u;
+      rank[base + k] = wet ? (int)r : -1;
+      r += wet;
+    }
+  }
+}
+
+// ROI pixel (y, x) of the [3nx, 4nx] east | west.T[::-1] image -> LLC cell
+__device__ __forceinline__ long long llc_cell(int Y, int X, int nx) {
+  const long long n2 = (long long)nx * nx;
+  if (X < nx) return (long long)Y * nx + X;
+  if (X < 2 * nx) return 3 * n2 + (long long)Y * nx + (X - nx);
+  return 7 * n2 + (long long)(X - 2 * nx) * 3 * nx + (3 * nx - 1 - Y);
+}
+
+__global__ void __launch_bounds__(256) llc_map_kernel(const int* __restrict__ rank, int nx, int y0, int ys, int x0,
+                                                      int xs, int* __restrict__ idx) {
+  const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (long long)ys * xs) return;
+  const int y = (int)(p / xs), x = (int)(p - (long long)y * xs);
+  idx[p] = rank[llc_cell(y0 + y, x0 + x, nx)];
+}
+
+int llc_index_map_workspace(long long n, size_t* bytes) {
+  if (n < 1) return SRMI_ERR_SHAPE;
+  const long long nb = (n + kScanBlk - 1) / kScanBlk;
+  *bytes = (size_t)n * 4 + (size_t)nb * 4 + (size_t)nb * 8 + 64;
+  return 0;
+}
+
+int llc_index_map_launch(const uint32_t* tmpl, long long n, int nx, int y0, int ys, int x0, int xs, int* idx,
+                         long long* n_wet, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (nx < 1 || n != 13LL * nx * nx || ys < 1 || xs < 1 || y0 < 0 || x0 < 0 || y0 + ys > 3 * nx ||
+      x0 + xs > 4 * nx)
+    return SRMI_ERR_SHAPE;
+  size_t need = 0;
+  llc_index_map_workspace(n, &need);
+  if (!tmpl || !idx || !n_wet || !ws || ws_bytes < need) return SRMI_ERR_ARG;
+  const long long nb = (n + kScanBlk - 1) / kScanBlk;
+  char* w = static_cast<char*>(ws);
+  int* rank = reinterpret_cast<int*>(w);
+  long long* blkoff = reinterpret_cast<long long*>(w + (((size_t)n * 4 + 7) & ~(size_t)7));
+  int* blkcnt = reinterpret_cast<int*>(reinterpret_cast<char*>(blkoff) + (size_t)nb * 8);
+  hipLaunchKernelGGL(llc_count_kernel, dim3((unsigned)nb), dim3(kScanThreads), 0, st, tmpl, n, blkcnt);
+  hipLaunchKernelGGL(llc_scan_counts_kernel, dim3(1), dim3(kScanThreads), 0, st, blkcnt, (int)nb, blkoff, n_wet);
+  hipLaunchKernelGGL(llc_rank_kernel, dim3((unsigned)nb), dim3(kScanThreads), 0, st, tmpl, n, blkoff, rank);
+  const long long np = (long long)ys * xs;
+  hipLaunchKernelGGL(llc_map_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, rank, nx, y0, ys, x0, xs,
+                     idx);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// out[p] = float(bswap(data[idx[p]])), NaN for land (idx < 0) or idx >= nvals
+__global__ void __launch_bounds__(256) llc_gather_kernel(const uint32_t* __restrict__ data, long long nvals,
+                                                         const int* __restrict__ idx, long long np,
+                                                         float* __restrict__ out) {
+  const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= np) return;
+  const int i = idx[p];
+  out[p] = (i >= 0 && i < nvals) ? __uint_as_float(__builtin_bswap32(data[i])) : __int_as_float(0x7fc00000);
+}
+
+int llc_gather_launch(const uint32_t* data, long long nvals, const int* idx, long long np, float* out,
+                      hipStream_t st) {
+  if (np < 1 || nvals < 0) return SRMI_ERR_SHAPE;
+  if (!data || !idx || !out) return SRMI_ERR_ARG;
+  hipLaunchKernelGGL(llc_gather_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, data, nvals, idx, np,
+                     out);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// get_tiles' keep mask: bad[c * gy*gx + t] = 1 when tile t of channel c holds a
+// non-finite value (its mean is then not finite).  grid (gy*gx, C)
+__global__ void __launch_bounds__(256) tiles_nonfinite_kernel(const float* __restrict__ region, int H, int W, int ty,
+                                                              int tx, int gx, int* __restrict__ bad) {
+  const int t = blockIdx.x, c = blockIdx.y;
+  const int y0 = (t / gx) * ty, x0 = (t % gx) * tx;
+  const float* src = region + (size_t)c * H * W + (size_t)y0 * W + x0;
+  int nf = 0;
+  for (int i = threadIdx.x; i < ty * tx; i += 256) nf |= !isfinite(src[(size_t)(i / tx) * W + (i % tx)]);
+  nf = __syncthreads_or(nf);
+  if (threadIdx.x == 0) bad[(size_t)c * gridDim.x + t] = nf;
+}
+
+int tiles_nonfinite_launch(const float* region, int C, int H, int W, int ty, int tx, int* bad, hipStream_t st) {
+  if (C < 1 || ty < 1 || tx < 1 || H < ty || W < tx) return SRMI_ERR_SHAPE;
+  if (!region || !bad) return SRMI_ERR_ARG;
+  hipLaunchKernelGGL(tiles_nonfinite_kernel, dim3((H / ty) * (W / tx), C), dim3(256), 0, st, region, H, W, ty, tx,
+                     W / tx, bad);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// out plane m (= [m / C][m % C] of the [n/C][C][ty][tx] result) <- tile plane
+// src[m] = c * gy*gx + t of the channel-major flattening.  grid (ceil(ty*tx/1024), nslots)
+__global__ void __launch_bounds__(256) tiles_gather_kernel(const float* __restrict__ region, int H, int W, int ty,
+                                                           int tx, int gx, int ntile, const int* __restrict__ src,
+                                                           float* __restrict__ out) {
+  const int m = blockIdx.y, j = src[m];
+  const int c = j / ntile, t = j - c * ntile;
+  const int y0 = (t / gx) * ty, x0 = (t % gx) * tx;
+  const float* s = region + (size_t)c * H * W + (size_t)y0 * W + x0;
+  float* d = out + (size_t)m * ty * tx;
+  for (int i = blockIdx.x * 1024 + threadIdx.x; i < min(ty * tx, (int)(blockIdx.x + 1) * 1024); i += 256)
+    d[i] = s[(size_t)(i / tx) * W + (i % tx)];
+}
+
+int tiles_gather_launch(const float* region, int C, int H, int W, int ty, int tx, const int* src, int nslots,
+                        float* out, hipStream_t st) {
+  if (C < 1 || ty < 1 || tx < 1 || H < ty || W < tx || nslots < 0) return SRMI_ERR_SHAPE;
+  if (nslots == 0) return 0;
+  if (!region || !src || !out) return SRMI_ERR_ARG;
+  const int gx = W / tx, ntile = (H / ty) * gx;
+  hipLaunchKernelGGL(tiles_gather_kernel, dim3((ty * tx + 1023) / 1024, nslots), dim3(256), 0, st, region, H, W, ty,
+                     tx, gx, ntile, src, out);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

@@ -65,6 +65,12 @@ _SIGS = {
     "srmi_region_to_tiles": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P], C.c_int),
     "srmi_tiles_to_region": ([P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),
     "srmi_batch_prep": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P], C.c_int),
+    "srmi_llc_index_map_workspace": ([C.c_longlong, C.POINTER(C.c_size_t)], C.c_int),
+    "srmi_llc_index_map": ([P, C.c_longlong, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, C.c_size_t, P],
+                           C.c_int),
+    "srmi_llc_gather": ([P, C.c_longlong, P, C.c_longlong, P, P], C.c_int),
+    "srmi_tiles_nonfinite": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),
+    "srmi_tiles_gather": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int, P, P], C.c_int),
 }
 EXPORTED = tuple(_SIGS)
 
