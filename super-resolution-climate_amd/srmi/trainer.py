@@ -19,6 +19,7 @@ from typing import Dict, Optional
 
 import torch
 
+from . import checkpoint as ckpt
 from .dist import DistInfo, GradReducer, allreduce_sum_
 from .engine import Engine, NetSpec, adam_step, axpy, downsample, upsample
 
@@ -182,8 +183,23 @@ class FusedTrainer:
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
         """Reference-format model state_dict (CPU copies)."""
-        out = {}
-        host = self.params.detach().cpu()
-        for name, off, n, shape in self.eng.table:
-            out[name] = host[off:off + n].view(shape).clone()
-        return out
+        return ckpt.model_state_dict(self.params, self.eng.table)
+
+    def checkpoint(self, epoch: int = 0, itime: int = 0, loss: float = 0.0) -> Dict:
+        """What CheckpointManager.save_checkpoint writes (checkpoints.py:18-26): model
+        and torch.optim.Adam state dicts in the reference's layouts."""
+        return ckpt.checkpoint(epoch, itime, self.params, self.eng.table, self.m, self.v, self.t, self.lr,
+                               self.betas, self.eps, self.wd, loss)
+
+    def load_checkpoint(self, state: Dict) -> None:
+        """Resume from a reference-format checkpoint dict (checkpoints.py:35-51,
+        update_model=True): weights, Adam moments, step count and hyper-parameters;
+        the bf16 filter packs are rebuilt."""
+        ckpt.load_model_state_dict(self.params, self.eng.table, state["model_state_dict"], strict=False)
+        self.t, hp = ckpt.load_adam_state_dict(self.eng.table, state["optimizer_state_dict"], self.m, self.v)
+        self.lr, self.betas, self.eps, self.wd = hp["lr"], tuple(hp["betas"]), hp["eps"], hp["weight_decay"]
+        if self.info.enabled:
+            for t in (self.params, self.m, self.v):
+                torch.distributed.broadcast(t, 0)
+        for e in self.engines:
+            e.pack(self.params)

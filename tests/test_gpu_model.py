@@ -245,3 +245,33 @@ def test_micro_batch_step_matches_single_engine():
     assert abs(i1 - i2) <= 1e-6 * abs(i1)
     assert rel_l2(g2, g1) < 1e-5
     assert rel_l2(p2 - flat, p1 - flat) < 1e-4
+
+
+def test_checkpoint_resume_matches_uninterrupted():
+    """FusedTrainer.checkpoint() -> torch.save / torch.load(weights_only) ->
+    load_checkpoint() resumes bit-exactly (reference checkpoint layout, §8f row 4)."""
+    import io
+    d = dev()
+    spec = spec_of("rcan", 2, 2, 3)
+    table = _table(spec)
+    from srmi.trainer import default_init_
+    flat = torch.empty(sum(t[2] for t in table), device=d)
+    default_init_(flat, table, seed=9)
+    hr = torch.tensor(ro.synthetic_hr(8, 2, 192, 21)).to(d)
+    a = FusedTrainer(spec, 8, (48, 48), device=d, params=flat, micro=1, lr=2e-4)
+    for _ in range(3):
+        a.step(hr)
+    b = FusedTrainer(spec, 8, (48, 48), device=d, params=flat, micro=1, lr=2e-4)
+    for _ in range(2):
+        b.step(hr)
+    buf = io.BytesIO()
+    torch.save(b.checkpoint(epoch=1, itime=2, loss=0.5), buf)
+    buf.seek(0)
+    state = torch.load(buf, weights_only=True)
+    c = FusedTrainer(spec, 8, (48, 48), device=d, params=torch.zeros_like(flat), micro=1, lr=1.0)
+    c.load_checkpoint(state)
+    assert c.t == 2 and c.lr == 2e-4
+    c.step(hr)
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, c.params)
+    assert torch.equal(a.m, c.m) and torch.equal(a.v, c.v)
