@@ -17,8 +17,13 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(bf16_t, b);
 }
+// two floats -> one dword of 2 bf16 (a low): ONE v_cvt_pk_bf16_f32 (the scalar
+// form above made the compiler emit 2 converts + 4 shifts/ors per dword)
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  const f32x2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
 }
 
 // 16-byte chunk swizzle for an LDS image of 128-byte rows (64 bf16 channels per

@@ -372,7 +372,8 @@ __device__ __forceinline__ float relu_mask(uint32_t bits16, float v) {
 template <int NPT, int EPI>
 __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)[NPT][4], const EpiPre<NPT, EPI>& e,
                                                const float4 (&bias)[4], int n, int cb, int y, int x0, int strip,
-                                               int nstrips, float* red, int fr, int fk, int wave, int tid) {
+                                               int nstrips, float* red, int fr, int fk, int wave, int tid,
+                                               char* stage) {
   const size_t HW = (size_t)p.H * p.W;
   constexpr bool kPart1 = (EPI == EPI_POOL_BF16);
   constexpr bool kPart2 = (EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_CA);
@@ -448,14 +449,31 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       if constexpr (kPart1) {
         ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
       }
-      const uint2 packed = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-      if constexpr (EPI == EPI_PS_BF16) {
-        const int oy = 2 * y + (cb >> 1), ox = 2 * xx + (cb & 1);
-        const size_t oo = ((size_t)n * (2 * p.H) + oy) * (size_t)(2 * p.W) + ox;
-        *reinterpret_cast<uint2*>(p.yb + oo * 64 + col) = packed;
-      } else {
-        if (p.yb) *reinterpret_cast<uint2*>(p.yb + o) = packed;
+      // bf16 output staged in LDS (this wave's row, 128 B per pixel, chunk-swizzled)
+      if (p.yb) {
+        const int px = pt * 16 + fr, c16 = ct * 2 + (fk >> 1);
+        *reinterpret_cast<uint2*>(stage + px * 128 + ((c16 ^ (px & 7)) << 4) + (fk & 1) * 8) =
+            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
       }
+    }
+  }
+  // ... and written back as full 128-byte lines: one 1 KiB contiguous run per
+  // instruction (the per-lane 8-byte stores of the MFMA layout touched 32-byte
+  // pieces of 16 lines each and stalled the store path for ~2 K cycles per strip).
+  // The wave's own LDS writes precede its reads (in-order LDS per wave).
+  if (p.yb) {
+    const int lane = tid & 63;
+#pragma unroll
+    for (int i = 0; i < NPT * 2; ++i) {
+      const int lin = i * 1024 + lane * 16, px = lin >> 7, c = (lin >> 4) & 7;
+      const uint4 val = *reinterpret_cast<const uint4*>(stage + px * 128 + ((c ^ (px & 7)) << 4));
+      size_t line;
+      if constexpr (EPI == EPI_PS_BF16) {
+        line = (((size_t)n * (2 * p.H) + 2 * y + (cb >> 1)) * (size_t)(2 * p.W) + 2 * (x0 + px) + (cb & 1)) * 64;
+      } else {
+        line = ((size_t)n * HW + (size_t)y * p.W + x0 + px) * p.Cout + cb * 64;
+      }
+      *reinterpret_cast<uint4*>(p.yb + line + c * 8) = val;
     }
   }
   if constexpr (kPart1 || kPart2) {
@@ -670,7 +688,14 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
     wait_vm<0>();
     STAMP(sj + 1);
     STAMP(sj + 2);
-    conv_epilogue2<NPT, EPI>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx, nsy * nsx, red, fr, fk, wave, tid);
+    // every wave is past its last read of input group k: its ring slot stages the
+    // strip's bf16 output rows (slot k%3 is next written by group k+3's DMA,
+    // issued after the barrier that ends this strip)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    conv_epilogue2<NPT, EPI>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx, nsy * nsx, red, fr, fk, wave, tid,
+                             ring + (k % 3) * S::GROUPB + wave * TW * 128);
     STAMP(sj + 3);
     // LDS-only barrier: this strip's global stores stay in flight into the next strip
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
