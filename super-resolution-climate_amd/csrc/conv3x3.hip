@@ -368,6 +368,11 @@ __device__ __forceinline__ float relu_mask(uint32_t bits16, float v) {
   return (bits16 & 0x7FFFu) && !(bits16 & 0x8000u) ? v : 0.f;
 }
 
+// Orders one wave's LDS accesses across lanes: the hardware executes a wave's DS
+// instructions in order, but the compiler reasons per lane and would move a
+// lane's read of another lane's staged data above that lane's write.
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
 // Fused epilogue of the v2 kernel (same semantics as conv_epilogue).
 template <int NPT, int EPI>
 __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)[NPT][4], const EpiPre<NPT, EPI>& e,
@@ -378,6 +383,11 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
   constexpr bool kPart1 = (EPI == EPI_POOL_BF16);
   constexpr bool kPart2 = (EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_CA);
   float ps0[4][4], ps1[4][4];
+  // fp32 output staged through LDS (DG_ACC, whose epilogue also reads r2/r3 from
+  // global memory, measured faster with direct stores)
+  constexpr bool kF = (EPI == EPI_RESID || EPI == EPI_DG_ACC_CA);
+  float4 fv[NPT][4];  // fp32 outputs, written back through LDS after the loop
+  uint2 bv[NPT][4];   // bf16 outputs, likewise
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
@@ -404,7 +414,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
         const float4 rr = e.r1[pt][ct];
         v[0] = p.alpha * v[0] + rr.x; v[1] = p.alpha * v[1] + rr.y;
         v[2] = p.alpha * v[2] + rr.z; v[3] = p.alpha * v[3] + rr.w;
-        if (p.yf) *reinterpret_cast<float4*>(p.yf + o) = make_float4(v[0], v[1], v[2], v[3]);
+        fv[pt][ct] = make_float4(v[0], v[1], v[2], v[3]);
       }
       if constexpr (EPI == EPI_DG_RELUMASK) {
         const uint2 tt = e.aux[pt][ct];
@@ -437,7 +447,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       if constexpr (EPI == EPI_DG_ACC_CA) {
         const float4 rr = e.r1[pt][ct];
         v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
-        *reinterpret_cast<float4*>(p.yf + o) = make_float4(v[0], v[1], v[2], v[3]);
+        fv[pt][ct] = make_float4(v[0], v[1], v[2], v[3]);
         const uint2 uu = e.aux[pt][ct];
         ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
         ps1[ct][0] += v[0] * bf2f(uu.x & 0xFFFFu);
@@ -449,20 +459,57 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       if constexpr (kPart1) {
         ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
       }
-      // bf16 output staged in LDS (this wave's row, 128 B per pixel, chunk-swizzled)
-      if (p.yb) {
-        const int px = pt * 16 + fr, c16 = ct * 2 + (fk >> 1);
-        *reinterpret_cast<uint2*>(stage + px * 128 + ((c16 ^ (px & 7)) << 4) + (fk & 1) * 8) =
-            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      bv[pt][ct] = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    }
+  }
+  const int lane = tid & 63;
+  // fp32 output: staged in LDS in two halves of the wave's row (256 B per pixel,
+  // chunk-swizzled) and written back as 1 KiB contiguous runs (full lines)
+  if constexpr (kF) {
+    if (p.yf) {
+      constexpr int HALF = NPT * 8;  // pixels per half
+      const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int pt = 0; pt < NPT; ++pt)
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) {
+            const int px = pt * 16 + fr;
+            if ((px >= HALF) == (h == 1)) {
+              const int lpx = px - h * HALF, c16 = ct * 4 + fk;
+              *reinterpret_cast<float4*>(stage + lpx * 256 + ((c16 ^ (lpx & 15)) << 4)) = fv[pt][ct];
+            }
+          }
+        lds_order();
+#pragma unroll
+        for (int i = 0; i < HALF / 4; ++i) {
+          const int lin = i * 1024 + lane * 16, lpx = lin >> 8, c = (lin >> 4) & 15;
+          const float4 val = *reinterpret_cast<const float4*>(stage + lpx * 256 + ((c ^ (lpx & 15)) << 4));
+          *reinterpret_cast<float4*>(p.yf + (pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) = val;
+        }
+        lds_order();
       }
     }
   }
+  // bf16 output staged in LDS (this wave's row, 128 B per pixel, chunk-swizzled)
+  if constexpr (EPI != EPI_DG_ACC_CA) {
+    if (p.yb) {
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          const int px = pt * 16 + fr, c16 = ct * 2 + (fk >> 1);
+          *reinterpret_cast<uint2*>(stage + px * 128 + ((c16 ^ (px & 7)) << 4) + (fk & 1) * 8) = bv[pt][ct];
+        }
+    }
+  }
+  lds_order();
   // ... and written back as full 128-byte lines: one 1 KiB contiguous run per
   // instruction (the per-lane 8-byte stores of the MFMA layout touched 32-byte
   // pieces of 16 lines each and stalled the store path for ~2 K cycles per strip).
   // The wave's own LDS writes precede its reads (in-order LDS per wave).
-  if (p.yb) {
-    const int lane = tid & 63;
+  if (EPI != EPI_DG_ACC_CA && p.yb) {
 #pragma unroll
     for (int i = 0; i < NPT * 2; ++i) {
       const int lin = i * 1024 + lane * 16, px = lin >> 7, c = (lin >> 4) & 7;
