@@ -26,6 +26,30 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
 }
 
+// Write-through (sc1) 16-byte stores.  A kernel's end-of-launch release writes
+// back every dirty L2 line before the next dependent kernel starts (MI355X
+// kernel boundary: ~1.8 us + dirty bytes / 6 TB/s); stores that write through
+// reach memory while the kernel still computes, so the boundary finds nothing
+// to flush.  Used for the large outputs (activations, gradient streams, slabs).
+#ifndef SRMI_WT
+#define SRMI_WT 1
+#endif
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ void st_wt16(__amdgpu_buffer_rsrc_t r, void* base, uint32_t byte_off, const T& v) {
+  static_assert(sizeof(T) == 16, "16-byte store");
+#if SRMI_WT
+  (void)base;
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, byte_off, 0, 16);
+#else
+  (void)r;
+  *reinterpret_cast<T*>(static_cast<char*>(base) + byte_off) = v;
+#endif
+}
+
 // 16-byte chunk swizzle for an LDS image of 128-byte rows (64 bf16 channels per
 // pixel/row).  Chunk c of row q lives at slot c ^ ((q >> 1) & 7): 16 consecutive
 // rows read at one logical chunk by ds_read_b128 land on 16 distinct 16-B slots

@@ -380,6 +380,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
                                                int nstrips, float* red, int fr, int fk, int wave, int tid,
                                                char* stage) {
   const size_t HW = (size_t)p.H * p.W;
+  [[maybe_unused]] const auto rfa = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
   constexpr bool kPart1 = (EPI == EPI_POOL_BF16);
   constexpr bool kPart2 = (EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_CA);
   float ps0[4][4], ps1[4][4];
@@ -434,7 +435,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
           const float4 q = *reinterpret_cast<const float4*>(p.r3 + o);
           v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
         }
-        *reinterpret_cast<float4*>(p.yf + o) = make_float4(v[0], v[1], v[2], v[3]);
+        st_wt16(rfa, p.yf, (uint32_t)(o * 4), make_float4(v[0], v[1], v[2], v[3]));
         if (p.part) {
           const uint2 uu = e.aux[pt][ct];
           ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
@@ -468,6 +469,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
   if constexpr (kF) {
     if (p.yf) {
       constexpr int HALF = NPT * 8;  // pixels per half
+      const auto rf = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
       const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -486,7 +488,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
         for (int i = 0; i < HALF / 4; ++i) {
           const int lin = i * 1024 + lane * 16, lpx = lin >> 8, c = (lin >> 4) & 15;
           const float4 val = *reinterpret_cast<const float4*>(stage + lpx * 256 + ((c ^ (lpx & 15)) << 4));
-          *reinterpret_cast<float4*>(p.yf + (pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) = val;
+          st_wt16(rf, p.yf, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 4), val);
         }
         lds_order();
       }
@@ -510,6 +512,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
   // pieces of 16 lines each and stalled the store path for ~2 K cycles per strip).
   // The wave's own LDS writes precede its reads (in-order LDS per wave).
   if (EPI != EPI_DG_ACC_CA && p.yb) {
+    const auto rb = wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
 #pragma unroll
     for (int i = 0; i < NPT * 2; ++i) {
       const int lin = i * 1024 + lane * 16, px = lin >> 7, c = (lin >> 4) & 7;
@@ -520,7 +523,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       } else {
         line = ((size_t)n * HW + (size_t)y * p.W + x0 + px) * p.Cout + cb * 64;
       }
-      *reinterpret_cast<uint4*>(p.yb + line + c * 8) = val;
+      st_wt16(rb, p.yb, (uint32_t)((line + c * 8) * 2), val);
     }
   }
   if constexpr (kPart1 || kPart2) {

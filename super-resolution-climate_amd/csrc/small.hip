@@ -642,7 +642,8 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const bf16_t* __restrict__ 
     }
     if (tid < CR) r[C + tid] = z1[tid];
   }
-  // 4. elementwise
+  // 4. elementwise (plain stores: h_out's 16-byte halves of 32-byte lane runs
+  // measured 8 us slower written through; the L2 merges them into full lines)
 #pragma unroll
   for (int k = 0; k < kCaVec; ++k) {
     const size_t v = v0 + (size_t)k * blockDim.x;
@@ -760,6 +761,7 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
     }
     if (tid < CR) br[C + tid] = dz1[tid];
   }
+  const auto rdu = wt_rsrc(du, (uint32_t)((size_t)gridDim.y * HW * C * 2));  // lane-contiguous 16 B: write-through
 #pragma unroll
   for (int k = 0; k < kCaVec; ++k) {
     const size_t v = v0 + (size_t)k * blockDim.x;
@@ -773,7 +775,7 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
     ob.y = pack2(g0[k].z * s[c0 + 2] + dmh[2], g0[k].w * s[c0 + 3] + dmh[3]);
     ob.z = pack2(g1[k].x * s[c0 + 4] + dmh[4], g1[k].y * s[c0 + 5] + dmh[5]);
     ob.w = pack2(g1[k].z * s[c0 + 6] + dmh[6], g1[k].w * s[c0 + 7] + dmh[7]);
-    *reinterpret_cast<uint4*>(du + base + v * 8) = ob;
+    st_wt16(rdu, du, (uint32_t)((base + v * 8) * 2), ob);
   }
 }
 
