@@ -50,6 +50,19 @@ __device__ __forceinline__ void st_wt16(__amdgpu_buffer_rsrc_t r, void* base, ui
 #endif
 }
 
+template <typename T>
+__device__ __forceinline__ void st_wt8(__amdgpu_buffer_rsrc_t r, void* base, uint32_t byte_off, const T& v) {
+  static_assert(sizeof(T) == 8, "8-byte store");
+#if SRMI_WT
+  (void)base;
+  typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, byte_off, 0, 16);
+#else
+  (void)r;
+  *reinterpret_cast<T*>(static_cast<char*>(base) + byte_off) = v;
+#endif
+}
+
 // 16-byte chunk swizzle for an LDS image of 128-byte rows (64 bf16 channels per
 // pixel/row).  Chunk c of row q lives at slot c ^ ((q >> 1) & 7): 16 consecutive
 // rows read at one logical chunk by ds_read_b128 land on 16 distinct 16-B slots

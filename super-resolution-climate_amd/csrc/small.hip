@@ -595,18 +595,20 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const bf16_t* __restrict__ 
   const float bj = b1[jc];
   const float bc = b2[c4];
   __builtin_amdgcn_sched_barrier(0);
-  // 2. this thread's stream loads (independent of s), in flight during the MLP
+  // 2. this thread's stream loads (independent of s), in flight during the MLP.
+  //    Units of 4 channels, consecutive lanes on consecutive units: every load and
+  //    store instruction covers one contiguous run (1 KiB fp32 / 512 B bf16).
+  constexpr int NU = 2 * kCaVec;
   const size_t base = (size_t)n * HW * C;
-  const size_t nv = (size_t)HW * C / 8;
-  const size_t v0 = ((size_t)blockIdx.x * kCaVec) * blockDim.x + tid;
-  uint4 uu[kCaVec];
-  float4 h0[kCaVec], h1[kCaVec];
+  const size_t nq = (size_t)HW * C / 4;
+  const size_t q0 = ((size_t)blockIdx.x * NU) * blockDim.x + tid;
+  uint2 uu[NU];
+  float4 hh[NU];
 #pragma unroll
-  for (int k = 0; k < kCaVec; ++k) {  // clamped, unconditional (tail lanes store nothing)
-    const size_t e = base + min(v0 + (size_t)k * blockDim.x, nv - 1) * 8;
-    uu[k] = *reinterpret_cast<const uint4*>(u + e);
-    h0[k] = *reinterpret_cast<const float4*>(h_in + e);
-    h1[k] = *reinterpret_cast<const float4*>(h_in + e + 4);
+  for (int k = 0; k < NU; ++k) {  // clamped, unconditional (tail lanes store nothing)
+    const size_t e = base + min(q0 + (size_t)k * blockDim.x, nq - 1) * 4;
+    uu[k] = *reinterpret_cast<const uint2*>(u + e);
+    hh[k] = *reinterpret_cast<const float4*>(h_in + e);
   }
   __builtin_amdgcn_sched_barrier(0);
   // 3. the MLP (LDS-only barriers: the stream loads stay in flight)
@@ -642,28 +644,23 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const bf16_t* __restrict__ 
     }
     if (tid < CR) r[C + tid] = z1[tid];
   }
-  // 4. elementwise (plain stores: h_out's 16-byte halves of 32-byte lane runs
-  // measured 8 us slower written through; the L2 merges them into full lines)
+  // 4. elementwise; lane-contiguous runs written through (common.hpp): the
+  //    boundary after this launch then has no dirty residual stream to flush
+  const auto rh = wt_rsrc(h_out, (uint32_t)((size_t)gridDim.y * HW * C * 4));
+  const auto rhb = wt_rsrc(hb_out, (uint32_t)((size_t)gridDim.y * HW * C * 2));
 #pragma unroll
-  for (int k = 0; k < kCaVec; ++k) {
-    const size_t v = v0 + (size_t)k * blockDim.x;
-    if (v >= nv) continue;
-    const size_t e = base + v * 8;
-    const int c0 = (int)((v * 8) % C);
-    float o[8];
-    o[0] = bf2f(uu[k].x & 0xFFFF) * s[c0 + 0] + h0[k].x;
-    o[1] = bf2f(uu[k].x >> 16) * s[c0 + 1] + h0[k].y;
-    o[2] = bf2f(uu[k].y & 0xFFFF) * s[c0 + 2] + h0[k].z;
-    o[3] = bf2f(uu[k].y >> 16) * s[c0 + 3] + h0[k].w;
-    o[4] = bf2f(uu[k].z & 0xFFFF) * s[c0 + 4] + h1[k].x;
-    o[5] = bf2f(uu[k].z >> 16) * s[c0 + 5] + h1[k].y;
-    o[6] = bf2f(uu[k].w & 0xFFFF) * s[c0 + 6] + h1[k].z;
-    o[7] = bf2f(uu[k].w >> 16) * s[c0 + 7] + h1[k].w;
-    *reinterpret_cast<float4*>(h_out + e) = make_float4(o[0], o[1], o[2], o[3]);
-    *reinterpret_cast<float4*>(h_out + e + 4) = make_float4(o[4], o[5], o[6], o[7]);
-    uint4 ob;
-    ob.x = pack2(o[0], o[1]); ob.y = pack2(o[2], o[3]); ob.z = pack2(o[4], o[5]); ob.w = pack2(o[6], o[7]);
-    *reinterpret_cast<uint4*>(hb_out + e) = ob;
+  for (int k = 0; k < NU; ++k) {
+    const size_t q = q0 + (size_t)k * blockDim.x;
+    if (q >= nq) continue;
+    const size_t e = base + q * 4;
+    const int c0 = (int)((q * 4) % C);
+    float o[4];
+    o[0] = bf2f(uu[k].x & 0xFFFF) * s[c0 + 0] + hh[k].x;
+    o[1] = bf2f(uu[k].x >> 16) * s[c0 + 1] + hh[k].y;
+    o[2] = bf2f(uu[k].y & 0xFFFF) * s[c0 + 2] + hh[k].z;
+    o[3] = bf2f(uu[k].y >> 16) * s[c0 + 3] + hh[k].w;
+    st_wt16(rh, h_out, (uint32_t)(e * 4), make_float4(o[0], o[1], o[2], o[3]));
+    st_wt8(rhb, hb_out, (uint32_t)(e * 2), make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3])));
   }
 }
 
