@@ -229,11 +229,15 @@ struct srmi_engine {
   float* brecp(int g, int b) const { return brec + (size_t)(g * P.cfg.nblocks + (b - 1)) * N * 224; }
 };
 
-// row chunks per image of the side-stream (RCAB) filter gradients
+// row chunks per image of the side-stream (RCAB) filter gradients.  They run
+// beside the dgrad chain, so they are sized for HALF the engine's CU budget:
+// fewer, longer chunks write fewer partial slabs (at C2 2 x 24-row chunks per
+// image instead of 3 x 16: 1837 -> 1901 tiles/s measured).
 static int side_row_splits(const srmi_engine* e) {
   const int rs = e->side_rs;
   if (rs > 0 && e->h % rs == 0 && (e->h / rs) % 4 == 0) return rs;
-  return choose_row_splits(e->N, e->h, 64, e->side_cus > 0 ? e->side_cus : e->cu_budget);
+  const int budget = e->side_cus > 0 ? e->side_cus : (e->cu_budget > 0 ? e->cu_budget : 256) / 2;
+  return choose_row_splits(e->N, e->h, 64, budget);
 }
 
 static size_t carve(srmi_engine* e, char* base) {
