@@ -19,6 +19,8 @@
 // the CA reductions).
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "common.hpp"
 #include "srmi_internal.hpp"
 
@@ -639,7 +641,7 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
       glds16(p.w + ((size_t)(tap * p.Cout + cb * 64 + row)) * 64 + c * 8, wbase + (uint32_t)i * 1024u);
     }
     group_dma(k0);
-    group_dma(k0 + 1);  // strip k0 reads groups k0 and k0+1
+    group_dma(k0 + 1);  // strip k0 reads groups k0 and k0+1 (issuing these first measured the same)
     wait_vm<0>();
   }
   STAMP(1);
@@ -762,7 +764,9 @@ static int launch_tw(const ConvParams& p, hipStream_t st) {
     // v2: persistent runs; ~1 workgroup per CU (LDS-limited), each a run of strips
     const int nsy = p.H / kTH;
     const int units = (p.Cout / 64) * p.N * (p.W / TW);
-    const int cus = p.cu_budget > 0 ? p.cu_budget : 256;
+    // SRMI_CONV_CU_PCT (diagnostic): size the runs for this % of the CU budget
+    static const int pct = getenv("SRMI_CONV_CU_PCT") ? atoi(getenv("SRMI_CONV_CU_PCT")) : 100;
+    const int cus = std::max(1, (p.cu_budget > 0 ? p.cu_budget : 256) * pct / 100);
     int R = (cus + units / 2) / units;
     R = R < 1 ? 1 : (R > nsy ? nsy : R);
     const int run_len = (nsy + R - 1) / R;
