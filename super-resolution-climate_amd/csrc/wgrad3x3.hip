@@ -462,15 +462,22 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
 
   // partial slab in the MFMA-native order (slab layout 1): every store instruction
   // writes 1 KiB contiguous; wgrad_reduce_kernel maps it back to (co, ci, tap)
-  // (plain stores: written through, the wgrad launch was 0.9 us shorter but the
-  // reduce that re-reads the slabs right after it 1.9 us longer)
-  float* slab = p.slab + (size_t)chunk * Cout * 576 + (size_t)cb * (64 * 576) + (size_t)wave * (9 * 4 * 256);
+#ifndef SRMI_WGRAD_SLAB_WT
+#define SRMI_WGRAD_SLAB_WT 0
+#endif
+  // (plain stores by default: written through, the wgrad launch was 0.9 us shorter
+  // but the reduce that re-reads the slabs right after it 1.9 us longer)
+  const size_t soff = (size_t)chunk * Cout * 576 + (size_t)cb * (64 * 576) + (size_t)wave * (9 * 4 * 256);
+  [[maybe_unused]] const auto rs = wt_rsrc(p.slab, (uint32_t)((size_t)gridDim.x * Cout * 576 * 4));
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
-      *reinterpret_cast<float4*>(slab + ((t * 4 + ct) * 64 + lane) * 4) =
-          make_float4(acc[ct][t][0], acc[ct][t][1], acc[ct][t][2], acc[ct][t][3]);
+    for (int ct = 0; ct < 4; ++ct) {
+      const float4 v = make_float4(acc[ct][t][0], acc[ct][t][1], acc[ct][t][2], acc[ct][t][3]);
+      const size_t o = soff + ((t * 4 + ct) * 64 + lane) * 4;
+      if (SRMI_WGRAD_SLAB_WT) st_wt16(rs, p.slab, (uint32_t)(o * 4), v);
+      else *reinterpret_cast<float4*>(p.slab + o) = v;
+    }
   if ((lane & 15) == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
