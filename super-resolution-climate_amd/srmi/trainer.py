@@ -15,6 +15,7 @@ gradients are all-reduced as described in srmi/dist.py.
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional
 
 import torch
@@ -72,6 +73,8 @@ class FusedTrainer:
         self.micro = micro
         self.mb = batch // micro
         budget = 256 // micro if micro > 1 else 0
+        if micro > 1 and os.environ.get("SRMI_MICRO_BUDGET"):  # diagnostic: CUs each engine's launches aim at
+            budget = int(os.environ["SRMI_MICRO_BUDGET"])
         self.engines = [Engine(spec, self.mb, lr_hw, train=True, device=self.device, cu_budget=budget)
                         for _ in range(micro)]
         self.eng = self.engines[0]
