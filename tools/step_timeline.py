@@ -25,7 +25,16 @@ def main(path, nsteps=2):
     if len(adam) < 2:
         print("fewer than 2 adam launches")
         return
-    for k in range(max(1, len(adam) - nsteps), len(adam)):
+    # training steps of the headline config only (RCAN: the step holds ca_fwd
+    # launches; later benches in the same trace -- EDSR -- do not)
+    # training steps of the headline RCAN config only: other phases of a bench
+    # trace (roofline leg, tiled inference, the EDSR line) end in an Adam too
+    def is_train(seg):
+        names = [e[2] for e in seg]
+        return (any("ca_bwd_du_kernel" in n for n in names) and not any("region_to_tiles" in n for n in names)
+                and not any("<32," in n for n in names))
+    ks = [k for k in range(1, len(adam)) if is_train(ev[adam[k - 1] + 1:adam[k] + 1])]
+    for k in ks[-nsteps:]:
         seg = ev[adam[k - 1] + 1:adam[k] + 1]
         ds = [i for i, e in enumerate(seg) if "downsample_kernel" in e[2]]
         if ds:
