@@ -33,7 +33,8 @@ from .engine import Engine, NetSpec, downsample, upsample
 
 class TiledInference:
     def __init__(self, spec: NetSpec, params: torch.Tensor, region_chw: Tuple[int, int, int],
-                 tile_hr: Tuple[int, int] = (192, 192), device: Optional[torch.device] = None, graph: bool = True):
+                 tile_hr: Tuple[int, int] = (192, 192), device: Optional[torch.device] = None, graph: bool = True,
+                 micro: Optional[int] = None):
         self.spec = spec
         self.device = device or params.device
         C, H, W = region_chw
@@ -69,8 +70,24 @@ class TiledInference:
             "interpolated": torch.empty(hr_shape, **f32),
             "model": torch.empty(hr_shape, **f32),
         }
-        self.eng = Engine(spec, n, (ty // s, tx // s), train=False, device=d)
-        self.eng.pack(params)
+        # the tile batch is split over `micro` engines on their own streams, each
+        # sized for 1/micro of the chip (as srmi.trainer.FusedTrainer does): each
+        # engine's launch ramps and tails overlap the other's work
+        if micro is None:
+            micro = 2 if n >= 32 else 1
+        self.micro = max(1, min(int(micro), n))
+        per = (n + self.micro - 1) // self.micro
+        self.split = [min(per, n - k * per) for k in range(self.micro)]
+        budget = 256 // self.micro if self.micro > 1 else 0
+        self.engs = [Engine(spec, m, (ty // s, tx // s), train=False, device=d, cu_budget=budget)
+                     for m in self.split]
+        self.eng = self.engs[0]
+        for e in self.engs:
+            e.pack(params)
+        self.streams = [None] + [torch.cuda.Stream(device=d) for _ in range(self.micro - 1)]
+        # fork / join events, created once (also valid inside a graph capture)
+        self.ev_fork = torch.cuda.Event()
+        self.ev_join = [torch.cuda.Event() for _ in range(self.micro - 1)]
         self._graph = None
         self._use_graph = graph and self.device.type == "cuda"
 
@@ -83,7 +100,23 @@ class TiledInference:
     def _model_and_mosaic(self, tiles, lr, sr, interp, mean, std, inv, nt):
         st = stream_handle()
         downsample(tiles, self.s, out=lr)
-        self.eng.forward(self.params, lr, out=sr)
+        main = torch.cuda.current_stream(self.device)
+        self.ev_fork.record(main)
+        for sk in self.streams[1:]:
+            sk.wait_event(self.ev_fork)
+        a = 0
+        for k, e in enumerate(self.engs):
+            b = min(nt, a + self.split[k])
+            if b > a:
+                if self.streams[k] is None:
+                    e.forward(self.params, lr[a:b], out=sr[a:b])
+                else:
+                    with torch.cuda.stream(self.streams[k]):
+                        e.forward(self.params, lr[a:b], out=sr[a:b])
+            a = b
+        for sk, ev in zip(self.streams[1:], self.ev_join):
+            ev.record(sk)
+            main.wait_event(ev)
         upsample(lr, self.s, out=interp)
         count = float(tiles.numel())
         for pred, l4 in ((sr, self.loss_m), (interp, self.loss_i)):
