@@ -23,6 +23,8 @@ the channel axis, SURVEY.md §8f row 3 -- identical for the 1-variable C5 case).
 """
 from __future__ import annotations
 
+import os
+
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -74,7 +76,7 @@ class TiledInference:
         # sized for 1/micro of the chip (as srmi.trainer.FusedTrainer does): each
         # engine's launch ramps and tails overlap the other's work
         if micro is None:
-            micro = 2 if n >= 32 else 1
+            micro = int(os.environ.get("SRMI_INFER_MICRO", "0")) or (2 if n >= 32 else 1)
         self.micro = max(1, min(int(micro), n))
         per = (n + self.micro - 1) // self.micro
         self.split = [min(per, n - k * per) for k in range(self.micro)]
