@@ -10,6 +10,7 @@
 //  * Adam (torch.optim.Adam defaults, dual_trainer.py:126,323)
 //  * fp32 -> bf16 filter packing for the MFMA conv kernels
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.hpp"
 #include "srmi_internal.hpp"
@@ -205,10 +206,76 @@ __global__ void __launch_bounds__(4 * TWT) tail_fwd_kernel(const bf16_t* __restr
     if (co < C) y[(((size_t)n * C + co) * H + y0 + r) * W + x0 + px] = acc[co] + b[co];
 }
 
+// MFMA form of the same conv: implicit GEMM with A = filters (16 output-channel
+// rows, only the C < 16 real ones ever written or stored), B = halo pixels,
+// K = 9 taps x 64 ci, v_mfma_f32_16x16x32_bf16.  Workgroup = 4 output rows x TW
+// pixels (wave w = row w), halo and bf16 filters staged in LDS with the conv
+// kernels' chunk swizzle.  The VALU form above spent ~1 K FMAs per pixel with
+// per-FMA weight loads; this one is bound by reading the 64-channel input once.
+template <int TW>
+__global__ void __launch_bounds__(256) tail_fwd_mfma_kernel(const bf16_t* __restrict__ x, const float* __restrict__ w,
+                                                            const float* __restrict__ b, int C, int H, int W,
+                                                            float* __restrict__ y) {
+  constexpr int NPT = TW / 16, WP = TW + 2, HALO = 6 * WP;
+  extern __shared__ __attribute__((aligned(16))) char tsm[];
+  char* halo = tsm;               // [6][WP] px x 128 B
+  char* wl = tsm + HALO * 128;    // [9 taps][16 co rows] x 128 B
+  const int n = blockIdx.z, y0 = blockIdx.y * 4, x0 = blockIdx.x * TW, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, fr = lane & 15, fk = lane >> 4;
+  for (int i = tid; i < HALO * 8; i += 256) {
+    const int q = i >> 3, c = i & 7;
+    const int hy = q / WP, hx = q - hy * WP;
+    const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+      v = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + c * 8);
+    *reinterpret_cast<uint4*>(halo + swz128(q, c)) = v;
+  }
+  // filters w[co][ci][tap] (fp32, torch layout) -> bf16 rows co < C of [tap][co][ci];
+  // rows >= C stay unwritten: they only feed output rows that are never stored
+  for (int i = tid; i < C * 576; i += 256) {
+    const int co = i / 576, ci = (i / 9) % 64, tap = i % 9;
+    *reinterpret_cast<bf16_t*>(wl + tap * 2048 + swz128(co, ci >> 3) + (ci & 7) * 2) = f2bf(w[i]);
+  }
+  __syncthreads();
+  f32x4 acc[NPT];
+#pragma unroll
+  for (int pt = 0; pt < NPT; ++pt) acc[pt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int ky = tap / 3, kx = tap % 3;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 a = lds_frag(wl, tap * 2048 + swz128(fr, kk * 4 + fk));
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt)
+        acc[pt] = mfma16(a, lds_frag(halo, swz128((wave + ky) * WP + pt * 16 + fr + kx, kk * 4 + fk)), acc[pt]);
+    }
+  }
+  // lane (fr, fk) holds output channels 4 fk + i of pixel pt * 16 + fr
+  if (fk == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < C) {
+        const float bb = b[i];
+#pragma unroll
+        for (int pt = 0; pt < NPT; ++pt)
+          y[(((size_t)n * C + i) * H + y0 + wave) * W + x0 + pt * 16 + fr] = acc[pt][i] + bb;
+      }
+  }
+}
+
 int tail_fwd_launch(const bf16_t* x, const float* w, const float* b, int N, int C, int H, int W, float* y,
                     hipStream_t st) {
   if (C < 1 || C > 4 || H % 4) return SRMI_ERR_SHAPE;
-  if (W % 64 == 0) {
+  static const bool valu = getenv("SRMI_TAIL_VALU") && atoi(getenv("SRMI_TAIL_VALU"));
+  if (!valu && W % 48 == 0) {
+    hipLaunchKernelGGL(tail_fwd_mfma_kernel<48>, dim3(W / 48, H / 4, N), dim3(256), 6 * 50 * 128 + 9 * 2048, st, x,
+                       w, b, C, H, W, y);
+  } else if (!valu && W % 32 == 0) {
+    hipLaunchKernelGGL(tail_fwd_mfma_kernel<32>, dim3(W / 32, H / 4, N), dim3(256), 6 * 34 * 128 + 9 * 2048, st, x,
+                       w, b, C, H, W, y);
+  } else if (W % 64 == 0) {
     hipLaunchKernelGGL(tail_fwd_kernel<64>, dim3(W / 64, H / 4, N), dim3(256), 6 * 66 * 128, st, x, w, b, C, H, W, y);
   } else if (W % 32 == 0) {
     hipLaunchKernelGGL(tail_fwd_kernel<32>, dim3(W / 32, H / 4, N), dim3(128), 6 * 34 * 128, st, x, w, b, C, H, W, y);

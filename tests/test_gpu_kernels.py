@@ -262,3 +262,19 @@ def test_adam_matches_reference():
         gk = torch.tensor(gd["adam_g"][k], dtype=torch.float32).to(d)
         call("srmi_adam_step", ptr(p), ptr(gk), ptr(m), ptr(v), p.numel(), k + 1, 1e-3, 0.9, 0.999, 1e-8, 0.0, S())
     np.testing.assert_allclose(p.double().cpu().numpy(), gd["adam_p3"], rtol=0, atol=2e-6)
+
+
+@pytest.mark.parametrize("C,H,W", [(1, 8, 192), (2, 12, 192), (4, 8, 256), (3, 4, 96)])
+def test_tail_forward(C, H, W):
+    """Tail conv 64 -> C (network.py:16 / EDSR tail) through srmi_tail_forward: MFMA
+    implicit GEMM with bf16 operands vs an fp64 conv of the same bf16 input."""
+    d = dev()
+    g = torch.Generator(device="cpu").manual_seed(12)
+    N = 2
+    x = bf(torch.randn(N, H, W, 64, generator=g)).to(d)
+    w = (torch.randn(C, 64, 3, 3, generator=g) * 0.05).to(d)
+    b = (torch.randn(C, generator=g) * 0.1).to(d)
+    y = torch.empty(N, C, H, W, device=d)
+    call("srmi_tail_forward", ptr(x), ptr(w), ptr(b), N, C, H, W, ptr(y), S())
+    ref = Fn.conv2d(nchw(x).double().cpu(), w.double().cpu(), b.double().cpu(), padding=1)
+    assert rel_l2(y, ref) < 4e-3
