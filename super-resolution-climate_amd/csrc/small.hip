@@ -124,17 +124,29 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(const float* __restrict
   float acc[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) acc[k] = 0.f;
-  for (int px = 0; px < 4 * W; ++px) {
-    const int r = px / W, x = px - r * W;
-    const float gv = g[(((size_t)n * H + y0 + r) * W + x) * 64 + co];
+  // 8 pixels per round, their gradient loads unconditional (clamped) so they issue
+  // back to back: the walk was latency-bound at ~1.5 workgroups per CU
+  for (int p0 = 0; p0 < 4 * W; p0 += 8) {
+    float gv8[8];
 #pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      const int j = grp + 4 * k;
-      if (j < nj - 1) {
-        const int c = j / 9, t = j % 9;
-        acc[k] += gv * hs[(c * 6 + r + t / 3) * Wp + x + t % 3];
-      } else if (j == nj - 1) {
-        acc[k] += gv;
+    for (int u = 0; u < 8; ++u) {
+      const int px = min(p0 + u, 4 * W - 1), r = px / W, x = px - r * W;
+      gv8[u] = g[(((size_t)n * H + y0 + r) * W + x) * 64 + co];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (p0 + u >= 4 * W) break;  // uniform
+      const int px = p0 + u, r = px / W, x = px - r * W;
+      const float gv = gv8[u];
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        const int j = grp + 4 * k;
+        if (j < nj - 1) {
+          const int c = j / 9, t = j % 9;
+          acc[k] += gv * hs[(c * 6 + r + t / 3) * Wp + x + t % 3];
+        } else if (j == nj - 1) {
+          acc[k] += gv;
+        }
       }
     }
   }
