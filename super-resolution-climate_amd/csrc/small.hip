@@ -445,15 +445,104 @@ __global__ void __launch_bounds__(256) tail_wgrad_kernel(const float* __restrict
   for (int i = tid; i < CC * 577; i += 256) out[i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
 }
 
+// LDS-staged form: per 64-pixel segment the workgroup stages the 6 input rows its
+// 4 waves need (66 px x 64 ch bf16) and the RMSE gradient of its 4 rows; lane = ci
+// reads the x window from LDS (128 B per wave read, conflict-free) and the pixel's
+// dy by LDS broadcast -- no readlane, no 2-byte global loads per pixel.
+template <int CC>
+__global__ void __launch_bounds__(256) tail_wgrad_lds_kernel(const float* __restrict__ yv,
+                                                            const float* __restrict__ hr,
+                                                            const float* __restrict__ loss,
+                                                            const bf16_t* __restrict__ x, int H, int W,
+                                                            float* __restrict__ slab) {
+  constexpr int SEG = 64, SP = SEG + 2;
+  __shared__ __attribute__((aligned(16))) bf16_t xs[6 * SP * 64];  // [row][px][ci]
+  __shared__ float dyl[CC][kTailRows][SEG];
+  __shared__ float red[4][CC * 577];
+  const int n = blockIdx.y, band = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int y0 = band * kTailRows;
+  const float sc = loss ? loss[2] : 1.f;
+  float acc[9][CC], bacc[CC];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int c = 0; c < CC; ++c) acc[t][c] = 0.f;
+#pragma unroll
+  for (int c = 0; c < CC; ++c) bacc[c] = 0.f;
+  for (int x0 = 0; x0 < W; x0 += SEG) {
+    const int nx = min(SEG, W - x0);
+    __syncthreads();  // previous segment's readers are done
+    for (int i = tid; i < 6 * SP * 8; i += 256) {
+      const int q = i >> 3, ch = i & 7, r = q / SP, px = q - r * SP;
+      const int yy = y0 - 1 + r, xx = x0 - 1 + px;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W && px <= nx + 1)
+        v = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + ch * 8);
+      *reinterpret_cast<uint4*>(xs + q * 64 + ch * 8) = v;
+    }
+    for (int i = tid; i < CC * kTailRows * SEG; i += 256) {
+      const int c = i / (kTailRows * SEG), r = (i / SEG) % kTailRows, px = i % SEG;
+      float v = 0.f;
+      if (px < nx) {
+        const size_t o = (((size_t)n * CC + c) * H + y0 + r) * W + x0 + px;
+        v = hr ? (yv[o] - hr[o]) * sc : yv[o] * sc;
+      }
+      dyl[c][r][px] = v;
+    }
+    __syncthreads();
+    float win[3][3];
+#pragma unroll
+    for (int rr = 0; rr < 3; ++rr) {
+      win[rr][0] = bf2f(xs[((wave + rr) * SP + 0) * 64 + lane]);
+      win[rr][1] = bf2f(xs[((wave + rr) * SP + 1) * 64 + lane]);
+    }
+    for (int j = 0; j < nx; ++j) {
+#pragma unroll
+      for (int rr = 0; rr < 3; ++rr) win[rr][2] = bf2f(xs[((wave + rr) * SP + j + 2) * 64 + lane]);
+#pragma unroll
+      for (int c = 0; c < CC; ++c) {
+        const float dd = dyl[c][wave][j];
+        bacc[c] += dd;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[t][c] += dd * win[t / 3][t % 3];
+      }
+#pragma unroll
+      for (int rr = 0; rr < 3; ++rr) {
+        win[rr][0] = win[rr][1];
+        win[rr][1] = win[rr][2];
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CC; ++c) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) red[wave][c * 577 + lane * 9 + t] = acc[t][c];
+    if (lane == 0) red[wave][c * 577 + 576] = bacc[c];  // every lane holds the same sum
+  }
+  __syncthreads();
+  float* out = slab + ((size_t)n * gridDim.x + band) * CC * 577;
+  for (int i = tid; i < CC * 577; i += 256) out[i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+}
+
 int tail_wgrad_launch(const float* y, const float* hr, const float* loss, const bf16_t* x, int N, int C, int H,
                       int W, float* slab, int* nslab, hipStream_t st) {
   if (C < 1 || C > 4 || H % kTailRows) return SRMI_ERR_SHAPE;
   const dim3 grid(H / kTailRows, N);
-  switch (C) {
-    case 1: hipLaunchKernelGGL(tail_wgrad_kernel<1>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
-    case 2: hipLaunchKernelGGL(tail_wgrad_kernel<2>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
-    case 3: hipLaunchKernelGGL(tail_wgrad_kernel<3>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
-    default: hipLaunchKernelGGL(tail_wgrad_kernel<4>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+  static const bool valu = getenv("SRMI_TAIL_VALU") && atoi(getenv("SRMI_TAIL_VALU"));
+  if (valu) {
+    switch (C) {
+      case 1: hipLaunchKernelGGL(tail_wgrad_kernel<1>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+      case 2: hipLaunchKernelGGL(tail_wgrad_kernel<2>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+      case 3: hipLaunchKernelGGL(tail_wgrad_kernel<3>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+      default: hipLaunchKernelGGL(tail_wgrad_kernel<4>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+    }
+  } else {
+    switch (C) {
+      case 1: hipLaunchKernelGGL(tail_wgrad_lds_kernel<1>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+      case 2: hipLaunchKernelGGL(tail_wgrad_lds_kernel<2>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+      case 3: hipLaunchKernelGGL(tail_wgrad_lds_kernel<3>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+      default: hipLaunchKernelGGL(tail_wgrad_lds_kernel<4>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+    }
   }
   SRMI_CHECK_LAUNCH();
   *nslab = N * (H / kTailRows);
