@@ -326,6 +326,7 @@ __global__ void __launch_bounds__(256) tail_dgrad_kernel(const float* __restrict
   }
   __syncthreads();
   const int ck = tid & 7;
+  const auto rdx = wt_rsrc(dx, (uint32_t)((size_t)gridDim.z * H * W * 64 * 2));
   for (int px = tid >> 3; px < 4 * TWT; px += 32) {
     const int r = px / TWT, xx = px - r * TWT;
     float acc[8];
@@ -345,7 +346,8 @@ __global__ void __launch_bounds__(256) tail_dgrad_kernel(const float* __restrict
     uint4 o;
     o.x = pack2(acc[0], acc[1]); o.y = pack2(acc[2], acc[3]);
     o.z = pack2(acc[4], acc[5]); o.w = pack2(acc[6], acc[7]);
-    *reinterpret_cast<uint4*>(dx + (((size_t)n * H + y0 + r) * W + x0 + xx) * 64 + ck * 8) = o;
+    // 8 lanes per pixel: 128-byte lines, written through (common.hpp)
+    st_wt16(rdx, dx, (uint32_t)(((((size_t)n * H + y0 + r) * W + x0 + xx) * 64 + ck * 8) * 2), o);
   }
 }
 
