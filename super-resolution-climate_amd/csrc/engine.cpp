@@ -297,7 +297,7 @@ static size_t carve(srmi_engine* e, char* base) {
     for (int k = 0; k < P.nups; ++k) upd(e->h << k, e->w << k, 256);
     // head / tail slabs
     const int Hs = e->h * e->S;
-    sf = std::max(sf, (size_t)N * (e->h / 4) * 64 * (9 * e->C + 1));
+    sf = std::max(sf, (size_t)N * (e->h / 2) * 64 * (9 * e->C + 1));  // head wgrad: 2-row bands
     sf = std::max(sf, (size_t)N * (Hs / 4) * e->Co * 577);  // tail_wgrad: 4-row bands
     e->slab_floats = sf;
     e->bslab_floats = bf;

@@ -106,65 +106,70 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
 }
 
 // dW[co][c][tap] = sum_p g[p][co] * lr[c][p+off];  db[co] = sum_p g[p][co]
-// one workgroup per (image, 4-row strip); slab [co][9C + 1]
+// One workgroup per (image, 2-row band); lane = co, the 4 waves split the band's
+// pixels and each keeps ALL 9C + 1 accumulators, so every (coalesced, 256-byte)
+// gradient load feeds 9C + 1 FMAs; loads are issued 4 pixels at a time.  The
+// 4 waves' partials are added in LDS (fixed order) -> slab [co][9C + 1].
+constexpr int kHeadRows = 2;
 __global__ void __launch_bounds__(256) head_wgrad_kernel(const float* __restrict__ lr, const float* __restrict__ g,
                                                          int C, int H, int W, float* __restrict__ slab) {
-  extern __shared__ float hs[];
-  const int n = blockIdx.y, y0 = blockIdx.x * 4, tid = threadIdx.x;
-  const int Wp = W + 2;
-  const int hsz = C * 6 * Wp;
+  extern __shared__ float hs[];  // [C][kHeadRows + 2][W + 2], then red[4][64 * 37]
+  const int n = blockIdx.y, y0 = blockIdx.x * kHeadRows, tid = threadIdx.x;
+  const int co = tid & 63, wave = tid >> 6;
+  const int Wp = W + 2, HR = kHeadRows + 2;
+  const int hsz = C * HR * Wp;
   for (int i = tid; i < hsz; i += 256) {
-    const int c = i / (6 * Wp), r = (i / Wp) % 6, xx = i % Wp;
+    const int c = i / (HR * Wp), r = (i / Wp) % HR, xx = i % Wp;
     const int y = y0 - 1 + r, x = xx - 1;
     hs[i] = (y >= 0 && y < H && x >= 0 && x < W) ? lr[(((size_t)n * C + c) * H + y) * W + x] : 0.f;
   }
   __syncthreads();
-  const int co = tid & 63, grp = tid >> 6;
   const int nj = 9 * C + 1;  // last = bias
-  float acc[10];
+  float acc[37];
 #pragma unroll
-  for (int k = 0; k < 10; ++k) acc[k] = 0.f;
-  // 8 pixels per round, their gradient loads unconditional (clamped) so they issue
-  // back to back: the walk was latency-bound at ~1.5 workgroups per CU
-  for (int p0 = 0; p0 < 4 * W; p0 += 8) {
-    float gv8[8];
+  for (int k = 0; k < 37; ++k) acc[k] = 0.f;
+  for (int r = 0; r < kHeadRows; ++r) {
+    const float* grow = g + (((size_t)n * H + y0 + r) * W) * 64 + co;
+    for (int x0 = wave; x0 < W; x0 += 16) {  // this wave's pixels x0, x0+4, x0+8, x0+12
+      float gv[4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int px = min(p0 + u, 4 * W - 1), r = px / W, x = px - r * W;
-      gv8[u] = g[(((size_t)n * H + y0 + r) * W + x) * 64 + co];
-    }
+      for (int u = 0; u < 4; ++u) gv[u] = grow[(size_t)min(x0 + 4 * u, W - 1) * 64];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (p0 + u >= 4 * W) break;  // uniform
-      const int px = p0 + u, r = px / W, x = px - r * W;
-      const float gv = gv8[u];
+      for (int u = 0; u < 4; ++u) {
+        const int x = x0 + 4 * u;
+        if (x >= W) break;  // uniform
 #pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        const int j = grp + 4 * k;
-        if (j < nj - 1) {
-          const int c = j / 9, t = j % 9;
-          acc[k] += gv * hs[(c * 6 + r + t / 3) * Wp + x + t % 3];
-        } else if (j == nj - 1) {
-          acc[k] += gv;
+        for (int c = 0; c < 4; ++c) {
+          if (c < C) {
+#pragma unroll
+            for (int t = 0; t < 9; ++t) acc[c * 9 + t] += gv[u] * hs[(c * HR + r + t / 3) * Wp + x + t % 3];
+          }
         }
+        acc[36] += gv[u];
       }
     }
   }
-  float* out = slab + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 64 * nj;
+  float* red = hs + hsz;
 #pragma unroll
-  for (int k = 0; k < 10; ++k) {
-    const int j = grp + 4 * k;
-    if (j < nj) out[co * nj + j] = acc[k];
+  for (int k = 0; k < 36; ++k)
+    if (k < nj - 1) red[(wave * 64 + co) * 37 + k] = acc[k];
+  red[(wave * 64 + co) * 37 + 36] = acc[36];
+  __syncthreads();
+  float* out = slab + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 64 * nj;
+  for (int i = tid; i < 64 * nj; i += 256) {
+    const int c2 = i / nj, j = i - c2 * nj, k = (j == nj - 1) ? 36 : j;
+    out[i] = (red[(0 * 64 + c2) * 37 + k] + red[(1 * 64 + c2) * 37 + k]) +
+             (red[(2 * 64 + c2) * 37 + k] + red[(3 * 64 + c2) * 37 + k]);
   }
 }
 
 int head_wgrad_launch(const float* lr, const float* g, int N, int C, int H, int W, float* slab, int* nslab,
                       hipStream_t st) {
-  if (C < 1 || C > 4 || H % 4) return SRMI_ERR_SHAPE;
-  const int smem = C * 6 * (W + 2) * 4;
-  hipLaunchKernelGGL(head_wgrad_kernel, dim3(H / 4, N), dim3(256), smem, st, lr, g, C, H, W, slab);
+  if (C < 1 || C > 4 || H % kHeadRows) return SRMI_ERR_SHAPE;
+  const int smem = (C * (kHeadRows + 2) * (W + 2) + 4 * 64 * 37) * 4;
+  hipLaunchKernelGGL(head_wgrad_kernel, dim3(H / kHeadRows, N), dim3(256), smem, st, lr, g, C, H, W, slab);
   SRMI_CHECK_LAUNCH();
-  *nslab = N * (H / 4);
+  *nslab = N * (H / kHeadRows);
   return 0;
 }
 
