@@ -280,14 +280,19 @@ def main():
     loss = float(out["loss"])
     tiles = B * world * args.steps
     value = tiles / dt
+    del tr, hr  # the extra lines below run on their own engines
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     if info.rank == 0:
         roof, roof_conv = rooflines(dev, B)
-        infer = None
-        if not args.no_inference and world == 1:
-            infer = inference_bench(dev, args.infer_region, args.infer_iters)
         edsr = None
         if not args.no_edsr and world == 1:
             edsr = edsr_bench(dev, args.edsr_batch, 5, 2)
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        infer = None
+        if not args.no_inference and world == 1:
+            infer = inference_bench(dev, args.infer_region, args.infer_iters)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(C, args.cpu_steps)
