@@ -200,6 +200,7 @@ struct srmi_engine {
   hipEvent_t ev_du[2] = {}, ev_dz[2] = {}, ev_w2[2] = {}, ev_w1[2] = {}, ev_grp = nullptr, ev_side = nullptr;
   bf16_t *DUr[2] = {}, *DZr[2] = {};  // double-buffered RCAB gradients (ring of 2 blocks)
   float *slab_s = nullptr, *bslab_s = nullptr;
+  float *slab_s2 = nullptr, *bslab_s2 = nullptr;  // second side slab set (paired reductions)
   size_t slab_s_floats = 0, bslab_s_floats = 0;
   float* lpart;
   int lpart_n;
@@ -309,6 +310,8 @@ static size_t carve(srmi_engine* e, char* base) {
       e->bslab_s_floats = ns * 64;
       e->slab_s = cv.take<float>(e->slab_s_floats);
       e->bslab_s = cv.take<float>(e->bslab_s_floats);
+      e->slab_s2 = cv.take<float>(e->slab_s_floats);
+      e->bslab_s2 = cv.take<float>(e->bslab_s_floats);
     }
   }
   e->packs = cv.take<bf16_t>(P.pack_elems);
@@ -423,8 +426,11 @@ static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n,
   return conv3x3_launch(p, epi, st);
 }
 
+// side: the launch runs on the side stream with its own slabs (set `sset`); with
+// `defer` the reduction is not launched but returned in *out (see reduce2 below).
 static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const bf16_t* dy, int n, int H, int W,
-                      float* grads, bool with_bias, float alpha, hipStream_t st, bool side = false) {
+                      float* grads, bool with_bias, float alpha, hipStream_t st, bool side = false, int sset = 0,
+                      ReduceSet* defer = nullptr) {
   WgradParams p{};
   p.x = x;
   p.dy = dy;
@@ -435,14 +441,19 @@ static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const b
   p.dy_mode = c.ps ? IN_UNSHUF : IN_PLAIN;
   p.imgs_per_wg = 1;
   p.row_splits = side ? side_row_splits(e) : choose_row_splits(n, H, c.cout, e->cu_budget);
-  p.slab = side ? e->slab_s : e->slab;
-  p.bslab = side ? e->bslab_s : e->bslab;
+  p.slab = side ? (sset ? e->slab_s2 : e->slab_s) : e->slab;
+  p.bslab = side ? (sset ? e->bslab_s2 : e->bslab_s) : e->bslab;
   p.zeros = e->zeros;
   const size_t ns = (size_t)wgrad3x3_nslabs(p);
   const size_t cap = side ? e->slab_s_floats : e->slab_floats, bcap = side ? e->bslab_s_floats : e->bslab_floats;
   if (ns * c.cout * 576 > cap || ns * c.cout > bcap) return SRMI_ERR_WORKSPACE;
   int rc = wgrad3x3_launch(p, st);
   if (rc) return rc;
+  if (defer) {
+    *defer = ReduceSet{p.slab, p.bslab, (int)ns, c.cout, c.ps, wgrad3x3_slab_layout(p), alpha, grads + c.w,
+                       with_bias ? grads + c.b : nullptr};
+    return 0;
+  }
   return wgrad_reduce_launch(p.slab, p.bslab, (int)ns, c.cout, c.ps, wgrad3x3_slab_layout(p), alpha, grads + c.w,
                              with_bias ? grads + c.b : nullptr, st);
 }
@@ -579,15 +590,17 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
                             e->brecp(g, b), st));
         HC(hipEventRecord(e->ev_du[q], st));
         HC(hipStreamWaitEvent(e->side, e->ev_du[q], 0));
-        RC(conv_wgrad(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, e->side, true));
+        ReduceSet red2, red1;
+        RC(conv_wgrad(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, e->side, true, 0, &red2));
         HC(hipEventRecord(e->ev_w2[q], e->side));
         if (reuse) HC(hipStreamWaitEvent(st, e->ev_w1[q], 0));
         RC(conv_dgrad(e, r.c2, du, n, h, w, EPI_DG_RELUMASK, dz, nullptr, nullptr, nullptr, nullptr, e->Tm(g, b),
                       nullptr, 1.f, st));
         HC(hipEventRecord(e->ev_dz[q], st));
         HC(hipStreamWaitEvent(e->side, e->ev_dz[q], 0));
-        RC(conv_wgrad(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, e->side, true));
+        RC(conv_wgrad(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, e->side, true, 1, &red1));
         HC(hipEventRecord(e->ev_w1[q], e->side));
+        RC(wgrad_reduce2_launch(red2, red1, e->side));  // both slab sets in one launch
         const bool last = (b == 1);
         RC(conv_dgrad(e, r.c1, dz, n, h, w, EPI_DG_ACC, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
                       (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),

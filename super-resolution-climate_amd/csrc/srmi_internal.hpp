@@ -70,6 +70,15 @@ int wgrad3x3_nslabs(const WgradParams& p);
 int wgrad3x3_slab_layout(const WgradParams& p);
 // slab reduction into the torch-layout grad [Cout][64][3][3] (+ bias [Cout]);
 // ps != 0 un-permutes the packed PixelShuffle channel order (c'' = 64q + c -> 4c + q)
+struct ReduceSet {  // one slab reduction: slabs -> torch-layout dW (and db)
+  const float* slab;
+  const float* bslab;
+  int nslab, Cout, ps, layout;
+  float alpha;
+  float* gw;
+  float* gb;
+};
+int wgrad_reduce2_launch(const ReduceSet& r0, const ReduceSet& r1, hipStream_t st);
 int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, int layout, float alpha,
                         float* gw, float* gb, hipStream_t st);
 

@@ -535,10 +535,9 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
 // blocks for a 64->64 conv (the former 256-output blocks left 112 CUs idle).
 // The bias slab ([nslab][Cout]) is handled by the last block(s).
 constexpr int kRedQ = 16, kRedPh = 32;
-__global__ void __launch_bounds__(kRedQ * kRedPh) wgrad_reduce_kernel(const float* __restrict__ slab,
-                                                                      const float* __restrict__ bslab, int nslab,
-                                                                      int Cout, int ps, int layout, float alpha,
-                                                                      float* __restrict__ gw, float* __restrict__ gb) {
+__device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab, const float* __restrict__ bslab,
+                                                  int nslab, int Cout, int ps, int layout, float alpha,
+                                                  float* __restrict__ gw, float* __restrict__ gb) {
   __shared__ float4 red[kRedPh][kRedQ], red2[4][kRedQ];
   const int per = Cout * 576;
   const int nwb = per / (4 * kRedQ);  // weight blocks (per % 64 == 0 since Cout % 64 == 0)
@@ -629,12 +628,31 @@ __global__ void __launch_bounds__(kRedQ * kRedPh) wgrad_reduce_kernel(const floa
   }
 }
 
+__global__ void __launch_bounds__(kRedQ * kRedPh) wgrad_reduce_kernel(ReduceSet r) {
+  wgrad_reduce_body(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb);
+}
+
+// two independent reductions in one launch (blockIdx.y selects the set): the two
+// filter gradients of an RCAB on the side stream share one launch and one boundary
+__global__ void __launch_bounds__(kRedQ * kRedPh) wgrad_reduce2_kernel(ReduceSet r0, ReduceSet r1) {
+  const ReduceSet& r = blockIdx.y ? r1 : r0;
+  wgrad_reduce_body(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb);
+}
+
 int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, int layout, float alpha,
                         float* gw, float* gb, hipStream_t st) {
   if (Cout % 64) return SRMI_ERR_SHAPE;
   const int blocks = Cout * 576 / (4 * kRedQ) + (Cout + 4 * kRedQ - 1) / (4 * kRedQ);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(kRedQ * kRedPh), 0, st, slab, bslab, nslab, Cout, ps, layout,
-                     alpha, gw, gb);
+  const ReduceSet r{slab, bslab, nslab, Cout, ps, layout, alpha, gw, gb};
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(kRedQ * kRedPh), 0, st, r);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+int wgrad_reduce2_launch(const ReduceSet& r0, const ReduceSet& r1, hipStream_t st) {
+  if (r0.Cout % 64 || r1.Cout != r0.Cout) return SRMI_ERR_SHAPE;
+  const int blocks = r0.Cout * 576 / (4 * kRedQ) + (r0.Cout + 4 * kRedQ - 1) / (4 * kRedQ);
+  hipLaunchKernelGGL(wgrad_reduce2_kernel, dim3(blocks, 2), dim3(kRedQ * kRedPh), 0, st, r0, r1);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
