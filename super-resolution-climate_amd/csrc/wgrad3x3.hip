@@ -238,6 +238,11 @@ constexpr int NGP = 2 * GD + 2 * GX;                             // groups per p
 #ifndef SRMI_WGRAD_ILV
 #define SRMI_WGRAD_ILV 1
 #endif
+// diagnostic builds only (garbage results): 1 = no MFMAs, 2 = no in-loop DMA,
+// 4 = no per-pair wait/barrier, 8 = no in-loop fragment reads
+#ifndef SRMI_WGRAD_EXP
+#define SRMI_WGRAD_EXP 0
+#endif
 
 // The body is instantiated once per wave (WV = wave index): the wave's DMA groups,
 // taps and tile rotation are compile-time constants (no SGPR pressure, no branches).
@@ -422,16 +427,21 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
 #pragma unroll
       for (int kc = 0; kc < 3; ++kc) {
         const int cur = (3 * q + kc) & 1, nxt = cur ^ 1;
-        if (pf) dma_pair_part(j + PF, kc == 0 ? 0 : (kc == 1 ? 3 : 5), kc == 0 ? 3 : (kc == 1 ? 5 : 7));
+        if (!(SRMI_WGRAD_EXP & 2) && pf)
+          dma_pair_part(j + PF, kc == 0 ? 0 : (kc == 1 ? 3 : 5), kc == 0 ? 3 : (kc == 1 ? 5 : 7));
         __builtin_amdgcn_sched_barrier(0);
-        const bool ld = kc < 2 || more;
-        if (kc < 2) load_step(ra, rb, kc + 1, A[nxt], B[nxt]);
-        else if (more) load_step(ran, rbn, 0, A[nxt], B[nxt]);  // next pair's first K-step
+        const bool ld = !(SRMI_WGRAD_EXP & 8) && (kc < 2 || more);
+        if (!(SRMI_WGRAD_EXP & 8)) {
+          if (kc < 2) load_step(ra, rb, kc + 1, A[nxt], B[nxt]);
+          else if (more) load_step(ran, rbn, 0, A[nxt], B[nxt]);  // next pair's first K-step
+        }
+        if (!(SRMI_WGRAD_EXP & 1)) {
 #pragma unroll
-        for (int t = 0; t < 9; ++t)
+          for (int t = 0; t < 9; ++t)
 #pragma unroll
-          for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(A[cur][ct], B[cur][t], acc[ct][t]);
-        bacc = mfma16(A[cur][0], ones, bacc);  // slot 0 = this wave's own co tile
+            for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(A[cur][ct], B[cur][t], acc[ct][t]);
+          bacc = mfma16(A[cur][0], ones, bacc);  // slot 0 = this wave's own co tile
+        }
 #if SRMI_WGRAD_ILV
         // the next K-step's 26 transposed reads issued behind the MFMAs, one per MFMA
         if (ld) {
@@ -444,7 +454,7 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
         }
 #endif
         __builtin_amdgcn_sched_barrier(0);
-        if (kc == 1) {
+        if (kc == 1 && !(SRMI_WGRAD_EXP & 4)) {
           // pair j+1 must have landed before K-step 2 reads its first fragments.  In
           // flight may stay: pair j+2 (whole) and the 5 groups of pair j+PF issued above.
           if (j + 2 < np) wait_groups(1, pf ? 5 : 0);
@@ -460,6 +470,7 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
     }
   }
 
+  if (SRMI_WGRAD_EXP & 4) wait_vm<0>();
   // partial slab in the MFMA-native order (slab layout 1): every store instruction
   // writes 1 KiB contiguous; wgrad_reduce_kernel maps it back to (co, ci, tap)
 #ifndef SRMI_WGRAD_SLAB_WT
