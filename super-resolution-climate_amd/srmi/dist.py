@@ -119,15 +119,29 @@ class GradReducer:
         self.buckets = grad_buckets(table, arch, nlayers)
         self.n_events = max([b.event_index for b in self.buckets if b.event_index is not None], default=-1) + 1
         self.cuda = device.type == "cuda"
-        self.events = [torch.cuda.Event() for _ in range(max(self.n_events, 0))] if self.cuda else []
+        self.device = device
         self.stream = torch.cuda.Stream(device=device) if self.cuda else None
+        self.events = self.new_events()
 
     def covered(self) -> int:
         return sum(n for b in self.buckets for _, n in b.ranges)
 
     def new_events(self) -> List:
-        """One more set of group events (one set per micro-batch engine)."""
-        return [torch.cuda.Event() for _ in range(max(self.n_events, 0))] if self.cuda else []
+        """One more set of group events (one set per micro-batch engine).
+
+        torch.cuda.Event creates its HIP event lazily on the first torch-side record():
+        until then `cuda_event` is NULL, the engine would skip recording it and
+        `Stream.wait_event` on it is a no-op -- the bucket all-reduce would not wait
+        for backward at all.  So each event is created here by one record on the
+        reducer's stream."""
+        if not self.cuda:
+            return []
+        evs = [torch.cuda.Event() for _ in range(max(self.n_events, 0))]
+        for ev in evs:
+            ev.record(self.stream)
+            if not ev.cuda_event:
+                raise RuntimeError("group event was not created")
+        return evs
 
     def reduce(self, grads: torch.Tensor, events_recorded: bool = True, extra: Sequence[torch.Tensor] = (),
                extra_events: Sequence[Sequence] = ()):

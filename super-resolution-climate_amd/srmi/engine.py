@@ -148,6 +148,8 @@ class Engine:
                  dy=None, events: Optional[Sequence] = None, stream=None):
         evp = None
         if events is not None:
+            if any(e is not None and not e.cuda_event for e in events):
+                raise RuntimeError("backward: group event not created yet (record it once before passing it)")
             evp = (C.c_void_p * len(events))(*[e.cuda_event if e is not None else None for e in events])
         call("srmi_backward", self._h, ptr(params), ptr(lr), ptr(sr), ptr(hr), ptr(loss4), ptr(dy), ptr(grads), evp,
              stream_handle(stream))

@@ -83,3 +83,22 @@ def test_dp_world2_micro2_matches_single_process():
         # (strong cancellation in weight gradients amplifies that to ~4e-5)
         assert np.linalg.norm(g_r - g) / np.linalg.norm(g) < 2e-4
     np.testing.assert_array_equal(res[0][4], res[1][4])  # replicas stay identical after Adam
+
+
+def test_group_events_exist_before_backward():
+    """The reducer's per-group events (and every micro-batch engine's extra set) must
+    hold a real HIP event before the first backward: torch.cuda.Event creates it
+    lazily, and a NULL handle would make the engine skip the record and the bucket's
+    wait_event a no-op (the all-reduce would then race the backward)."""
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "super-resolution-climate_amd"), ROOT]
+    from srmi.dist import DistInfo, GradReducer
+    from srmi.engine import Engine, param_table
+    d = torch.device("cuda", 0)
+    spec = _spec()
+    red = GradReducer(param_table(spec), "rcan", spec.nlayers, DistInfo(rank=0, world=2), d)
+    assert red.n_events == spec.nlayers
+    for evs in (red.events, red.new_events()):
+        assert len(evs) == spec.nlayers and all(ev.cuda_event for ev in evs)
+    with pytest.raises(RuntimeError, match="group event"):
+        Engine.backward(None, None, None, None, events=[torch.cuda.Event()])
