@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--micro", type=int, default=None, help="micro-batches per step (default: trainer's choice)")
     ap.add_argument("--infer-region", type=int, default=4096, help="C5 HR region side (BASELINE: 4096)")
     ap.add_argument("--infer-iters", type=int, default=5)
+    ap.add_argument("--force-dp", action="store_true",
+                    help="diagnostic: the DP path (RCCL group, reducer stream, bucketed all-reduce) at one rank")
     return ap.parse_args()
 
 
@@ -246,7 +248,14 @@ def main():
     from srmi.engine import NetSpec
     from srmi.trainer import FusedTrainer
 
-    info = init_from_env()
+    aff0 = len(os.sched_getaffinity(0))
+    info = init_from_env(os.environ.get("SRMI_DP_BACKEND") or None, force=args.force_dp)
+    if os.environ.get("SRMI_PG_ONLY"):  # diagnostic: the process group exists but is never used
+        info.force = False
+    if os.environ.get("SRMI_BENCH_DIAG"):
+        thr = [l for l in open("/proc/self/status") if l.startswith("Threads")][0].strip()
+        print(f"diag: affinity {aff0} -> {len(os.sched_getaffinity(0))} cpus, {thr}, "
+              f"torch threads {torch.get_num_threads()}", file=sys.stderr)
     world = info.world
     if world != args.gpus and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
@@ -268,6 +277,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = tr.step(hr)
+    t_host = time.perf_counter() - t0  # host enqueue time of the K steps (GPU may still run)
     torch.cuda.synchronize()
     if info.enabled:
         torch.distributed.barrier()
@@ -298,7 +308,8 @@ def main():
             cpu = cpu_baseline(C, args.cpu_steps)
         rec = {
             "metric": METRIC, "value": round(value, 2), "unit": "tiles/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True,
+            "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3),
+            "host_enqueue_ms_per_step": round(1000 * t_host / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {"workload": "rcan-10-20-64 train step (down4 + fwd + RMSE + interp RMSE + bwd + Adam), "
                                    f"{C}-var 48x48->192x192 tiles",

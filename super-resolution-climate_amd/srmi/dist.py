@@ -32,29 +32,34 @@ class DistInfo:
     rank: int = 0
     world: int = 1
     local_rank: int = 0
+    force: bool = False  # diagnostic: the data-parallel machinery with a single rank
 
     @property
     def enabled(self) -> bool:
-        return self.world > 1
+        return self.world > 1 or self.force
 
 
-def init_from_env(backend: Optional[str] = None) -> DistInfo:
+def init_from_env(backend: Optional[str] = None, force: bool = False) -> DistInfo:
+    """force: run the DP path (process group, reducer stream, bucketed all-reduce)
+    even at world size 1 -- measures its on-GPU cost without a second GPU."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world <= 1:
+    if world <= 1 and not force:
         return DistInfo()
+    if world <= 1:
+        os.environ.setdefault("MASTER_PORT", "29511")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if not dist.is_initialized():
-        if backend == "nccl":
+        if backend == "nccl" and not os.environ.get("SRMI_DP_LAZY"):
             torch.cuda.set_device(local)
             dist.init_process_group(backend, rank=rank, world_size=world,
                                     device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
-    return DistInfo(rank, world, local)
+    return DistInfo(rank, world, local, force=force and world <= 1)
 
 
 def shard_range(global_batch: int, info: DistInfo) -> Tuple[int, int]:

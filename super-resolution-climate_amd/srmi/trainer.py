@@ -71,6 +71,9 @@ class FusedTrainer:
         if batch % micro:
             raise ValueError(f"batch {batch} not divisible into {micro} micro-batches")
         self.micro = micro
+        # SRMI_DP_FLAT=1: gradients all-reduced once after backward instead of per
+        # residual group on the reducer stream overlapped with backward
+        self.dp_flat = int(os.environ.get("SRMI_DP_FLAT", "0"))  # 2/3: diagnostic, no grad (3: no) all-reduce
         self.mb = batch // micro
         budget = 256 // micro if micro > 1 else 0
         if micro > 1 and os.environ.get("SRMI_MICRO_BUDGET"):  # diagnostic: CUs each engine's launches aim at
@@ -136,11 +139,13 @@ class FusedTrainer:
         for st in self.streams[1:]:
             main.wait_stream(st)
         self._combine(self.loss4, self.mloss4)
-        allreduce_sum_(self.loss4[0:1], self.info)
+        if self.dp_flat != 3:
+            allreduce_sum_(self.loss4[0:1], self.info)
         Engine.rmse_finalize(self.loss4)
         if self.interp_loss:
             self._combine(self.iloss4, self.miloss4)
-            allreduce_sum_(self.iloss4[0:1], self.info)
+            if self.dp_flat != 3:
+                allreduce_sum_(self.iloss4[0:1], self.info)
             Engine.rmse_finalize(self.iloss4)
         for st in self.streams[1:]:
             st.wait_stream(main)
@@ -148,7 +153,7 @@ class FusedTrainer:
         # engine records its residual-group events; the reducer adds the engines'
         # gradients bucket by bucket on its stream and all-reduces each bucket as
         # soon as all engines are past it (overlapped with the rest of backward).
-        dp = self.info.enabled and self.reducer.cuda
+        dp = self.info.enabled and self.reducer.cuda and not self.dp_flat
         evs = [self.reducer.events] + self.xevents if dp else [None] * self.micro
         for k, eng in enumerate(self.engines):
             sl = slice(k * mb, (k + 1) * mb)
@@ -159,6 +164,12 @@ class FusedTrainer:
             main.wait_stream(st)
         if dp:
             self.reducer.reduce(self.grads, events_recorded=True, extra=self.mgrads[1:], extra_events=self.xevents)
+        elif self.dp_flat and self.info.enabled:
+            # one flat SUM all-reduce after backward (no reducer stream, no group events)
+            for g in self.mgrads[1:]:
+                axpy(self.grads, g, 1.0)
+            if self.dp_flat == 1:
+                allreduce_sum_(self.grads, self.info)
         else:
             for g in self.mgrads[1:]:
                 axpy(self.grads, g, 1.0)  # exact gradient of the whole batch
