@@ -177,6 +177,11 @@ struct srmi_engine {
   // `bmain` (bwd_budget CUs), the RCAB filter gradients on `side` (side_cus CUs,
   // side_rs row chunks per image).  0 = unpartitioned defaults.
   int bwd_budget = 0, side_cus = 0, side_rs = 0;
+  // SRMI_SEP_WAITS=1: main waits for the side's c2 and c1 filter gradients of RCAB
+  // i-2 separately (before rewriting DU and DZ); default: one wait on the c1 event
+  // before rewriting DU covers both (the side runs c2 then c1 in order) -- one
+  // record and one wait fewer per RCAB on the host-bound enqueue path
+  int sep_waits = 0;
   hipStream_t bmain = nullptr;
   hipEvent_t ev_bin = nullptr, ev_bout = nullptr;
   size_t mapn = 0;  // elements of one [N][h][w][64] map
@@ -335,6 +340,7 @@ static int init_engine(srmi_engine* e, const srmi_model_config* cfg, int train) 
   auto envi = [](const char* k) { const char* v = getenv(k); return v ? atoi(v) : 0; };
   e->side_cus = std::max(0, std::min(255, envi("SRMI_SIDE_CUS")));
   e->side_rs = std::max(0, envi("SRMI_SIDE_RS"));
+  e->sep_waits = envi("SRMI_SEP_WAITS") ? 1 : 0;
   e->bwd_budget = e->side_cus > 0 ? 256 - e->side_cus : std::max(0, envi("SRMI_BWD_BUDGET"));
   e->mapn = (size_t)e->N * e->h * e->w * 64;
   if (e->h % 4 || (e->w % 32 && e->w % 48)) return SRMI_ERR_SHAPE;
@@ -585,15 +591,15 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         ++it;
         bf16_t* du = e->DUr[q];
         bf16_t* dz = e->DZr[q];
-        if (reuse) HC(hipStreamWaitEvent(st, e->ev_w2[q], 0));
+        if (reuse) HC(hipStreamWaitEvent(st, e->sep_waits ? e->ev_w2[q] : e->ev_w1[q], 0));
         RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
                             e->brecp(g, b), st));
         HC(hipEventRecord(e->ev_du[q], st));
         HC(hipStreamWaitEvent(e->side, e->ev_du[q], 0));
         ReduceSet red2, red1;
         RC(conv_wgrad(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, e->side, true, 0, &red2));
-        HC(hipEventRecord(e->ev_w2[q], e->side));
-        if (reuse) HC(hipStreamWaitEvent(st, e->ev_w1[q], 0));
+        if (e->sep_waits) HC(hipEventRecord(e->ev_w2[q], e->side));
+        if (reuse && e->sep_waits) HC(hipStreamWaitEvent(st, e->ev_w1[q], 0));
         RC(conv_dgrad(e, r.c2, du, n, h, w, EPI_DG_RELUMASK, dz, nullptr, nullptr, nullptr, nullptr, e->Tm(g, b),
                       nullptr, 1.f, st));
         HC(hipEventRecord(e->ev_dz[q], st));

@@ -206,3 +206,34 @@ def test_conv_abi_rejects_missing_operands():
         args = [dummy, dummy, None, 1, 4, 48, 64, 256 if epi == 3 else 64, 0, epi, None, None, None, None, None,
                 None, None, 1.0, None]
         assert lib.srmi_conv3x3(*args) == -10001, (epi, "expected SRMI_ERR_ARG")
+
+
+def _force_dp_rank(port, q):
+    import os as _os
+    import sys as _sys
+    _sys.path[:0] = [_os.path.join(ROOT, "super-resolution-climate_amd"), ROOT]
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        _os.environ.pop(k, None)
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from srmi.dist import allreduce_sum_, init_from_env
+    info = init_from_env("gloo", force=True)
+    t = torch.tensor([3.0])
+    allreduce_sum_(t, info)
+    q.put((info.enabled, info.world, dist.get_world_size(), float(t)))
+    dist.destroy_process_group()
+
+
+def test_force_dp_single_rank_gloo():
+    """bench.py --force-dp: the data-parallel path (process group, collectives) at
+    world size 1, used to measure its on-GPU cost without a second GPU."""
+    import multiprocessing as mp
+    import random
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_force_dp_rank, args=(29500 + random.randint(2001, 4000), q))
+    p.start()
+    enabled, world, pg_world, v = q.get(timeout=120)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert enabled and world == 1 and pg_world == 1 and v == 3.0
