@@ -250,6 +250,9 @@ def main():
 
     aff0 = len(os.sched_getaffinity(0))
     info = init_from_env(os.environ.get("SRMI_DP_BACKEND") or None, force=args.force_dp)
+    if os.environ.get("SRMI_PIN"):  # diagnostic: pin this thread to CPUs a-b (e.g. off RCCL's proxy cores)
+        a_, b_ = (int(x) for x in os.environ["SRMI_PIN"].split("-"))
+        os.sched_setaffinity(0, set(range(a_, b_ + 1)) & os.sched_getaffinity(0) or os.sched_getaffinity(0))
     if os.environ.get("SRMI_PG_ONLY"):  # diagnostic: the process group exists but is never used
         info.force = False
     if os.environ.get("SRMI_BENCH_DIAG"):
