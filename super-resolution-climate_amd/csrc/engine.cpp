@@ -203,7 +203,9 @@ struct srmi_engine {
   // side stream for the RCAB filter gradients (overlapped with the dgrad chain)
   hipStream_t side = nullptr;
   hipEvent_t ev_du[2] = {}, ev_dz[2] = {}, ev_w2[2] = {}, ev_w1[2] = {}, ev_grp = nullptr, ev_side = nullptr;
-  bf16_t *DUr[2] = {}, *DZr[2] = {};  // double-buffered RCAB gradients (ring of 2 blocks)
+  // RCAB gradient buffers: a ring of 4 (default) or 2 (SRMI_RING2 / SRMI_SEP_WAITS)
+  bf16_t *DUr[4] = {}, *DZr[4] = {};
+  int ring = 4;
   float *slab_s = nullptr, *bslab_s = nullptr;
   float *slab_s2 = nullptr, *bslab_s2 = nullptr;  // second side slab set (paired reductions)
   size_t slab_s_floats = 0, bslab_s_floats = 0;
@@ -286,8 +288,11 @@ static size_t carve(srmi_engine* e, char* base) {
     e->DZ = cv.take<bf16_t>(m);
     e->DUr[0] = e->DU;
     e->DZr[0] = e->DZ;
-    e->DUr[1] = rcan ? cv.take<bf16_t>(m) : e->DU;
-    e->DZr[1] = rcan ? cv.take<bf16_t>(m) : e->DZ;
+    for (int k = 1; k < 4; ++k) {
+      const bool own = rcan && k < e->ring;
+      e->DUr[k] = own ? cv.take<bf16_t>(m) : e->DU;
+      e->DZr[k] = own ? cv.take<bf16_t>(m) : e->DZ;
+    }
     e->dRESb = cv.take<bf16_t>(m);
     for (int k = 0; k < 3; ++k) e->dPS[k] = nullptr;
     for (int k = 0; k < P.nups; ++k) e->dPS[k] = cv.take<bf16_t>(m << (2 * (k + 1)));
@@ -341,6 +346,7 @@ static int init_engine(srmi_engine* e, const srmi_model_config* cfg, int train) 
   e->side_cus = std::max(0, std::min(255, envi("SRMI_SIDE_CUS")));
   e->side_rs = std::max(0, envi("SRMI_SIDE_RS"));
   e->sep_waits = envi("SRMI_SEP_WAITS") ? 1 : 0;
+  e->ring = (e->sep_waits || envi("SRMI_RING2")) ? 2 : 4;
   e->bwd_budget = e->side_cus > 0 ? 256 - e->side_cus : std::max(0, envi("SRMI_BWD_BUDGET"));
   e->mapn = (size_t)e->N * e->h * e->w * 64;
   if (e->h % 4 || (e->w % 32 && e->w % 48)) return SRMI_ERR_SHAPE;
@@ -584,28 +590,37 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
       for (int b = nb; b >= 1; --b) {
         const RCABRef& r = P.groups[g][b - 1];
         // The two filter gradients of this RCAB run on the side stream, overlapped with
-        // the dgrad chain; DU/DZ alternate between two buffers, and a buffer is only
-        // rewritten after the side stream has finished the wgrad that read it.
-        const int q = it & 1;
-        const bool reuse = it >= 2;
-        ++it;
+        // the dgrad chain; DU/DZ rotate through a ring of buffers, and a buffer is only
+        // rewritten after the side stream has finished the wgrads that read it.  Ring
+        // of 4: the side records its c1 event only after odd RCABs, and main waits
+        // only before even RCAB i >= 4, on the event of RCAB i-3 -- that covers the
+        // reuse of the slots of RCABs i-4 and i-3 (= i and i+1): one record and one
+        // wait per two RCABs.  Ring of 2: one wait per RCAB.
+        const int it0 = it++;
+        const bool r4 = e->ring == 4;
+        const int q = r4 ? (it0 & 3) : (it0 & 1);
+        const int qe = it0 & 1;  // ev_du / ev_dz: recorded and waited at once
+        const bool reuse = r4 ? (it0 >= 4 && !(it0 & 1)) : it0 >= 2;
         bf16_t* du = e->DUr[q];
         bf16_t* dz = e->DZr[q];
-        if (reuse) HC(hipStreamWaitEvent(st, e->sep_waits ? e->ev_w2[q] : e->ev_w1[q], 0));
+        if (reuse)
+          HC(hipStreamWaitEvent(st, r4 ? e->ev_w1[((it0 - 3) >> 1) & 1] : (e->sep_waits ? e->ev_w2[q] : e->ev_w1[q]),
+                                0));
         RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
                             e->brecp(g, b), st));
-        HC(hipEventRecord(e->ev_du[q], st));
-        HC(hipStreamWaitEvent(e->side, e->ev_du[q], 0));
+        HC(hipEventRecord(e->ev_du[qe], st));
+        HC(hipStreamWaitEvent(e->side, e->ev_du[qe], 0));
         ReduceSet red2, red1;
         RC(conv_wgrad(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, e->side, true, 0, &red2));
         if (e->sep_waits) HC(hipEventRecord(e->ev_w2[q], e->side));
         if (reuse && e->sep_waits) HC(hipStreamWaitEvent(st, e->ev_w1[q], 0));
         RC(conv_dgrad(e, r.c2, du, n, h, w, EPI_DG_RELUMASK, dz, nullptr, nullptr, nullptr, nullptr, e->Tm(g, b),
                       nullptr, 1.f, st));
-        HC(hipEventRecord(e->ev_dz[q], st));
-        HC(hipStreamWaitEvent(e->side, e->ev_dz[q], 0));
+        HC(hipEventRecord(e->ev_dz[qe], st));
+        HC(hipStreamWaitEvent(e->side, e->ev_dz[qe], 0));
         RC(conv_wgrad(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, e->side, true, 1, &red1));
-        HC(hipEventRecord(e->ev_w1[q], e->side));
+        if (!r4) HC(hipEventRecord(e->ev_w1[q], e->side));
+        else if (it0 & 1) HC(hipEventRecord(e->ev_w1[(it0 >> 1) & 1], e->side));
         RC(wgrad_reduce2_launch(red2, red1, e->side));  // both slab sets in one launch
         const bool last = (b == 1);
         RC(conv_dgrad(e, r.c1, dz, n, h, w, EPI_DG_ACC, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
