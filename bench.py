@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=64, help="tiles per GPU")
     ap.add_argument("--channels", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=12, help="timed CPU oracle steps (~1 s each at B=4)")
+    ap.add_argument("--cpu-steps", type=int, default=4, help="timed CPU oracle steps per config (median, >= 3)")
     ap.add_argument("--no-interp-loss", action="store_true")
     ap.add_argument("--no-inference", action="store_true", help="skip the C5 tiled-region inference line")
     ap.add_argument("--no-edsr", action="store_true", help="skip the C4 EDSR x8 line")
@@ -209,25 +209,56 @@ def edsr_bench(dev, batch, steps, warmup):
                                    "4-var 32x32->256x256 tiles", "batch": batch}}
 
 
-def cpu_baseline(channels, steps):
-    """Oracle (PyTorch-CPU restatement of the reference step) on this host's cores."""
-    from oracle import rcan_oracle as ro
+def _log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def _cpu_share():
+    """CPUs this process may use: its affinity, capped by the cgroup CPU quota
+    (cpu.max) -- on a GPU box the affinity lists the whole host while the quota
+    holds the box's share."""
     try:
-        avail = len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except Exception:
-        avail = os.cpu_count() or 1
-    threads = max(1, min(16, avail))
+        n = os.cpu_count() or 1
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except Exception:
+        pass
+    return n
+
+
+def cpu_baseline(steps):
+    """the oracle (PyTorch-CPU restatement of the reference step,
+    dual_trainer.py:310-323 with array2tensor's requires_grad, the interp-loss
+    metric and .item()) for C1 = rcan-10-20-64, B=4, fp32, with C=1 (as BASELINE
+    words it) and C=2 (the bench workload's 2-var task), on all host cores
+    available to this process (_cpu_share); warm-up 1 step, median of `steps`
+    (>= 3) steps.  `value` is the C=2 number (the bench workload's shape)."""
+    import statistics
+    from oracle import rcan_oracle as ro
+    threads = _cpu_share()
     torch.set_num_threads(threads)
     B = 4
-    model = ro.RCANOracle(nchannels_in=channels, nchannels_out=channels, nlayers=10, nblocks=20)
-    ro.init_params_numpy(model, 0)
-    opt = ro.AdamOracle(list(model.parameters()), lr=1e-4)
-    hr = torch.tensor(ro.synthetic_hr(B, channels, 192, 1234))
-    ro.train_step(model, opt, hr, 4, interp_loss=True)   # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        ro.train_step(model, opt, hr, 4, interp_loss=True)
-    dt = time.perf_counter() - t0
+    per = {}
+    t_all = 0.0
+    for C in (1, 2):
+        model = ro.RCANOracle(nchannels_in=C, nchannels_out=C, nlayers=10, nblocks=20)
+        ro.init_params_numpy(model, 0)
+        opt = ro.AdamOracle(list(model.parameters()), lr=1e-4)
+        hr = torch.tensor(ro.synthetic_hr(B, C, 192, 1234))
+        ro.train_step(model, opt, hr, 4, interp_loss=True)   # warm-up
+        _log(f"cpu baseline C={C}: warm-up done")
+        ts = []
+        for _ in range(max(3, steps)):
+            t0 = time.perf_counter()
+            ro.train_step(model, opt, hr, 4, interp_loss=True)
+            ts.append(time.perf_counter() - t0)
+        t_all += sum(ts)
+        med = statistics.median(ts)
+        per[f"C{C}"] = {"tiles_per_s": round(B / med, 3), "median_s_per_step": round(med, 3), "steps": len(ts)}
     model_name = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -236,10 +267,12 @@ def cpu_baseline(channels, steps):
                 break
     except Exception:
         pass
-    return {"value": round(B * steps / dt, 3), "unit": "tiles/s", "cores": threads, "kind": "port",
-            "sample": f"oracle rcan-10-20-64 fp32 train step (down4+fwd+RMSE+interp RMSE+bwd+Adam), "
-                      f"B={B}, C={channels}, 1 warm-up + {steps} timed steps, {dt:.1f} s, torch CPU threads="
-                      f"{threads}, cpu='{model_name}'"}
+    return {"value": per["C2"]["tiles_per_s"], "unit": "tiles/s", "cores": threads, "kind": "port",
+            "configs": per,
+            "sample": f"oracle rcan-10-20-64 fp32 train step (down4+fwd+RMSE+interp RMSE+bwd+Adam), B={B}, "
+                      f"C=1 and C=2, 1 warm-up + median of {max(3, steps)} steps each ({t_all:.1f} s timed), "
+                      f"torch CPU threads={threads} (this process's CPU share: affinity capped by the cgroup "
+                      f"quota), cpu='{model_name}'"}
 
 
 def main():
@@ -248,17 +281,7 @@ def main():
     from srmi.engine import NetSpec
     from srmi.trainer import FusedTrainer
 
-    aff0 = len(os.sched_getaffinity(0))
-    info = init_from_env(os.environ.get("SRMI_DP_BACKEND") or None, force=args.force_dp)
-    if os.environ.get("SRMI_PIN"):  # diagnostic: pin this thread to CPUs a-b (e.g. off RCCL's proxy cores)
-        a_, b_ = (int(x) for x in os.environ["SRMI_PIN"].split("-"))
-        os.sched_setaffinity(0, set(range(a_, b_ + 1)) & os.sched_getaffinity(0) or os.sched_getaffinity(0))
-    if os.environ.get("SRMI_PG_ONLY"):  # diagnostic: the process group exists but is never used
-        info.force = False
-    if os.environ.get("SRMI_BENCH_DIAG"):
-        thr = [l for l in open("/proc/self/status") if l.startswith("Threads")][0].strip()
-        print(f"diag: affinity {aff0} -> {len(os.sched_getaffinity(0))} cpus, {thr}, "
-              f"torch threads {torch.get_num_threads()}", file=sys.stderr)
+    info = init_from_env(None, force=args.force_dp)
     world = info.world
     if world != args.gpus and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
@@ -271,9 +294,11 @@ def main():
                       micro=args.micro)
     hr = torch.tensor(synthetic_hr(B, C, 192, 1234 + info.rank)).to(dev)
 
+    _log(f"trainer ready (B={B}, C={C}, micro={tr.micro}, world={world})")
     for _ in range(args.warmup):
         tr.step(hr)
     torch.cuda.synchronize()
+    _log("warm-up done")
     if info.enabled:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -296,19 +321,23 @@ def main():
     del tr, hr  # the extra lines below run on their own engines
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
+    _log(f"timed: {value:.1f} tiles/s")
     if info.rank == 0:
         roof, roof_conv = rooflines(dev, B)
+        _log("rooflines done")
         edsr = None
         if not args.no_edsr and world == 1:
             edsr = edsr_bench(dev, args.edsr_batch, 5, 2)
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
+            _log("edsr done")
         infer = None
         if not args.no_inference and world == 1:
             infer = inference_bench(dev, args.infer_region, args.infer_iters)
+            _log("inference done")
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(C, args.cpu_steps)
+            cpu = cpu_baseline(args.cpu_steps)
         rec = {
             "metric": METRIC, "value": round(value, 2), "unit": "tiles/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3),

@@ -15,7 +15,8 @@
  *   srmi_forward                 -> RCAN.forward sres/model/rcan/network.py:22-27,
  *                                   EDSR.forward sres/model/edsr/network.py:27-32
  *   srmi_backward                -> autograd of the above (dual_trainer.py:322)
- *   srmi_rmse_*                  -> l2loss sres/controller/stats.py:5-8
+ *   srmi_rmse_*, srmi_loss_*     -> l2loss sres/controller/stats.py:5-8
+ *   srmi_charbonnier_partial     -> ModelTrainer.charbonnier dual_trainer.py:196-198
  *   srmi_downsample/_upsample    -> sres/base/util/array.py:72-76 / :84-87
  *   srmi_adam_step               -> torch.optim.Adam, dual_trainer.py:126,323
  *   srmi_conv3x3* / srmi_wgrad*  -> nn.Conv2d of default_conv
@@ -107,6 +108,28 @@ int srmi_backward(srmi_engine* e, const float* params, const float* lr, const fl
 int srmi_rmse_partial(srmi_engine* e, const float* pred, const float* target, size_t n, double count_global,
                       float* loss4, void* stream);
 int srmi_rmse_finalize(float* loss4, void* stream);
+
+/* Charbonnier loss (model.loss_fn 'charbonnier', ModelTrainer.charbonnier
+ * sres/controller/dual_trainer.py:196-198): loss4[0] = sum sqrt(d^2 + eps) (this
+ * rank), loss4[1] = count_global; dy (optional, like pred) = d / sqrt(d^2 + eps) /
+ * count_global -- the upstream gradient srmi_backward takes.  Finalise with
+ * srmi_loss_finalize(loss4, SRMI_LOSS_MEAN): loss4[3] = loss4[0] / loss4[1]. */
+#define SRMI_LOSS_RMSE 0
+#define SRMI_LOSS_MEAN 1
+int srmi_charbonnier_partial(srmi_engine* e, const float* pred, const float* target, size_t n, double count_global,
+                             float eps, float* loss4, float* dy, void* stream);
+int srmi_loss_finalize(float* loss4, int kind, void* stream);
+/* per-batch losses of process_image / evaluate (dual_trainer.py:417-446, :509-532):
+ * pred/target [ntiles][tile_elems] scored in batches of batch_size tiles (the last
+ * one may be short), loss of a batch over all its elements (kind RMSE or MEAN =
+ * Charbonnier with eps); out[0] = mean of the batch losses, out[1 + b] = batch b's
+ * loss (at most 1024 batches); work: ntiles floats */
+int srmi_batch_losses(const float* pred, const float* target, int ntiles, long long tile_elems, int batch_size,
+                      int kind, float eps, float* work, float* out, void* stream);
+/* loss4 = the sum over nparts micro-batch records parts4[k][4] (S summed in a fixed
+ * order, the count of part 0), then finalised as `kind` (-1: not finalised, e.g.
+ * before a data-parallel all-reduce of loss4[0]) */
+int srmi_loss_combine(float* loss4, const float* parts4, int nparts, int kind, void* stream);
 
 /* interp baseline / data path */
 int srmi_downsample(const float* hr, int N, int C, int H, int W, int scale, float* lr, void* stream);

@@ -323,9 +323,32 @@ def assemble(tiles: np.ndarray, mean: Optional[np.ndarray], std: Optional[np.nda
     return out
 
 
-def process_region(model, region: np.ndarray, ty: int, tx: int, scale: int):
-    """process_image (dual_trainer.py:396-480) on one region, all tiles in one batch.
-    Returns (images dict, losses dict) with the reference's image types."""
+def charbonnier(prd: torch.Tensor, tar: torch.Tensor, eps: float = 1e-6) -> torch.Tensor:
+    """ModelTrainer.charbonnier (dual_trainer.py:196-198), eps = self.eps (:122)."""
+    return torch.mean(torch.sqrt((prd - tar) ** 2 + eps))
+
+
+def single_product_loss(prd: torch.Tensor, tar: torch.Tensor, loss_fn: str = "l2") -> torch.Tensor:
+    """dual_trainer.py:205-212."""
+    if loss_fn == "l2":
+        return l2loss(prd, tar)
+    if loss_fn == "charbonnier":
+        return charbonnier(prd, tar)
+    raise Exception("Unknown single-product loss function {}".format(loss_fn))
+
+
+def batch_losses(prd: torch.Tensor, tar: torch.Tensor, batch_size: int, loss_fn: str = "l2") -> List[float]:
+    """The per-batch losses of process_image / evaluate (dual_trainer.py:417-430):
+    TileBatchIterator batches [0, bs), [bs, 2bs), ... (the last one short)."""
+    return [float(single_product_loss(prd[a:a + batch_size], tar[a:a + batch_size], loss_fn))
+            for a in range(0, prd.shape[0], batch_size)]
+
+
+def process_region(model, region: np.ndarray, ty: int, tx: int, scale: int, batch_size: Optional[int] = None,
+                   loss_fn: str = "l2"):
+    """process_image (dual_trainer.py:396-480) on one region: tiles scored in batches
+    of batch_size (None: one batch of all tiles); loss = mean of the batch losses
+    (:443-446).  Returns (images dict, losses dict) with the reference's image types."""
     tiles, mean, std, ids, grid = region_to_tiles(region, ty, tx)
     dt = torch.float64 if tiles.dtype == np.float64 else torch.float32
     target = torch.tensor(tiles, dtype=dt)
@@ -333,11 +356,37 @@ def process_region(model, region: np.ndarray, ty: int, tx: int, scale: int):
     with torch.no_grad():
         sr = model(lr)
     interp = upsample(lr, scale)
-    losses = {"model": float(l2loss(sr, target)), "interpolated": float(l2loss(interp, target))}
+    bs = batch_size or target.shape[0]
+    bm = batch_losses(sr, target, bs, loss_fn)
+    bi = batch_losses(interp, target, bs, loss_fn)
+    losses = {"model": float(np.array(bm).mean()), "interpolated": float(np.array(bi).mean()),
+              "batch_model": bm, "batch_interpolated": bi}
     images = {"input": assemble(lr.numpy(), mean, std, ids, grid), "target": assemble(tiles, mean, std, ids, grid),
               "interpolated": assemble(interp.numpy(), mean, std, ids, grid),
               "model": assemble(sr.numpy(), mean, std, ids, grid)}
     return images, losses
+
+
+def evaluate(model, regions: Sequence[np.ndarray], ty: int, tx: int, scale: int, batch_size: int,
+             loss_fn: str = "l2"):
+    """ModelTrainer.evaluate (dual_trainer.py:482-543) over the time slices of a
+    tset (no flips): losses = mean over all batches of all regions; results = the
+    normalised tiles concatenated along the tile axis (merge_results_tiles, :38-42)."""
+    bm, bi, res = [], [], {k: [] for k in ("input", "target", "model", "interpolated")}
+    for region in regions:
+        tiles, _, _, _, _ = region_to_tiles(region, ty, tx)
+        dt = torch.float64 if tiles.dtype == np.float64 else torch.float32
+        target = torch.tensor(tiles, dtype=dt)
+        lr = downsample(target, scale)
+        with torch.no_grad():
+            sr = model(lr)
+        interp = upsample(lr, scale)
+        bm += batch_losses(sr, target, batch_size, loss_fn)
+        bi += batch_losses(interp, target, batch_size, loss_fn)
+        for k, v in (("input", lr), ("target", target), ("model", sr), ("interpolated", interp)):
+            res[k].append(v.numpy())
+    results = {k: np.concatenate(v, axis=0) for k, v in res.items()}
+    return results, {"model": float(np.array(bm).mean()), "interpolated": float(np.array(bi).mean())}
 
 
 # --------------------------------------------------------------------------

@@ -704,16 +704,10 @@ __global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int r
     for (int s = 0; s < 18; ++s) {
       // group k+2's DMA pieces and the epilogue operands are issued one or two per
       // K-step, so a full memory queue stalls the wave between MFMA groups only
-#ifndef SRMI_CONV_DBG
-#define SRMI_CONV_DBG 0
-#endif
-      // SRMI_CONV_DBG (diagnostic builds only, wrong results): bit0 no DMA in the K loop,
-      // bit1 no fragment reads after the first, bit2 no epilogue prefetch
-      if (!(SRMI_CONV_DBG & 1) && s < NGW && pf && wv_s + 4 * s < NGRP) group_dma_one(k + 2, s);
-      if (!(SRMI_CONV_DBG & 4) && s >= 2 && s - 2 < NPT * 4)
-        epi_prefetch_one<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk, s - 2);
+      if (s < NGW && pf && wv_s + 4 * s < NGRP) group_dma_one(k + 2, s);
+      if (s >= 2 && s - 2 < NPT * 4) epi_prefetch_one<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk, s - 2);
       __builtin_amdgcn_sched_barrier(0);
-      const bool ld = !(SRMI_CONV_DBG & 2) && s + LA < 18;
+      const bool ld = s + LA < 18;
       if (ld) load_step(s + LA, A[(s + LA) % kFragBuf], B[(s + LA) % kFragBuf]);
 #pragma unroll
       for (int pt = 0; pt < NPT; ++pt)
@@ -764,9 +758,7 @@ static int launch_tw(const ConvParams& p, hipStream_t st) {
     // v2: persistent runs; ~1 workgroup per CU (LDS-limited), each a run of strips
     const int nsy = p.H / kTH;
     const int units = (p.Cout / 64) * p.N * (p.W / TW);
-    // SRMI_CONV_CU_PCT (diagnostic): size the runs for this % of the CU budget
-    static const int pct = getenv("SRMI_CONV_CU_PCT") ? atoi(getenv("SRMI_CONV_CU_PCT")) : 100;
-    const int cus = std::max(1, (p.cu_budget > 0 ? p.cu_budget : 256) * pct / 100);
+    const int cus = p.cu_budget > 0 ? p.cu_budget : 256;
     int R = (cus + units / 2) / units;
     R = R < 1 ? 1 : (R > nsy ? nsy : R);
     const int run_len = (nsy + R - 1) / R;

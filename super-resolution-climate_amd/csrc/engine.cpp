@@ -173,22 +173,6 @@ struct srmi_engine {
   int train = 0;
   int N = 0, h = 0, w = 0, C = 0, Co = 0, S = 0;
   int cu_budget = 0;  // CUs one launch aims to fill (0 = all)
-  // backward partition of the chip (RCAN train engines): the dgrad chain runs on
-  // `bmain` (bwd_budget CUs), the RCAB filter gradients on `side` (side_cus CUs,
-  // side_rs row chunks per image).  0 = unpartitioned defaults.
-  int bwd_budget = 0, side_cus = 0, side_rs = 0;
-  // SRMI_SEP_WAITS=1: main waits for the side's c2 and c1 filter gradients of RCAB
-  // i-2 separately (before rewriting DU and DZ); default: one wait on the c1 event
-  // before rewriting DU covers both (the side runs c2 then c1 in order) -- one
-  // record and one wait fewer per RCAB on the host-bound enqueue path
-  int sep_waits = 0;
-  // the side stream waits once per RCAB (on dz) before both of its filter gradients:
-  // it runs behind main anyway, so gating c2 on dz instead of du costs no overlap and
-  // saves a record + wait (1962 -> 2028 tiles/s over 3 A/B pairs).
-  // SRMI_TWO_SIDE_WAITS=1: wait on du before c2 and on dz before c1
-  int one_side_wait = 1;
-  hipStream_t bmain = nullptr;
-  hipEvent_t ev_bin = nullptr, ev_bout = nullptr;
   size_t mapn = 0;  // elements of one [N][h][w][64] map
   // forward state
   float *X0f, *Rf, *Hf;
@@ -207,10 +191,9 @@ struct srmi_engine {
   size_t slab_floats, bslab_floats;
   // side stream for the RCAB filter gradients (overlapped with the dgrad chain)
   hipStream_t side = nullptr;
-  hipEvent_t ev_du[2] = {}, ev_dz[2] = {}, ev_w2[2] = {}, ev_w1[2] = {}, ev_grp = nullptr, ev_side = nullptr;
-  // RCAB gradient buffers: a ring of 4 (default) or 2 (SRMI_RING2 / SRMI_SEP_WAITS)
+  hipEvent_t ev_dz[2] = {}, ev_w1[2] = {}, ev_grp = nullptr, ev_side = nullptr;
+  // RCAB gradient buffers: a ring of 4 (du, dz of RCABs i .. i+3), see backward_impl
   bf16_t *DUr[4] = {}, *DZr[4] = {};
-  int ring = 4;
   float *slab_s = nullptr, *bslab_s = nullptr;
   float *slab_s2 = nullptr, *bslab_s2 = nullptr;  // second side slab set (paired reductions)
   size_t slab_s_floats = 0, bslab_s_floats = 0;
@@ -247,10 +230,7 @@ struct srmi_engine {
 // fewer, longer chunks write fewer partial slabs (at C2 2 x 24-row chunks per
 // image instead of 3 x 16: 1837 -> 1901 tiles/s measured).
 static int side_row_splits(const srmi_engine* e) {
-  const int rs = e->side_rs;
-  if (rs > 0 && e->h % rs == 0 && (e->h / rs) % 4 == 0) return rs;
-  const int budget = e->side_cus > 0 ? e->side_cus : (e->cu_budget > 0 ? e->cu_budget : 256) / 2;
-  return choose_row_splits(e->N, e->h, 64, budget);
+  return choose_row_splits(e->N, e->h, 64, (e->cu_budget > 0 ? e->cu_budget : 256) / 2);
 }
 
 static size_t carve(srmi_engine* e, char* base) {
@@ -294,7 +274,7 @@ static size_t carve(srmi_engine* e, char* base) {
     e->DUr[0] = e->DU;
     e->DZr[0] = e->DZ;
     for (int k = 1; k < 4; ++k) {
-      const bool own = rcan && k < e->ring;
+      const bool own = rcan;
       e->DUr[k] = own ? cv.take<bf16_t>(m) : e->DU;
       e->DZr[k] = own ? cv.take<bf16_t>(m) : e->DZ;
     }
@@ -304,10 +284,13 @@ static size_t carve(srmi_engine* e, char* base) {
     // slab: max over all wgrads
     size_t sf = 0, bf = 0;
     auto upd = [&](int H, int W, int Cout) {
-      const int rs = choose_row_splits(N, H, Cout, e->cu_budget);
-      const size_t ns = (size_t)N * rs;
-      sf = std::max(sf, ns * Cout * 576);
-      bf = std::max(bf, ns * Cout);
+      // a call may pass fewer tiles than the capacity (a short last batch), and
+      // fewer tiles get more row splits: size for the largest n * rs(n)
+      for (int n = 1; n <= N; ++n) {
+        const size_t ns = (size_t)n * choose_row_splits(n, H, Cout, e->cu_budget);
+        sf = std::max(sf, ns * Cout * 576);
+        bf = std::max(bf, ns * Cout);
+      }
     };
     upd(e->h, e->w, 64);
     for (int k = 0; k < P.nups; ++k) upd(e->h << k, e->w << k, 256);
@@ -347,13 +330,6 @@ static int init_engine(srmi_engine* e, const srmi_model_config* cfg, int train) 
   e->Co = cfg->nchannels_out;
   e->S = cfg->scale;
   e->cu_budget = cfg->cu_budget > 0 ? cfg->cu_budget : 0;
-  auto envi = [](const char* k) { const char* v = getenv(k); return v ? atoi(v) : 0; };
-  e->side_cus = std::max(0, std::min(255, envi("SRMI_SIDE_CUS")));
-  e->side_rs = std::max(0, envi("SRMI_SIDE_RS"));
-  e->sep_waits = envi("SRMI_SEP_WAITS") ? 1 : 0;
-  e->one_side_wait = (!e->sep_waits && !envi("SRMI_TWO_SIDE_WAITS")) ? 1 : 0;  // (ev_w2 must follow c2)
-  e->ring = (e->sep_waits || envi("SRMI_RING2")) ? 2 : 4;
-  e->bwd_budget = e->side_cus > 0 ? 256 - e->side_cus : std::max(0, envi("SRMI_BWD_BUDGET"));
   e->mapn = (size_t)e->N * e->h * e->w * 64;
   if (e->h % 4 || (e->w % 32 && e->w % 48)) return SRMI_ERR_SHAPE;
   const int Hs = e->h * e->S;
@@ -438,7 +414,7 @@ static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n,
   p.part_stride = 128;
   p.alpha = alpha;
   p.zeros = e->zeros;
-  p.cu_budget = e->bwd_budget > 0 ? e->bwd_budget : e->cu_budget;
+  p.cu_budget = e->cu_budget;
   if (epi == EPI_DG_ACC && r1 && aux && part && !yb && !r2 && !r3 && yf && c.cout == 64 && !c.ps)
     epi = EPI_DG_ACC_CA;  // the hot RCAB case: specialised epilogue without runtime operand checks
   return conv3x3_launch(p, epi, st);
@@ -596,48 +572,36 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
       for (int b = nb; b >= 1; --b) {
         const RCABRef& r = P.groups[g][b - 1];
         // The two filter gradients of this RCAB run on the side stream, overlapped with
-        // the dgrad chain; DU/DZ rotate through a ring of buffers, and a buffer is only
-        // rewritten after the side stream has finished the wgrads that read it.  Ring
-        // of 4: the side records its c1 event only after odd RCABs, and main waits
-        // only before even RCAB i >= 4, on the event of RCAB i-3 -- that covers the
-        // reuse of the slots of RCABs i-4 and i-3 (= i and i+1): one record and one
-        // wait per two RCABs.  Ring of 2: one wait per RCAB.
+        // the dgrad chain; DU/DZ rotate through a ring of 4 buffers, and a buffer is
+        // only rewritten after the side stream has finished the wgrads that read it:
+        // the side records its c1 event only after odd RCABs, and main waits only
+        // before even RCAB i >= 4, on the event of RCAB i-3 -- that covers the reuse
+        // of the slots of RCABs i-4 and i-3 (= i and i+1): one record and one wait per
+        // two RCABs.  The side stream waits once per RCAB, on dz, before both filter
+        // gradients (it runs behind main anyway).
         const int it0 = it++;
-        const bool r4 = e->ring == 4;
-        const int q = r4 ? (it0 & 3) : (it0 & 1);
-        const int qe = it0 & 1;  // ev_du / ev_dz: recorded and waited at once
-        const bool reuse = r4 ? (it0 >= 4 && !(it0 & 1)) : it0 >= 2;
+        const int q = it0 & 3, qe = it0 & 1;
+        const bool reuse = it0 >= 4 && !(it0 & 1);
         bf16_t* du = e->DUr[q];
         bf16_t* dz = e->DZr[q];
-        if (reuse)
-          HC(hipStreamWaitEvent(st, r4 ? e->ev_w1[((it0 - 3) >> 1) & 1] : (e->sep_waits ? e->ev_w2[q] : e->ev_w1[q]),
-                                0));
+        if (reuse) HC(hipStreamWaitEvent(st, e->ev_w1[((it0 - 3) >> 1) & 1], 0));
         RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
                             e->brecp(g, b), st));
         ReduceSet red2, red1;
-        if (!e->one_side_wait) {
-          HC(hipEventRecord(e->ev_du[qe], st));
-          HC(hipStreamWaitEvent(e->side, e->ev_du[qe], 0));
-          RC(conv_wgrad(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, e->side, true, 0, &red2));
-        }
-        if (e->sep_waits) HC(hipEventRecord(e->ev_w2[q], e->side));
-        if (reuse && e->sep_waits) HC(hipStreamWaitEvent(st, e->ev_w1[q], 0));
         RC(conv_dgrad(e, r.c2, du, n, h, w, EPI_DG_RELUMASK, dz, nullptr, nullptr, nullptr, nullptr, e->Tm(g, b),
                       nullptr, 1.f, st));
         HC(hipEventRecord(e->ev_dz[qe], st));
         HC(hipStreamWaitEvent(e->side, e->ev_dz[qe], 0));
-        if (e->one_side_wait)
-          RC(conv_wgrad(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, e->side, true, 0, &red2));
+        RC(conv_wgrad(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, e->side, true, 0, &red2));
         RC(conv_wgrad(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, e->side, true, 1, &red1));
-        if (!r4) HC(hipEventRecord(e->ev_w1[q], e->side));
-        else if (it0 & 1) HC(hipEventRecord(e->ev_w1[(it0 >> 1) & 1], e->side));
+        if (it0 & 1) HC(hipEventRecord(e->ev_w1[(it0 >> 1) & 1], e->side));
         RC(wgrad_reduce2_launch(red2, red1, e->side));  // both slab sets in one launch
         const bool last = (b == 1);
         RC(conv_dgrad(e, r.c1, dz, n, h, w, EPI_DG_ACC, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
                       (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
                       last ? nullptr : e->pacc, 1.f, st));
       }
-      RC(ca_param_grads_batched_launch(e->recp(g, 1), e->brecp(g, 1), nb, n, 64, R, e->d_caoffs + (size_t)g * nb * 5,
+      RC(ca_param_grads_batched_launch(e->recp(g, 1), e->brecp(g, 1), nb, n, e->N, 64, R, e->d_caoffs + (size_t)g * nb * 5,
                                        grads, st));
       std::swap(gRf, ghf);
       std::swap(gRb, ghb);
@@ -724,25 +688,9 @@ int srmi_engine_create(const srmi_model_config* cfg, void* workspace, size_t ws_
     return SRMI_ERR_WORKSPACE;
   }
   carve(e, base);
-  if (train && e->P.cfg.arch == SRMI_ARCH_RCAN && e->side_cus > 0) {
-    // spatial partition: side_cus CUs spread evenly over the mask for the filter
-    // gradients, the rest for the dgrad chain
-    uint32_t ms[8] = {}, mm[8] = {};
-    const int nc = 256, k = e->side_cus;
-    for (int i = 0; i < k; ++i) {
-      const int cu = (int)(((long long)i * nc) / k);
-      ms[cu >> 5] |= 1u << (cu & 31);
-    }
-    for (int w = 0; w < 8; ++w) mm[w] = ~ms[w];
-    HC(hipExtStreamCreateWithCUMask(&e->side, 8, ms));
-    HC(hipExtStreamCreateWithCUMask(&e->bmain, 8, mm));
-    HC(hipEventCreateWithFlags(&e->ev_bin, hipEventDisableTiming));
-    HC(hipEventCreateWithFlags(&e->ev_bout, hipEventDisableTiming));
-  }
   if (train && e->P.cfg.arch == SRMI_ARCH_RCAN) {
-    if (!e->side) HC(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
-    hipEvent_t* evs[] = {&e->ev_du[0], &e->ev_du[1], &e->ev_dz[0], &e->ev_dz[1], &e->ev_w2[0],
-                         &e->ev_w2[1], &e->ev_w1[0], &e->ev_w1[1], &e->ev_grp, &e->ev_side};
+    HC(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
+    hipEvent_t* evs[] = {&e->ev_dz[0], &e->ev_dz[1], &e->ev_w1[0], &e->ev_w1[1], &e->ev_grp, &e->ev_side};
     for (hipEvent_t* ev : evs) HC(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   }
   *out = e;
@@ -751,16 +699,9 @@ int srmi_engine_create(const srmi_model_config* cfg, void* workspace, size_t ws_
 
 int srmi_engine_destroy(srmi_engine* e) {
   if (!e) return 0;
-  hipEvent_t evs[] = {e->ev_du[0], e->ev_du[1], e->ev_dz[0], e->ev_dz[1], e->ev_w2[0],
-                      e->ev_w2[1], e->ev_w1[0], e->ev_w1[1], e->ev_grp, e->ev_side};
+  hipEvent_t evs[] = {e->ev_dz[0], e->ev_dz[1], e->ev_w1[0], e->ev_w1[1], e->ev_grp, e->ev_side};
   for (hipEvent_t ev : evs)
     if (ev) (void)hipEventDestroy(ev);
-  if (e->ev_bin) (void)hipEventDestroy(e->ev_bin);
-  if (e->ev_bout) (void)hipEventDestroy(e->ev_bout);
-  if (e->bmain) {
-    (void)hipStreamSynchronize(e->bmain);
-    (void)hipStreamDestroy(e->bmain);
-  }
   if (e->side) {
     (void)hipStreamSynchronize(e->side);
     (void)hipStreamDestroy(e->side);
@@ -786,15 +727,7 @@ int srmi_backward(srmi_engine* e, const float* params, const float* lr, const fl
                   const float* loss4, const float* dy, float* grads, void** group_events, void* stream) {
   if (!e || !e->train || !params || !lr || !grads || e->last_n < 1) return SRMI_ERR_ARG;
   if (!dy && (!sr || !hr || !loss4)) return SRMI_ERR_ARG;
-  if (!e->bmain) return backward_impl(e, params, lr, sr, hr, loss4, dy, grads, group_events, S_(stream));
-  // partitioned backward: the dgrad chain runs on the CU-masked stream, joined to
-  // the caller's stream on both sides
-  HC(hipEventRecord(e->ev_bin, S_(stream)));
-  HC(hipStreamWaitEvent(e->bmain, e->ev_bin, 0));
-  RC(backward_impl(e, params, lr, sr, hr, loss4, dy, grads, group_events, e->bmain));
-  HC(hipEventRecord(e->ev_bout, e->bmain));
-  HC(hipStreamWaitEvent(S_(stream), e->ev_bout, 0));
-  return 0;
+  return backward_impl(e, params, lr, sr, hr, loss4, dy, grads, group_events, S_(stream));
 }
 
 int srmi_rmse_partial(srmi_engine* e, const float* pred, const float* target, size_t n, double count_global,
@@ -804,7 +737,33 @@ int srmi_rmse_partial(srmi_engine* e, const float* pred, const float* target, si
   return sqerr_finish_launch(e->lpart, e->lpart_n, count_global, loss4, S_(stream));
 }
 
-int srmi_rmse_finalize(float* loss4, void* stream) { return loss_finalize_launch(loss4, S_(stream)); }
+int srmi_rmse_finalize(float* loss4, void* stream) {
+  if (!loss4) return SRMI_ERR_ARG;
+  return loss_finalize_launch(loss4, LOSS_RMSE, S_(stream));
+}
+
+int srmi_charbonnier_partial(srmi_engine* e, const float* pred, const float* target, size_t n, double count_global,
+                             float eps, float* loss4, float* dy, void* stream) {
+  if (!e || !pred || !target || !loss4 || count_global <= 0) return SRMI_ERR_ARG;
+  RC(charb_partial_launch(pred, target, n, eps, count_global, dy, e->lpart, e->lpart_n, S_(stream)));
+  return sqerr_finish_launch(e->lpart, e->lpart_n, count_global, loss4, S_(stream));
+}
+
+int srmi_loss_finalize(float* loss4, int kind, void* stream) {
+  if (!loss4 || (kind != SRMI_LOSS_RMSE && kind != SRMI_LOSS_MEAN)) return SRMI_ERR_ARG;
+  return loss_finalize_launch(loss4, kind, S_(stream));
+}
+
+int srmi_batch_losses(const float* pred, const float* target, int ntiles, long long tile_elems, int batch_size,
+                      int kind, float eps, float* work, float* out, void* stream) {
+  if (!pred || !target || !work || !out || (kind != SRMI_LOSS_RMSE && kind != SRMI_LOSS_MEAN)) return SRMI_ERR_ARG;
+  return batch_losses_launch(pred, target, ntiles, tile_elems, batch_size, kind, eps, work, out, S_(stream));
+}
+
+int srmi_loss_combine(float* loss4, const float* parts4, int nparts, int kind, void* stream) {
+  if (!loss4 || !parts4 || nparts < 1 || kind < -1 || kind > SRMI_LOSS_MEAN) return SRMI_ERR_ARG;
+  return loss_combine_launch(loss4, parts4, nparts, kind, S_(stream));
+}
 
 int srmi_downsample(const float* hr, int N, int C, int H, int W, int scale, float* lr, void* stream) {
   return downsample_launch(hr, N, C, H, W, scale, lr, S_(stream));

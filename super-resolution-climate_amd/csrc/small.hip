@@ -182,48 +182,7 @@ int head_wgrad_reduce_launch(const float* slab, int nslab, int C, float* gw, flo
 
 // =========================================================================== tail
 // y[n][c][yy][xx] = b[c] + sum_{tap,ci} x[n][yy+ky-1][xx+kx-1][ci] * w[c][ci][tap]
-template <int TWT>
-__global__ void __launch_bounds__(4 * TWT) tail_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ w,
-                                                          const float* __restrict__ b, int C, int H, int W,
-                                                          float* __restrict__ y) {
-  extern __shared__ __attribute__((aligned(16))) char ts[];
-  constexpr int NT = 4 * TWT, WP = TWT + 2, HP = 6 * WP;
-  const int n = blockIdx.z, y0 = blockIdx.y * 4, x0 = blockIdx.x * TWT, tid = threadIdx.x;
-  for (int i = tid; i < HP * 8; i += NT) {
-    const int q = i >> 3, c = i & 7;
-    const int hy = q / WP, hx = q - hy * WP;
-    const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (yy >= 0 && yy < H && xx >= 0 && xx < W)
-      v = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + c * 8);
-    *reinterpret_cast<uint4*>(ts + swz128(q, c)) = v;
-  }
-  __syncthreads();
-  const int r = tid / TWT, px = tid - r * TWT;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int t = 0; t < 9; ++t) {
-    const int q = (r + t / 3) * WP + px + t % 3;
-#pragma unroll
-    for (int c8 = 0; c8 < 8; ++c8) {
-      const uint4 v = *reinterpret_cast<const uint4*>(ts + swz128(q, c8));
-      const float xv[8] = {bf2f(v.x & 0xFFFF), bf2f(v.x >> 16), bf2f(v.y & 0xFFFF), bf2f(v.y >> 16),
-                           bf2f(v.z & 0xFFFF), bf2f(v.z >> 16), bf2f(v.w & 0xFFFF), bf2f(v.w >> 16)};
-#pragma unroll
-      for (int co = 0; co < 4; ++co) {
-        if (co < C) {
-          const float* wp = w + ((size_t)co * 64 + c8 * 8) * 9 + t;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) acc[co] += xv[e] * wp[e * 9];
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int co = 0; co < 4; ++co)
-    if (co < C) y[(((size_t)n * C + co) * H + y0 + r) * W + x0 + px] = acc[co] + b[co];
-}
-
-// MFMA form of the same conv: implicit GEMM with A = filters (16 output-channel
+// As an MFMA implicit GEMM with A = filters (16 output-channel
 // rows, only the C < 16 real ones ever written or stored), B = halo pixels,
 // K = 9 taps x 64 ci, v_mfma_f32_16x16x32_bf16.  Workgroup = 4 output rows x TW
 // pixels (wave w = row w), halo and bf16 filters staged in LDS with the conv
@@ -285,17 +244,12 @@ __global__ void __launch_bounds__(256) tail_fwd_mfma_kernel(const bf16_t* __rest
 int tail_fwd_launch(const bf16_t* x, const float* w, const float* b, int N, int C, int H, int W, float* y,
                     hipStream_t st) {
   if (C < 1 || C > 4 || H % 4) return SRMI_ERR_SHAPE;
-  static const bool valu = getenv("SRMI_TAIL_VALU") && atoi(getenv("SRMI_TAIL_VALU"));
-  if (!valu && W % 48 == 0) {
+  if (W % 48 == 0) {
     hipLaunchKernelGGL(tail_fwd_mfma_kernel<48>, dim3(W / 48, H / 4, N), dim3(256), 6 * 50 * 128 + 9 * 2048, st, x,
                        w, b, C, H, W, y);
-  } else if (!valu && W % 32 == 0) {
+  } else if (W % 32 == 0) {
     hipLaunchKernelGGL(tail_fwd_mfma_kernel<32>, dim3(W / 32, H / 4, N), dim3(256), 6 * 34 * 128 + 9 * 2048, st, x,
                        w, b, C, H, W, y);
-  } else if (W % 64 == 0) {
-    hipLaunchKernelGGL(tail_fwd_kernel<64>, dim3(W / 64, H / 4, N), dim3(256), 6 * 66 * 128, st, x, w, b, C, H, W, y);
-  } else if (W % 32 == 0) {
-    hipLaunchKernelGGL(tail_fwd_kernel<32>, dim3(W / 32, H / 4, N), dim3(128), 6 * 34 * 128, st, x, w, b, C, H, W, y);
   } else {
     return SRMI_ERR_SHAPE;
   }
@@ -374,85 +328,8 @@ int tail_dgrad_launch(const float* y, const float* hr, const float* loss, const 
 
 // dW[c][ci][tap] = sum_p dy[c][p] * x[p+off][ci];  db[c] = sum_p dy[c][p]
 // dy = (y - hr) * loss[2] is formed on the fly (RMSE gradient, stats.py:5-8).
-// Lane = input channel ci; each wave walks whole rows keeping the 3x3 window of
-// x[.][ci] in registers (3 new coalesced 128-B loads per pixel).  dy for 64
-// consecutive pixels is loaded once per row segment with lane = pixel and
-// broadcast with readlane.  Workgroup = (band of kTailRows rows, image); the 4
-// waves' partials are summed in LDS -> slab [n][band][C][577].
 constexpr int kTailRows = 4;
-template <int CC>
-__global__ void __launch_bounds__(256) tail_wgrad_kernel(const float* __restrict__ yv, const float* __restrict__ hr,
-                                                        const float* __restrict__ loss, const bf16_t* __restrict__ x,
-                                                        int H, int W, float* __restrict__ slab) {
-  __shared__ float red[4][CC * 577];
-  const int n = blockIdx.y, band = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const float sc = loss ? loss[2] : 1.f;
-  float acc[9][CC], bacc[CC];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int c = 0; c < CC; ++c) acc[t][c] = 0.f;
-#pragma unroll
-  for (int c = 0; c < CC; ++c) bacc[c] = 0.f;
-  const bf16_t* xn = x + (size_t)n * H * W * 64 + lane;
-  auto xat = [&](int yy, int xx) -> float {
-    return (yy >= 0 && yy < H && xx >= 0 && xx < W) ? bf2f(xn[((size_t)yy * W + xx) * 64]) : 0.f;
-  };
-  for (int y = band * kTailRows + wave; y < (band + 1) * kTailRows; y += 4) {
-    float win[3][3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      win[r][0] = 0.f;
-      win[r][1] = xat(y - 1 + r, 0);
-    }
-    for (int x0 = 0; x0 < W; x0 += 64) {
-      float dv[CC];
-#pragma unroll
-      for (int c = 0; c < CC; ++c) {
-        const int xx = x0 + lane;
-        float v = 0.f;
-        if (xx < W) {
-          const size_t o = (((size_t)n * CC + c) * H + y) * W + xx;
-          v = hr ? (yv[o] - hr[o]) * sc : yv[o] * sc;
-        }
-        dv[c] = v;
-        bacc[c] += v;
-      }
-      const int nx = min(64, W - x0);
-
-      for (int j = 0; j < nx; ++j) {
-        const int xx = x0 + j;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) win[r][2] = xat(y - 1 + r, xx + 1);
-#pragma unroll
-        for (int c = 0; c < CC; ++c) {
-          const float dd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv[c]), j));
-#pragma unroll
-          for (int t = 0; t < 9; ++t) acc[t][c] += dd * win[t / 3][t % 3];
-        }
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          win[r][0] = win[r][1];
-          win[r][1] = win[r][2];
-        }
-      }
-    }
-  }
-  // bias: sum the per-lane pixel sums of each wave
-#pragma unroll
-  for (int c = 0; c < CC; ++c) bacc[c] = wave_sum(bacc[c]);
-#pragma unroll
-  for (int c = 0; c < CC; ++c) {
-#pragma unroll
-    for (int t = 0; t < 9; ++t) red[wave][c * 577 + lane * 9 + t] = acc[t][c];
-    if (lane == 0) red[wave][c * 577 + 576] = bacc[c];
-  }
-  __syncthreads();
-  float* out = slab + ((size_t)n * gridDim.x + band) * CC * 577;
-  for (int i = tid; i < CC * 577; i += 256) out[i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
-}
-
-// LDS-staged form: per 64-pixel segment the workgroup stages the 6 input rows its
+// Per 64-pixel segment the workgroup stages the 6 input rows its
 // 4 waves need (66 px x 64 ch bf16) and the RMSE gradient of its 4 rows; lane = ci
 // reads the x window from LDS (128 B per wave read, conflict-free) and the pixel's
 // dy by LDS broadcast -- no readlane, no 2-byte global loads per pixel.
@@ -535,21 +412,11 @@ int tail_wgrad_launch(const float* y, const float* hr, const float* loss, const 
                       int W, float* slab, int* nslab, hipStream_t st) {
   if (C < 1 || C > 4 || H % kTailRows) return SRMI_ERR_SHAPE;
   const dim3 grid(H / kTailRows, N);
-  static const bool valu = getenv("SRMI_TAIL_VALU") && atoi(getenv("SRMI_TAIL_VALU"));
-  if (valu) {
-    switch (C) {
-      case 1: hipLaunchKernelGGL(tail_wgrad_kernel<1>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
-      case 2: hipLaunchKernelGGL(tail_wgrad_kernel<2>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
-      case 3: hipLaunchKernelGGL(tail_wgrad_kernel<3>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
-      default: hipLaunchKernelGGL(tail_wgrad_kernel<4>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
-    }
-  } else {
-    switch (C) {
-      case 1: hipLaunchKernelGGL(tail_wgrad_lds_kernel<1>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
-      case 2: hipLaunchKernelGGL(tail_wgrad_lds_kernel<2>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
-      case 3: hipLaunchKernelGGL(tail_wgrad_lds_kernel<3>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
-      default: hipLaunchKernelGGL(tail_wgrad_lds_kernel<4>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
-    }
+  switch (C) {
+    case 1: hipLaunchKernelGGL(tail_wgrad_lds_kernel<1>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+    case 2: hipLaunchKernelGGL(tail_wgrad_lds_kernel<2>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+    case 3: hipLaunchKernelGGL(tail_wgrad_lds_kernel<3>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+    default: hipLaunchKernelGGL(tail_wgrad_lds_kernel<4>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
   }
   SRMI_CHECK_LAUNCH();
   *nslab = N * (H / kTailRows);
@@ -699,15 +566,122 @@ int sqerr_finish_launch(const float* partial, int nblk, double count, float* los
   return 0;
 }
 
-// loss[3] = L = sqrt(S / count), loss[2] = dL/dy scale = 1 / (count * L)
-__global__ void loss_finalize_kernel(float* loss) {
-  const float L = sqrtf(loss[0] / loss[1]);
-  loss[3] = L;
-  loss[2] = 1.f / (loss[1] * L);
+// Charbonnier loss of ModelTrainer.charbonnier (sres/controller/dual_trainer.py:196-198):
+// L = mean(sqrt(d^2 + eps)), d = y - t; partial sums like sqerr_partial_kernel and,
+// when dy != NULL, the elementwise gradient dL/dy = d / sqrt(d^2 + eps) / count.
+__global__ void __launch_bounds__(256) charb_partial_kernel(const float* __restrict__ y, const float* __restrict__ t,
+                                                            size_t n, float eps, float inv_count,
+                                                            float* __restrict__ dy, float* __restrict__ partial) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float d = y[i] - t[i];
+    const float r = sqrtf(d * d + eps);
+    s += r;
+    if (dy) dy[i] = d / r * inv_count;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-int loss_finalize_launch(float* loss, hipStream_t st) {
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1), 0, st, loss);
+int charb_partial_launch(const float* y, const float* t, size_t n, float eps, double count, float* dy,
+                         float* partial, int nblk, hipStream_t st) {
+  hipLaunchKernelGGL(charb_partial_kernel, dim3(nblk), dim3(256), 0, st, y, t, n, eps, (float)(1.0 / count), dy,
+                     partial);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// kind LOSS_RMSE: loss[3] = L = sqrt(S / count), loss[2] = dL/dy scale = 1 / (count * L);
+// kind LOSS_MEAN (Charbonnier): loss[3] = S / count, loss[2] = 1 / count
+__device__ __forceinline__ void loss_finalize_one(float* loss, int kind) {
+  if (kind == LOSS_MEAN) {
+    loss[3] = loss[0] / loss[1];
+    loss[2] = 1.f / loss[1];
+  } else {
+    const float L = sqrtf(loss[0] / loss[1]);
+    loss[3] = L;
+    loss[2] = 1.f / (loss[1] * L);
+  }
+}
+
+__global__ void loss_finalize_kernel(float* loss, int kind) { loss_finalize_one(loss, kind); }
+
+int loss_finalize_launch(float* loss, int kind, hipStream_t st) {
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1), 0, st, loss, kind);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// loss4 of a whole batch from the loss4 records of its micro-batches (parts[k][4]):
+// sums of S in a fixed order, the (global) count of part 0; finalised when kind >= 0
+__global__ void loss_combine_kernel(float* loss, const float* __restrict__ parts, int nparts, int kind) {
+  float s = 0.f;
+  for (int k = 0; k < nparts; ++k) s += parts[4 * k];
+  loss[0] = s;
+  loss[1] = parts[1];
+  if (kind >= 0) loss_finalize_one(loss, kind);
+}
+
+int loss_combine_launch(float* loss, const float* parts, int nparts, int kind, hipStream_t st) {
+  hipLaunchKernelGGL(loss_combine_kernel, dim3(1), dim3(1), 0, st, loss, parts, nparts, kind);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// Per-batch losses of ModelTrainer.process_image / evaluate (sres/controller/
+// dual_trainer.py:417-446, :509-532): the tiles are scored in batches of
+// task.batch_size (TileBatchIterator, sres/data/tiles.py:48-74; the last batch may
+// be short), each batch's loss is the loss over all its elements, and the
+// reported loss is the mean of the batch losses.  Pass 1: one block per tile sums
+// its elements' (p - t)^2 (RMSE) or sqrt((p - t)^2 + eps) (Charbonnier) in a fixed
+// order; pass 2 (one block) forms the batch losses and their mean in fp64.
+__global__ void __launch_bounds__(256) tile_loss_sums_kernel(const float* __restrict__ y,
+                                                             const float* __restrict__ t, long long tile_elems,
+                                                             int kind, float eps, float* __restrict__ sums) {
+  __shared__ float red[4];
+  const size_t base = (size_t)blockIdx.x * (size_t)tile_elems;
+  float s = 0.f;
+  for (long long i = threadIdx.x; i < tile_elems; i += 256) {
+    const float d = y[base + i] - t[base + i];
+    s += kind == LOSS_MEAN ? sqrtf(d * d + eps) : d * d;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) sums[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void __launch_bounds__(256) batch_loss_mean_kernel(const float* __restrict__ sums, int ntiles,
+                                                              long long tile_elems, int bs, int kind,
+                                                              float* __restrict__ out) {
+  __shared__ double bl[1024];
+  const int nb = (ntiles + bs - 1) / bs;
+  for (int b = threadIdx.x; b < nb; b += 256) {
+    const int t0 = b * bs, t1 = min(ntiles, t0 + bs);
+    double s = 0.0;
+    for (int k = t0; k < t1; ++k) s += sums[k];
+    const double mean = s / ((double)(t1 - t0) * (double)tile_elems);
+    const double l = kind == LOSS_MEAN ? mean : sqrt(mean);
+    bl[b] = l;
+    out[1 + b] = (float)l;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = 0.0;
+    for (int b = 0; b < nb; ++b) m += bl[b];
+    out[0] = (float)(m / nb);
+  }
+}
+
+int batch_losses_launch(const float* y, const float* t, int ntiles, long long tile_elems, int bs, int kind, float eps,
+                        float* work, float* out, hipStream_t st) {
+  if (ntiles < 1 || tile_elems < 1 || bs < 1 || (ntiles + bs - 1) / bs > 1024) return SRMI_ERR_SHAPE;
+  hipLaunchKernelGGL(tile_loss_sums_kernel, dim3(ntiles), dim3(256), 0, st, y, t, tile_elems, kind, eps, work);
+  SRMI_CHECK_LAUNCH();
+  hipLaunchKernelGGL(batch_loss_mean_kernel, dim3(1), dim3(256), 0, st, work, ntiles, tile_elems, bs, kind, out);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
@@ -964,15 +938,17 @@ int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float
 // the conv2 bias grad.  offs[k*5 + {0..4}] = grad offsets of
 // conv_du.0.weight, conv_du.0.bias, conv_du.2.weight, conv_du.2.bias, conv2.bias
 __global__ void __launch_bounds__(256) ca_param_grads_kernel(const float* __restrict__ recs,
-                                                             const float* __restrict__ brecs, int N, int C, int CR,
-                                                             const long long* __restrict__ offs,
+                                                             const float* __restrict__ brecs, int N, int Ncap, int C,
+                                                             int CR, const long long* __restrict__ offs,
                                                              float* __restrict__ grads) {
   // blockIdx.y < 2*C*CR/256: one weight gradient per thread; the last y slice
-  // does the biases.  Image sums run in a fixed order (deterministic).
+  // does the biases.  Image sums run in a fixed order (deterministic).  The
+  // records of consecutive RCABs are Ncap (the engine's capacity) images apart;
+  // the first N images are summed.
   const int k = blockIdx.x;
   const int rs = 2 * C + CR;
-  const float* rec = recs + (size_t)k * N * rs;
-  const float* brec = brecs + (size_t)k * N * (rs + C);  // [N][rs] then dm[N][C]
+  const float* rec = recs + (size_t)k * Ncap * rs;
+  const float* brec = brecs + (size_t)k * Ncap * (rs + C);  // [N][rs] then dm[N][C]
   const int nw = 2 * C * CR;
   const int o = blockIdx.y * 256 + threadIdx.x;
   if ((int)blockIdx.y * 256 < nw) {
@@ -1012,11 +988,13 @@ __global__ void __launch_bounds__(256) ca_param_grads_kernel(const float* __rest
   }
 }
 
-int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int C, int R,
+int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int Ncap, int C, int R,
                                   const long long* offs, float* grads, hipStream_t st) {
+  if (N < 1 || N > Ncap) return SRMI_ERR_ARG;
   const int CR = C / R;
   const int ny = (2 * C * CR + 255) / 256 + 1;
-  hipLaunchKernelGGL(ca_param_grads_kernel, dim3(nblocks, ny), dim3(256), 0, st, recs, brecs, N, C, CR, offs, grads);
+  hipLaunchKernelGGL(ca_param_grads_kernel, dim3(nblocks, ny), dim3(256), 0, st, recs, brecs, N, Ncap, C, CR, offs,
+                     grads);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

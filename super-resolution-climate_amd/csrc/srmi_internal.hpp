@@ -60,7 +60,6 @@ struct WgradParams {
   float* bslab;        // [nslab][Cout]
   const void* zeros;   // >= 16 zero bytes in global memory (DMA source for padding)
   unsigned long long* stamps;  // diagnostic (null in production)
-  int dbg;             // debug: bit0 skip MFMA, bit1 skip DMA, bit2 nt loads
 };
 void wgrad3x3_set_debug_stamps(unsigned long long* buf);
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st);
@@ -103,7 +102,13 @@ int upsample_launch(const float* lr, int N, int C, int h, int w, int scale, floa
 // loss[0] = sum (y-t)^2 (this rank), loss[1] = element count (global after all-reduce)
 int sqerr_partial_launch(const float* y, const float* t, size_t n, float* partial, int nblk, hipStream_t st);
 int sqerr_finish_launch(const float* partial, int nblk, double count, float* loss, hipStream_t st);
-int loss_finalize_launch(float* loss, hipStream_t st);
+enum LossKind { LOSS_RMSE = 0, LOSS_MEAN = 1 };
+int loss_finalize_launch(float* loss, int kind, hipStream_t st);
+int loss_combine_launch(float* loss, const float* parts, int nparts, int kind, hipStream_t st);
+int batch_losses_launch(const float* y, const float* t, int ntiles, long long tile_elems, int bs, int kind, float eps,
+                        float* work, float* out, hipStream_t st);
+int charb_partial_launch(const float* y, const float* t, size_t n, float eps, double count, float* dy,
+                         float* partial, int nblk, hipStream_t st);
 
 // channel attention
 int ca_fwd_launch(const bf16_t* u, const float* part, int nstrips, const float* w1, const float* b1,
@@ -111,9 +116,8 @@ int ca_fwd_launch(const bf16_t* u, const float* part, int nstrips, const float* 
                   bf16_t* hb_out, float* rec, hipStream_t st);
 int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
                      const float* w2, int N, int HW, int C, int R, bf16_t* du, float* brec, hipStream_t st);
-int ca_param_grads_launch(const float* rec, const float* brec, int nblocks, int N, int C, int R,
-                          float* const* gptrs, hipStream_t st);
-int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int C, int R,
+// records of consecutive RCABs Ncap images apart (the engine capacity), N summed
+int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int Ncap, int C, int R,
                                   const long long* offs, float* grads, hipStream_t st);
 
 int adam_launch(float* p, const float* g, float* m, float* v, size_t n, float lr, float b1, float b2, float eps,

@@ -80,7 +80,6 @@ __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
   // DMA group m (0 .. NGW-1) of this wave for stage st into buffer buf
   constexpr int NGW = (NG + 3) / 4;
   auto dma_group = [&](int st, int buf, int m) {
-    if (p.dbg & 2) return;
     const int xb = st / nrp, rp = st - xb * nrp;
     const int y0 = ybase + S::SR * rp, x0 = xb * TW;
     const uint32_t base = lds0 + buf * S::STAGE;
@@ -94,16 +93,14 @@ __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
         src = dyn + ((size_t)y * p.W + xx) * p.Cout + c * 8;
       else
         src = dyn + ((size_t)(2 * y + (cb >> 1)) * (2 * p.W) + 2 * xx + (cb & 1)) * 64 + c * 8;
-      if (p.dbg & 4) glds16_nt(src, base + (uint32_t)(r * TW + 8 * (k % GD)) * 128u);
-      else glds16(src, base + (uint32_t)(r * TW + 8 * (k % GD)) * 128u);
+      glds16(src, base + (uint32_t)(r * TW + 8 * (k % GD)) * 128u);
     } else if (k < NG) {
       const int kk = k - NDY, r = kk / GX, hx = 8 * (kk % GX) + dq;
       const int c = ls ^ fsw(r * S::XP + hx);
       const int y = y0 - 1 + r, xx = x0 - 1 + hx;
       const bool ok = hx < TW + 2 && y >= 0 && y < p.H && xx >= 0 && xx < p.W;
       const void* src = ok ? (const void*)(xn + ((size_t)y * p.W + xx) * 64 + c * 8) : (const void*)kZerosW;
-      if (p.dbg & 4) glds16_nt(src, base + (uint32_t)(S::DY_BYTES + (r * S::XP + 8 * (kk % GX)) * 128));
-      else glds16(src, base + (uint32_t)(S::DY_BYTES + (r * S::XP + 8 * (kk % GX)) * 128));
+      glds16(src, base + (uint32_t)(S::DY_BYTES + (r * S::XP + 8 * (kk % GX)) * 128));
     }
   };
   auto dma_stage = [&](int st, int buf) {
@@ -175,7 +172,6 @@ __global__ void __launch_bounds__(256, 1) wgrad3x3_kernel(WgradParams p) {
       }
       if (kb + 1 < S::KSTEPS) load_step(kb + 1, A[(kb + 1) & 1], B[(kb + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
-      if (p.dbg & 1) continue;
 #pragma unroll
       for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -235,14 +231,6 @@ constexpr int GD = TW / 8, GX = 7;                               // 8-px groups 
 constexpr int NGP = 2 * GD + 2 * GX;                             // groups per pair (26)
 }  // namespace v4
 
-#ifndef SRMI_WGRAD_ILV
-#define SRMI_WGRAD_ILV 1
-#endif
-// diagnostic builds only (garbage results): 1 = no MFMAs, 2 = no in-loop DMA,
-// 4 = no per-pair wait/barrier, 8 = no in-loop fragment reads
-#ifndef SRMI_WGRAD_EXP
-#define SRMI_WGRAD_EXP 0
-#endif
 
 // The body is instantiated once per wave (WV = wave index): the wave's DMA groups,
 // taps and tile rotation are compile-time constants (no SGPR pressure, no branches).
@@ -427,22 +415,17 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
 #pragma unroll
       for (int kc = 0; kc < 3; ++kc) {
         const int cur = (3 * q + kc) & 1, nxt = cur ^ 1;
-        if (!(SRMI_WGRAD_EXP & 2) && pf)
+        if (pf)
           dma_pair_part(j + PF, kc == 0 ? 0 : (kc == 1 ? 3 : 5), kc == 0 ? 3 : (kc == 1 ? 5 : 7));
         __builtin_amdgcn_sched_barrier(0);
-        const bool ld = !(SRMI_WGRAD_EXP & 8) && (kc < 2 || more);
-        if (!(SRMI_WGRAD_EXP & 8)) {
-          if (kc < 2) load_step(ra, rb, kc + 1, A[nxt], B[nxt]);
-          else if (more) load_step(ran, rbn, 0, A[nxt], B[nxt]);  // next pair's first K-step
-        }
-        if (!(SRMI_WGRAD_EXP & 1)) {
+        const bool ld = kc < 2 || more;
+        if (kc < 2) load_step(ra, rb, kc + 1, A[nxt], B[nxt]);
+        else if (more) load_step(ran, rbn, 0, A[nxt], B[nxt]);  // next pair's first K-step
 #pragma unroll
-          for (int t = 0; t < 9; ++t)
+        for (int t = 0; t < 9; ++t)
 #pragma unroll
-            for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(A[cur][ct], B[cur][t], acc[ct][t]);
-          bacc = mfma16(A[cur][0], ones, bacc);  // slot 0 = this wave's own co tile
-        }
-#if SRMI_WGRAD_ILV
+          for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(A[cur][ct], B[cur][t], acc[ct][t]);
+        bacc = mfma16(A[cur][0], ones, bacc);  // slot 0 = this wave's own co tile
         // the next K-step's 26 transposed reads issued behind the MFMAs, one per MFMA
         if (ld) {
 #pragma unroll
@@ -452,9 +435,8 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
           }
           __builtin_amdgcn_sched_group_barrier(0x008, 11, 0);
         }
-#endif
         __builtin_amdgcn_sched_barrier(0);
-        if (kc == 1 && !(SRMI_WGRAD_EXP & 4)) {
+        if (kc == 1) {
           // pair j+1 must have landed before K-step 2 reads its first fragments.  In
           // flight may stay: pair j+2 (whole) and the 5 groups of pair j+PF issued above.
           if (j + 2 < np) wait_groups(1, pf ? 5 : 0);
@@ -470,24 +452,18 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
     }
   }
 
-  if (SRMI_WGRAD_EXP & 4) wait_vm<0>();
   // partial slab in the MFMA-native order (slab layout 1): every store instruction
   // writes 1 KiB contiguous; wgrad_reduce_kernel maps it back to (co, ci, tap)
-#ifndef SRMI_WGRAD_SLAB_WT
-#define SRMI_WGRAD_SLAB_WT 0
-#endif
-  // (plain stores by default: written through, the wgrad launch was 0.9 us shorter
-  // but the reduce that re-reads the slabs right after it 1.9 us longer)
+  // (plain stores: written through, the wgrad launch was 0.9 us shorter but the
+  // reduce that re-reads the slabs right after it 1.9 us longer)
   const size_t soff = (size_t)chunk * Cout * 576 + (size_t)cb * (64 * 576) + (size_t)wave * (9 * 4 * 256);
-  [[maybe_unused]] const auto rs = wt_rsrc(p.slab, (uint32_t)((size_t)gridDim.x * Cout * 576 * 4));
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {
       const float4 v = make_float4(acc[ct][t][0], acc[ct][t][1], acc[ct][t][2], acc[ct][t][3]);
       const size_t o = soff + ((t * 4 + ct) * 64 + lane) * 4;
-      if (SRMI_WGRAD_SLAB_WT) st_wt16(rs, p.slab, (uint32_t)(o * 4), v);
-      else *reinterpret_cast<float4*>(p.slab + o) = v;
+      *reinterpret_cast<float4*>(p.slab + o) = v;
     }
   if ((lane & 15) == 0) {
 #pragma unroll
@@ -510,9 +486,8 @@ __global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
 int wgrad3x3_nslabs(const WgradParams& p) { return p.N * p.row_splits; }
 
 static bool use_wgrad48(const WgradParams& p) {
-  // v4 (row-pair rings, per-wave specialised) for W == 48; SRMI_WGRAD_V3=1 forces v3
-  static const bool use_v4 = !(getenv("SRMI_WGRAD_V3") && atoi(getenv("SRMI_WGRAD_V3")));
-  return use_v4 && p.W == 48 && p.row_splits > 0 && (p.H / p.row_splits) % 2 == 0;
+  // v4 (row-pair rings, per-wave specialised) for W == 48
+  return p.W == 48 && p.row_splits > 0 && (p.H / p.row_splits) % 2 == 0;
 }
 
 int wgrad3x3_slab_layout(const WgradParams& p) { return use_wgrad48(p) ? 1 : 0; }
@@ -523,8 +498,6 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
   dim3 grid(wgrad3x3_nslabs(p), p.Cout / 64);
   WgradParams q = p;
   q.stamps = g_wg_stamps;
-  static const int dbg = getenv("SRMI_WGRAD_DBG") ? atoi(getenv("SRMI_WGRAD_DBG")) : 0;
-  q.dbg = dbg;
   if (use_wgrad48(p)) {
     hipLaunchKernelGGL(wgrad48_kernel, grid, dim3(256), v4::LDS, st, q);
   } else if (p.W % 48 == 0) {

@@ -15,6 +15,8 @@ LIB_PATH = os.environ.get("SRMI_LIB") or os.path.join(_HERE, "libsrmi.so")  # SR
 
 SRMI_ARCH_RCAN = 0
 SRMI_ARCH_EDSR = 1
+SRMI_LOSS_RMSE = 0
+SRMI_LOSS_MEAN = 1
 
 ERRORS = {-10001: "SRMI_ERR_ARG", -10002: "SRMI_ERR_SHAPE", -10003: "SRMI_ERR_WORKSPACE",
           -10004: "SRMI_ERR_UNSUPPORTED"}
@@ -45,6 +47,10 @@ _SIGS = {
     "srmi_backward": ([P, P, P, P, P, P, P, P, C.POINTER(P), P], C.c_int),
     "srmi_rmse_partial": ([P, P, P, C.c_size_t, C.c_double, P, P], C.c_int),
     "srmi_rmse_finalize": ([P, P], C.c_int),
+    "srmi_charbonnier_partial": ([P, P, P, C.c_size_t, C.c_double, C.c_float, P, P, P], C.c_int),
+    "srmi_loss_finalize": ([P, C.c_int, P], C.c_int),
+    "srmi_loss_combine": ([P, P, C.c_int, C.c_int, P], C.c_int),
+    "srmi_batch_losses": ([P, P, C.c_int, C.c_longlong, C.c_int, C.c_int, C.c_float, P, P, P], C.c_int),
     "srmi_downsample": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),
     "srmi_upsample": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),
     "srmi_adam_step": ([P, P, P, P, C.c_size_t, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, P],

@@ -26,23 +26,35 @@ def model_state_dict(flat: torch.Tensor, table) -> Dict[str, torch.Tensor]:
     return {name: host[off:off + n].view(shape).clone() for name, off, n, shape in table}
 
 
-def load_model_state_dict(flat: torch.Tensor, table, sd: Dict[str, torch.Tensor], strict: bool = True) -> None:
-    """Copy a reference state dict into the flat buffer.  strict=False mirrors
-    FModule.load_state_dict (sres/model/common/common.py:50-71): keys under
-    'tail' whose shapes differ are skipped."""
+def load_model_state_dict(flat: torch.Tensor, table, sd: Dict[str, torch.Tensor], strict: bool = True,
+                          apply: bool = True) -> torch.Tensor:
+    """A reference state dict -> the flat layout, with FModule.load_state_dict's
+    semantics (sres/model/common/common.py:50-71): a key whose shape differs is
+    skipped if it is under 'tail' (a re-shaped upsampler) and raises otherwise;
+    with strict, unexpected keys not under 'tail' and missing keys raise.  Returns
+    the host buffer; apply copies it into `flat`."""
     host = flat.detach().cpu().clone()
+    names = {name for name, _, _, _ in table}
+    if strict:
+        extra = [k for k in sd if k not in names and "tail" not in k]
+        if extra:
+            raise KeyError(f'unexpected key "{extra[0]}" in state_dict')
+        missing = names - set(sd)
+        if missing:
+            raise KeyError(f'missing keys in state_dict: "{missing}"')
     for name, off, n, shape in table:
         if name not in sd:
-            if strict:
-                raise KeyError(f"missing key {name}")
             continue
         t = sd[name]
         if tuple(t.shape) != tuple(shape):
-            if not strict and name.startswith("tail"):
+            if "tail" in name:
                 continue
-            raise ValueError(f"{name}: shape {tuple(t.shape)} != {tuple(shape)}")
+            raise RuntimeError(f"While copying the parameter named {name}, whose dimensions in the model are "
+                               f"{tuple(shape)} and whose dimensions in the checkpoint are {tuple(t.shape)}.")
         host[off:off + n] = t.detach().float().reshape(-1)
-    flat.copy_(host)
+    if apply:
+        flat.copy_(host)
+    return host
 
 
 def adam_state_dict(table, m: torch.Tensor, v: torch.Tensor, step: int, lr: float, betas=(0.9, 0.999),
@@ -60,9 +72,11 @@ def adam_state_dict(table, m: torch.Tensor, v: torch.Tensor, step: int, lr: floa
     return {"state": state, "param_groups": [group]}
 
 
-def load_adam_state_dict(table, sd: Dict, m: torch.Tensor, v: torch.Tensor) -> Tuple[int, Dict]:
-    """Flat moments from a torch Adam state dict -> (step, param-group hyper-parameters).
-    All parameters must share one step count (one param group, as dual_trainer.py:126)."""
+def load_adam_state_dict(table, sd: Dict, m: torch.Tensor, v: torch.Tensor, apply: bool = True):
+    """Flat moments from a torch Adam state dict.  All parameters must share one step
+    count (one param group, as dual_trainer.py:126).  apply=True copies the moments
+    into m, v and returns (step, param-group hyper-parameters); apply=False leaves
+    them and returns (step, hyper-parameters, m_host, v_host)."""
     groups = sd["param_groups"]
     if len(groups) != 1 or len(groups[0]["params"]) != len(table):
         raise ValueError("expected one Adam param group over all model parameters")
@@ -75,14 +89,20 @@ def load_adam_state_dict(table, sd: Dict, m: torch.Tensor, v: torch.Tensor) -> T
             steps.add(0)
             continue
         steps.add(int(float(st["step"])))
-        mh[off:off + n] = st["exp_avg"].float().reshape(-1)
-        vh[off:off + n] = st["exp_avg_sq"].float().reshape(-1)
+        for key, dst in (("exp_avg", mh), ("exp_avg_sq", vh)):
+            x = st[key]
+            if x.numel() != n:
+                raise ValueError(f"{name}: Adam {key} has {x.numel()} elements, expected {n}")
+            dst[off:off + n] = x.float().reshape(-1)
     if len(steps) != 1:
         raise ValueError(f"parameters at different Adam steps: {sorted(steps)}")
+    g = groups[0]
+    hp = {k: g[k] for k in ("lr", "betas", "eps", "weight_decay")}
+    if not apply:
+        return steps.pop(), hp, mh, vh
     m.copy_(mh)
     v.copy_(vh)
-    g = groups[0]
-    return steps.pop(), {k: g[k] for k in ("lr", "betas", "eps", "weight_decay")}
+    return steps.pop(), hp
 
 
 def checkpoint(epoch: int, itime: int, flat, table, m, v, step, lr, betas, eps, wd, loss: float) -> Dict:

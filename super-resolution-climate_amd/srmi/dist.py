@@ -53,7 +53,7 @@ def init_from_env(backend: Optional[str] = None, force: bool = False) -> DistInf
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if not dist.is_initialized():
-        if backend == "nccl" and not os.environ.get("SRMI_DP_LAZY"):
+        if backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group(backend, rank=rank, world_size=world,
                                     device_id=torch.device("cuda", local))
@@ -86,11 +86,16 @@ def global_rmse_scale(local_sq_sum: torch.Tensor, count_global: float, info: Dis
 @dataclass
 class Bucket:
     ranges: List[Tuple[int, int]]   # (offset, numel) in the flat grad buffer
-    event_index: Optional[int]      # backward group event that finalises it (None = end of backward)
+    # index g of the backward group event that finalises it (None = end of backward):
+    # srmi_backward records group_events[g] once residual group g's gradients are
+    # final (include/srmi.h), walking g from nlayers-1 down to 0
+    event_index: Optional[int]
 
 
 def grad_buckets(table, arch: str, nlayers: int) -> List[Bucket]:
-    """Partition the flat gradient into buckets in backward-completion order."""
+    """Partition the flat gradient into buckets in backward-completion order: residual
+    group nlayers-1 (with the tail / upsampler / body-tail parameters, finalised
+    before it) first, group 0 last but one, the head last."""
     def ranges_where(pred):
         out = []
         for name, off, n, _ in table:
@@ -104,11 +109,11 @@ def grad_buckets(table, arch: str, nlayers: int) -> List[Bucket]:
     buckets: List[Bucket] = []
     tailish = lambda nm: nm.startswith("tail.") or nm.startswith(f"body.{nlayers}.")
     if arch == "rcan":
-        for k, g in enumerate(range(nlayers - 1, -1, -1)):
+        for g in range(nlayers - 1, -1, -1):
             rg = ranges_where(lambda nm, g=g: nm.startswith(f"body.{g}."))
-            if k == 0:
+            if g == nlayers - 1:
                 rg = ranges_where(tailish) + rg
-            buckets.append(Bucket(rg, k))
+            buckets.append(Bucket(rg, g))
         buckets.append(Bucket(ranges_where(lambda nm: nm.startswith("head.")), None))
     else:
         buckets.append(Bucket(ranges_where(lambda nm: not nm.startswith("head.")), None))

@@ -140,9 +140,25 @@ class Engine:
         call("srmi_rmse_partial", self._h, ptr(pred), ptr(target), pred.numel(), float(count_global), ptr(loss4),
              stream_handle(stream))
 
+    def charbonnier_partial(self, pred: torch.Tensor, target: torch.Tensor, loss4: torch.Tensor,
+                            count_global: float, eps: float = 1e-6, dy: Optional[torch.Tensor] = None, stream=None):
+        """ModelTrainer.charbonnier (dual_trainer.py:196-198) partial sums (+ dL/dpred into dy)."""
+        call("srmi_charbonnier_partial", self._h, ptr(pred), ptr(target), pred.numel(), float(count_global),
+             float(eps), ptr(loss4), ptr(dy), stream_handle(stream))
+
     @staticmethod
     def rmse_finalize(loss4: torch.Tensor, stream=None):
         call("srmi_rmse_finalize", ptr(loss4), stream_handle(stream))
+
+    @staticmethod
+    def loss_finalize(loss4: torch.Tensor, kind: int, stream=None):
+        call("srmi_loss_finalize", ptr(loss4), int(kind), stream_handle(stream))
+
+    @staticmethod
+    def loss_combine(loss4: torch.Tensor, parts: torch.Tensor, kind: int = -1, stream=None):
+        """loss4 <- sum of the micro-batch records parts[k][4] (finalised as `kind` if >= 0)."""
+        assert parts.is_contiguous() and parts.shape[-1] == 4
+        call("srmi_loss_combine", ptr(loss4), ptr(parts), parts.numel() // 4, int(kind), stream_handle(stream))
 
     def backward(self, params: torch.Tensor, lr: torch.Tensor, grads: torch.Tensor, sr=None, hr=None, loss4=None,
                  dy=None, events: Optional[Sequence] = None, stream=None):

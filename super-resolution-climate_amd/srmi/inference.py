@@ -1,13 +1,17 @@
-"""Tiled-region inference: drop-in for ModelTrainer.process_image + assemble_images.
+"""Tiled-region inference: drop-in for ModelTrainer.process_image + assemble_images
+and ModelTrainer.evaluate.
 
-Reference (sres/controller/dual_trainer.py:396-512, sres/base/source/swot/raw.py:169-233):
+Reference (sres/controller/dual_trainer.py:396-543, sres/base/source/swot/raw.py:169-233):
 a region [C, H, W] is cut floor-wise into a gy x gx grid of HR tiles (tile id =
 y * gx + x), tiles holding a non-finite value are dropped, every tile/channel is
 'lnorm'-normalised (mean/std over the tile, ddof 0), the LR input is the bicubic
 1/s of the tile (apply_network, :557-571), the model output and the bicubic
-interpolation baseline (upsample) are scored with RMSE against the tile, and each
-image type (input, target, interpolated, model) is de-normalised and mosaicked
-back into the grid (NaN where a tile was dropped).
+interpolation baseline (upsample) are scored against the tile in batches of
+task.batch_size tiles (TileBatchIterator, sres/data/tiles.py:48-74) with
+model.loss_fn ('l2' = RMSE, 'charbonnier'), the reported loss being the mean of
+the batch losses (:443-446), and each image type (input, target, interpolated,
+model) is de-normalised and mosaicked back into the grid (NaN where a tile was
+dropped).
 
 Every step runs in srmi's HIP kernels (region_to_tiles, downsample, the RCAN/EDSR
 inference engine, upsample, RMSE, tiles_to_region) on one stream; the whole
@@ -15,28 +19,34 @@ per-region sequence is captured once in a HIP graph (torch.cuda.CUDAGraph drives
 hipGraph capture of the ctypes launches on the capture stream) and replayed per
 region, so a region costs one graph launch.
 
-Differences from the reference, by design: losses are the RMSE over all kept
-tiles of the region (the reference averages per-batch RMSEs of task.batch_size
-tiles); for C > 1 channel c of tile t is region channel c at tile t (the
-reference's channel-major flattening packs neighbouring tiles of one variable into
-the channel axis, SURVEY.md §8f row 3 -- identical for the 1-variable C5 case).
+Difference from the reference, by design: for C > 1 channel c of tile t is region
+channel c at tile t (the reference's channel-major flattening packs neighbouring
+tiles of one variable into the channel axis, SURVEY.md §8f row 3 -- identical for
+the 1-variable C5 case).
 """
 from __future__ import annotations
 
-import os
-
-from typing import Dict, Optional, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from ._lib import call, ptr, stream_handle
+from ._lib import SRMI_LOSS_MEAN, SRMI_LOSS_RMSE, call, ptr, stream_handle
 from .engine import Engine, NetSpec, downsample, upsample
+
+LOSS_KINDS = {"l2": SRMI_LOSS_RMSE, "charbonnier": SRMI_LOSS_MEAN}
+CHARBONNIER_EPS = 1e-6  # dual_trainer.py:122
 
 
 class TiledInference:
     def __init__(self, spec: NetSpec, params: torch.Tensor, region_chw: Tuple[int, int, int],
                  tile_hr: Tuple[int, int] = (192, 192), device: Optional[torch.device] = None, graph: bool = True,
-                 micro: Optional[int] = None):
+                 micro: Optional[int] = None, batch_size: int = 36, loss_fn: str = "l2"):
+        """batch_size: task.batch_size (the tiles scored per batch; 36 in every
+        reference task yaml); loss_fn: model.loss_fn."""
+        if loss_fn not in LOSS_KINDS:
+            raise ValueError(f"Unknown single-product loss function {loss_fn}")
+        self.loss_kind = LOSS_KINDS[loss_fn]
+        self.batch_size = int(batch_size)
         self.spec = spec
         self.device = device or params.device
         C, H, W = region_chw
@@ -63,8 +73,11 @@ class TiledInference:
         self.lr = torch.empty((n, C, ty // s, tx // s), **f32)
         self.sr = torch.empty((n, C, ty, tx), **f32)
         self.interp = torch.empty((n, C, ty, tx), **f32)
-        self.loss_m = torch.zeros(4, **f32)
-        self.loss_i = torch.zeros(4, **f32)
+        nb = (n + self.batch_size - 1) // self.batch_size
+        self.loss_m = torch.zeros(1 + nb, **f32)   # [mean of batch losses, batch losses...]
+        self.loss_i = torch.zeros(1 + nb, **f32)
+        self.loss_work = torch.zeros(n, **f32)
+        self.n_kept = n
         hr_shape = (C, self.gy * ty, self.gx * tx)
         self.images = {
             "input": torch.empty((C, self.gy * ty // s, self.gx * tx // s), **f32),
@@ -76,7 +89,7 @@ class TiledInference:
         # sized for 1/micro of the chip (as srmi.trainer.FusedTrainer does): each
         # engine's launch ramps and tails overlap the other's work
         if micro is None:
-            micro = int(os.environ.get("SRMI_INFER_MICRO", "0")) or (2 if n >= 32 else 1)
+            micro = 2 if n >= 32 else 1
         self.micro = max(1, min(int(micro), n))
         per = (n + self.micro - 1) // self.micro
         self.split = [min(per, n - k * per) for k in range(self.micro)]
@@ -120,10 +133,10 @@ class TiledInference:
             ev.record(sk)
             main.wait_event(ev)
         upsample(lr, self.s, out=interp)
-        count = float(tiles.numel())
-        for pred, l4 in ((sr, self.loss_m), (interp, self.loss_i)):
-            self.eng.rmse_partial(pred, tiles, l4, count)
-            Engine.rmse_finalize(l4)
+        te = self.C * self.ty * self.tx
+        for pred, lo in ((sr, self.loss_m), (interp, self.loss_i)):
+            call("srmi_batch_losses", ptr(pred), ptr(tiles), nt, te, self.batch_size, self.loss_kind,
+                 CHARBONNIER_EPS, ptr(self.loss_work), ptr(lo), st)
         C, gy, gx, s = self.C, self.gy, self.gx, self.s
         for name, src, ty, tx in (("input", lr, self.ty // s, self.tx // s), ("target", tiles, self.ty, self.tx),
                                   ("interpolated", interp, self.ty, self.tx), ("model", sr, self.ty, self.tx)):
@@ -131,17 +144,21 @@ class TiledInference:
                  ptr(self.images[name]), st)
 
     def _all_tiles(self):
+        self._kept_tiles = self.tiles
         self._model_and_mosaic(self.tiles, self.lr, self.sr, self.interp, self.mean, self.std, None, self.n)
 
     # ------------------------------------------------------------------- API
     def process_region(self, region: torch.Tensor) -> Tuple[Dict[str, torch.Tensor], Dict[str, torch.Tensor]]:
-        """region [C, H, W] fp32 (device) -> (images, losses); images are device tensors
-        (input [C, gy*ty/s, gx*tx/s], target/interpolated/model [C, gy*ty, gx*tx]),
-        losses {'model', 'interpolated'} 1-element device tensors (RMSE)."""
+        """process_image (dual_trainer.py:396-447) on one region.  region [C, H, W]
+        fp32 (device) -> (images, losses); images are device tensors (input
+        [C, gy*ty/s, gx*tx/s], target/interpolated/model [C, gy*ty, gx*tx]), losses
+        {'model', 'interpolated'} 1-element device tensors = the mean of the batch
+        losses; batch_losses() gives the per-batch values."""
         if tuple(region.shape) != (self.C, self.H, self.W):
             raise ValueError(f"region shape {tuple(region.shape)} != {(self.C, self.H, self.W)}")
         self.region.copy_(region)
         self._tile()
+        self.n_kept = self.n
         if bool(self.bad.any()):  # rare: drop non-finite tiles (reference get_tiles mask)
             self._run_compacted()
         elif self._use_graph:
@@ -150,7 +167,51 @@ class TiledInference:
             self._graph.replay()
         else:
             self._all_tiles()
-        return self.images, {"model": self.loss_m[3:4], "interpolated": self.loss_i[3:4]}
+        return self.images, {"model": self.loss_m[0:1], "interpolated": self.loss_i[0:1]}
+
+    def batch_losses(self) -> Dict[str, torch.Tensor]:
+        """The per-batch losses of the last region (batch_model_losses /
+        batch_interp_losses of process_image, dual_trainer.py:428-430)."""
+        nb = (self.n_kept + self.batch_size - 1) // self.batch_size
+        return {"model": self.loss_m[1:1 + nb], "interpolated": self.loss_i[1:1 + nb]}
+
+    def set_params(self, params: torch.Tensor) -> None:
+        """Load new weights (e.g. the validation checkpoint, dual_trainer.py:402/491):
+        copied into the parameter buffer the engines (and the captured graph) read,
+        filter packs rebuilt."""
+        self.params.copy_(params)
+        for e in self.engs:
+            e.pack(self.params)
+
+    def evaluate(self, regions: Sequence[torch.Tensor]) -> Tuple[Dict[str, torch.Tensor], Dict[str, float]]:
+        """ModelTrainer.evaluate (dual_trainer.py:482-543) over the time slices of a
+        tset: every region is tiled, normalised and scored batch by batch; the loss
+        is the mean over ALL batches of all regions (:532, :541) and the results are
+        the normalised tiles of every batch concatenated along the tile axis
+        (merge_results / merge_results_tiles, :551-555, :38-42): input [n, C, ty/s,
+        tx/s], target / model / interpolated [n, C, ty, tx] (device tensors).  The
+        validation-checkpoint policy applied to the returned loss is
+        ValidationCheckpoint.update (srmi.harness)."""
+        bm: List[torch.Tensor] = []
+        bi: List[torch.Tensor] = []
+        merged: Dict[str, List[torch.Tensor]] = {k: [] for k in ("input", "target", "model", "interpolated")}
+        for region in regions:
+            self.process_region(region)
+            nt = self.n_kept
+            b = self.batch_losses()
+            bm.append(b["model"].clone())
+            bi.append(b["interpolated"].clone())
+            if nt:
+                merged["input"].append(self.lr[:nt].clone())
+                merged["target"].append(self._kept_tiles[:nt].clone())
+                merged["model"].append(self.sr[:nt].clone())
+                merged["interpolated"].append(self.interp[:nt].clone())
+        results = {k: torch.cat(v, 0) if v else torch.empty(0, device=self.device) for k, v in merged.items()}
+        m = torch.cat(bm).double().cpu()
+        i = torch.cat(bi).double().cpu()
+        losses = {"model": float(m.mean()) if m.numel() else float("nan"),
+                  "interpolated": float(i.mean()) if i.numel() else float("nan")}
+        return results, losses
 
     def replay(self):
         """Re-run the captured per-region graph on the current region buffer (bench)."""
@@ -174,6 +235,7 @@ class TiledInference:
     def _run_compacted(self):
         keep = torch.nonzero(self.bad == 0).flatten()
         nt = int(keep.numel())
+        self.n_kept = nt
         inv = torch.full((self.n,), -1, dtype=torch.int32, device=self.device)
         if nt == 0:
             for img in self.images.values():
@@ -183,6 +245,7 @@ class TiledInference:
             return
         inv[keep] = torch.arange(nt, dtype=torch.int32, device=self.device)
         tiles = self.tiles.index_select(0, keep).contiguous()
+        self._kept_tiles = tiles
         mean = self.mean.index_select(0, keep).contiguous()
         std = self.std.index_select(0, keep).contiguous()
         self._model_and_mosaic(tiles, self.lr[:nt], self.sr[:nt], self.interp[:nt], mean, std, inv, nt)

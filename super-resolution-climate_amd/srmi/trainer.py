@@ -3,9 +3,13 @@
 Restates one iteration of ModelTrainer.train (sres/controller/dual_trainer.py:310-323)
 with apply_network (:557-571) for the RCAN/EDSR plugins:
 
-    HR tile batch -> bicubic 1/s (array.py:72-76) -> network -> RMSE (stats.py:5-8)
-    [-> interp-baseline RMSE metric, dual_trainer.py:315-318]
+    HR tile batch -> bicubic 1/s (array.py:72-76) -> network -> loss
+    [-> interp-baseline loss metric, dual_trainer.py:315-318]
     -> backward -> Adam (lr = task.lr, weight_decay = task.weight_decay or 0)
+
+The loss is model.loss_fn (single_product_loss, dual_trainer.py:205-212): 'l2' =
+RMSE (l2loss, stats.py:5-8), 'charbonnier' = mean(sqrt(d^2 + 1e-6)) (:196-198);
+anything else raises, as the reference does.
 
 Everything runs asynchronously on one HIP stream: the per-step losses stay on
 the device (no .item() sync) until the caller asks for them.
@@ -15,14 +19,17 @@ gradients are all-reduced as described in srmi/dist.py.
 from __future__ import annotations
 
 import math
-import os
 from typing import Dict, Optional
 
 import torch
 
 from . import checkpoint as ckpt
+from ._lib import SRMI_LOSS_MEAN, SRMI_LOSS_RMSE
 from .dist import DistInfo, GradReducer, allreduce_sum_
 from .engine import Engine, NetSpec, adam_step, axpy, downsample, upsample
+
+LOSS_KINDS = {"l2": SRMI_LOSS_RMSE, "charbonnier": SRMI_LOSS_MEAN}
+CHARBONNIER_EPS = 1e-6  # ModelTrainer.eps, sres/controller/dual_trainer.py:122
 
 
 class _Null:
@@ -61,7 +68,11 @@ class FusedTrainer:
     def __init__(self, spec: NetSpec, batch: int, lr_hw=(48, 48), lr: float = 1e-4, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.0, interp_loss: bool = True,
                  info: Optional[DistInfo] = None, device: Optional[torch.device] = None, seed: int = 0,
-                 params: Optional[torch.Tensor] = None, micro: Optional[int] = None):
+                 params: Optional[torch.Tensor] = None, micro: Optional[int] = None, loss_fn: str = "l2"):
+        if loss_fn not in LOSS_KINDS:  # single_product_loss, dual_trainer.py:210-211
+            raise ValueError(f"Unknown single-product loss function {loss_fn}")
+        self.loss_fn = loss_fn
+        self.loss_kind = LOSS_KINDS[loss_fn]
         self.info = info or DistInfo()
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.spec = spec
@@ -71,13 +82,8 @@ class FusedTrainer:
         if batch % micro:
             raise ValueError(f"batch {batch} not divisible into {micro} micro-batches")
         self.micro = micro
-        # SRMI_DP_FLAT=1: gradients all-reduced once after backward instead of per
-        # residual group on the reducer stream overlapped with backward
-        self.dp_flat = int(os.environ.get("SRMI_DP_FLAT", "0"))  # 2/3: diagnostic, no grad (3: no) all-reduce
         self.mb = batch // micro
         budget = 256 // micro if micro > 1 else 0
-        if micro > 1 and os.environ.get("SRMI_MICRO_BUDGET"):  # diagnostic: CUs each engine's launches aim at
-            budget = int(os.environ["SRMI_MICRO_BUDGET"])
         self.engines = [Engine(spec, self.mb, lr_hw, train=True, device=self.device, cu_budget=budget)
                         for _ in range(micro)]
         self.eng = self.engines[0]
@@ -101,10 +107,12 @@ class FusedTrainer:
         self.lrbuf = torch.empty((batch, C, h, w), dtype=torch.float32, device=self.device)
         self.sr = torch.empty((batch, spec.nchannels_out, h * s, w * s), dtype=torch.float32, device=self.device)
         self.up = torch.empty_like(self.sr) if interp_loss else None
+        # Charbonnier: the elementwise loss gradient is the backward's upstream gradient
+        self.dy = torch.empty_like(self.sr) if self.loss_kind == SRMI_LOSS_MEAN else None
         self.loss4 = torch.zeros(4, dtype=torch.float32, device=self.device)
         self.iloss4 = torch.zeros(4, dtype=torch.float32, device=self.device)
-        self.mloss4 = [torch.zeros(4, dtype=torch.float32, device=self.device) for _ in range(micro)]
-        self.miloss4 = [torch.zeros(4, dtype=torch.float32, device=self.device) for _ in range(micro)]
+        self.mloss4 = torch.zeros((micro, 4), dtype=torch.float32, device=self.device)   # per micro-batch
+        self.miloss4 = torch.zeros((micro, 4), dtype=torch.float32, device=self.device)
         self.streams = [None] + [torch.cuda.Stream(device=self.device) for _ in range(micro - 1)]
         self.reducer = GradReducer(self.eng.table, spec.arch, spec.nlayers, self.info, self.device)
         # group events of engines 1.. (engine 0 records into reducer.events)
@@ -116,64 +124,85 @@ class FusedTrainer:
         st = self.streams[k]
         return torch.cuda.stream(st) if st is not None else _Null()
 
+    def _loss_partial(self, eng: Engine, pred, target, loss4, count, dy=None):
+        if self.loss_kind == SRMI_LOSS_MEAN:
+            eng.charbonnier_partial(pred, target, loss4, count, CHARBONNIER_EPS, dy=dy)
+        else:
+            eng.rmse_partial(pred, target, loss4, count)
+
+    def _reduce_loss(self, loss4, parts):
+        """loss4 of the whole (global) batch: micro-batch partials summed, all-reduced
+        over ranks, finalised -- one launch without data parallelism."""
+        if self.info.enabled:
+            Engine.loss_combine(loss4, parts, -1)
+            allreduce_sum_(loss4[0:1], self.info)
+            Engine.loss_finalize(loss4, self.loss_kind)
+        else:
+            Engine.loss_combine(loss4, parts, self.loss_kind)
+
     def step(self, hr: torch.Tensor) -> Dict[str, torch.Tensor]:
-        """hr: this rank's HR tiles [b, C, H, W] fp32 on the device (already normalised)."""
+        """hr: this rank's HR tiles [b, C, H, W] fp32 on the device (already normalised),
+        b <= the trainer's batch (a short last batch of a time slice, as the
+        reference's TileBatchIterator yields, sres/data/tiles.py:55-72)."""
         b = hr.shape[0]
-        if b != self.batch:
-            raise ValueError(f"batch {b} != trainer batch {self.batch}")
-        s, mb = self.spec.scale, self.mb
+        if b < 1 or b > self.batch:
+            raise ValueError(f"batch {b} outside 1..{self.batch}")
+        s = self.spec.scale
+        mb = (b + self.micro - 1) // self.micro
+        sls = [slice(min(b, k * mb), min(b, (k + 1) * mb)) for k in range(self.micro)]
         main = torch.cuda.current_stream(self.device)
         count = float(hr.numel()) * self.info.world
         for st in self.streams[1:]:
             st.wait_stream(main)
-        # forward + squared-error partials per micro-batch
+        # forward + loss partials per micro-batch (an empty micro-batch adds nothing)
         for k, eng in enumerate(self.engines):
-            sl = slice(k * mb, (k + 1) * mb)
+            sl = sls[k]
+            if sl.stop == sl.start:
+                self.mloss4[k].zero_()
+                self.miloss4[k].zero_()
+                continue
             with self._ctx(k):
                 downsample(hr[sl], s, out=self.lrbuf[sl])
                 eng.forward(self.params, self.lrbuf[sl], out=self.sr[sl])
-                eng.rmse_partial(self.sr[sl], hr[sl], self.mloss4[k], count)
-                if self.interp_loss:
+                self._loss_partial(eng, self.sr[sl], hr[sl], self.mloss4[k], count,
+                                   None if self.dy is None else self.dy[sl])
+                if self.interp_loss:  # self.loss(btarget, binterp), dual_trainer.py:316-317
                     up = upsample(self.lrbuf[sl], s, out=self.up[sl])
-                    eng.rmse_partial(hr[sl], up, self.miloss4[k], count)
+                    self._loss_partial(eng, hr[sl], up, self.miloss4[k], count)
         for st in self.streams[1:]:
             main.wait_stream(st)
-        self._combine(self.loss4, self.mloss4)
-        if self.dp_flat != 3:
-            allreduce_sum_(self.loss4[0:1], self.info)
-        Engine.rmse_finalize(self.loss4)
+        self._reduce_loss(self.loss4, self.mloss4)
         if self.interp_loss:
-            self._combine(self.iloss4, self.miloss4)
-            if self.dp_flat != 3:
-                allreduce_sum_(self.iloss4[0:1], self.info)
-            Engine.rmse_finalize(self.iloss4)
+            self._reduce_loss(self.iloss4, self.miloss4)
         for st in self.streams[1:]:
             st.wait_stream(main)
         # backward per micro-batch with the global loss scale.  Data parallel: every
         # engine records its residual-group events; the reducer adds the engines'
         # gradients bucket by bucket on its stream and all-reduces each bucket as
         # soon as all engines are past it (overlapped with the rest of backward).
-        dp = self.info.enabled and self.reducer.cuda and not self.dp_flat
+        dp = self.info.enabled and self.reducer.cuda
         evs = [self.reducer.events] + self.xevents if dp else [None] * self.micro
         for k, eng in enumerate(self.engines):
-            sl = slice(k * mb, (k + 1) * mb)
+            sl = sls[k]
             with self._ctx(k):
-                eng.backward(self.params, self.lrbuf[sl], self.mgrads[k], sr=self.sr[sl], hr=hr[sl],
-                             loss4=self.loss4, events=evs[k])
+                if sl.stop == sl.start:  # no tiles: zero gradient (and its group events)
+                    self.mgrads[k].zero_()
+                    if evs[k] is not None:
+                        for ev in evs[k]:
+                            ev.record()
+                    continue
+                if self.dy is not None:
+                    eng.backward(self.params, self.lrbuf[sl], self.mgrads[k], dy=self.dy[sl], events=evs[k])
+                else:
+                    eng.backward(self.params, self.lrbuf[sl], self.mgrads[k], sr=self.sr[sl], hr=hr[sl],
+                                 loss4=self.loss4, events=evs[k])
         for st in self.streams[1:]:
             main.wait_stream(st)
         if dp:
             self.reducer.reduce(self.grads, events_recorded=True, extra=self.mgrads[1:], extra_events=self.xevents)
-        elif self.dp_flat and self.info.enabled:
-            # one flat SUM all-reduce after backward (no reducer stream, no group events)
-            for g in self.mgrads[1:]:
-                axpy(self.grads, g, 1.0)
-            if self.dp_flat == 1:
-                allreduce_sum_(self.grads, self.info)
         else:
             for g in self.mgrads[1:]:
                 axpy(self.grads, g, 1.0)  # exact gradient of the whole batch
-            self.reducer.reduce(self.grads, events_recorded=False)
         self.t += 1
         adam_step(self.params, self.grads, self.m, self.v, self.t, self.lr, self.betas, self.eps, self.wd)
         for k, eng in enumerate(self.engines):
@@ -184,16 +213,6 @@ class FusedTrainer:
         for st in self.streams[1:]:
             main.wait_stream(st)
         return {"loss": self.loss4[3:4], "interp_loss": self.iloss4[3:4]}
-
-    @staticmethod
-    def _combine(dst, parts):
-        """loss4 of the whole batch from the micro-batches' partials (sum of squares, count)."""
-        if len(parts) == 1:
-            dst.copy_(parts[0])
-            return
-        dst.copy_(parts[0])
-        for q in parts[1:]:
-            dst[0:1].add_(q[0:1])
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
         """Reference-format model state_dict (CPU copies)."""
@@ -208,12 +227,22 @@ class FusedTrainer:
     def load_checkpoint(self, state: Dict) -> None:
         """Resume from a reference-format checkpoint dict (checkpoints.py:35-51,
         update_model=True): weights, Adam moments, step count and hyper-parameters;
-        the bf16 filter packs are rebuilt."""
-        ckpt.load_model_state_dict(self.params, self.eng.table, state["model_state_dict"], strict=False)
-        self.t, hp = ckpt.load_adam_state_dict(self.eng.table, state["optimizer_state_dict"], self.m, self.v)
+        the bf16 filter packs are rebuilt.  The model dict is loaded with FModule's
+        strict semantics (common.py:50-71: unexpected or missing keys raise, only a
+        re-shaped 'tail' is skipped).  Both dicts are validated into host buffers
+        before anything on the device changes, so a failed load leaves the trainer
+        as it was."""
+        host_p = ckpt.load_model_state_dict(self.params, self.eng.table, state["model_state_dict"], strict=True,
+                                            apply=False)
+        t, hp, mh, vh = ckpt.load_adam_state_dict(self.eng.table, state["optimizer_state_dict"], self.m, self.v,
+                                                  apply=False)
+        self.params.copy_(host_p)
+        self.m.copy_(mh)
+        self.v.copy_(vh)
+        self.t = t
         self.lr, self.betas, self.eps, self.wd = hp["lr"], tuple(hp["betas"]), hp["eps"], hp["weight_decay"]
         if self.info.enabled:
-            for t in (self.params, self.m, self.v):
-                torch.distributed.broadcast(t, 0)
+            for x in (self.params, self.m, self.v):
+                torch.distributed.broadcast(x, 0)
         for e in self.engines:
             e.pack(self.params)

@@ -102,3 +102,54 @@ def test_group_events_exist_before_backward():
         assert len(evs) == spec.nlayers and all(ev.cuda_event for ev in evs)
     with pytest.raises(RuntimeError, match="group event"):
         Engine.backward(None, None, None, None, events=[torch.cuda.Event()])
+
+
+def _force_dp_rccl_worker(port, q):
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "super-resolution-climate_amd"), ROOT]
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from oracle import rcan_oracle as ro
+    from srmi.dist import init_from_env
+    from srmi.engine import param_table
+    from srmi.trainer import FusedTrainer, default_init_
+    info = init_from_env("nccl", force=True)
+    assert info.enabled and dist.get_backend() == "nccl"
+    d = torch.device("cuda", 0)
+    spec = _spec()
+    table = param_table(spec)
+    flat = torch.empty(sum(t[2] for t in table), device=d)
+    default_init_(flat, table, seed=6)
+    hr = torch.tensor(ro.synthetic_hr(16, 2, 192, 23)).to(d)
+    dp = FusedTrainer(spec, 16, (48, 48), device=d, params=flat, micro=2, info=info)
+    ref = FusedTrainer(spec, 16, (48, 48), device=d, params=flat, micro=2)
+    out = []
+    for _ in range(2):
+        a, b = dp.step(hr), ref.step(hr)
+        torch.cuda.synchronize()
+        out.append((float(a["loss"]), float(b["loss"]), torch.equal(dp.grads, ref.grads),
+                    float((dp.grads - ref.grads).abs().max())))
+    q.put((out, torch.equal(dp.params, ref.params)))
+    dist.destroy_process_group()
+
+
+def test_force_dp_rccl_bucketed_allreduce_waits_for_backward():
+    """The DP path over a real RCCL communicator (backend "nccl", one rank): every
+    bucket's micro-batch gradient sum and all-reduce run on the reducer stream
+    behind the engines' group events.  At one rank the SUM all-reduce is the
+    identity, so the gradients must equal the non-DP step's bit for bit -- a
+    bucket that did not wait for its backward group would read unfinished
+    gradients and differ."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_force_dp_rccl_worker, args=(33000 + random.randint(0, 2000), q))
+    p.start()
+    out, params_equal = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    for l_dp, l_ref, g_equal, gmax in out:
+        assert l_dp == l_ref and g_equal, (l_dp, l_ref, gmax)
+    assert params_equal

@@ -122,9 +122,16 @@ def test_grad_buckets_partition_every_parameter_once():
         assert np.all(mask == 1)
         r = GradReducer(tab, spec.arch, spec.nlayers, DistInfo(), torch.device("cpu"))
         assert r.covered() == n
-    # rcan: one bucket per residual group in backward order, head last
-    b = grad_buckets(param_table(NetSpec(arch="rcan", nlayers=3, nblocks=2)), "rcan", 3)
-    assert [x.event_index for x in b] == [0, 1, 2, None]
+    # rcan: one bucket per residual group in backward order, head last; the bucket of
+    # body.{g} waits on group event g, which srmi_backward records after group g
+    tab = param_table(NetSpec(arch="rcan", nlayers=3, nblocks=2))
+    b = grad_buckets(tab, "rcan", 3)
+    assert [x.event_index for x in b] == [2, 1, 0, None]
+    names = {off: nm for nm, off, _, _ in tab}
+    for bk in b[:-1]:
+        groups = {int(names[off].split(".")[1]) for off, _ in bk.ranges
+                  if names[off].startswith("body.") and names[off].split(".")[2] == "body"}
+        assert groups == {bk.event_index}
 
 
 def _dp_rank(rank, world, port, q, micro=1):
