@@ -35,6 +35,7 @@ import torch  # noqa: E402
 
 METRIC = "training tiles/sec (48→192, bf16) at 1/2/4/8 MI355X; inference MPix/sec"
 PEAK_BF16_TFLOPS = 2516.6          # 256 CU x 2.4 GHz x 4096 FLOP/clk (MI355X_MICROARCH.md, dense)
+PEAK_FP32_TFLOPS = 157.3           # f32-input MFMA = the f32 vector rate (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 TRAIN_GFLOP_PER_TILE_C2 = 219.9    # 6 x conv MACs per tile
 EDSR_TRAIN_GFLOP_PER_TILE = 27.4   # C4 EDSR x8 4-var, 6 x 4.57 G MAC
@@ -117,14 +118,14 @@ def rooflines(dev, batch):
     fp = torch.empty(64 * 64 * 9, dtype=torch.bfloat16, device=dev)
     dp = torch.empty_like(fp)
     pb = torch.empty(64, device=dev)
-    call("srmi_pack_conv", ptr(w), ptr(b), 64, 64, 0, ptr(fp), ptr(dp), ptr(pb), st.cuda_stream)
+    call("srmi_pack_conv", ptr(w), ptr(b), 64, 64, 0, ptr(fp), ptr(dp), ptr(pb), 0, st.cuda_stream)
     y = torch.empty_like(x)
     flop = CONV64_FLOP_PER_TILE * N
     act = N * H * W * 64 * 2  # one bf16 activation tensor
 
     # dominant: filter gradient (partial slabs; the deterministic slab reduction is a separate launch)
     ms_w = _time_launches(lambda: call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, 0, ptr(slab),
-                                       slab.numel() * 4, 0, 1.0, None, None, st.cuda_stream), st)
+                                       slab.numel() * 4, 0, 1.0, None, None, 0, st.cuda_stream), st)
     bytes_w = 2 * act + 64 * 577 * 4          # x + dY read once, dW + db written once
     t_hbm, t_mfma = bytes_w / (HBM_PEAK_GBS * 1e9), flop / (PEAK_BF16_TFLOPS * 1e12)
     tr = _pmc_traffic("wgrad48_kernel")
@@ -137,7 +138,7 @@ def rooflines(dev, batch):
            "traffic_source": tr["source"] if tr else None}
     # secondary: forward conv, fused bias + ReLU epilogue
     ms_c = _time_launches(lambda: call("srmi_conv3x3", ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, 0, ptr(y), None,
-                                       None, None, None, None, None, 1.0, st.cuda_stream), st)
+                                       None, None, None, None, None, 1.0, 0, st.cuda_stream), st)
     trc = _pmc_traffic("conv64_kernel<48, 0")
     ach_c = flop / (ms_c * 1e-3) / 1e12
     conv = {"bound": "mfma", "achieved": round(ach_c, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
@@ -185,12 +186,13 @@ def inference_bench(dev, side, iters):
 
 def edsr_bench(dev, batch, steps, warmup):
     """BASELINE config 4: EDSR-style x8 (16 ResBlocks, 64 features, 3 x [conv 64->256 +
-    PixelShuffle 2]), 4-variable tiles 32x32 -> 256x256, full train step (down8, fwd,
-    RMSE + interp RMSE, bwd, Adam) on this GPU.  Operands bf16 / fp32 accumulate
-    (BASELINE names fp32; the engine's one compute type is stated in `dtype`)."""
+    PixelShuffle 2]), 4-variable tiles 32x32 -> 256x256, fp32 as BASELINE names it:
+    the engine's exact-fp32 mode (v_mfma_f32_16x16x4_f32, fp32 activations, packs and
+    gradients).  Full train step (down8, fwd, RMSE + interp RMSE, bwd, Adam) on this
+    GPU; the step's MFMA fraction is against the fp32 matrix peak (157.3 TF)."""
     from srmi.engine import NetSpec
     from srmi.trainer import FusedTrainer
-    spec = NetSpec(arch="edsr", nchannels_in=4, nchannels_out=4, nfeatures=64, nlayers=16, scale=8)
+    spec = NetSpec(arch="edsr", nchannels_in=4, nchannels_out=4, nfeatures=64, nlayers=16, scale=8, dtype="fp32")
     tr = FusedTrainer(spec, batch, (32, 32), lr=1e-4, device=dev, seed=0)
     hr = torch.tensor(synthetic_hr(batch, 4, 256, 4321)).to(dev)
     for _ in range(warmup):
@@ -202,11 +204,14 @@ def edsr_bench(dev, batch, steps, warmup):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     v = batch * steps / dt
-    return {"metric": "EDSR x8 training tiles/sec (32->256, 4-var)", "value": round(v, 2), "unit": "tiles/s",
-            "ms_per_step": round(1000 * dt / steps, 3), "steps": steps, "warmup": warmup, "dtype": "bf16",
-            "data": "synthetic", "model_tflops": round(v * EDSR_TRAIN_GFLOP_PER_TILE / 1000.0, 1),
+    tf = v * EDSR_TRAIN_GFLOP_PER_TILE / 1000.0
+    return {"metric": "EDSR x8 training tiles/sec (32->256, 4-var, fp32)", "value": round(v, 2), "unit": "tiles/s",
+            "ms_per_step": round(1000 * dt / steps, 3), "steps": steps, "warmup": warmup, "dtype": "f32",
+            "data": "synthetic", "model_tflops": round(tf, 1),
+            "roofline_step": {"bound": "mfma", "achieved": round(tf, 1), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                              "frac": round(tf / PEAK_FP32_TFLOPS, 4)},
             "config": {"workload": "edsr-16-64 x8 train step (down8 + fwd + RMSE + interp RMSE + bwd + Adam), "
-                                   "4-var 32x32->256x256 tiles", "batch": batch}}
+                                   "4-var 32x32->256x256 tiles, exact fp32", "batch": batch}}
 
 
 def _log(msg):
@@ -327,7 +332,7 @@ def main():
         _log("rooflines done")
         edsr = None
         if not args.no_edsr and world == 1:
-            edsr = edsr_bench(dev, args.edsr_batch, 5, 2)
+            edsr = edsr_bench(dev, args.edsr_batch, 6, 2)
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
             _log("edsr done")

@@ -3,8 +3,10 @@
  *
  * C ABI: plain pointers, sizes and a hipStream_t (passed as void*).  No torch
  * types.  All device memory is owned by the caller (PyTorch's caching
- * allocator on the Python side); the library allocates nothing persistent
- * except what the caller hands it as workspace.  Every entry point returns 0
+ * allocator on the Python side) and handed in as workspace; the library's own
+ * allocations are host-side: the srmi_engine object (plan, layout, tables) and,
+ * for RCAN training engines, one side stream and six events, all created by
+ * srmi_engine_create and released by srmi_engine_destroy.  Every entry point returns 0
  * on success or a negative status (SRMI_ERR_*, or -hipError_t), which the
  * Python binding raises as RuntimeError (the reference raises Python
  * exceptions; sres/controller/dual_trainer.py:557 @exception_handled).
@@ -49,6 +51,17 @@ extern "C" {
 #define SRMI_ARCH_RCAN 0
 #define SRMI_ARCH_EDSR 1
 
+/* operand type of the engine (srmi_model_config.dtype, and the op-level entry
+ * points' dtype argument):
+ *   SRMI_DTYPE_BF16: activations / gradient maps / filter packs in bf16, fp32
+ *     accumulation (v_mfma_f32_16x16x32_bf16), fp32 residual stream and master
+ *     weights -- BASELINE configs 2, 3, 5;
+ *   SRMI_DTYPE_F32: everything fp32, exact f32 MFMA (v_mfma_f32_16x16x4_f32) --
+ *     the reference's own arithmetic (array2tensor fp32, sres/base/util/array.py:70;
+ *     nn.Conv2d fp32, sres/model/common/cnn.py:8-9), BASELINE config 4. */
+#define SRMI_DTYPE_BF16 0
+#define SRMI_DTYPE_F32 1
+
 typedef struct srmi_model_config {
   int arch;          /* SRMI_ARCH_RCAN | SRMI_ARCH_EDSR                     */
   int nchannels_in;  /* len(task.input_variables)   (1..4)                  */
@@ -63,6 +76,7 @@ typedef struct srmi_model_config {
   int lr_h, lr_w;    /* LR tile size, e.g. 48 x 48                          */
   int cu_budget;     /* CUs one launch should fill (0 = the whole GPU); two
                         engines on two streams each take half the chip     */
+  int dtype;         /* SRMI_DTYPE_BF16 | SRMI_DTYPE_F32                    */
 } srmi_model_config;
 
 typedef struct srmi_param_info {
@@ -86,7 +100,7 @@ int srmi_engine_create(const srmi_model_config* cfg, void* workspace, size_t ws_
                        srmi_engine** out);
 int srmi_engine_destroy(srmi_engine* e);
 
-/* fp32 master weights -> bf16 MFMA filter packs (call after every update) */
+/* fp32 master weights -> MFMA filter packs of the engine's dtype (call after every update) */
 int srmi_pack_weights(srmi_engine* e, const float* params, void* stream);
 
 /* lr: NCHW fp32 [n][Cin][lr_h][lr_w] -> sr: NCHW fp32 [n][Cout][lr_h*s][lr_w*s] */
@@ -143,39 +157,41 @@ int srmi_adam_step(float* p, const float* g, float* m, float* v, size_t n, int s
 int srmi_axpy(float* y, const float* x, float a, size_t n, void* stream);
 
 /* ---- op-level entry points (kernel parity tests, custom graphs) ---------- */
-/* forward conv: x NHWC bf16 [N][H][W][Cin], packed filters (srmi_pack_conv),
- * epi: 0 relu->bf16, 1 bf16+channel sums (part[N][strips][64]), 2 alpha*(y+b)+r1
- * -> yf fp32 (opt) + yb bf16, 3 PixelShuffle(2) bf16, 6 plain bf16           */
+/* dtype: SRMI_DTYPE_BF16 (x / yb / aux / packs bf16) or SRMI_DTYPE_F32 (fp32) */
+/* forward conv: x NHWC [N][H][W][Cin], packed filters (srmi_pack_conv),
+ * epi: 0 relu, 1 + channel sums (part[N][strips][64]), 2 alpha*(y+b)+r1
+ * -> yf fp32 (opt) + yb, 3 PixelShuffle(2), 4 dgrad * (aux > 0), 5 dgrad + r1 + r2
+ * + r3 -> yf (+ sums of g, g*aux), 6 plain (+ bias)                           */
 int srmi_conv3x3(const void* x, const void* wpack, const float* bias, int N, int H, int W, int Cin, int Cout,
                  int in_unshuffle, int epi, void* yb, float* yf, const float* r1, const float* r2, const float* r3,
-                 const void* aux, float* part, float alpha, void* stream);
+                 const void* aux, float* part, float alpha, int dtype, void* stream);
 int srmi_conv3x3_nstrips(int H, int W);
 /* diagnostic: record s_memtime phase stamps of the Cin=64 conv kernel into buf
  * (64 x u64 per workgroup); NULL turns it off */
 int srmi_debug_conv_stamps(void* buf);
 int srmi_debug_wgrad_stamps(void* buf);
-/* fp32 torch filter [Cout][Cin][3][3] -> bf16 packs: fwd [Cin/64][9][Cout][64],
+/* fp32 torch filter [Cout][Cin][3][3] -> packs of dtype: fwd [Cin/64][9][Cout][64],
  * dgrad [Cout/64][9][Cin][64] (flipped), bias [Cout]; ps != 0 permutes the
  * PixelShuffle channel order (packed c'' = 64q + c <- torch 4c + q)         */
 int srmi_pack_conv(const float* w, const float* b, int Cout, int Cin, int ps, void* fpack, void* dpack, float* pbias,
-                   void* stream);
+                   int dtype, void* stream);
 /* filter + bias gradient of a 3x3 conv (nn.Conv2d backward, weight half):
- * x NHWC bf16 [N][H][W][64], dy NHWC bf16 [N][H][W][Cout] (or, dy_unshuffle,
+ * x NHWC [N][H][W][64], dy NHWC [N][H][W][Cout] (or, dy_unshuffle,
  * the PixelShuffle output [N][2H][2W][64] with Cout = 256); slab: workspace of
  * N*rs*Cout*577 floats; gw torch layout [Cout][64][3][3], gb [Cout] (both NULL:
  * leave the per-chunk partial slabs, skip the reduction) */
 int srmi_wgrad3x3(const void* x, const void* dy, int N, int H, int W, int Cout, int dy_unshuffle, int row_splits,
-                  float* slab, size_t slab_bytes, int ps, float alpha, float* gw, float* gb, void* stream);
+                  float* slab, size_t slab_bytes, int ps, float alpha, float* gw, float* gb, int dtype, void* stream);
 int srmi_ca_forward(const void* u, const float* part, int nstrips, const float* w1, const float* b1, const float* w2,
                     const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, void* hb_out,
-                    float* rec, void* stream);
+                    float* rec, int dtype, void* stream);
 /* brec: N*(2C + C/R) floats (dz2 | dz1 | conv2 bias grad per image) followed by
  * N*C floats of dm (gradient of the pooled mean) -- N*(3C + C/R) in total */
 int srmi_ca_backward(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
-                     const float* w2, int N, int HW, int C, int R, void* du, float* brec, void* stream);
+                     const float* w2, int N, int HW, int C, int R, void* du, float* brec, int dtype, void* stream);
 int srmi_head_forward(const float* lr, const float* w, const float* b, int N, int C, int H, int W, float* x0f,
-                      void* x0b, void* stream);
-int srmi_tail_forward(const void* x, const float* w, const float* b, int N, int C, int H, int W, float* y,
+                      void* x0b, int dtype, void* stream);
+int srmi_tail_forward(const void* x, const float* w, const float* b, int N, int C, int H, int W, float* y, int dtype,
                       void* stream);
 
 /* ---- tiled-region inference data path --------------------------------- */

@@ -17,6 +17,16 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(bf16_t, b);
 }
+// storage-type conversions of the two engine modes (bf16 operands / exact fp32)
+template <typename T>
+__device__ __forceinline__ T from_f32(float v);
+template <>
+__device__ __forceinline__ bf16_t from_f32<bf16_t>(float v) { return f2bf(v); }
+template <>
+__device__ __forceinline__ float from_f32<float>(float v) { return v; }
+__device__ __forceinline__ float to_f32(bf16_t v) { return bf2f(v); }
+__device__ __forceinline__ float to_f32(float v) { return v; }
+
 // two floats -> one dword of 2 bf16 (a low): ONE v_cvt_pk_bf16_f32 (the scalar
 // form above made the compiler emit 2 converts + 4 shifts/ors per dword)
 typedef __attribute__((ext_vector_type(2))) float f32x2;

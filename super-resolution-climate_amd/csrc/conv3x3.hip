@@ -794,6 +794,7 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
   if (p.Cin % 64 || p.Cout % 64 || p.N <= 0 || p.H % kTH) return SRMI_ERR_SHAPE;
   // operands each epilogue dereferences unconditionally: refuse, never fault
   if (!p.x || !p.w) return SRMI_ERR_ARG;
+  if (epi == EPI_DG_ACC_CA && (!p.r1 || !p.aux || !p.part || p.yb || p.r2 || p.r3 || !p.yf)) return SRMI_ERR_ARG;
   switch (epi) {
     case EPI_PS_BF16:
       if (!p.yb) return SRMI_ERR_ARG;
@@ -815,6 +816,7 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
   }
   if (epi == EPI_PS_BF16 && p.Cout != 256) return SRMI_ERR_SHAPE;
   if (p.in_mode == IN_UNSHUF && p.Cin != 256) return SRMI_ERR_SHAPE;
+  if (p.f32) return conv3x3_f32_launch(p, epi, st);
   switch (epi) {
     case EPI_RELU_BF16: return launch_epi<EPI_RELU_BF16>(p, st);
     case EPI_POOL_BF16: return launch_epi<EPI_POOL_BF16>(p, st);
@@ -823,9 +825,7 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
     case EPI_DG_RELUMASK: return launch_epi<EPI_DG_RELUMASK>(p, st);
     case EPI_DG_ACC: return launch_epi<EPI_DG_ACC>(p, st);
     case EPI_PLAIN_BF16: return launch_epi<EPI_PLAIN_BF16>(p, st);
-    case EPI_DG_ACC_CA:
-      if (!p.r1 || !p.aux || !p.part || p.yb || p.r2 || p.r3 || !p.yf) return SRMI_ERR_ARG;
-      return launch_epi<EPI_DG_ACC_CA>(p, st);
+    case EPI_DG_ACC_CA: return launch_epi<EPI_DG_ACC_CA>(p, st);
     default: return SRMI_ERR_ARG;
   }
 }

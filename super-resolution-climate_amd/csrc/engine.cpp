@@ -81,6 +81,7 @@ int build_plan(const srmi_model_config* cfg, Plan& P) {
   if (c.nlayers < 1 || c.batch < 1 || c.lr_h < 4 || c.lr_w < 16) return SRMI_ERR_ARG;
   if (c.arch == SRMI_ARCH_RCAN && (c.nblocks < 1 || c.reduction < 1 || 64 % c.reduction)) return SRMI_ERR_ARG;
   if (c.arch != SRMI_ARCH_RCAN && c.arch != SRMI_ARCH_EDSR) return SRMI_ERR_ARG;
+  if (c.dtype != SRMI_DTYPE_BF16 && c.dtype != SRMI_DTYPE_F32) return SRMI_ERR_ARG;
   P = Plan();
   P.cfg = c;
   const int F = 64;
@@ -114,7 +115,7 @@ int build_plan(const srmi_model_config* cfg, Plan& P) {
     P.ups.push_back(u);
   }
   P.tail = add_conv(P, F, c.nchannels_out, 3);
-  // MFMA convs get bf16 packs
+  // MFMA convs get filter packs in the operand type (bf16 or fp32)
   for (auto& grp : P.groups)
     for (auto& r : grp) {
       P.mfma_convs.push_back(&r.c1);
@@ -171,6 +172,12 @@ int choose_row_splits(int N, int H, int Cout, int cu_budget = 0) {
 struct srmi_engine {
   Plan P;
   int train = 0;
+  // operand storage: bf16 (SRMI_DTYPE_BF16: bf16 MFMA operands, fp32 accumulation
+  // and residual stream) or fp32 (SRMI_DTYPE_F32: exact fp32 everywhere).  The
+  // activation / gradient-map / filter-pack pointers below are typed bf16_t* but
+  // hold esz-byte elements; at() does their element arithmetic.
+  int f32 = 0;
+  size_t esz = 2;
   int N = 0, h = 0, w = 0, C = 0, Co = 0, S = 0;
   int cu_budget = 0;  // CUs one launch aims to fill (0 = all)
   size_t mapn = 0;  // elements of one [N][h][w][64] map
@@ -211,14 +218,17 @@ struct srmi_engine {
   bool tables_uploaded = false;
   int last_n = 0;
 
+  bf16_t* at(bf16_t* base, size_t elems) const {
+    return reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(base) + elems * esz);
+  }
   bf16_t* hb(int g, int b) const {
     const int nb1 = P.cfg.arch == SRMI_ARCH_RCAN ? P.cfg.nblocks + 1 : 1;
     const int k = g * nb1 + b;
-    return HB + (size_t)(train ? k : (k % n_hb)) * mapn;
+    return at(HB, (size_t)(train ? k : (k % n_hb)) * mapn);
   }
   int nbe() const { return P.cfg.arch == SRMI_ARCH_RCAN ? P.cfg.nblocks : 1; }
-  bf16_t* Tm(int g, int b) const { return train ? T + (size_t)(g * nbe() + (b - 1)) * mapn : T; }
-  bf16_t* Um(int g, int b) const { return train ? U + (size_t)(g * P.cfg.nblocks + (b - 1)) * mapn : U; }
+  bf16_t* Tm(int g, int b) const { return train ? at(T, (size_t)(g * nbe() + (b - 1)) * mapn) : T; }
+  bf16_t* Um(int g, int b) const { return train ? at(U, (size_t)(g * P.cfg.nblocks + (b - 1)) * mapn) : U; }
   float* recp(int g, int b) const {
     return train ? rec + (size_t)(g * P.cfg.nblocks + (b - 1)) * N * 160 : rec;
   }
@@ -236,6 +246,7 @@ static int side_row_splits(const srmi_engine* e) {
 static size_t carve(srmi_engine* e, char* base) {
   Carver cv;
   cv.base = base;
+  auto act = [&](size_t count) { return reinterpret_cast<bf16_t*>(cv.take<char>(count * e->esz)); };
   const Plan& P = e->P;
   const int N = e->N;
   const size_t m = e->mapn;
@@ -246,13 +257,13 @@ static size_t carve(srmi_engine* e, char* base) {
   e->Hf = cv.take<float>(m);
   const int nslots = rcan ? nl * (nb + 1) + 1 : nl + 1;
   e->n_hb = e->train ? nslots : 3;
-  e->HB = cv.take<bf16_t>(m * e->n_hb);
+  e->HB = act(m * e->n_hb);
   const int nconv1 = rcan ? nl * nb : nl;
-  e->T = cv.take<bf16_t>(m * (e->train ? nconv1 : 1));
-  e->U = rcan ? cv.take<bf16_t>(m * (e->train ? nconv1 : 1)) : nullptr;
-  e->RESb = cv.take<bf16_t>(m);
+  e->T = act(m * (e->train ? nconv1 : 1));
+  e->U = rcan ? act(m * (e->train ? nconv1 : 1)) : nullptr;
+  e->RESb = act(m);
   for (int k = 0; k < 3; ++k) e->PS[k] = nullptr;
-  for (int k = 0; k < P.nups; ++k) e->PS[k] = cv.take<bf16_t>(m << (2 * (k + 1)));
+  for (int k = 0; k < P.nups; ++k) e->PS[k] = act(m << (2 * (k + 1)));
   const int nstrips = conv3x3_nstrips(e->h, e->w);
   if (rcan) {
     e->rec = cv.take<float>((size_t)(e->train ? nl * nb : 1) * N * 160);
@@ -267,20 +278,20 @@ static size_t carve(srmi_engine* e, char* base) {
     e->GAf = cv.take<float>(m);
     e->GBf = cv.take<float>(m);
     e->dRESf = cv.take<float>(m);
-    e->GAb = cv.take<bf16_t>(m);
-    e->GBb = cv.take<bf16_t>(m);
-    e->DU = cv.take<bf16_t>(m);
-    e->DZ = cv.take<bf16_t>(m);
+    e->GAb = act(m);
+    e->GBb = act(m);
+    e->DU = act(m);
+    e->DZ = act(m);
     e->DUr[0] = e->DU;
     e->DZr[0] = e->DZ;
     for (int k = 1; k < 4; ++k) {
       const bool own = rcan;
-      e->DUr[k] = own ? cv.take<bf16_t>(m) : e->DU;
-      e->DZr[k] = own ? cv.take<bf16_t>(m) : e->DZ;
+      e->DUr[k] = own ? act(m) : e->DU;
+      e->DZr[k] = own ? act(m) : e->DZ;
     }
-    e->dRESb = cv.take<bf16_t>(m);
+    e->dRESb = act(m);
     for (int k = 0; k < 3; ++k) e->dPS[k] = nullptr;
-    for (int k = 0; k < P.nups; ++k) e->dPS[k] = cv.take<bf16_t>(m << (2 * (k + 1)));
+    for (int k = 0; k < P.nups; ++k) e->dPS[k] = act(m << (2 * (k + 1)));
     // slab: max over all wgrads
     size_t sf = 0, bf = 0;
     auto upd = [&](int H, int W, int Cout) {
@@ -312,7 +323,7 @@ static size_t carve(srmi_engine* e, char* base) {
       e->bslab_s2 = cv.take<float>(e->bslab_s_floats);
     }
   }
-  e->packs = cv.take<bf16_t>(P.pack_elems);
+  e->packs = act(P.pack_elems);
   e->pbias = cv.take<float>(P.pbias_elems);
   e->d_entries = cv.take<PackEntry>(P.mfma_convs.size());
   e->d_caoffs = cv.take<long long>((size_t)std::max(1, nl * nb) * 5);
@@ -323,6 +334,8 @@ static int init_engine(srmi_engine* e, const srmi_model_config* cfg, int train) 
   int rc = build_plan(cfg, e->P);
   if (rc) return rc;
   e->train = train;
+  e->f32 = cfg->dtype == SRMI_DTYPE_F32;
+  e->esz = e->f32 ? 4 : 2;
   e->N = cfg->batch;
   e->h = cfg->lr_h;
   e->w = cfg->lr_w;
@@ -371,8 +384,9 @@ static int conv_fwd(srmi_engine* e, const ConvRef& c, const bf16_t* x, int n, in
                     float* yf, const float* r1, float* part, float alpha, hipStream_t st) {
   ConvParams p{};
   p.x = x;
-  p.w = e->packs + c.f_off;
+  p.w = e->at(e->packs, c.f_off);
   p.bias = e->pbias + c.pb_off;
+  p.f32 = e->f32;
   p.N = n;
   p.H = H;
   p.W = W;
@@ -396,8 +410,9 @@ static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n,
                       float alpha, hipStream_t st) {
   ConvParams p{};
   p.x = dy;
-  p.w = e->packs + c.d_off;
+  p.w = e->at(e->packs, c.d_off);
   p.bias = nullptr;
+  p.f32 = e->f32;
   p.N = n;
   p.H = H;
   p.W = W;
@@ -428,6 +443,7 @@ static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const b
   WgradParams p{};
   p.x = x;
   p.dy = dy;
+  p.f32 = e->f32;
   p.N = n;
   p.H = H;
   p.W = W;
@@ -486,7 +502,7 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
   const Plan& P = e->P;
   const int h = e->h, w = e->w, HW = h * w;
   const int nstrips = conv3x3_nstrips(h, w);
-  RC(head_fwd_launch(lr, prm + P.head.w, prm + P.head.b, n, e->C, h, w, e->X0f, e->hb(0, 0), st));
+  RC(head_fwd_launch(lr, prm + P.head.w, prm + P.head.b, n, e->C, h, w, e->X0f, e->hb(0, 0), e->f32, st));
   if (P.cfg.arch == SRMI_ARCH_RCAN) {
     const int nl = P.cfg.nlayers, nb = P.cfg.nblocks, R = P.cfg.reduction;
     for (int g = 0; g < nl; ++g) {
@@ -496,7 +512,7 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
         RC(conv_fwd(e, r.c1, e->hb(g, b - 1), n, h, w, EPI_RELU_BF16, e->Tm(g, b), nullptr, nullptr, nullptr, 1.f, st));
         RC(conv_fwd(e, r.c2, e->Tm(g, b), n, h, w, EPI_POOL_BF16, e->Um(g, b), nullptr, nullptr, e->ppool, 1.f, st));
         RC(ca_fwd_launch(e->Um(g, b), e->ppool, nstrips, prm + r.ca_w1, prm + r.ca_b1, prm + r.ca_w2, prm + r.ca_b2, n,
-                         HW, 64, R, b == 1 ? rin : e->Hf, e->Hf, e->hb(g, b), e->recp(g, b), st));
+                         HW, 64, R, b == 1 ? rin : e->Hf, e->Hf, e->hb(g, b), e->recp(g, b), e->f32, st));
       }
       RC(conv_fwd(e, P.group_tail[g], e->hb(g, nb), n, h, w, EPI_RESID, e->hb(g + 1, 0), e->Rf, rin, nullptr, 1.f,
                   st));
@@ -520,7 +536,7 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
     H *= 2;
     W *= 2;
   }
-  RC(tail_fwd_launch(cur, prm + P.tail.w, prm + P.tail.b, n, e->Co, H, W, sr, st));
+  RC(tail_fwd_launch(cur, prm + P.tail.w, prm + P.tail.b, n, e->Co, H, W, sr, e->f32, st));
   e->last_n = n;
   return 0;
 }
@@ -537,9 +553,9 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
   const float* yv = dy ? dy : sr;
   const float* tv = dy ? nullptr : hr;
   const float* lv = dy ? nullptr : loss4;
-  RC(tail_dgrad_launch(yv, tv, lv, prm + P.tail.w, n, e->Co, H, W, e->dPS[P.nups - 1], st));
+  RC(tail_dgrad_launch(yv, tv, lv, prm + P.tail.w, n, e->Co, H, W, e->dPS[P.nups - 1], e->f32, st));
   int nsl = 0;
-  RC(tail_wgrad_launch(yv, tv, lv, xlast, n, e->Co, H, W, e->slab, &nsl, st));
+  RC(tail_wgrad_launch(yv, tv, lv, xlast, n, e->Co, H, W, e->slab, &nsl, e->f32, st));
   RC(tail_wgrad_reduce_launch(e->slab, nsl, e->Co, grads + P.tail.w, grads + P.tail.b, st));
   // upsamplers, last to first
   for (int k = P.nups - 1; k >= 0; --k) {
@@ -586,7 +602,7 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         bf16_t* dz = e->DZr[q];
         if (reuse) HC(hipStreamWaitEvent(st, e->ev_w1[((it0 - 3) >> 1) & 1], 0));
         RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
-                            e->brecp(g, b), st));
+                            e->brecp(g, b), e->f32, st));
         ReduceSet red2, red1;
         RC(conv_dgrad(e, r.c2, du, n, h, w, EPI_DG_RELUMASK, dz, nullptr, nullptr, nullptr, nullptr, e->Tm(g, b),
                       nullptr, 1.f, st));
@@ -643,7 +659,7 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
 // =================================================================== C ABI
 extern "C" {
 
-int srmi_version(void) { return 100; }
+int srmi_version(void) { return 200; }
 
 int srmi_param_count(const srmi_model_config* cfg, long long* n_params, int* n_tensors) {
   Plan P;
@@ -713,7 +729,7 @@ int srmi_engine_destroy(srmi_engine* e) {
 int srmi_pack_weights(srmi_engine* e, const float* params, void* stream) {
   if (!e || !params) return SRMI_ERR_ARG;
   RC(upload_tables(e, S_(stream)));
-  return pack_launch(params, e->d_entries, (int)e->h_entries.size(), e->max_pack_elems, e->packs, e->pbias,
+  return pack_launch(params, e->d_entries, (int)e->h_entries.size(), e->max_pack_elems, e->packs, e->pbias, e->f32,
                      S_(stream));
 }
 
@@ -786,8 +802,10 @@ int srmi_adam_step(float* p, const float* g, float* m, float* v, size_t n, int s
 // ---------------------------------------------------------------- op level
 int srmi_conv3x3(const void* x, const void* wpack, const float* bias, int N, int H, int W, int Cin, int Cout,
                  int in_unshuffle, int epi, void* yb, float* yf, const float* r1, const float* r2, const float* r3,
-                 const void* aux, float* part, float alpha, void* stream) {
+                 const void* aux, float* part, float alpha, int dtype, void* stream) {
+  if (dtype != SRMI_DTYPE_BF16 && dtype != SRMI_DTYPE_F32) return SRMI_ERR_ARG;
   ConvParams p{};
+  p.f32 = dtype == SRMI_DTYPE_F32;
   p.x = (const bf16_t*)x;
   p.w = (const bf16_t*)wpack;
   p.bias = bias;
@@ -823,13 +841,16 @@ int srmi_debug_wgrad_stamps(void* buf) {
 }
 
 int srmi_pack_conv(const float* w, const float* b, int Cout, int Cin, int ps, void* fpack, void* dpack, float* pbias,
-                   void* stream) {
-  return pack_one_launch(w, b, Cout, Cin, ps, (bf16_t*)fpack, (bf16_t*)dpack, pbias, S_(stream));
+                   int dtype, void* stream) {
+  if (dtype != SRMI_DTYPE_BF16 && dtype != SRMI_DTYPE_F32) return SRMI_ERR_ARG;
+  return pack_one_launch(w, b, Cout, Cin, ps, fpack, dpack, pbias, dtype == SRMI_DTYPE_F32, S_(stream));
 }
 
 int srmi_wgrad3x3(const void* x, const void* dy, int N, int H, int W, int Cout, int dy_unshuffle, int row_splits,
-                  float* slab, size_t slab_bytes, int ps, float alpha, float* gw, float* gb, void* stream) {
+                  float* slab, size_t slab_bytes, int ps, float alpha, float* gw, float* gb, int dtype, void* stream) {
+  if (dtype != SRMI_DTYPE_BF16 && dtype != SRMI_DTYPE_F32) return SRMI_ERR_ARG;
   WgradParams p{};
+  p.f32 = dtype == SRMI_DTYPE_F32;
   p.x = (const bf16_t*)x;
   p.dy = (const bf16_t*)dy;
   p.N = N;
@@ -851,24 +872,28 @@ int srmi_wgrad3x3(const void* x, const void* dy, int N, int H, int W, int Cout, 
 
 int srmi_ca_forward(const void* u, const float* part, int nstrips, const float* w1, const float* b1, const float* w2,
                     const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, void* hb_out,
-                    float* rec, void* stream) {
-  return ca_fwd_launch((const bf16_t*)u, part, nstrips, w1, b1, w2, b2, N, HW, C, R, h_in, h_out, (bf16_t*)hb_out,
-                       rec, S_(stream));
+                    float* rec, int dtype, void* stream) {
+  if (dtype != SRMI_DTYPE_BF16 && dtype != SRMI_DTYPE_F32) return SRMI_ERR_ARG;
+  return ca_fwd_launch(u, part, nstrips, w1, b1, w2, b2, N, HW, C, R, h_in, h_out, hb_out, rec,
+                       dtype == SRMI_DTYPE_F32, S_(stream));
 }
 
 int srmi_ca_backward(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
-                     const float* w2, int N, int HW, int C, int R, void* du, float* brec, void* stream) {
-  return ca_bwd_du_launch(g, part, nstrips, rec, w1, w2, N, HW, C, R, (bf16_t*)du, brec, S_(stream));
+                     const float* w2, int N, int HW, int C, int R, void* du, float* brec, int dtype, void* stream) {
+  if (dtype != SRMI_DTYPE_BF16 && dtype != SRMI_DTYPE_F32) return SRMI_ERR_ARG;
+  return ca_bwd_du_launch(g, part, nstrips, rec, w1, w2, N, HW, C, R, du, brec, dtype == SRMI_DTYPE_F32, S_(stream));
 }
 
 int srmi_head_forward(const float* lr, const float* w, const float* b, int N, int C, int H, int W, float* x0f,
-                      void* x0b, void* stream) {
-  return head_fwd_launch(lr, w, b, N, C, H, W, x0f, (bf16_t*)x0b, S_(stream));
+                      void* x0b, int dtype, void* stream) {
+  if (dtype != SRMI_DTYPE_BF16 && dtype != SRMI_DTYPE_F32) return SRMI_ERR_ARG;
+  return head_fwd_launch(lr, w, b, N, C, H, W, x0f, x0b, dtype == SRMI_DTYPE_F32, S_(stream));
 }
 
-int srmi_tail_forward(const void* x, const float* w, const float* b, int N, int C, int H, int W, float* y,
+int srmi_tail_forward(const void* x, const float* w, const float* b, int N, int C, int H, int W, float* y, int dtype,
                       void* stream) {
-  return tail_fwd_launch((const bf16_t*)x, w, b, N, C, H, W, y, S_(stream));
+  if (dtype != SRMI_DTYPE_BF16 && dtype != SRMI_DTYPE_F32) return SRMI_ERR_ARG;
+  return tail_fwd_launch(x, w, b, N, C, H, W, y, dtype == SRMI_DTYPE_F32, S_(stream));
 }
 
 int srmi_llc_index_map_workspace(long long n_template, size_t* bytes) {

@@ -19,9 +19,10 @@ namespace srmi {
 
 // =========================================================================== head
 // x0[n][y][x][co] = b[co] + sum_{c,tap} lr[n][c][y+ky-1][x+kx-1] * w[co][c][tap]
+template <typename T>
 __global__ void __launch_bounds__(256) head_fwd_kernel(const float* __restrict__ lr, const float* __restrict__ w,
                                                        const float* __restrict__ b, int C, int H, int W,
-                                                       float* __restrict__ x0f, bf16_t* __restrict__ x0b) {
+                                                       float* __restrict__ x0f, T* __restrict__ x0b) {
   extern __shared__ float hs[];  // [C][6][W+2] halo, then [64][9C] weights
   const int n = blockIdx.y, y0 = blockIdx.x * 4, tid = threadIdx.x;
   const int Wp = W + 2;
@@ -51,15 +52,20 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const float* __restrict__
     }
     const size_t o = (((size_t)n * H + y0 + r) * W + x) * 64 + co;
     x0f[o] = s;
-    x0b[o] = f2bf(s);
+    x0b[o] = from_f32<T>(s);
   }
 }
 
 int head_fwd_launch(const float* lr, const float* w, const float* b, int N, int C, int H, int W, float* x0f,
-                    bf16_t* x0b, hipStream_t st) {
+                    void* x0b, int f32, hipStream_t st) {
   if (C < 1 || C > 4 || H % 4) return SRMI_ERR_SHAPE;
   const int smem = C * 6 * (W + 2) * 4;
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(H / 4, N), dim3(256), smem, st, lr, w, b, C, H, W, x0f, x0b);
+  if (f32)
+    hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(H / 4, N), dim3(256), smem, st, lr, w, b, C, H, W, x0f,
+                       static_cast<float*>(x0b));
+  else
+    hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, dim3(H / 4, N), dim3(256), smem, st, lr, w, b, C, H, W, x0f,
+                       static_cast<bf16_t*>(x0b));
   SRMI_CHECK_LAUNCH();
   return 0;
 }
@@ -241,9 +247,66 @@ __global__ void __launch_bounds__(256) tail_fwd_mfma_kernel(const bf16_t* __rest
   }
 }
 
-int tail_fwd_launch(const bf16_t* x, const float* w, const float* b, int N, int C, int H, int W, float* y,
+// Exact-fp32 form (fp32 engine mode) on the VALU: one output pixel per thread, 4 rows
+// x 64 px per workgroup; per 16-channel slice the 6 x 66 halo is staged channel-major
+// in LDS ([c][row][px]: a wave reads 64 consecutive floats), the filters [C][9][64] in
+// LDS (broadcast reads).  C <= 4 outputs per pixel: an MFMA form would waste 12 of its
+// 16 output rows at 1/16 of the bf16 rate.
+__global__ void __launch_bounds__(256) tail_fwd_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                           const float* __restrict__ b, int C, int H, int W,
+                                                           float* __restrict__ y) {
+  constexpr int TX = 64, WP = TX + 2, CS = 16;
+  __shared__ float hs[CS][6][WP];
+  __shared__ float wl[4][9][64];
+  const int n = blockIdx.z, y0 = blockIdx.y * 4, x0 = blockIdx.x * TX, tid = threadIdx.x;
+  for (int i = tid; i < C * 576; i += 256) {
+    const int co = i / 576, ci = (i / 9) % 64, tap = i % 9;
+    wl[co][tap][ci] = w[i];
+  }
+  const int r = tid / TX, px = tid % TX;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int cs = 0; cs < 64; cs += CS) {
+    __syncthreads();
+    for (int i = tid; i < 6 * WP * (CS / 4); i += 256) {
+      const int q = i / (CS / 4), c4 = i % (CS / 4);
+      const int hy = q / WP, hx = q % WP;
+      const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+        v = *reinterpret_cast<const float4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + cs + c4 * 4);
+      hs[c4 * 4 + 0][hy][hx] = v.x;
+      hs[c4 * 4 + 1][hy][hx] = v.y;
+      hs[c4 * 4 + 2][hy][hx] = v.z;
+      hs[c4 * 4 + 3][hy][hx] = v.w;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int c = 0; c < CS; ++c)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const float v = hs[c][r + tap / 3][px + tap % 3];
+#pragma unroll
+        for (int co = 0; co < 4; ++co)
+          if (co < C) acc[co] = fmaf(v, wl[co][tap][cs + c], acc[co]);
+      }
+  }
+  if (x0 + px < W) {
+#pragma unroll
+    for (int co = 0; co < 4; ++co)
+      if (co < C) y[(((size_t)n * C + co) * H + y0 + r) * W + x0 + px] = acc[co] + b[co];
+  }
+}
+
+int tail_fwd_launch(const void* xv, const float* w, const float* b, int N, int C, int H, int W, float* y, int f32,
                     hipStream_t st) {
   if (C < 1 || C > 4 || H % 4) return SRMI_ERR_SHAPE;
+  if (f32) {
+    hipLaunchKernelGGL(tail_fwd_f32_kernel, dim3((W + 63) / 64, H / 4, N), dim3(256), 0, st,
+                       static_cast<const float*>(xv), w, b, C, H, W, y);
+    SRMI_CHECK_LAUNCH();
+    return 0;
+  }
+  const bf16_t* x = static_cast<const bf16_t*>(xv);
   if (W % 48 == 0) {
     hipLaunchKernelGGL(tail_fwd_mfma_kernel<48>, dim3(W / 48, H / 4, N), dim3(256), 6 * 50 * 128 + 9 * 2048, st, x,
                        w, b, C, H, W, y);
@@ -259,10 +322,10 @@ int tail_fwd_launch(const bf16_t* x, const float* w, const float* b, int N, int 
 
 // dx[n][yy][xx][ci] = sum_{tap,c} dy[n][c][yy-ky+1][xx-kx+1] * w[c][ci][tap],
 // dy = (y - hr) * loss[2]   (gradient of the RMSE, stats.py:5-8)
-template <int TWT>
+template <int TWT, typename T>
 __global__ void __launch_bounds__(256) tail_dgrad_kernel(const float* __restrict__ yv, const float* __restrict__ hr,
                                                         const float* __restrict__ loss, const float* __restrict__ w,
-                                                        int C, int H, int W, bf16_t* __restrict__ dx) {
+                                                        int C, int H, int W, T* __restrict__ dx) {
   extern __shared__ __attribute__((aligned(16))) float tds[];
   constexpr int WP = TWT + 2;
   const int n = blockIdx.z, y0 = blockIdx.y * 4, x0 = blockIdx.x * TWT, tid = threadIdx.x;
@@ -285,7 +348,7 @@ __global__ void __launch_bounds__(256) tail_dgrad_kernel(const float* __restrict
   }
   __syncthreads();
   const int ck = tid & 7;
-  const auto rdx = wt_rsrc(dx, (uint32_t)((size_t)gridDim.z * H * W * 64 * 2));
+  const auto rdx = wt_rsrc(dx, (uint32_t)((size_t)gridDim.z * H * W * 64 * sizeof(T)));
   for (int px = tid >> 3; px < 4 * TWT; px += 32) {
     const int r = px / TWT, xx = px - r * TWT;
     float acc[8];
@@ -302,23 +365,31 @@ __global__ void __launch_bounds__(256) tail_dgrad_kernel(const float* __restrict
         acc[4] += d * w1.x; acc[5] += d * w1.y; acc[6] += d * w1.z; acc[7] += d * w1.w;
       }
     }
-    uint4 o;
-    o.x = pack2(acc[0], acc[1]); o.y = pack2(acc[2], acc[3]);
-    o.z = pack2(acc[4], acc[5]); o.w = pack2(acc[6], acc[7]);
-    // 8 lanes per pixel: 128-byte lines, written through (common.hpp)
-    st_wt16(rdx, dx, (uint32_t)(((((size_t)n * H + y0 + r) * W + x0 + xx) * 64 + ck * 8) * 2), o);
+    const size_t e = (((size_t)n * H + y0 + r) * W + x0 + xx) * 64 + ck * 8;
+    if constexpr (sizeof(T) == 2) {
+      uint4 o;
+      o.x = pack2(acc[0], acc[1]); o.y = pack2(acc[2], acc[3]);
+      o.z = pack2(acc[4], acc[5]); o.w = pack2(acc[6], acc[7]);
+      // 8 lanes per pixel: 128-byte lines, written through (common.hpp)
+      st_wt16(rdx, dx, (uint32_t)(e * 2), o);
+    } else {
+      st_wt16(rdx, dx, (uint32_t)(e * 4), make_float4(acc[0], acc[1], acc[2], acc[3]));
+      st_wt16(rdx, dx, (uint32_t)(e * 4 + 16), make_float4(acc[4], acc[5], acc[6], acc[7]));
+    }
   }
 }
 
-int tail_dgrad_launch(const float* y, const float* hr, const float* loss, const float* w, int N, int C, int H, int W,
-                      bf16_t* dx, hipStream_t st) {
-  if (C < 1 || C > 4 || H % 4) return SRMI_ERR_SHAPE;
+template <typename T>
+static int tail_dgrad_t(const float* y, const float* hr, const float* loss, const float* w, int N, int C, int H, int W,
+                        T* dx, hipStream_t st) {
   if (W % 64 == 0) {
     const int smem = (4 * 6 * 66 + 4 * 576) * 4;
-    hipLaunchKernelGGL(tail_dgrad_kernel<64>, dim3(W / 64, H / 4, N), dim3(256), smem, st, y, hr, loss, w, C, H, W, dx);
+    hipLaunchKernelGGL((tail_dgrad_kernel<64, T>), dim3(W / 64, H / 4, N), dim3(256), smem, st, y, hr, loss, w, C, H,
+                       W, dx);
   } else if (W % 32 == 0) {
     const int smem = (4 * 6 * 34 + 4 * 576) * 4;
-    hipLaunchKernelGGL(tail_dgrad_kernel<32>, dim3(W / 32, H / 4, N), dim3(256), smem, st, y, hr, loss, w, C, H, W, dx);
+    hipLaunchKernelGGL((tail_dgrad_kernel<32, T>), dim3(W / 32, H / 4, N), dim3(256), smem, st, y, hr, loss, w, C, H,
+                       W, dx);
   } else {
     return SRMI_ERR_SHAPE;
   }
@@ -326,26 +397,35 @@ int tail_dgrad_launch(const float* y, const float* hr, const float* loss, const 
   return 0;
 }
 
+int tail_dgrad_launch(const float* y, const float* hr, const float* loss, const float* w, int N, int C, int H, int W,
+                      void* dx, int f32, hipStream_t st) {
+  if (C < 1 || C > 4 || H % 4) return SRMI_ERR_SHAPE;
+  return f32 ? tail_dgrad_t(y, hr, loss, w, N, C, H, W, static_cast<float*>(dx), st)
+             : tail_dgrad_t(y, hr, loss, w, N, C, H, W, static_cast<bf16_t*>(dx), st);
+}
+
 // dW[c][ci][tap] = sum_p dy[c][p] * x[p+off][ci];  db[c] = sum_p dy[c][p]
 // dy = (y - hr) * loss[2] is formed on the fly (RMSE gradient, stats.py:5-8).
 constexpr int kTailRows = 4;
-// Per 64-pixel segment the workgroup stages the 6 input rows its
-// 4 waves need (66 px x 64 ch bf16) and the RMSE gradient of its 4 rows; lane = ci
-// reads the x window from LDS (128 B per wave read, conflict-free) and the pixel's
-// dy by LDS broadcast -- no readlane, no 2-byte global loads per pixel.
-template <int CC>
+// Per segment of SEG pixels (64 bf16 / 32 fp32) the workgroup stages the 6 input
+// rows its 4 waves need (SEG+2 px x 64 ch) and the RMSE gradient of its 4 rows;
+// lane = ci reads the x window from LDS (one row per wave read, conflict-free) and
+// the pixel's dy by LDS broadcast.  The cross-wave reduction reuses the x buffer.
+template <int CC, typename T>
 __global__ void __launch_bounds__(256) tail_wgrad_lds_kernel(const float* __restrict__ yv,
                                                             const float* __restrict__ hr,
-                                                            const float* __restrict__ loss,
-                                                            const bf16_t* __restrict__ x, int H, int W,
-                                                            float* __restrict__ slab) {
-  constexpr int SEG = 64, SP = SEG + 2;
-  __shared__ __attribute__((aligned(16))) bf16_t xs[6 * SP * 64];  // [row][px][ci]
+                                                            const float* __restrict__ loss, const T* __restrict__ x,
+                                                            int H, int W, float* __restrict__ slab) {
+  constexpr int SEG = sizeof(T) == 2 ? 64 : 32, SP = SEG + 2;
+  constexpr int XS_BYTES = 6 * SP * 64 * (int)sizeof(T), RED_BYTES = 4 * CC * 577 * 4;
+  __shared__ __attribute__((aligned(16))) char sbuf[XS_BYTES > RED_BYTES ? XS_BYTES : RED_BYTES];
   __shared__ float dyl[CC][kTailRows][SEG];
-  __shared__ float red[4][CC * 577];
+  T* xs = reinterpret_cast<T*>(sbuf);                       // [row][px][ci]
+  float(*red)[CC * 577] = reinterpret_cast<float(*)[CC * 577]>(sbuf);
   const int n = blockIdx.y, band = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int y0 = band * kTailRows;
   const float sc = loss ? loss[2] : 1.f;
+  constexpr int VPC = 16 / (int)sizeof(T);                // elements per 16-byte chunk
   float acc[9][CC], bacc[CC];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -356,13 +436,13 @@ __global__ void __launch_bounds__(256) tail_wgrad_lds_kernel(const float* __rest
   for (int x0 = 0; x0 < W; x0 += SEG) {
     const int nx = min(SEG, W - x0);
     __syncthreads();  // previous segment's readers are done
-    for (int i = tid; i < 6 * SP * 8; i += 256) {
-      const int q = i >> 3, ch = i & 7, r = q / SP, px = q - r * SP;
+    for (int i = tid; i < 6 * SP * (64 / VPC); i += 256) {
+      const int q = i / (64 / VPC), ch = i % (64 / VPC), r = q / SP, px = q - r * SP;
       const int yy = y0 - 1 + r, xx = x0 - 1 + px;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (yy >= 0 && yy < H && xx >= 0 && xx < W && px <= nx + 1)
-        v = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + ch * 8);
-      *reinterpret_cast<uint4*>(xs + q * 64 + ch * 8) = v;
+        v = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + ch * VPC);
+      *reinterpret_cast<uint4*>(xs + q * 64 + ch * VPC) = v;
     }
     for (int i = tid; i < CC * kTailRows * SEG; i += 256) {
       const int c = i / (kTailRows * SEG), r = (i / SEG) % kTailRows, px = i % SEG;
@@ -377,12 +457,12 @@ __global__ void __launch_bounds__(256) tail_wgrad_lds_kernel(const float* __rest
     float win[3][3];
 #pragma unroll
     for (int rr = 0; rr < 3; ++rr) {
-      win[rr][0] = bf2f(xs[((wave + rr) * SP + 0) * 64 + lane]);
-      win[rr][1] = bf2f(xs[((wave + rr) * SP + 1) * 64 + lane]);
+      win[rr][0] = to_f32(xs[((wave + rr) * SP + 0) * 64 + lane]);
+      win[rr][1] = to_f32(xs[((wave + rr) * SP + 1) * 64 + lane]);
     }
     for (int j = 0; j < nx; ++j) {
 #pragma unroll
-      for (int rr = 0; rr < 3; ++rr) win[rr][2] = bf2f(xs[((wave + rr) * SP + j + 2) * 64 + lane]);
+      for (int rr = 0; rr < 3; ++rr) win[rr][2] = to_f32(xs[((wave + rr) * SP + j + 2) * 64 + lane]);
 #pragma unroll
       for (int c = 0; c < CC; ++c) {
         const float dd = dyl[c][wave][j];
@@ -397,6 +477,7 @@ __global__ void __launch_bounds__(256) tail_wgrad_lds_kernel(const float* __rest
       }
     }
   }
+  __syncthreads();  // every wave is done with xs: red reuses its bytes
 #pragma unroll
   for (int c = 0; c < CC; ++c) {
 #pragma unroll
@@ -408,16 +489,25 @@ __global__ void __launch_bounds__(256) tail_wgrad_lds_kernel(const float* __rest
   for (int i = tid; i < CC * 577; i += 256) out[i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
 }
 
-int tail_wgrad_launch(const float* y, const float* hr, const float* loss, const bf16_t* x, int N, int C, int H,
-                      int W, float* slab, int* nslab, hipStream_t st) {
-  if (C < 1 || C > 4 || H % kTailRows) return SRMI_ERR_SHAPE;
+template <typename T>
+static void tail_wgrad_t(const float* y, const float* hr, const float* loss, const T* x, int N, int C, int H, int W,
+                         float* slab, hipStream_t st) {
   const dim3 grid(H / kTailRows, N);
   switch (C) {
-    case 1: hipLaunchKernelGGL(tail_wgrad_lds_kernel<1>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
-    case 2: hipLaunchKernelGGL(tail_wgrad_lds_kernel<2>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
-    case 3: hipLaunchKernelGGL(tail_wgrad_lds_kernel<3>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
-    default: hipLaunchKernelGGL(tail_wgrad_lds_kernel<4>, grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+    case 1: hipLaunchKernelGGL((tail_wgrad_lds_kernel<1, T>), grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+    case 2: hipLaunchKernelGGL((tail_wgrad_lds_kernel<2, T>), grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+    case 3: hipLaunchKernelGGL((tail_wgrad_lds_kernel<3, T>), grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
+    default: hipLaunchKernelGGL((tail_wgrad_lds_kernel<4, T>), grid, dim3(256), 0, st, y, hr, loss, x, H, W, slab); break;
   }
+}
+
+int tail_wgrad_launch(const float* y, const float* hr, const float* loss, const void* x, int N, int C, int H,
+                      int W, float* slab, int* nslab, int f32, hipStream_t st) {
+  if (C < 1 || C > 4 || H % kTailRows) return SRMI_ERR_SHAPE;
+  if (f32)
+    tail_wgrad_t(y, hr, loss, static_cast<const float*>(x), N, C, H, W, slab, st);
+  else
+    tail_wgrad_t(y, hr, loss, static_cast<const bf16_t*>(x), N, C, H, W, slab, st);
   SRMI_CHECK_LAUNCH();
   *nslab = N * (H / kTailRows);
   return 0;
@@ -707,6 +797,32 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
+// 4-channel units of an activation map in either storage type: raw loads kept
+// packed (bf16: one dword pair) until use, written through as one store
+template <typename T>
+struct Unit4;
+template <>
+struct Unit4<bf16_t> {
+  using raw = uint2;
+  static __device__ __forceinline__ raw ld(const bf16_t* p) { return *reinterpret_cast<const uint2*>(p); }
+  static __device__ __forceinline__ float get(const raw& v, int i) {
+    const uint32_t w = i < 2 ? v.x : v.y;
+    return bf2f((i & 1) ? (w >> 16) : (w & 0xFFFF));
+  }
+  static __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, bf16_t* base, size_t e, const float (&o)[4]) {
+    st_wt8(r, base, (uint32_t)(e * 2), make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3])));
+  }
+};
+template <>
+struct Unit4<float> {
+  using raw = float4;
+  static __device__ __forceinline__ raw ld(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  static __device__ __forceinline__ float get(const raw& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+  static __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, float* base, size_t e, const float (&o)[4]) {
+    st_wt16(r, base, (uint32_t)(e * 4), make_float4(o[0], o[1], o[2], o[3]));
+  }
+};
+
 // elementwise passes: each thread handles kCaVec groups of 8 channels (4: the
 // per-block MLP is amortised over 2x the data of the former 2; 18 blocks per
 // 48x48 image, every block resident at once; ca_fwd 22.6 -> 20.0 us, ca_bwd
@@ -716,13 +832,14 @@ __device__ __forceinline__ void lds_barrier() {
 #endif
 constexpr int kCaVec = SRMI_CA_VEC;
 
-// h_out = u * s + h_in  (fp32 + bf16 copy); grid (chunks, N)
-__global__ void __launch_bounds__(256) ca_fwd_kernel(const bf16_t* __restrict__ u, const float* __restrict__ part,
+// h_out = u * s + h_in  (fp32 + operand-type copy); grid (chunks, N)
+template <typename T>
+__global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, const float* __restrict__ part,
                                                      int nstrips, int HW, const float* __restrict__ w1,
                                                      const float* __restrict__ b1, const float* __restrict__ w2,
                                                      const float* __restrict__ b2, int C, int CR,
                                                      const float* __restrict__ h_in, float* __restrict__ h_out,
-                                                     bf16_t* __restrict__ hb_out, float* __restrict__ rec) {
+                                                     T* __restrict__ hb_out, float* __restrict__ rec) {
   __shared__ float red[4][64], m[64], z1[32], s[64];
   const int n = blockIdx.y, tid = threadIdx.x;
   // 1. the MLP operands (L2 hits), issued first so that waiting for them does not
@@ -751,12 +868,12 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const bf16_t* __restrict__ 
   const size_t base = (size_t)n * HW * C;
   const size_t nq = (size_t)HW * C / 4;
   const size_t q0 = ((size_t)blockIdx.x * NU) * blockDim.x + tid;
-  uint2 uu[NU];
+  typename Unit4<T>::raw uu[NU];
   float4 hh[NU];
 #pragma unroll
   for (int k = 0; k < NU; ++k) {  // clamped, unconditional (tail lanes store nothing)
     const size_t e = base + min(q0 + (size_t)k * blockDim.x, nq - 1) * 4;
-    uu[k] = *reinterpret_cast<const uint2*>(u + e);
+    uu[k] = Unit4<T>::ld(u + e);
     hh[k] = *reinterpret_cast<const float4*>(h_in + e);
   }
   __builtin_amdgcn_sched_barrier(0);
@@ -796,7 +913,7 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const bf16_t* __restrict__ 
   // 4. elementwise; lane-contiguous runs written through (common.hpp): the
   //    boundary after this launch then has no dirty residual stream to flush
   const auto rh = wt_rsrc(h_out, (uint32_t)((size_t)gridDim.y * HW * C * 4));
-  const auto rhb = wt_rsrc(hb_out, (uint32_t)((size_t)gridDim.y * HW * C * 2));
+  const auto rhb = wt_rsrc(hb_out, (uint32_t)((size_t)gridDim.y * HW * C * sizeof(T)));
 #pragma unroll
   for (int k = 0; k < NU; ++k) {
     const size_t q = q0 + (size_t)k * blockDim.x;
@@ -804,12 +921,12 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const bf16_t* __restrict__ 
     const size_t e = base + q * 4;
     const int c0 = (int)((q * 4) % C);
     float o[4];
-    o[0] = bf2f(uu[k].x & 0xFFFF) * s[c0 + 0] + hh[k].x;
-    o[1] = bf2f(uu[k].x >> 16) * s[c0 + 1] + hh[k].y;
-    o[2] = bf2f(uu[k].y & 0xFFFF) * s[c0 + 2] + hh[k].z;
-    o[3] = bf2f(uu[k].y >> 16) * s[c0 + 3] + hh[k].w;
+    o[0] = Unit4<T>::get(uu[k], 0) * s[c0 + 0] + hh[k].x;
+    o[1] = Unit4<T>::get(uu[k], 1) * s[c0 + 1] + hh[k].y;
+    o[2] = Unit4<T>::get(uu[k], 2) * s[c0 + 2] + hh[k].z;
+    o[3] = Unit4<T>::get(uu[k], 3) * s[c0 + 3] + hh[k].w;
     st_wt16(rh, h_out, (uint32_t)(e * 4), make_float4(o[0], o[1], o[2], o[3]));
-    st_wt8(rhb, hb_out, (uint32_t)(e * 2), make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3])));
+    Unit4<T>::st(rhb, hb_out, e, o);
   }
 }
 
@@ -819,12 +936,18 @@ static int ca_grid_x(int HW, int C) {
   return gx < 1 ? 1 : gx;
 }
 
-int ca_fwd_launch(const bf16_t* u, const float* part, int nstrips, const float* w1, const float* b1, const float* w2,
-                  const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, bf16_t* hb_out,
-                  float* rec, hipStream_t st) {
+int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1, const float* b1, const float* w2,
+                  const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, void* hb_out,
+                  float* rec, int f32, hipStream_t st) {
   if (C != 64 || C % R || (C / R) > 32 || (C / R) % 4 || (HW * C) % 8) return SRMI_ERR_SHAPE;
-  hipLaunchKernelGGL(ca_fwd_kernel, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, u, part, nstrips, HW, w1, b1, w2,
-                     b2, C, C / R, h_in, h_out, hb_out, rec);
+  if (f32)
+    hipLaunchKernelGGL(ca_fwd_kernel<float>, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st,
+                       static_cast<const float*>(u), part, nstrips, HW, w1, b1, w2, b2, C, C / R, h_in, h_out,
+                       static_cast<float*>(hb_out), rec);
+  else
+    hipLaunchKernelGGL(ca_fwd_kernel<bf16_t>, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st,
+                       static_cast<const bf16_t*>(u), part, nstrips, HW, w1, b1, w2, b2, C, C / R, h_in, h_out,
+                       static_cast<bf16_t*>(hb_out), rec);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
@@ -834,11 +957,12 @@ int ca_fwd_launch(const bf16_t* u, const float* part, int nstrips, const float* 
 // backward while its g loads are in flight; block 0 of the image writes
 // brec per image: dz2[C] dz1[CR] dbconv2[C]; followed (after all N images) by
 // dm[N][C] = W1^T dz1 (the gradient of the pooled mean).
-// du = g * s + dm / HW  (bf16)
+// du = g * s + dm / HW  (operand type)
+template <typename T>
 __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict__ g, const float* __restrict__ part,
                                                         int nstrips, const float* __restrict__ rec,
                                                         const float* __restrict__ w1, const float* __restrict__ w2,
-                                                        int N, int HW, int C, int CR, bf16_t* __restrict__ du,
+                                                        int N, int HW, int C, int CR, T* __restrict__ du,
                                                         float* __restrict__ brec) {
   __shared__ float red[2][128], s[64], dz2[64], dz1[32], dm[64];
   const int n = blockIdx.y, tid = threadIdx.x;
@@ -907,7 +1031,7 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
     }
     if (tid < CR) br[C + tid] = dz1[tid];
   }
-  const auto rdu = wt_rsrc(du, (uint32_t)((size_t)gridDim.y * HW * C * 2));  // lane-contiguous 16 B: write-through
+  const auto rdu = wt_rsrc(du, (uint32_t)((size_t)gridDim.y * HW * C * sizeof(T)));  // lane-contiguous: write-through
 #pragma unroll
   for (int k = 0; k < kCaVec; ++k) {
     const size_t v = v0 + (size_t)k * blockDim.x;
@@ -916,20 +1040,28 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
     float dmh[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) dmh[i] = dm[c0 + i] * (1.f / (float)HW);
-    uint4 ob;
-    ob.x = pack2(g0[k].x * s[c0 + 0] + dmh[0], g0[k].y * s[c0 + 1] + dmh[1]);
-    ob.y = pack2(g0[k].z * s[c0 + 2] + dmh[2], g0[k].w * s[c0 + 3] + dmh[3]);
-    ob.z = pack2(g1[k].x * s[c0 + 4] + dmh[4], g1[k].y * s[c0 + 5] + dmh[5]);
-    ob.w = pack2(g1[k].z * s[c0 + 6] + dmh[6], g1[k].w * s[c0 + 7] + dmh[7]);
-    st_wt16(rdu, du, (uint32_t)((base + v * 8) * 2), ob);
+    const float o[8] = {g0[k].x * s[c0 + 0] + dmh[0], g0[k].y * s[c0 + 1] + dmh[1], g0[k].z * s[c0 + 2] + dmh[2],
+                        g0[k].w * s[c0 + 3] + dmh[3], g1[k].x * s[c0 + 4] + dmh[4], g1[k].y * s[c0 + 5] + dmh[5],
+                        g1[k].z * s[c0 + 6] + dmh[6], g1[k].w * s[c0 + 7] + dmh[7]};
+    if constexpr (sizeof(T) == 2) {
+      const uint4 ob = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+      st_wt16(rdu, du, (uint32_t)((base + v * 8) * 2), ob);
+    } else {
+      st_wt16(rdu, du, (uint32_t)((base + v * 8) * 4), make_float4(o[0], o[1], o[2], o[3]));
+      st_wt16(rdu, du, (uint32_t)((base + v * 8) * 4 + 16), make_float4(o[4], o[5], o[6], o[7]));
+    }
   }
 }
 
 int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
-                     const float* w2, int N, int HW, int C, int R, bf16_t* du, float* brec, hipStream_t st) {
+                     const float* w2, int N, int HW, int C, int R, void* du, float* brec, int f32, hipStream_t st) {
   if (C != 64 || C % R || (C / R) > 32 || (C / R) % 4 || (HW * C) % 8) return SRMI_ERR_SHAPE;
-  hipLaunchKernelGGL(ca_bwd_du_kernel, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, g, part, nstrips, rec, w1, w2, N,
-                     HW, C, C / R, du, brec);
+  if (f32)
+    hipLaunchKernelGGL(ca_bwd_du_kernel<float>, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, g, part, nstrips, rec,
+                       w1, w2, N, HW, C, C / R, static_cast<float*>(du), brec);
+  else
+    hipLaunchKernelGGL(ca_bwd_du_kernel<bf16_t>, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, g, part, nstrips, rec,
+                       w1, w2, N, HW, C, C / R, static_cast<bf16_t*>(du), brec);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
@@ -1033,9 +1165,10 @@ int adam_launch(float* p, const float* g, float* m, float* v, size_t n, float lr
 // taps flipped (dgrad == forward conv of dY with W'[ci][co][8-tap]); PixelShuffle
 // convs store output channel c'' = 64q + c for torch channel 4c + q, so each
 // 64-wide output block is one sub-pixel position.
+template <typename T>
 __device__ __forceinline__ void pack_elem(const float* __restrict__ W, const float* __restrict__ B, int Cout, int Cin,
-                                          int ps, int which, long long idx, bf16_t* __restrict__ fpack,
-                                          bf16_t* __restrict__ dpack, float* __restrict__ pbias) {
+                                          int ps, int which, long long idx, T* __restrict__ fpack,
+                                          T* __restrict__ dpack, float* __restrict__ pbias) {
   if (which == 0) {
     const int ci_l = idx & 63;
     long long rest = idx >> 6;
@@ -1043,7 +1176,7 @@ __device__ __forceinline__ void pack_elem(const float* __restrict__ W, const flo
     rest /= Cout;
     const int tap = rest % 9, cc = (int)(rest / 9);
     const int cot = ps ? (4 * (cop & 63) + (cop >> 6)) : cop;
-    fpack[idx] = f2bf(W[((size_t)cot * Cin + cc * 64 + ci_l) * 9 + tap]);
+    fpack[idx] = from_f32<T>(W[((size_t)cot * Cin + cc * 64 + ci_l) * 9 + tap]);
   } else if (which == 1) {
     const int co_l = idx & 63;
     long long rest = idx >> 6;
@@ -1052,7 +1185,7 @@ __device__ __forceinline__ void pack_elem(const float* __restrict__ W, const flo
     const int tapd = rest % 9, ccd = (int)(rest / 9);
     const int cop = ccd * 64 + co_l;
     const int cot = ps ? (4 * (cop & 63) + (cop >> 6)) : cop;
-    dpack[idx] = f2bf(W[((size_t)cot * Cin + ci) * 9 + (8 - tapd)]);
+    dpack[idx] = from_f32<T>(W[((size_t)cot * Cin + ci) * 9 + (8 - tapd)]);
   } else if (idx < Cout) {
     const int cop = (int)idx;
     const int cot = ps ? (4 * (cop & 63) + (cop >> 6)) : cop;
@@ -1060,8 +1193,9 @@ __device__ __forceinline__ void pack_elem(const float* __restrict__ W, const flo
   }
 }
 
+template <typename T>
 __global__ void pack_kernel(const float* __restrict__ params, const PackEntry* __restrict__ ents,
-                            bf16_t* __restrict__ packs, float* __restrict__ pbias) {
+                            T* __restrict__ packs, float* __restrict__ pbias) {
   const PackEntry e = ents[blockIdx.y];
   const long long total = (long long)e.Cout * e.Cin * 9;
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
@@ -1070,31 +1204,40 @@ __global__ void pack_kernel(const float* __restrict__ params, const PackEntry* _
               packs + e.d_off, pbias + e.pb_off);
 }
 
-int pack_launch(const float* params, const PackEntry* dev_entries, int nentries, long long max_elems, bf16_t* packs,
-                float* pbias, hipStream_t st) {
+int pack_launch(const float* params, const PackEntry* dev_entries, int nentries, long long max_elems, void* packs,
+                float* pbias, int f32, hipStream_t st) {
   long long bx = (max_elems + 255) / 256;
   if (bx > 1024) bx = 1024;
-  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)bx, nentries, 3), dim3(256), 0, st, params, dev_entries, packs,
-                     pbias);
+  if (f32)
+    hipLaunchKernelGGL(pack_kernel<float>, dim3((unsigned)bx, nentries, 3), dim3(256), 0, st, params, dev_entries,
+                       static_cast<float*>(packs), pbias);
+  else
+    hipLaunchKernelGGL(pack_kernel<bf16_t>, dim3((unsigned)bx, nentries, 3), dim3(256), 0, st, params, dev_entries,
+                       static_cast<bf16_t*>(packs), pbias);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
 
+template <typename T>
 __global__ void pack_one_kernel(const float* __restrict__ W, const float* __restrict__ B, int Cout, int Cin, int ps,
-                                bf16_t* __restrict__ fpack, bf16_t* __restrict__ dpack, float* __restrict__ pbias) {
+                                T* __restrict__ fpack, T* __restrict__ dpack, float* __restrict__ pbias) {
   const long long total = (long long)Cout * Cin * 9;
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x)
     pack_elem(W, B, Cout, Cin, ps, blockIdx.y, idx, fpack, dpack, pbias);
 }
 
-int pack_one_launch(const float* w, const float* b, int Cout, int Cin, int ps, bf16_t* fpack, bf16_t* dpack,
-                    float* pbias, hipStream_t st) {
+int pack_one_launch(const float* w, const float* b, int Cout, int Cin, int ps, void* fpack, void* dpack,
+                    float* pbias, int f32, hipStream_t st) {
   if (Cout % 64 || Cin % 64) return SRMI_ERR_SHAPE;
   long long bx = ((long long)Cout * Cin * 9 + 255) / 256;
   if (bx > 1024) bx = 1024;
-  hipLaunchKernelGGL(pack_one_kernel, dim3((unsigned)bx, 3), dim3(256), 0, st, w, b, Cout, Cin, ps, fpack, dpack,
-                     pbias);
+  if (f32)
+    hipLaunchKernelGGL(pack_one_kernel<float>, dim3((unsigned)bx, 3), dim3(256), 0, st, w, b, Cout, Cin, ps,
+                       static_cast<float*>(fpack), static_cast<float*>(dpack), pbias);
+  else
+    hipLaunchKernelGGL(pack_one_kernel<bf16_t>, dim3((unsigned)bx, 3), dim3(256), 0, st, w, b, Cout, Cin, ps,
+                       static_cast<bf16_t*>(fpack), static_cast<bf16_t*>(dpack), pbias);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

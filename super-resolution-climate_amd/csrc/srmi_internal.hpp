@@ -42,10 +42,13 @@ struct ConvParams {
   const void* zeros;   // >= 16 zero bytes in global memory (DMA padding source)
   unsigned long long* stamps;  // diagnostic s_memtime stamps (null in production)
   int cu_budget;               // CUs a launch should fill (0 = all 256)
+  int f32;                     // exact-fp32 mode: x, w, yb, aux point at fp32 data
+                               // (the bf16_t* fields are plain addresses then)
 };
 
 void conv3x3_set_debug_stamps(unsigned long long* buf);
-int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st);
+int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st);  // dispatches p.f32
+int conv3x3_f32_launch(const ConvParams& p, int epi, hipStream_t st);
 int conv3x3_nstrips(int H, int W);
 
 // weight gradient of a 3x3 conv: slab[s][Cout][9][64] + bias slab[s][Cout]
@@ -60,9 +63,11 @@ struct WgradParams {
   float* bslab;        // [nslab][Cout]
   const void* zeros;   // >= 16 zero bytes in global memory (DMA source for padding)
   unsigned long long* stamps;  // diagnostic (null in production)
+  int f32;             // exact-fp32 mode: x, dy point at fp32 data
 };
 void wgrad3x3_set_debug_stamps(unsigned long long* buf);
-int wgrad3x3_launch(const WgradParams& p, hipStream_t st);
+int wgrad3x3_launch(const WgradParams& p, hipStream_t st);  // dispatches p.f32
+int wgrad_f32_launch(const WgradParams& p, hipStream_t st);
 int wgrad3x3_nslabs(const WgradParams& p);
 // order of the partial slabs the launch writes: 0 = [tap][ci][Cout], 1 = wgrad48's
 // MFMA-native [Cout/64][wave][9][4][lane][4]
@@ -82,19 +87,20 @@ int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Co
                         float* gw, float* gb, hipStream_t st);
 
 // small-channel kernels (head / tail), bicubic resampling, loss, CA, Adam, packing
+// f32 != 0: the operand-type outputs / inputs below are fp32 (exact-fp32 engine mode)
 int head_fwd_launch(const float* lr, const float* w, const float* b, int N, int C, int H, int W, float* x0f,
-                    bf16_t* x0b, hipStream_t st);
+                    void* x0b, int f32, hipStream_t st);
 int head_wgrad_launch(const float* lr, const float* g, int N, int C, int H, int W, float* slab, int* nslab,
                       hipStream_t st);
 int head_wgrad_reduce_launch(const float* slab, int nslab, int C, float* gw, float* gb, hipStream_t st);
 
-int tail_fwd_launch(const bf16_t* x, const float* w, const float* b, int N, int C, int H, int W, float* y,
+int tail_fwd_launch(const void* x, const float* w, const float* b, int N, int C, int H, int W, float* y, int f32,
                     hipStream_t st);
 // dy is formed on the fly: dy = (y - hr) * scale, scale from loss[2]
 int tail_dgrad_launch(const float* y, const float* hr, const float* loss, const float* w, int N, int C, int H,
-                      int W, bf16_t* dx, hipStream_t st);
-int tail_wgrad_launch(const float* y, const float* hr, const float* loss, const bf16_t* x, int N, int C, int H,
-                      int W, float* slab, int* nslab, hipStream_t st);
+                      int W, void* dx, int f32, hipStream_t st);
+int tail_wgrad_launch(const float* y, const float* hr, const float* loss, const void* x, int N, int C, int H,
+                      int W, float* slab, int* nslab, int f32, hipStream_t st);
 int tail_wgrad_reduce_launch(const float* slab, int nslab, int C, float* gw, float* gb, hipStream_t st);
 
 int downsample_launch(const float* hr, int N, int C, int H, int W, int scale, float* lr, hipStream_t st);
@@ -111,11 +117,11 @@ int charb_partial_launch(const float* y, const float* t, size_t n, float eps, do
                          float* partial, int nblk, hipStream_t st);
 
 // channel attention
-int ca_fwd_launch(const bf16_t* u, const float* part, int nstrips, const float* w1, const float* b1,
+int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1, const float* b1,
                   const float* w2, const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out,
-                  bf16_t* hb_out, float* rec, hipStream_t st);
+                  void* hb_out, float* rec, int f32, hipStream_t st);
 int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
-                     const float* w2, int N, int HW, int C, int R, bf16_t* du, float* brec, hipStream_t st);
+                     const float* w2, int N, int HW, int C, int R, void* du, float* brec, int f32, hipStream_t st);
 // records of consecutive RCABs Ncap images apart (the engine capacity), N summed
 int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int Ncap, int C, int R,
                                   const long long* offs, float* grads, hipStream_t st);
@@ -132,10 +138,10 @@ struct PackEntry {
   int Cout, Cin, ps, pad;
 };
 int pack_launch(const float* params, const PackEntry* dev_entries, int nentries, long long max_elems,
-                bf16_t* packs, float* pbias, hipStream_t st);
+                void* packs, float* pbias, int f32, hipStream_t st);
 
-int pack_one_launch(const float* w, const float* b, int Cout, int Cin, int ps, bf16_t* fpack, bf16_t* dpack,
-                    float* pbias, hipStream_t st);
+int pack_one_launch(const float* w, const float* b, int Cout, int Cin, int ps, void* fpack, void* dpack,
+                    float* pbias, int f32, hipStream_t st);
 
 int scale_add_launch(float* y, const float* x, float a, size_t n, hipStream_t st);
 

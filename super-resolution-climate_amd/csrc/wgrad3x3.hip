@@ -490,9 +490,10 @@ static bool use_wgrad48(const WgradParams& p) {
   return p.W == 48 && p.row_splits > 0 && (p.H / p.row_splits) % 2 == 0;
 }
 
-int wgrad3x3_slab_layout(const WgradParams& p) { return use_wgrad48(p) ? 1 : 0; }
+int wgrad3x3_slab_layout(const WgradParams& p) { return !p.f32 && use_wgrad48(p) ? 1 : 0; }
 
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
+  if (p.f32) return wgrad_f32_launch(p, st);
   if (p.Cout % 64 || p.H % p.row_splits || (p.H / p.row_splits) % 4) return SRMI_ERR_SHAPE;
   if (p.dy_mode == IN_UNSHUF && p.Cout != 256) return SRMI_ERR_SHAPE;
   dim3 grid(wgrad3x3_nslabs(p), p.Cout / 64);

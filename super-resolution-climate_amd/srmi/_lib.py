@@ -15,6 +15,8 @@ LIB_PATH = os.environ.get("SRMI_LIB") or os.path.join(_HERE, "libsrmi.so")  # SR
 
 SRMI_ARCH_RCAN = 0
 SRMI_ARCH_EDSR = 1
+SRMI_DTYPE_BF16 = 0
+SRMI_DTYPE_F32 = 1
 SRMI_LOSS_RMSE = 0
 SRMI_LOSS_MEAN = 1
 
@@ -26,7 +28,7 @@ class ModelConfig(C.Structure):
     _fields_ = [("arch", C.c_int), ("nchannels_in", C.c_int), ("nchannels_out", C.c_int),
                 ("nfeatures", C.c_int), ("nlayers", C.c_int), ("nblocks", C.c_int), ("reduction", C.c_int),
                 ("scale", C.c_int), ("res_scale", C.c_float), ("batch", C.c_int), ("lr_h", C.c_int),
-                ("lr_w", C.c_int), ("cu_budget", C.c_int)]
+                ("lr_w", C.c_int), ("cu_budget", C.c_int), ("dtype", C.c_int)]
 
 
 class ParamInfo(C.Structure):
@@ -56,17 +58,18 @@ _SIGS = {
     "srmi_adam_step": ([P, P, P, P, C.c_size_t, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, P],
                        C.c_int),
     "srmi_conv3x3": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P,
-                      C.c_float, P], C.c_int),
+                      C.c_float, C.c_int, P], C.c_int),
     "srmi_conv3x3_nstrips": ([C.c_int, C.c_int], C.c_int),
     "srmi_debug_conv_stamps": ([P], C.c_int),
     "srmi_debug_wgrad_stamps": ([P], C.c_int),
-    "srmi_pack_conv": ([P, P, C.c_int, C.c_int, C.c_int, P, P, P, P], C.c_int),
+    "srmi_pack_conv": ([P, P, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int, P], C.c_int),
     "srmi_wgrad3x3": ([P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_size_t, C.c_int, C.c_float,
-                       P, P, P], C.c_int),
-    "srmi_ca_forward": ([P, P, C.c_int, P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P], C.c_int),
-    "srmi_ca_backward": ([P, P, C.c_int, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P], C.c_int),
-    "srmi_head_forward": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P], C.c_int),
-    "srmi_tail_forward": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),
+                       P, P, C.c_int, P], C.c_int),
+    "srmi_ca_forward": ([P, P, C.c_int, P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, C.c_int, P],
+                        C.c_int),
+    "srmi_ca_backward": ([P, P, C.c_int, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, C.c_int, P], C.c_int),
+    "srmi_head_forward": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, C.c_int, P], C.c_int),
+    "srmi_tail_forward": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int, P], C.c_int),
     "srmi_axpy": ([P, P, C.c_float, C.c_size_t, P], C.c_int),
     "srmi_region_to_tiles": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P], C.c_int),
     "srmi_tiles_to_region": ([P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),

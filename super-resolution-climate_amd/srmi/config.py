@@ -27,7 +27,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 CONFIG_DIR = os.path.join(os.path.dirname(_HERE), "config")
 
 COMMON_PARMS = dict(nchannels_in=1, nchannels_out=1, nfeatures=64, kernel_size=3, nlayers=16,
-                    downscale_factors=[2, 2], bias=True, batch_norm=False, res_scale=1.0, ups_mode="bicubic")
+                    downscale_factors=[2, 2], bias=True, batch_norm=False, res_scale=1.0, ups_mode="bicubic",
+                    # srmi's own key (absent from the reference yaml): the engine's operand type,
+                    # "bf16" (bf16 MFMA operands, fp32 accumulate) or "fp32" (exact fp32)
+                    dtype="bf16")
 MODEL_PARMS = {"rcan": dict(cbottleneck=2, nblocks=20), "edsr": {}}
 
 

@@ -20,6 +20,7 @@ from . import _lib
 from ._lib import ModelConfig, ParamInfo, call, ptr, stream_handle
 
 ARCHS = {"rcan": _lib.SRMI_ARCH_RCAN, "edsr": _lib.SRMI_ARCH_EDSR}
+DTYPES = {"bf16": _lib.SRMI_DTYPE_BF16, "fp32": _lib.SRMI_DTYPE_F32}
 
 
 @dataclass
@@ -34,9 +35,10 @@ class NetSpec:
     cbottleneck: int = 2
     scale: int = 4
     res_scale: float = 1.0
+    dtype: str = "bf16"   # engine operand type: "bf16" (bf16 MFMA operands) or "fp32" (exact fp32)
 
     @staticmethod
-    def from_parms(arch: str, parms: Dict) -> "NetSpec":
+    def from_parms(arch: str, parms: Dict, dtype: str = "bf16") -> "NetSpec":
         if parms.get("kernel_size", 3) != 3:
             raise _lib.SrmiError("srmi supports kernel_size 3 only")
         if parms.get("batch_norm", False):
@@ -46,12 +48,14 @@ class NetSpec:
         return NetSpec(arch=arch, nchannels_in=int(parms["nchannels_in"]), nchannels_out=int(parms["nchannels_out"]),
                        nfeatures=int(parms["nfeatures"]), nlayers=int(parms["nlayers"]),
                        nblocks=int(parms.get("nblocks", 0) or 0), cbottleneck=int(parms.get("cbottleneck", 2) or 2),
-                       scale=int(parms["scale"]), res_scale=float(parms.get("res_scale", 1.0)))
+                       scale=int(parms["scale"]), res_scale=float(parms.get("res_scale", 1.0)), dtype=dtype)
 
     def cstruct(self, batch: int, lr_h: int, lr_w: int, cu_budget: int = 0) -> ModelConfig:
+        if self.dtype not in DTYPES:
+            raise _lib.SrmiError(f"unknown engine dtype {self.dtype!r} (bf16 | fp32)")
         return ModelConfig(ARCHS[self.arch], self.nchannels_in, self.nchannels_out, self.nfeatures, self.nlayers,
                            self.nblocks if self.arch == "rcan" else 0, self.cbottleneck if self.arch == "rcan" else 1,
-                           self.scale, self.res_scale, batch, lr_h, lr_w, int(cu_budget))
+                           self.scale, self.res_scale, batch, lr_h, lr_w, int(cu_budget), DTYPES[self.dtype])
 
 
 def param_names(spec: NetSpec) -> List[str]:

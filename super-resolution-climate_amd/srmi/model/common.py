@@ -61,7 +61,7 @@ class SRNet(nn.Module):
         custom = {k: v for k, v in kwargs.items()}
         parms = init_parms(self.arch, custom)
         self.parms = parms
-        self.spec = NetSpec.from_parms(self.arch, parms)
+        self.spec = NetSpec.from_parms(self.arch, parms, dtype=str(parms.get("dtype", "bf16")))
         self._table = None
         self._n_params = 0
         self._engines: Dict[Tuple[bool, int, int], Engine] = {}

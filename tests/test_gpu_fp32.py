@@ -1,0 +1,151 @@
+"""The exact-fp32 engine mode (SRMI_DTYPE_F32, v_mfma_f32_16x16x4_f32) against the
+reference's own fp32/fp64 arithmetic: north-star "outputs match the reference
+PyTorch model on identical inputs within 1e-5 relative fp32" and BASELINE config
+4 (EDSR x8, fp32).
+
+Tolerances (measured on the reference): its fp32 forward drifts
+5.5e-7 rel-L2 from fp64 and its loss 1.5e-8, so outputs are held to 1e-5 rel-L2
+and losses to 1e-5 rel; its fp32 parameter gradients drift up to 3.3e-4 rel-L2 per
+tensor from fp64, so gradients are held to 1e-3 rel-L2 per tensor."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from gpu_oracle import exact_fp32  # noqa: E402
+from oracle import rcan_oracle as ro  # noqa: E402
+from srmi.engine import Engine, NetSpec, downsample, param_table  # noqa: E402
+from srmi.trainer import FusedTrainer  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def dev():
+    assert torch.cuda.is_available()
+    return torch.device("cuda", 0)
+
+
+def rel_l2(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def _flat(model, table):
+    sd = dict(model.named_parameters())
+    return torch.cat([sd[n].detach().reshape(-1).float() for n, _, _, _ in table])
+
+
+def _spec(arch, C, nl, nb=0, scale=4):
+    return NetSpec(arch=arch, nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=nl, nblocks=nb, cbottleneck=2,
+                   scale=scale, dtype="fp32")
+
+
+@pytest.mark.parametrize("arch,C,nl,nb,scale,S,B,gname", [
+    ("rcan", 1, 2, 2, 4, 192, 2, "rcan_small_c1_f64.npz"),
+    ("rcan", 2, 2, 2, 4, 192, 2, "rcan_small_c2_f64.npz"),
+    ("edsr", 4, 2, 0, 8, 256, 1, "edsr_small_c4_f64.npz"),
+])
+def test_fp32_small_model_step_vs_golden(arch, C, nl, nb, scale, S, B, gname):
+    d = dev()
+    gd = np.load(os.path.join(GOLDEN, gname))
+    kw = dict(nchannels_in=C, nchannels_out=C, nlayers=nl, nfeatures=64)
+    model = (ro.RCANOracle(nblocks=nb, cbottleneck=2, **kw) if arch == "rcan"
+             else ro.EDSROracle(downscale_factors=[2, 2, 2], **kw))
+    ro.init_params_numpy(model, int(gd["seed_w"]))
+    spec = _spec(arch, C, nl, nb, scale)
+    table = param_table(spec)
+    tr = FusedTrainer(spec, B, (S // scale, S // scale), lr=float(gd["lr"]), device=d,
+                      params=_flat(model, table).to(d))
+    model = model.double()
+    hr = ro.synthetic_hr(B, C, S, int(gd["seed_x"]))
+    model.zero_grad()
+    h = torch.tensor(hr, dtype=torch.float64)
+    loss_ref = ro.l2loss(model(ro.downsample(h, scale)), h)
+    loss_ref.backward()
+    res = tr.step(torch.tensor(hr, device=d))
+    torch.cuda.synchronize()
+    assert abs(float(res["loss"]) - float(gd["loss0"])) / float(gd["loss0"]) < 1e-5
+    assert abs(float(res["interp_loss"]) - float(gd["iloss0"])) / float(gd["iloss0"]) < 1e-5
+    assert rel_l2(tr.sr[:B].cpu()[:, :, ::4, ::4], gd["out_sub"]) < 1e-5
+    grads = tr.grads.cpu()
+    g = dict(model.named_parameters())
+    worst = max(rel_l2(grads[off:off + n].view(shape), g[name].grad) for name, off, n, shape in table)
+    print(f"\n{gname}: fp32 engine worst per-tensor grad rel-L2 {worst:.2e}")
+    assert worst < 1e-3
+    np.testing.assert_allclose(np.array([float(grads[o:o + n].norm()) for _, o, n, _ in table]), gd["grad_l2"],
+                               rtol=1e-3)
+    res = tr.step(torch.tensor(hr, device=d))
+    torch.cuda.synchronize()
+    assert abs(float(res["loss"]) - float(gd["loss1"])) / float(gd["loss1"]) < 1e-5
+
+
+def test_fp32_full_rcan_vs_golden():
+    """rcan-10-20-64, 2-var, one tile, exact fp32: output and loss vs the fp64 golden
+    of the reference, and the golden's gradient samples."""
+    d = dev()
+    gd = np.load(os.path.join(GOLDEN, "rcan_full_c2_f64.npz"))
+    m = ro.RCANOracle(nchannels_in=2, nchannels_out=2, nlayers=10, nblocks=20, nfeatures=64, cbottleneck=2)
+    ro.init_params_numpy(m, int(gd["seed_w"]))
+    spec = _spec("rcan", 2, 10, 20)
+    table = param_table(spec)
+    flat = _flat(m, table).to(d)
+    hr = torch.tensor(ro.synthetic_hr(1, 2, 192, int(gd["seed_x"])), device=d)
+    eng = Engine(spec, 1, (48, 48), train=False, device=d)
+    eng.pack(flat)
+    out = eng.forward(flat, downsample(hr, 4))
+    torch.cuda.synchronize()
+    r_out = rel_l2(out.cpu()[:, :, ::4, ::4], gd["out_sub"])
+    loss = float(((out.double() - hr.double()) ** 2).mean().sqrt())
+    print(f"\nfull rcan fp32: output rel-L2 {r_out:.2e}, loss rel {abs(loss - float(gd['loss0'])) / float(gd['loss0']):.2e}")
+    assert r_out < 1e-5
+    assert abs(loss - float(gd["loss0"])) / float(gd["loss0"]) < 1e-5
+    tr = FusedTrainer(spec, 1, (48, 48), lr=float(gd["lr"]), device=d, params=flat)
+    tr.step(hr)
+    torch.cuda.synchronize()
+    g = tr.grads.double().cpu().numpy()
+    eng_s, per, k = [], [], 0
+    ref = gd["grad_sample"]
+    for name, off, n, shape in table:
+        idx = np.unique(np.linspace(0, n - 1, min(n, 48)).astype(np.int64))
+        a = g[off + idx]
+        b = ref[k:k + idx.size]
+        per.append(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+        eng_s.append(a)
+        k += idx.size
+    r_all = np.linalg.norm(np.concatenate(eng_s) - ref) / np.linalg.norm(ref)
+    print(f"full rcan fp32: grad samples rel-L2 {r_all:.2e}, per-tensor max {max(per):.2e}")
+    assert r_all < 1e-3
+    assert np.median(per) < 1e-3 and max(per) < 1e-2
+
+
+@pytest.mark.timeout(600)
+def test_c4_edsr_x8_fp32_full_config_vs_oracle():
+    """BASELINE config 4 itself: EDSR, 16 ResBlocks, 64 features, x8 (32 -> 256),
+    4 channels, fp32 -- one train step against the oracle in fp32 on the GPU."""
+    d = dev()
+    B = 4
+    spec = _spec("edsr", 4, 16, 0, 8)
+    table = param_table(spec)
+    hr = torch.tensor(ro.synthetic_hr(B, 4, 256, 77), device=d)
+    with exact_fp32():
+        m = ro.EDSROracle(nchannels_in=4, nchannels_out=4, nlayers=16, nfeatures=64, downscale_factors=[2, 2, 2])
+        ro.init_params_numpy(m, 3)
+        m = m.to(d)
+        flat = _flat(m, table)
+        lr_in = ro.downsample(hr, 8)
+        out_ref = m(lr_in)
+        loss_ref = ro.l2loss(out_ref, hr)
+        loss_ref.backward()
+        g = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    tr = FusedTrainer(spec, B, (32, 32), lr=1e-4, device=d, params=flat)
+    res = tr.step(hr)
+    torch.cuda.synchronize()
+    assert abs(float(res["loss"]) - float(loss_ref)) / float(loss_ref) < 1e-5
+    assert rel_l2(tr.sr, out_ref.detach()) < 1e-5
+    worst = max(rel_l2(tr.grads[off:off + n].view(shape), g[name]) for name, off, n, shape in table)
+    print(f"\nC4 EDSR x8 fp32: loss {float(res['loss']):.7f} vs {float(loss_ref):.7f}, worst grad rel-L2 {worst:.2e}")
+    assert worst < 1e-3

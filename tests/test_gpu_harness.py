@@ -74,8 +74,8 @@ def test_short_batch_equals_exact_batch():
     # fp32 partial sums in another order (as in test_gpu_dp)
     assert rel_l2(a.grads, b.grads) < 2e-4
     # one tile: the second engine gets no tiles at all
-    r1 = a.step(hr[:1])
     c = FusedTrainer(spec, 1, (48, 48), device=d, params=a.params.clone(), micro=1)
+    r1 = a.step(hr[:1])
     rc = c.step(hr[:1])
     torch.cuda.synchronize()
     assert abs(float(r1["loss"]) - float(rc["loss"])) <= 1e-6 * float(rc["loss"])

@@ -1,5 +1,8 @@
 """Kernel-level parity of the HIP conv / wgrad / CA / resampling / Adam kernels
-against fp64 references of the same op (on the same bf16-rounded operands)."""
+against fp64 references of the same op, in both engine operand types: bf16
+(references on the same bf16-rounded operands; bf16 outputs within 4e-3 rel-L2)
+and exact fp32 (SRMI_DTYPE_F32: outputs within 1e-5 rel-L2 of fp64, the
+north-star's fp32 tolerance)."""
 import math
 
 import numpy as np
@@ -28,16 +31,27 @@ def rel_l2(a, b):
     return float((a - b).norm() / max(b.norm(), 1e-30))
 
 
+DTS = ["bf16", "fp32"]
+TORCH_DT = {"bf16": torch.bfloat16, "fp32": torch.float32}
+ABI_DT = {"bf16": _lib.SRMI_DTYPE_BF16, "fp32": _lib.SRMI_DTYPE_F32}
+TOL = {"bf16": 4e-3, "fp32": 1e-5}   # rel-L2 of operand-type outputs vs fp64
+
+
 def bf(t):
     return t.to(torch.bfloat16)
 
 
-def pack(w, b, ps=0):
+def op(t, dt):
+    """an operand in the engine's storage type"""
+    return t.to(TORCH_DT[dt])
+
+
+def pack(w, b, ps=0, dt="bf16"):
     Cout, Cin = w.shape[0], w.shape[1]
-    fp = torch.empty(Cout * Cin * 9, dtype=torch.bfloat16, device=w.device)
+    fp = torch.empty(Cout * Cin * 9, dtype=TORCH_DT[dt], device=w.device)
     dp = torch.empty_like(fp)
     pb = torch.empty(Cout, dtype=torch.float32, device=w.device)
-    call("srmi_pack_conv", ptr(w), ptr(b), Cout, Cin, ps, ptr(fp), ptr(dp), ptr(pb), S())
+    call("srmi_pack_conv", ptr(w), ptr(b), Cout, Cin, ps, ptr(fp), ptr(dp), ptr(pb), ABI_DT[dt], S())
     return fp, dp, pb
 
 
@@ -58,144 +72,156 @@ SHAPES = [(2, 48, 48), (1, 8, 96), (1, 4, 32), (2, 12, 64), (64, 48, 48), (16, 9
 
 
 def conv(x, fp, pb, N, H, W, Cin, Cout, epi, unshuf=0, yb=None, yf=None, r1=None, r2=None, r3=None, aux=None,
-         part=None, alpha=1.0):
+         part=None, alpha=1.0, dt="bf16"):
     call("srmi_conv3x3", ptr(x), ptr(fp), ptr(pb), N, H, W, Cin, Cout, unshuf, epi, ptr(yb), ptr(yf), ptr(r1), ptr(r2),
-         ptr(r3), ptr(aux), ptr(part), float(alpha), S())
+         ptr(r3), ptr(aux), ptr(part), float(alpha), ABI_DT[dt], S())
 
 
+def wref(w, dt):
+    """the filter as the kernel sees it (bf16-rounded in the bf16 mode)"""
+    return (bf(w) if dt == "bf16" else w).double().cpu()
+
+
+@pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("N,H,W", SHAPES)
-def test_conv_forward_epilogues(N, H, W):
+def test_conv_forward_epilogues(N, H, W, dt):
     d = dev()
     g = torch.Generator(device="cpu").manual_seed(1)
-    x = bf(torch.randn(N, H, W, 64, generator=g)).to(d)
+    x = op(torch.randn(N, H, W, 64, generator=g), dt).to(d)
     w = (torch.randn(64, 64, 3, 3, generator=g) * 0.06).to(d)
     b = (torch.randn(64, generator=g) * 0.1).to(d)
-    fp, dp, pb = pack(w, b)
-    ref = Fn.conv2d(nchw(x).double().cpu(), bf(w).double().cpu(), b.double().cpu(), padding=1)
+    fp, dp, pb = pack(w, b, dt=dt)
+    ref = Fn.conv2d(nchw(x).double().cpu(), wref(w, dt), b.double().cpu(), padding=1)
     ref = nhwc(ref)
-    # relu -> bf16
-    yb = torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=d)
-    conv(x, fp, pb, N, H, W, 64, 64, 0, yb=yb)
-    assert rel_l2(yb.float(), ref.clamp_min(0)) < 4e-3
-    # pool: bf16 + per-strip channel sums
+    # relu -> operand type
+    yb = torch.empty(N, H, W, 64, dtype=TORCH_DT[dt], device=d)
+    conv(x, fp, pb, N, H, W, 64, 64, 0, yb=yb, dt=dt)
+    assert rel_l2(yb.float(), ref.clamp_min(0)) < TOL[dt]
+    # pool: + per-strip channel sums
     ns = call("srmi_conv3x3_nstrips", H, W)
     part = torch.zeros(N, ns, 64, device=d)
-    conv(x, fp, pb, N, H, W, 64, 64, 1, yb=yb, part=part)
-    assert rel_l2(yb.float(), ref) < 4e-3
+    conv(x, fp, pb, N, H, W, 64, 64, 1, yb=yb, part=part, dt=dt)
+    assert rel_l2(yb.float(), ref) < TOL[dt]
     np.testing.assert_allclose(part.sum(1).double().cpu().numpy(), ref.sum((1, 2)).numpy(), rtol=1e-4, atol=1e-3)
     # resid: alpha*(conv+b) + r1 -> fp32 exact-ish
     r1 = torch.randn(N, H, W, 64, generator=g).to(d)
     yf = torch.empty(N, H, W, 64, device=d)
-    conv(x, fp, pb, N, H, W, 64, 64, 2, yb=yb, yf=yf, r1=r1, alpha=0.5)
+    conv(x, fp, pb, N, H, W, 64, 64, 2, yb=yb, yf=yf, r1=r1, alpha=0.5, dt=dt)
     exp = 0.5 * ref + r1.double().cpu()
     np.testing.assert_allclose(yf.double().cpu().numpy(), exp.numpy(), rtol=1e-5, atol=2e-5)
-    assert rel_l2(yb.float(), exp) < 4e-3
+    assert rel_l2(yb.float(), exp) < TOL[dt]
 
 
-@pytest.mark.parametrize("N,H,W", [(2, 48, 48), (1, 4, 96)])
-def test_conv_pixelshuffle_forward(N, H, W):
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("N,H,W", [(2, 48, 48), (1, 4, 96), (2, 8, 32)])
+def test_conv_pixelshuffle_forward(N, H, W, dt):
     d = dev()
     g = torch.Generator(device="cpu").manual_seed(2)
-    x = bf(torch.randn(N, H, W, 64, generator=g)).to(d)
+    x = op(torch.randn(N, H, W, 64, generator=g), dt).to(d)
     w = (torch.randn(256, 64, 3, 3, generator=g) * 0.06).to(d)
     b = (torch.randn(256, generator=g) * 0.1).to(d)
-    fp, dp, pb = pack(w, b, ps=1)
-    y = torch.empty(N, 2 * H, 2 * W, 64, dtype=torch.bfloat16, device=d)
-    conv(x, fp, pb, N, H, W, 64, 256, 3, yb=y)
-    ref = Fn.pixel_shuffle(Fn.conv2d(nchw(x).double().cpu(), bf(w).double().cpu(), b.double().cpu(), padding=1), 2)
-    assert rel_l2(y.float(), nhwc(ref)) < 4e-3
+    fp, dp, pb = pack(w, b, ps=1, dt=dt)
+    y = torch.empty(N, 2 * H, 2 * W, 64, dtype=TORCH_DT[dt], device=d)
+    conv(x, fp, pb, N, H, W, 64, 256, 3, yb=y, dt=dt)
+    ref = Fn.pixel_shuffle(Fn.conv2d(nchw(x).double().cpu(), wref(w, dt), b.double().cpu(), padding=1), 2)
+    assert rel_l2(y.float(), nhwc(ref)) < TOL[dt]
 
 
+@pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("N,H,W", SHAPES)
-def test_conv_dgrad_epilogues(N, H, W):
+def test_conv_dgrad_epilogues(N, H, W, dt):
     d = dev()
     g = torch.Generator(device="cpu").manual_seed(3)
     w = (torch.randn(64, 64, 3, 3, generator=g) * 0.06).to(d)
     b = torch.zeros(64, device=d)
-    fp, dp, pb = pack(w, b)
-    dy = bf(torch.randn(N, H, W, 64, generator=g)).to(d)
-    ref = torch.nn.grad.conv2d_input((N, 64, H, W), bf(w).double().cpu(), nchw(dy).double().cpu(), padding=1)
+    fp, dp, pb = pack(w, b, dt=dt)
+    dy = op(torch.randn(N, H, W, 64, generator=g), dt).to(d)
+    ref = torch.nn.grad.conv2d_input((N, 64, H, W), wref(w, dt), nchw(dy).double().cpu(), padding=1)
     ref = nhwc(ref)
-    out = torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=d)
-    conv(dy, dp, None, N, H, W, 64, 64, 6, yb=out)
-    assert rel_l2(out.float(), ref) < 4e-3
+    out = torch.empty(N, H, W, 64, dtype=TORCH_DT[dt], device=d)
+    conv(dy, dp, None, N, H, W, 64, 64, 6, yb=out, dt=dt)
+    assert rel_l2(out.float(), ref) < TOL[dt]
     # relu mask with t
-    t = bf(torch.randn(N, H, W, 64, generator=g).clamp_min(0)).to(d)
-    conv(dy, dp, None, N, H, W, 64, 64, 4, yb=out, aux=t, alpha=2.0)
+    t = op(torch.randn(N, H, W, 64, generator=g).clamp_min(0), dt).to(d)
+    conv(dy, dp, None, N, H, W, 64, 64, 4, yb=out, aux=t, alpha=2.0, dt=dt)
     exp = 2.0 * ref * (t.double().cpu() > 0)
-    assert rel_l2(out.float(), exp) < 4e-3
+    assert rel_l2(out.float(), exp) < TOL[dt]
     # acc: g = acc + r1 + r2 + r3, with G / ds partial sums
     r1, r2, r3 = [torch.randn(N, H, W, 64, generator=g).to(d) for _ in range(3)]
-    u = bf(torch.randn(N, H, W, 64, generator=g)).to(d)
+    u = op(torch.randn(N, H, W, 64, generator=g), dt).to(d)
     ns = call("srmi_conv3x3_nstrips", H, W)
     part = torch.zeros(N, ns, 128, device=d)
     yf = r1.clone()
-    conv(dy, dp, None, N, H, W, 64, 64, 5, yb=out, yf=yf, r1=yf, r2=r2, r3=r3, aux=u, part=part)
+    conv(dy, dp, None, N, H, W, 64, 64, 5, yb=out, yf=yf, r1=yf, r2=r2, r3=r3, aux=u, part=part, dt=dt)
     exp = ref + r1.double().cpu() + r2.double().cpu() + r3.double().cpu()
     np.testing.assert_allclose(yf.double().cpu().numpy(), exp.numpy(), rtol=1e-5, atol=5e-5)
-    assert rel_l2(out.float(), exp) < 4e-3
+    assert rel_l2(out.float(), exp) < TOL[dt]
     Gs = part[:, :, :64].sum(1).double().cpu()
     ds = part[:, :, 64:].sum(1).double().cpu()
     np.testing.assert_allclose(Gs.numpy(), exp.sum((1, 2)).numpy(), rtol=1e-4, atol=2e-3)
     np.testing.assert_allclose(ds.numpy(), (exp * u.double().cpu()).sum((1, 2)).numpy(), rtol=1e-4, atol=2e-3)
 
 
-@pytest.mark.parametrize("N,H,W", [(2, 48, 48), (1, 4, 96)])
-def test_conv_dgrad_unshuffle(N, H, W):
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("N,H,W", [(2, 48, 48), (1, 4, 96), (2, 8, 32)])
+def test_conv_dgrad_unshuffle(N, H, W, dt):
     d = dev()
     g = torch.Generator(device="cpu").manual_seed(4)
     w = (torch.randn(256, 64, 3, 3, generator=g) * 0.06).to(d)
     b = torch.zeros(256, device=d)
-    fp, dp, pb = pack(w, b, ps=1)
-    dyp = bf(torch.randn(N, 2 * H, 2 * W, 64, generator=g)).to(d)   # grad wrt PS output
+    fp, dp, pb = pack(w, b, ps=1, dt=dt)
+    dyp = op(torch.randn(N, 2 * H, 2 * W, 64, generator=g), dt).to(d)  # grad wrt PS output
     dy_log = Fn.pixel_unshuffle(nchw(dyp).double().cpu(), 2)          # grad wrt conv output (torch order)
-    ref = nhwc(torch.nn.grad.conv2d_input((N, 64, H, W), bf(w).double().cpu(), dy_log, padding=1))
-    out = torch.empty(N, H, W, 64, dtype=torch.bfloat16, device=d)
-    conv(dyp, dp, None, N, H, W, 256, 64, 6, unshuf=1, yb=out)
-    assert rel_l2(out.float(), ref) < 4e-3
+    ref = nhwc(torch.nn.grad.conv2d_input((N, 64, H, W), wref(w, dt), dy_log, padding=1))
+    out = torch.empty(N, H, W, 64, dtype=TORCH_DT[dt], device=d)
+    conv(dyp, dp, None, N, H, W, 256, 64, 6, unshuf=1, yb=out, dt=dt)
+    assert rel_l2(out.float(), ref) < TOL[dt]
 
 
+@pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("N,H,W,rs", [(2, 48, 48, 0), (2, 48, 48, 1), (1, 8, 96, 0), (1, 4, 32, 0), (3, 12, 64, 3),
                                        (64, 48, 48, 0), (4, 96, 96, 0), (3, 12, 48, 3), (2, 48, 48, 12), (1, 8, 48, 2),
-                                       (2, 24, 48, 2)])
-def test_wgrad(N, H, W, rs):
+                                       (2, 24, 48, 2), (4, 32, 32, 4), (2, 16, 128, 2)])
+def test_wgrad(N, H, W, rs, dt):
     d = dev()
     g = torch.Generator(device="cpu").manual_seed(5)
-    x = bf(torch.randn(N, H, W, 64, generator=g)).to(d)
-    dy = bf(torch.randn(N, H, W, 64, generator=g)).to(d)
+    x = op(torch.randn(N, H, W, 64, generator=g), dt).to(d)
+    dy = op(torch.randn(N, H, W, 64, generator=g), dt).to(d)
     slab = torch.empty(64 << 20, dtype=torch.float32, device=d)
     gw = torch.empty(64, 64, 3, 3, device=d)
     gb = torch.empty(64, device=d)
     call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, rs, ptr(slab), slab.numel() * 4, 0, 1.0, ptr(gw), ptr(gb),
-         S())
+         ABI_DT[dt], S())
     ref = torch.nn.grad.conv2d_weight(nchw(x).double().cpu(), (64, 64, 3, 3), nchw(dy).double().cpu(), padding=1)
     assert rel_l2(gw, ref) < 1e-5
     np.testing.assert_allclose(gb.double().cpu().numpy(), dy.double().cpu().sum((0, 1, 2)).numpy(), rtol=1e-4,
                                atol=1e-3)
 
 
-@pytest.mark.parametrize("N,H,W", [(2, 48, 48), (1, 4, 96)])
-def test_wgrad_pixelshuffle(N, H, W):
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("N,H,W", [(2, 48, 48), (1, 4, 96), (2, 8, 32)])
+def test_wgrad_pixelshuffle(N, H, W, dt):
     d = dev()
     g = torch.Generator(device="cpu").manual_seed(6)
-    x = bf(torch.randn(N, H, W, 64, generator=g)).to(d)
-    dyp = bf(torch.randn(N, 2 * H, 2 * W, 64, generator=g)).to(d)
+    x = op(torch.randn(N, H, W, 64, generator=g), dt).to(d)
+    dyp = op(torch.randn(N, 2 * H, 2 * W, 64, generator=g), dt).to(d)
     slab = torch.empty(64 << 20, dtype=torch.float32, device=d)
     gw = torch.empty(256, 64, 3, 3, device=d)
     gb = torch.empty(256, device=d)
     call("srmi_wgrad3x3", ptr(x), ptr(dyp), N, H, W, 256, 1, 0, ptr(slab), slab.numel() * 4, 1, 1.0, ptr(gw), ptr(gb),
-         S())
+         ABI_DT[dt], S())
     dy_log = Fn.pixel_unshuffle(nchw(dyp).double().cpu(), 2)
     ref = torch.nn.grad.conv2d_weight(nchw(x).double().cpu(), (256, 64, 3, 3), dy_log, padding=1)
     assert rel_l2(gw, ref) < 1e-5
     np.testing.assert_allclose(gb.double().cpu().numpy(), dy_log.sum((0, 2, 3)).numpy(), rtol=1e-4, atol=1e-3)
 
 
-def test_channel_attention_fwd_bwd():
+@pytest.mark.parametrize("dt", DTS)
+def test_channel_attention_fwd_bwd(dt):
     d = dev()
     N, H, W, Cc, R = 2, 48, 48, 64, 2
     g = torch.Generator(device="cpu").manual_seed(7)
-    u = bf(torch.randn(N, H, W, Cc, generator=g)).to(d)
+    u = op(torch.randn(N, H, W, Cc, generator=g), dt).to(d)
     h_in = torch.randn(N, H, W, Cc, generator=g).to(d)
     w1 = (torch.randn(Cc // R, Cc, generator=g) * 0.1).to(d)
     b1 = (torch.randn(Cc // R, generator=g) * 0.1).to(d)
@@ -205,10 +231,10 @@ def test_channel_attention_fwd_bwd():
     part = torch.zeros(N, ns, Cc, device=d)
     part[:, 0, :] = u.float().sum((1, 2))
     h_out = torch.empty_like(h_in)
-    hb = torch.empty(N, H, W, Cc, dtype=torch.bfloat16, device=d)
+    hb = torch.empty(N, H, W, Cc, dtype=TORCH_DT[dt], device=d)
     rec = torch.empty(N, 160, device=d)
     call("srmi_ca_forward", ptr(u), ptr(part), ns, ptr(w1), ptr(b1), ptr(w2), ptr(b2), N, H * W, Cc, R, ptr(h_in),
-         ptr(h_out), ptr(hb), ptr(rec), S())
+         ptr(h_out), ptr(hb), ptr(rec), ABI_DT[dt], S())
     # torch reference (fp64 on CPU)
     U = u.double().cpu().requires_grad_(True)
     W1, B1, W2, B2 = [t.double().cpu().requires_grad_(True) for t in (w1, b1, w2, b2)]
@@ -218,17 +244,18 @@ def test_channel_attention_fwd_bwd():
     y = U * s[:, None, None, :] + h_in.double().cpu()
     np.testing.assert_allclose(h_out.double().cpu().numpy(), y.detach().numpy(), rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(rec[:, 96:].double().cpu().numpy(), s.detach().numpy(), rtol=1e-5, atol=1e-6)
+    assert rel_l2(hb.float(), y.detach()) < TOL[dt]
     # backward: g -> du, brec
     gy = torch.randn(N, H, W, Cc, generator=g).to(d)
     y.backward(gy.double().cpu())
     bpart = torch.zeros(N, ns, 2 * Cc, device=d)
     bpart[:, 0, :Cc] = gy.sum((1, 2))
     bpart[:, 0, Cc:] = (gy * u.float()).sum((1, 2))
-    du = torch.empty(N, H, W, Cc, dtype=torch.bfloat16, device=d)
+    du = torch.empty(N, H, W, Cc, dtype=TORCH_DT[dt], device=d)
     brec = torch.empty(N * 224, device=d)  # [N][160] then dm[N][64]
     call("srmi_ca_backward", ptr(gy), ptr(bpart), ns, ptr(rec), ptr(w1), ptr(w2), N, H * W, Cc, R, ptr(du), ptr(brec),
-         S())
-    assert rel_l2(du.float(), U.grad) < 4e-3
+         ABI_DT[dt], S())
+    assert rel_l2(du.float(), U.grad) < TOL[dt]
     # conv2-bias grad path: sum_p du = s*G + dm
     np.testing.assert_allclose(brec[:N * 160].view(N, 160)[:, 96:].double().cpu().numpy(), U.grad.sum((1, 2)).numpy(), rtol=1e-4, atol=1e-3)
 
@@ -264,17 +291,36 @@ def test_adam_matches_reference():
     np.testing.assert_allclose(p.double().cpu().numpy(), gd["adam_p3"], rtol=0, atol=2e-6)
 
 
+@pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("C,H,W", [(1, 8, 192), (2, 12, 192), (4, 8, 256), (3, 4, 96)])
-def test_tail_forward(C, H, W):
-    """Tail conv 64 -> C (network.py:16 / EDSR tail) through srmi_tail_forward: MFMA
-    implicit GEMM with bf16 operands vs an fp64 conv of the same bf16 input."""
+def test_tail_forward(C, H, W, dt):
+    """Tail conv 64 -> C (network.py:16 / EDSR tail) through srmi_tail_forward: bf16 =
+    MFMA implicit GEMM with bf16 operands (and bf16 filters) vs an fp64 conv of the
+    same bf16 input; fp32 = the exact fp32 form."""
     d = dev()
     g = torch.Generator(device="cpu").manual_seed(12)
     N = 2
-    x = bf(torch.randn(N, H, W, 64, generator=g)).to(d)
+    x = op(torch.randn(N, H, W, 64, generator=g), dt).to(d)
     w = (torch.randn(C, 64, 3, 3, generator=g) * 0.05).to(d)
     b = (torch.randn(C, generator=g) * 0.1).to(d)
     y = torch.empty(N, C, H, W, device=d)
-    call("srmi_tail_forward", ptr(x), ptr(w), ptr(b), N, C, H, W, ptr(y), S())
+    call("srmi_tail_forward", ptr(x), ptr(w), ptr(b), N, C, H, W, ptr(y), ABI_DT[dt], S())
     ref = Fn.conv2d(nchw(x).double().cpu(), w.double().cpu(), b.double().cpu(), padding=1)
-    assert rel_l2(y, ref) < 4e-3
+    assert rel_l2(y, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_head_forward(dt):
+    """Head conv C -> 64 (network.py:13): fp32 arithmetic, fp32 stream + operand copy."""
+    d = dev()
+    g = torch.Generator(device="cpu").manual_seed(13)
+    N, C, H, W = 2, 3, 48, 48
+    lr = torch.randn(N, C, H, W, generator=g).to(d)
+    w = (torch.randn(64, C, 3, 3, generator=g) * 0.2).to(d)
+    b = (torch.randn(64, generator=g) * 0.1).to(d)
+    x0f = torch.empty(N, H, W, 64, device=d)
+    x0b = torch.empty(N, H, W, 64, dtype=TORCH_DT[dt], device=d)
+    call("srmi_head_forward", ptr(lr), ptr(w), ptr(b), N, C, H, W, ptr(x0f), ptr(x0b), ABI_DT[dt], S())
+    ref = nhwc(Fn.conv2d(lr.double().cpu(), w.double().cpu(), b.double().cpu(), padding=1))
+    assert rel_l2(x0f, ref) < 1e-6
+    assert rel_l2(x0b.float(), ref) < TOL[dt]

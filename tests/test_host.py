@@ -210,9 +210,13 @@ def test_conv_abi_rejects_missing_operands():
     # epi 4 (dgrad * relu mask) without the mask, epi 2 (residual) without r1,
     # epi 1 (pool) without the partial-sum buffer, epi 3 (pixel shuffle) without yb
     for epi in (4, 2, 1, 3):
-        args = [dummy, dummy, None, 1, 4, 48, 64, 256 if epi == 3 else 64, 0, epi, None, None, None, None, None,
-                None, None, 1.0, None]
-        assert lib.srmi_conv3x3(*args) == -10001, (epi, "expected SRMI_ERR_ARG")
+        for dtype in (0, 1):
+            args = [dummy, dummy, None, 1, 4, 48, 64, 256 if epi == 3 else 64, 0, epi, None, None, None, None, None,
+                    None, None, 1.0, dtype, None]
+            assert lib.srmi_conv3x3(*args) == -10001, (epi, dtype, "expected SRMI_ERR_ARG")
+    # an unknown dtype is refused too
+    args = [dummy, dummy, dummy, 1, 4, 48, 64, 64, 0, 0, dummy, None, None, None, None, None, None, 1.0, 7, None]
+    assert lib.srmi_conv3x3(*args) == -10001
 
 
 def _force_dp_rank(port, q):

@@ -53,7 +53,7 @@ def main():
     fp = torch.empty(64 * 64 * 9, dtype=torch.bfloat16, device=d)
     dp = torch.empty_like(fp)
     pb = torch.empty(64, device=d)
-    call("srmi_pack_conv", ptr(w), ptr(b), 64, 64, 0, ptr(fp), ptr(dp), ptr(pb), S())
+    call("srmi_pack_conv", ptr(w), ptr(b), 64, 64, 0, ptr(fp), ptr(dp), ptr(pb), 0, S())
     ns = call("srmi_conv3x3_nstrips", H, W)
     part = torch.zeros(N, ns, 128, device=d)
     flop = 2.0 * N * H * W * 64 * 576
@@ -62,7 +62,7 @@ def main():
     def conv(epi, xin, wp, **kw):
         def f():
             call("srmi_conv3x3", ptr(xin), ptr(wp), ptr(kw.get("bias")), N, H, W, 64, 64, 0, epi, ptr(kw.get("yb")),
-                 ptr(kw.get("yf")), ptr(kw.get("r1")), None, None, ptr(kw.get("aux")), ptr(kw.get("part")), 1.0, S())
+                 ptr(kw.get("yf")), ptr(kw.get("r1")), None, None, ptr(kw.get("aux")), ptr(kw.get("part")), 1.0, 0, S())
         return f
 
     cases = {
@@ -82,12 +82,12 @@ def main():
 
     def wg():
         call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, 0, ptr(slab), slab.numel() * 4, 0, 1.0, ptr(gw),
-             ptr(gb), S())
+             ptr(gb), 0, S())
     us = timeit(wg, args.iters)
     res["wgrad+reduce"] = {"us": round(us, 2), "tflops": round(flop / us / 1e6, 1)}
 
     def wg_only():
-        call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, 0, ptr(slab), slab.numel() * 4, 0, 1.0, None, None, S())
+        call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, 0, ptr(slab), slab.numel() * 4, 0, 1.0, None, None, 0, S())
     us = timeit(wg_only, args.iters)
     res["wgrad"] = {"us": round(us, 2), "tflops": round(flop / us / 1e6, 1)}
     # channel attention elementwise kernels
@@ -102,11 +102,11 @@ def main():
 
     def caf():
         call("srmi_ca_forward", ptr(yb), ptr(pool), ns, ptr(w1), ptr(b1), ptr(w2), ptr(b2), N, H * W, 64, R, ptr(r1),
-             ptr(yf), ptr(x), ptr(rec), S())
+             ptr(yf), ptr(x), ptr(rec), 0, S())
 
     def cab():
         call("srmi_ca_backward", ptr(r1), ptr(part), ns, ptr(rec), ptr(w1), ptr(w2), N, H * W, 64, R, ptr(yb),
-             ptr(brec), S())
+             ptr(brec), 0, S())
     for k, f, byt in (("ca_fwd", caf, N * H * W * 64 * 12), ("ca_bwd_du", cab, N * H * W * 64 * 6)):
         us = timeit(f, args.iters)
         res[k] = {"us": round(us, 2), "GBps": round(byt / us / 1e3, 1)}
@@ -141,7 +141,7 @@ def stamps():
     fp = torch.empty(64 * 64 * 9, dtype=torch.bfloat16, device=d)
     dp = torch.empty_like(fp)
     pb = torch.empty(64, device=d)
-    call("srmi_pack_conv", ptr(w), ptr(b), 64, 64, 0, ptr(fp), ptr(dp), ptr(pb), S)
+    call("srmi_pack_conv", ptr(w), ptr(b), 64, 64, 0, ptr(fp), ptr(dp), ptr(pb), 0, S)
     yb = torch.empty_like(x)
     ns = call("srmi_conv3x3_nstrips", H, W)
     part = torch.zeros(N, ns, 128, device=d)
@@ -158,10 +158,10 @@ def stamps():
         else:
             args = (ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, epi, ptr(yb), None, None, None, None, None, None)
         for _ in range(3):
-            call("srmi_conv3x3", *args, 1.0, S)
+            call("srmi_conv3x3", *args, 1.0, 0, S)
         buf.zero_()
         call("srmi_debug_conv_stamps", ptr(buf))
-        call("srmi_conv3x3", *args, 1.0, S)
+        call("srmi_conv3x3", *args, 1.0, 0, S)
         call("srmi_debug_conv_stamps", None)
         torch.cuda.synchronize()
         st = buf.view(4096, 64).cpu().numpy()
@@ -199,7 +199,7 @@ def wstamps():
     for rs in [int(v) for v in os.environ.get("KBENCH_RS", "0").split(",")]:
         def run():
             call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, rs, ptr(slab), slab.numel() * 4, 0, 1.0,
-                 ptr(gw), ptr(gb), S)
+                 ptr(gw), ptr(gb), 0, S)
         us = timeit(run, 20)
         buf.zero_()
         call("srmi_debug_wgrad_stamps", ptr(buf))

@@ -36,14 +36,14 @@ def main():
     fp = torch.empty(64 * 64 * 9, dtype=torch.bfloat16, device=d)
     dp = torch.empty_like(fp)
     pb = torch.empty(64, device=d)
-    call("srmi_pack_conv", ptr(w), ptr(b), 64, 64, 0, ptr(fp), ptr(dp), ptr(pb), st)
+    call("srmi_pack_conv", ptr(w), ptr(b), 64, 64, 0, ptr(fp), ptr(dp), ptr(pb), 0, st)
     y = torch.empty_like(x)
     for _ in range(a.iters):
         call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, 0, ptr(slab), slab.numel() * 4, 0, 1.0, None, None,
-             st)
+             0, st)
     for _ in range(a.iters):
         call("srmi_conv3x3", ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, 0, ptr(y), None, None, None, None, None,
-             None, 1.0, st)
+             None, 1.0, 0, st)
     torch.cuda.synchronize()
     print("done")
 
