@@ -22,34 +22,13 @@
 #include <algorithm>
 
 #include "common.hpp"
+#include "conv64_body.hpp"
 #include "srmi_internal.hpp"
 
 namespace srmi {
 
-// zero bytes in global memory: the LDS-DMA source for padding pixels
-static __device__ uint4 kZeros[64];  // 1 KiB zero page (padding source, absent bias)
-
 static unsigned long long* g_debug_stamps = nullptr;
 void conv3x3_set_debug_stamps(unsigned long long* buf) { g_debug_stamps = buf; }
-
-// Phase stamps exist only in the diagnostic build (make stamps): even a disabled
-// stamp store makes the compiler drain vmcnt where its data registers are reused.
-#ifdef SRMI_STAMPS
-#define STAMP(i)                                                                                   \
-  do {                                                                                             \
-    if (p.stamps && tid == 0) {                                                                    \
-      p.stamps[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memtime();                              \
-      if ((i) == 0 || (i) == 61) p.stamps[blockIdx.x * 64 + 62 + ((i) == 61)] = __builtin_amdgcn_s_memrealtime(); \
-    }                                                                                              \
-  } while (0)
-#else
-#define STAMP(i) \
-  do {           \
-  } while (0)
-#endif
-
-constexpr int kTH = 4;
-constexpr int kThreads = 256;
 
 template <int TW>
 struct ConvSmem {
@@ -289,485 +268,15 @@ __global__ void __launch_bounds__(kThreads, 2) conv3x3_kernel(ConvParams p) {
                           wave, tid);
 }
 
-// ============================================================================
-// v2 (Cin == 64): persistent runs.  A workgroup owns a vertical run of strips of
-// one image column and one 64-wide output-channel block.  All 9 filter slices
-// ([9][64 co][64 ci] bf16, 72 KiB) stay resident in LDS for the whole run; the
-// input rows live in a ring of 3 groups of 4 rows (group g = rows 4g-3..4g), so
-// strip k reads groups k and k+1 while group k+2 is prefetched into registers
-// (issued before the MFMAs, written to LDS after them: hipcc counts these loads
-// itself).  Halo rows are therefore fetched once per run (1.17x input traffic at
-// 12-row runs instead of 1.5x), with one barrier per strip instead of one per tap.
-template <int TW>
-struct Conv2Smem {
-  static constexpr int ROWB = (TW + 2) * 128;      // one halo row (TW+2 px x 64 ch bf16)
-  static constexpr int GROUPB = 4 * ROWB;
-  static constexpr int WB = 9 * 64 * 128;          // resident filters
-  static constexpr int RING = 3 * GROUPB;
-  static constexpr int RED = 4 * 128 * 4;          // cross-wave channel sums
-  static constexpr int TOTAL = WB + RING + RED;
-  static constexpr int GCH = GROUPB / 16;          // 16-B chunks per group
-  static constexpr int GPT = (GCH + kThreads - 1) / kThreads;
-};
-
-// Epilogue operands that live in global memory are prefetched into registers
-// before the MFMA phase (one wave per SIMD: nothing else would hide their latency).
-template <int NPT, int EPI>
-struct EpiPre {
-  float4 r1[NPT][4];
-  uint2 aux[NPT][4];
-};
-
-template <int NPT, int EPI>
-__device__ __forceinline__ void epi_prefetch(const ConvParams& p, EpiPre<NPT, EPI>& e, int n, int cb, int y, int x0,
-                                             int fr, int fk) {
-  if constexpr (EPI == EPI_RESID || EPI == EPI_DG_ACC || EPI == EPI_DG_RELUMASK || EPI == EPI_DG_ACC_CA) {
-    const size_t HW = (size_t)p.H * p.W;
-#pragma unroll
-    for (int pt = 0; pt < NPT; ++pt) {
-      const size_t pix = (size_t)n * HW + (size_t)y * p.W + x0 + pt * 16 + fr;
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        const size_t o = pix * p.Cout + cb * 64 + ct * 16 + fk * 4;
-        if constexpr (EPI == EPI_RESID) e.r1[pt][ct] = *reinterpret_cast<const float4*>(p.r1 + o);
-        if constexpr (EPI == EPI_DG_ACC) {
-          e.r1[pt][ct] = p.r1 ? *reinterpret_cast<const float4*>(p.r1 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
-          e.aux[pt][ct] = p.part ? *reinterpret_cast<const uint2*>(p.aux + o) : make_uint2(0, 0);
-        }
-        if constexpr (EPI == EPI_DG_RELUMASK) e.aux[pt][ct] = *reinterpret_cast<const uint2*>(p.aux + o);
-        if constexpr (EPI == EPI_DG_ACC_CA) {
-          e.r1[pt][ct] = *reinterpret_cast<const float4*>(p.r1 + o);
-          e.aux[pt][ct] = *reinterpret_cast<const uint2*>(p.aux + o);
-        }
-      }
-    }
-  }
-}
-
-// one (pt, ct) element of epi_prefetch (e = pt * 4 + ct), for interleaving
-template <int NPT, int EPI>
-__device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT, EPI>& e, int n, int cb, int y,
-                                                 int x0, int fr, int fk, int idx) {
-  if constexpr (EPI == EPI_RESID || EPI == EPI_DG_ACC || EPI == EPI_DG_RELUMASK || EPI == EPI_DG_ACC_CA) {
-    const int pt = idx >> 2, ct = idx & 3;
-    const size_t HW = (size_t)p.H * p.W;
-    const size_t pix = (size_t)n * HW + (size_t)y * p.W + x0 + pt * 16 + fr;
-    const size_t o = pix * p.Cout + cb * 64 + ct * 16 + fk * 4;
-    if constexpr (EPI == EPI_RESID) e.r1[pt][ct] = *reinterpret_cast<const float4*>(p.r1 + o);
-    if constexpr (EPI == EPI_DG_ACC) {
-      e.r1[pt][ct] = p.r1 ? *reinterpret_cast<const float4*>(p.r1 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
-      e.aux[pt][ct] = p.part ? *reinterpret_cast<const uint2*>(p.aux + o) : make_uint2(0, 0);
-    }
-    if constexpr (EPI == EPI_DG_RELUMASK) e.aux[pt][ct] = *reinterpret_cast<const uint2*>(p.aux + o);
-    if constexpr (EPI == EPI_DG_ACC_CA) {
-      e.r1[pt][ct] = *reinterpret_cast<const float4*>(p.r1 + o);
-      e.aux[pt][ct] = *reinterpret_cast<const uint2*>(p.aux + o);
-    }
-  }
-}
-
-__device__ __forceinline__ float relu_mask(uint32_t bits16, float v) {
-  return (bits16 & 0x7FFFu) && !(bits16 & 0x8000u) ? v : 0.f;
-}
-
-// Orders one wave's LDS accesses across lanes: the hardware executes a wave's DS
-// instructions in order, but the compiler reasons per lane and would move a
-// lane's read of another lane's staged data above that lane's write.
-__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
-
-// Fused epilogue of the v2 kernel (same semantics as conv_epilogue).
-template <int NPT, int EPI>
-__device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)[NPT][4], const EpiPre<NPT, EPI>& e,
-                                               const float4 (&bias)[4], int n, int cb, int y, int x0, int strip,
-                                               int nstrips, float* red, int fr, int fk, int wave, int tid,
-                                               char* stage) {
-  const size_t HW = (size_t)p.H * p.W;
-  [[maybe_unused]] const auto rfa = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
-  constexpr bool kPart1 = (EPI == EPI_POOL_BF16);
-  constexpr bool kPart2 = (EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_CA);
-  float ps0[4][4], ps1[4][4];
-  // fp32 output staged through LDS (DG_ACC, whose epilogue also reads r2/r3 from
-  // global memory, measured faster with direct stores)
-  constexpr bool kF = (EPI == EPI_RESID || EPI == EPI_DG_ACC_CA);
-  float4 fv[NPT][4];  // fp32 outputs, written back through LDS after the loop
-  uint2 bv[NPT][4];   // bf16 outputs, likewise
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) ps0[ct][r] = ps1[ct][r] = 0.f;
-#pragma unroll
-  for (int pt = 0; pt < NPT; ++pt) {
-    const int xx = x0 + pt * 16 + fr;
-    const size_t pix = (size_t)n * HW + (size_t)y * p.W + xx;
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      const int col = ct * 16 + fk * 4;
-      const int co = cb * 64 + col;
-      const size_t o = pix * p.Cout + co;
-      f32x4 v = acc[pt][ct];
-      if constexpr (EPI == EPI_RELU_BF16 || EPI == EPI_POOL_BF16 || EPI == EPI_RESID || EPI == EPI_PS_BF16 ||
-                    EPI == EPI_PLAIN_BF16) {
-        v[0] += bias[ct].x; v[1] += bias[ct].y; v[2] += bias[ct].z; v[3] += bias[ct].w;
-      }
-      if constexpr (EPI == EPI_RELU_BF16) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-      }
-      if constexpr (EPI == EPI_RESID) {
-        const float4 rr = e.r1[pt][ct];
-        v[0] = p.alpha * v[0] + rr.x; v[1] = p.alpha * v[1] + rr.y;
-        v[2] = p.alpha * v[2] + rr.z; v[3] = p.alpha * v[3] + rr.w;
-        fv[pt][ct] = make_float4(v[0], v[1], v[2], v[3]);
-      }
-      if constexpr (EPI == EPI_DG_RELUMASK) {
-        const uint2 tt = e.aux[pt][ct];
-        v[0] = p.alpha * relu_mask(tt.x & 0xFFFFu, v[0]);
-        v[1] = p.alpha * relu_mask(tt.x >> 16, v[1]);
-        v[2] = p.alpha * relu_mask(tt.y & 0xFFFFu, v[2]);
-        v[3] = p.alpha * relu_mask(tt.y >> 16, v[3]);
-      }
-      if constexpr (EPI == EPI_DG_ACC) {
-        const float4 rr = e.r1[pt][ct];
-        v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
-        if (p.r2) {
-          const float4 q = *reinterpret_cast<const float4*>(p.r2 + o);
-          v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
-        }
-        if (p.r3) {
-          const float4 q = *reinterpret_cast<const float4*>(p.r3 + o);
-          v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
-        }
-        st_wt16(rfa, p.yf, (uint32_t)(o * 4), make_float4(v[0], v[1], v[2], v[3]));
-        if (p.part) {
-          const uint2 uu = e.aux[pt][ct];
-          ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
-          ps1[ct][0] += v[0] * bf2f(uu.x & 0xFFFFu);
-          ps1[ct][1] += v[1] * bf2f(uu.x >> 16);
-          ps1[ct][2] += v[2] * bf2f(uu.y & 0xFFFFu);
-          ps1[ct][3] += v[3] * bf2f(uu.y >> 16);
-        }
-      }
-      if constexpr (EPI == EPI_DG_ACC_CA) {
-        const float4 rr = e.r1[pt][ct];
-        v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
-        fv[pt][ct] = make_float4(v[0], v[1], v[2], v[3]);
-        const uint2 uu = e.aux[pt][ct];
-        ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
-        ps1[ct][0] += v[0] * bf2f(uu.x & 0xFFFFu);
-        ps1[ct][1] += v[1] * bf2f(uu.x >> 16);
-        ps1[ct][2] += v[2] * bf2f(uu.y & 0xFFFFu);
-        ps1[ct][3] += v[3] * bf2f(uu.y >> 16);
-        continue;  // no bf16 copy
-      }
-      if constexpr (kPart1) {
-        ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
-      }
-      bv[pt][ct] = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-    }
-  }
-  const int lane = tid & 63;
-  // fp32 output: staged in LDS in two halves of the wave's row (256 B per pixel,
-  // chunk-swizzled) and written back as 1 KiB contiguous runs (full lines)
-  if constexpr (kF) {
-    if (p.yf) {
-      constexpr int HALF = NPT * 8;  // pixels per half
-      const auto rf = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
-      const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-#pragma unroll
-        for (int pt = 0; pt < NPT; ++pt)
-#pragma unroll
-          for (int ct = 0; ct < 4; ++ct) {
-            const int px = pt * 16 + fr;
-            if ((px >= HALF) == (h == 1)) {
-              const int lpx = px - h * HALF, c16 = ct * 4 + fk;
-              *reinterpret_cast<float4*>(stage + lpx * 256 + ((c16 ^ (lpx & 15)) << 4)) = fv[pt][ct];
-            }
-          }
-        lds_order();
-#pragma unroll
-        for (int i = 0; i < HALF / 4; ++i) {
-          const int lin = i * 1024 + lane * 16, lpx = lin >> 8, c = (lin >> 4) & 15;
-          const float4 val = *reinterpret_cast<const float4*>(stage + lpx * 256 + ((c ^ (lpx & 15)) << 4));
-          st_wt16(rf, p.yf, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 4), val);
-        }
-        lds_order();
-      }
-    }
-  }
-  // bf16 output staged in LDS (this wave's row, 128 B per pixel, chunk-swizzled)
-  if constexpr (EPI != EPI_DG_ACC_CA) {
-    if (p.yb) {
-#pragma unroll
-      for (int pt = 0; pt < NPT; ++pt)
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-          const int px = pt * 16 + fr, c16 = ct * 2 + (fk >> 1);
-          *reinterpret_cast<uint2*>(stage + px * 128 + ((c16 ^ (px & 7)) << 4) + (fk & 1) * 8) = bv[pt][ct];
-        }
-    }
-  }
-  lds_order();
-  // ... and written back as full 128-byte lines: one 1 KiB contiguous run per
-  // instruction (the per-lane 8-byte stores of the MFMA layout touched 32-byte
-  // pieces of 16 lines each and stalled the store path for ~2 K cycles per strip).
-  // The wave's own LDS writes precede its reads (in-order LDS per wave).
-  if (EPI != EPI_DG_ACC_CA && p.yb) {
-    const auto rb = wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
-#pragma unroll
-    for (int i = 0; i < NPT * 2; ++i) {
-      const int lin = i * 1024 + lane * 16, px = lin >> 7, c = (lin >> 4) & 7;
-      const uint4 val = *reinterpret_cast<const uint4*>(stage + px * 128 + ((c ^ (px & 7)) << 4));
-      size_t line;
-      if constexpr (EPI == EPI_PS_BF16) {
-        line = (((size_t)n * (2 * p.H) + 2 * y + (cb >> 1)) * (size_t)(2 * p.W) + 2 * (x0 + px) + (cb & 1)) * 64;
-      } else {
-        line = ((size_t)n * HW + (size_t)y * p.W + x0 + px) * p.Cout + cb * 64;
-      }
-      st_wt16(rb, p.yb, (uint32_t)((line + c * 8) * 2), val);
-    }
-  }
-  if constexpr (kPart1 || kPart2) {
-    const bool on = EPI != EPI_DG_ACC || p.part;
-    if (on) {
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float s0 = sum16(ps0[ct][r]);
-          float s1 = 0.f;
-          if constexpr (kPart2) s1 = sum16(ps1[ct][r]);
-          if (fr == 0) {
-            red[(wave * 2 + 0) * 64 + ct * 16 + fk * 4 + r] = s0;
-            if constexpr (kPart2) red[(wave * 2 + 1) * 64 + ct * 16 + fk * 4 + r] = s1;
-          }
-        }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // red[] writes visible; global stores may stay in flight
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (on) {
-      if (tid < 64) {
-        const float sum = red[tid] + red[128 + tid] + red[256 + tid] + red[384 + tid];
-        p.part[((size_t)n * nstrips + strip) * p.part_stride + cb * 64 + tid] = sum;
-      } else if (kPart2 && tid < 128) {
-        const int c = tid - 64;
-        const float sum = red[64 + c] + red[192 + c] + red[320 + c] + red[448 + c];
-        p.part[((size_t)n * nstrips + strip) * p.part_stride + 64 + c] = sum;
-      }
-    }
-  }
-}
-
-#ifndef SRMI_CONV_FRAGBUF
-#define SRMI_CONV_FRAGBUF 2
-#endif
-constexpr int kFragBuf = SRMI_CONV_FRAGBUF;
-#ifndef SRMI_CONV_ILV
-#define SRMI_CONV_ILV 1
-#endif  // register buffers of A/B fragments (K-steps)
-
-template <int TW, int EPI, int PM>
-__global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int run_len) {
-  using S = Conv2Smem<TW>;
-  constexpr int NPT = TW / 16;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* wl = smem;
-  char* ring = smem + S::WB;
-  float* red = reinterpret_cast<float*>(smem + S::WB + S::RING);
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fk = lane >> 4;
-  const int nsx = p.W / TW, nsy = p.H / kTH;
-  const int runs_per_col = (nsy + run_len - 1) / run_len;
-  int r = blockIdx.x;
-  const int ry = r % runs_per_col;
-  r /= runs_per_col;
-  const int sx = r % nsx;
-  r /= nsx;
-  const int n = r % p.N;
-  const int cb = r / p.N;
-  const int k0 = ry * run_len, k1 = min(nsy, k0 + run_len);
-  const int x0 = sx * TW;
-  STAMP(0);
-
-  const bf16_t* xn = p.x + (size_t)n * p.H * p.W * 64;
-
-  // LDS-DMA of one 4-row input group into its ring slot: one wave instruction per
-  // 8 pixels (1 KiB), swizzle applied on the source side, halo lanes read the zero
-  // page.  No registers hold in-flight data, so no compiler-inserted vmcnt waits.
-  const int wv_s = __builtin_amdgcn_readfirstlane(wave);
-  const uint32_t rbase = lds_u32(ring);
-  const void* const zpage = uniform_ptr(kZeros);
-  constexpr int NGRP = S::GROUPB / 1024;         // 1 KiB DMA pieces per group
-  constexpr int NGW = (NGRP + 3) / 4;            // pieces per wave (upper bound)
-  // Per-lane parts of the DMA source, computed once: piece i = wv_s + 4m covers ring
-  // pixels q = 8i + lane/8, i.e. row rr and halo column hx of the group; the chunk
-  // swizzle of ring slot 1 differs from slots 0 and 2 by bit 2 (200 px per slot).
-  int loff[NGW], lrr[NGW];
-  uint32_t okx = 0;
-#pragma unroll
-  for (int m = 0; m < NGW; ++m) {
-    const int i = wv_s + 4 * m;
-    const int q = 8 * i + (lane >> 3);
-    const int c = (lane & 7) ^ ((q >> 1) & 7);
-    const int rr = q / (TW + 2), hx = q - rr * (TW + 2);
-    const int xx = x0 - 1 + hx;
-    okx |= (i < NGRP && xx >= 0 && xx < p.W) ? (1u << m) : 0u;
-    loff[m] = ((rr * p.W + hx - 1) * 64 + c * 8) * (int)sizeof(bf16_t);
-    lrr[m] = rr;
-  }
-  auto group_dma_one = [&](int gidx, int m) __attribute__((always_inline)) {
-    const int slot = gidx % 3, y0 = 4 * gidx - 3;
-    const char* base = reinterpret_cast<const char*>(xn + ((ptrdiff_t)y0 * p.W + x0) * 64);
-    const int o = loff[m] ^ (slot == 1 ? 64 : 0);  // chunk c ^ 4 (8 bf16 = 16 B per chunk)
-    const bool ok = ((okx >> m) & 1u) && y0 + lrr[m] >= 0 && y0 + lrr[m] < p.H;
-    const void* src = ok ? (const void*)(base + o) : zpage;
-    glds16(src, rbase + (uint32_t)(slot * 4 * (TW + 2)) * 128u + (uint32_t)(wv_s + 4 * m) * 1024u);
-  };
-  auto group_dma = [&](int gidx) __attribute__((always_inline)) {
-#pragma unroll
-    for (int m = 0; m < NGW; ++m)
-      if (wv_s + 4 * m < NGRP) group_dma_one(gidx, m);
-  };
-
-  // prologue: filters (all 9 taps, 72 KiB) and input groups k0, k0+1, all by LDS-DMA
-  // (swizzle on the source side), everything in flight before the one wait.
-  {
-    const uint32_t wbase = lds_u32(wl);
-    for (int i = wv_s; i < 72; i += 4) {
-      const int tap = i >> 3, row = 8 * (i & 7) + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
-      glds16(p.w + ((size_t)(tap * p.Cout + cb * 64 + row)) * 64 + c * 8, wbase + (uint32_t)i * 1024u);
-    }
-    group_dma(k0);
-    group_dma(k0 + 1);  // strip k0 reads groups k0 and k0+1 (issuing these first measured the same)
-    wait_vm<0>();
-  }
-  STAMP(1);
-  float4 bias[4];
-  {
-    const float* bp = p.bias ? p.bias : reinterpret_cast<const float*>(kZeros);  // pointer select, no branch
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) bias[ct] = *reinterpret_cast<const float4*>(bp + cb * 64 + ct * 16 + fk * 4);
-  }
-  // lane-constant A-fragment byte offsets (tap adds 8192)
-  uint32_t aoff[2][4];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) aoff[kk][ct] = swz128(ct * 16 + fr, kk * 4 + fk);
-  __syncthreads();
-
-#pragma unroll 1
-  for (int k = k0; k < k1; ++k) {
-    const int y = 4 * k + wave;
-    const bool pf = (k + 1 < k1);
-    // group k+2 -> ring slot (k+2)%3, which held group k-1 (last read by strip k-1,
-    // released by the barrier that ended it)
-    EpiPre<NPT, EPI> ep;
-    [[maybe_unused]] const int sj = 2 + 5 * min(k - k0, 11);
-    STAMP(sj);
-
-    // B-fragment byte offsets per (ky, kx, kk); +2048 per 16-pixel tile
-    uint32_t boff[3][3][2];
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      const int rr = y + ky - 1 + 3;  // >= 2
-      const int slot = ((rr >> 2) % 3) * 4 + (rr & 3);
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) boff[ky][kx][kk] = swz128(slot * (TW + 2) + fr + kx, kk * 4 + fk);
-    }
-
-    f32x4 acc[NPT][4];
-#pragma unroll
-    for (int i = 0; i < NPT; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // 18 K-steps (9 taps x 2 halves of 32 ci), fragments triple-buffered in
-    // registers: steps s+1 and s+2's ds_reads are in flight while step s's MFMAs run.
-    bf16x8 A[kFragBuf][4], B[kFragBuf][NPT];
-    auto load_step = [&](int s, bf16x8 (&a)[4], bf16x8 (&b)[NPT]) __attribute__((always_inline)) {
-      const int tap = s >> 1, kk = s & 1, ky = tap / 3, kx = tap % 3;
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) a[ct] = lds_frag(wl, tap * 8192 + aoff[kk][ct]);
-#pragma unroll
-      for (int pt = 0; pt < NPT; ++pt) b[pt] = lds_frag(ring, boff[ky][kx][kk] + pt * 2048);
-    };
-    constexpr int LA = kFragBuf - 1;  // K-steps of LDS reads in flight ahead of the MFMAs
-#pragma unroll
-    for (int s = 0; s < LA; ++s) load_step(s, A[s], B[s]);
-#pragma unroll
-    for (int s = 0; s < 18; ++s) {
-      // group k+2's DMA pieces and the epilogue operands are issued one or two per
-      // K-step, so a full memory queue stalls the wave between MFMA groups only
-      if (s < NGW && pf && wv_s + 4 * s < NGRP) group_dma_one(k + 2, s);
-      if (s >= 2 && s - 2 < NPT * 4) epi_prefetch_one<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk, s - 2);
-      __builtin_amdgcn_sched_barrier(0);
-      const bool ld = s + LA < 18;
-      if (ld) load_step(s + LA, A[(s + LA) % kFragBuf], B[(s + LA) % kFragBuf]);
-#pragma unroll
-      for (int pt = 0; pt < NPT; ++pt)
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct)
-          acc[pt][ct] = mfma16(A[s % kFragBuf][ct], B[s % kFragBuf][pt], acc[pt][ct]);
-#if SRMI_CONV_ILV
-      // one fragment read issued behind each MFMA: the reads' issue time hides under
-      // the MFMA pipe instead of stalling it between K-steps
-      if (ld) {
-#pragma unroll
-        for (int j = 0; j < 4 + NPT; ++j) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 4 * NPT - (4 + NPT), 0);
-      }
-#endif
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // group k+2's DMA, the epilogue operands and the previous strip's stores had the
-    // whole MFMA phase to land: drain them here, before the epilogue (the barrier at
-    // the end of the strip then publishes group k+2 to every wave)
-    wait_vm<0>();
-    STAMP(sj + 1);
-    STAMP(sj + 2);
-    // every wave is past its last read of input group k: its ring slot stages the
-    // strip's bf16 output rows (slot k%3 is next written by group k+3's DMA,
-    // issued after the barrier that ends this strip)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    conv_epilogue2<NPT, EPI>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx, nsy * nsx, red, fr, fk, wave, tid,
-                             ring + (k % 3) * S::GROUPB + wave * TW * 128);
-    STAMP(sj + 3);
-    // LDS-only barrier: this strip's global stores stay in flight into the next strip
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    STAMP(sj + 4);
-  }
-  STAMP(61);
-}
-
 template <int TW, int EPI>
 static int launch_tw(const ConvParams& p, hipStream_t st) {
   if (p.Cin == 64 && p.in_mode == IN_PLAIN) {
     // v2: persistent runs; ~1 workgroup per CU (LDS-limited), each a run of strips
-    const int nsy = p.H / kTH;
-    const int units = (p.Cout / 64) * p.N * (p.W / TW);
-    const int cus = p.cu_budget > 0 ? p.cu_budget : 256;
-    int R = (cus + units / 2) / units;
-    R = R < 1 ? 1 : (R > nsy ? nsy : R);
-    const int run_len = (nsy + R - 1) / R;
-    const int runs = (nsy + run_len - 1) / run_len;
-    dim3 grid(units * runs);
+    const int run_len = conv64_run_len(p, TW, p.cu_budget > 0 ? p.cu_budget : 256);
+    dim3 grid(conv64_blocks(p, TW, run_len));
     ConvParams q = p;
     q.stamps = g_debug_stamps;
-    // prologue mode 2 (filters by LDS-DMA, input groups register-staged) measured fastest
-    hipLaunchKernelGGL((conv64_kernel<TW, EPI, 2>), grid, dim3(kThreads), Conv2Smem<TW>::TOTAL, st, q, run_len);
+    hipLaunchKernelGGL((conv64_kernel<TW, EPI>), grid, dim3(kThreads), Conv2Smem<TW>::TOTAL, st, q, run_len);
   } else {
     constexpr int E1 = EPI == EPI_DG_ACC_CA ? EPI_DG_ACC : EPI;  // v1 handles the general form
     dim3 grid((p.H / kTH) * (p.W / TW), p.Cout / 64, p.N);

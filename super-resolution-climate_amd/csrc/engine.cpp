@@ -196,14 +196,10 @@ struct srmi_engine {
   bf16_t* dPS[3];
   float *slab, *bslab;
   size_t slab_floats, bslab_floats;
-  // side stream for the RCAB filter gradients (overlapped with the dgrad chain)
-  hipStream_t side = nullptr;
-  hipEvent_t ev_dz[2] = {}, ev_w1[2] = {}, ev_grp = nullptr, ev_side = nullptr;
-  // RCAB gradient buffers: a ring of 4 (du, dz of RCABs i .. i+3), see backward_impl
-  bf16_t *DUr[4] = {}, *DZr[4] = {};
-  float *slab_s = nullptr, *bslab_s = nullptr;
-  float *slab_s2 = nullptr, *bslab_s2 = nullptr;  // second side slab set (paired reductions)
-  size_t slab_s_floats = 0, bslab_s_floats = 0;
+  // RCAB filter-gradient slabs: [RCAB parity][conv2, conv1] (the reduction of RCAB
+  // i runs in RCAB i+1's CA-backward launch, while RCAB i+1 writes the other parity)
+  float *slab_r[2][2] = {}, *bslab_r[2][2] = {};
+  size_t slab_r_floats = 0, bslab_r_floats = 0;
   float* lpart;
   int lpart_n;
   float* zeros;  // 256 zero bytes (DMA padding source)
@@ -235,13 +231,12 @@ struct srmi_engine {
   float* brecp(int g, int b) const { return brec + (size_t)(g * P.cfg.nblocks + (b - 1)) * N * 224; }
 };
 
-// row chunks per image of the side-stream (RCAB) filter gradients.  They run
-// beside the dgrad chain, so they are sized for HALF the engine's CU budget:
-// fewer, longer chunks write fewer partial slabs (at C2 2 x 24-row chunks per
-// image instead of 3 x 16: 1837 -> 1901 tiles/s measured).
-static int side_row_splits(const srmi_engine* e) {
-  return choose_row_splits(e->N, e->h, 64, (e->cu_budget > 0 ? e->cu_budget : 256) / 2);
-}
+// The RCAB filter gradients run beside their dgrad convs (one fused launch, the
+// CU budget split in halves), so their row chunks are sized for HALF the engine's
+// budget: fewer, longer chunks write fewer partial slabs (at C2 2 x 24-row chunks
+// per image instead of 3 x 16).
+static int engine_cus(const srmi_engine* e) { return e->cu_budget > 0 ? e->cu_budget : 256; }
+static int rcab_row_splits(const srmi_engine* e, int n) { return choose_row_splits(n, e->h, 64, engine_cus(e) / 2); }
 
 static size_t carve(srmi_engine* e, char* base) {
   Carver cv;
@@ -282,13 +277,6 @@ static size_t carve(srmi_engine* e, char* base) {
     e->GBb = act(m);
     e->DU = act(m);
     e->DZ = act(m);
-    e->DUr[0] = e->DU;
-    e->DZr[0] = e->DZ;
-    for (int k = 1; k < 4; ++k) {
-      const bool own = rcan;
-      e->DUr[k] = own ? act(m) : e->DU;
-      e->DZr[k] = own ? act(m) : e->DZ;
-    }
     e->dRESb = act(m);
     for (int k = 0; k < 3; ++k) e->dPS[k] = nullptr;
     for (int k = 0; k < P.nups; ++k) e->dPS[k] = act(m << (2 * (k + 1)));
@@ -313,14 +301,16 @@ static size_t carve(srmi_engine* e, char* base) {
     e->bslab_floats = bf;
     e->slab = cv.take<float>(sf);
     e->bslab = cv.take<float>(bf);
-    if (rcan) {  // the side stream's own slabs (64-channel RCAB convs only)
-      const size_t ns = (size_t)N * side_row_splits(e);
-      e->slab_s_floats = ns * 64 * 576;
-      e->bslab_s_floats = ns * 64;
-      e->slab_s = cv.take<float>(e->slab_s_floats);
-      e->bslab_s = cv.take<float>(e->bslab_s_floats);
-      e->slab_s2 = cv.take<float>(e->slab_s_floats);
-      e->bslab_s2 = cv.take<float>(e->bslab_s_floats);
+    if (rcan) {  // the RCAB filter-gradient slab sets (64-channel convs only)
+      size_t ns = 0;
+      for (int n = 1; n <= N; ++n) ns = std::max(ns, (size_t)n * rcab_row_splits(e, n));
+      e->slab_r_floats = ns * 64 * 576;
+      e->bslab_r_floats = ns * 64;
+      for (int q = 0; q < 2; ++q)
+        for (int c = 0; c < 2; ++c) {
+          e->slab_r[q][c] = cv.take<float>(e->slab_r_floats);
+          e->bslab_r[q][c] = cv.take<float>(e->bslab_r_floats);
+        }
     }
   }
   e->packs = act(P.pack_elems);
@@ -405,9 +395,9 @@ static int conv_fwd(srmi_engine* e, const ConvRef& c, const bf16_t* x, int n, in
 }
 
 // dgrad of conv c: input dy (Cout channels, PS layout if c.ps), output Cin channels
-static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n, int H, int W, int epi, bf16_t* yb,
-                      float* yf, const float* r1, const float* r2, const float* r3, const bf16_t* aux, float* part,
-                      float alpha, hipStream_t st) {
+static ConvParams dgrad_params(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n, int H, int W, int* epi,
+                               bf16_t* yb, float* yf, const float* r1, const float* r2, const float* r3,
+                               const bf16_t* aux, float* part, float alpha) {
   ConvParams p{};
   p.x = dy;
   p.w = e->at(e->packs, c.d_off);
@@ -430,16 +420,23 @@ static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n,
   p.alpha = alpha;
   p.zeros = e->zeros;
   p.cu_budget = e->cu_budget;
-  if (epi == EPI_DG_ACC && r1 && aux && part && !yb && !r2 && !r3 && yf && c.cout == 64 && !c.ps)
-    epi = EPI_DG_ACC_CA;  // the hot RCAB case: specialised epilogue without runtime operand checks
+  if (*epi == EPI_DG_ACC && r1 && aux && part && !yb && !r2 && !r3 && yf && c.cout == 64 && !c.ps)
+    *epi = EPI_DG_ACC_CA;  // the hot RCAB case: specialised epilogue without runtime operand checks
+  return p;
+}
+
+static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n, int H, int W, int epi, bf16_t* yb,
+                      float* yf, const float* r1, const float* r2, const float* r3, const bf16_t* aux, float* part,
+                      float alpha, hipStream_t st) {
+  const ConvParams p = dgrad_params(e, c, dy, n, H, W, &epi, yb, yf, r1, r2, r3, aux, part, alpha);
   return conv3x3_launch(p, epi, st);
 }
 
-// side: the launch runs on the side stream with its own slabs (set `sset`); with
-// `defer` the reduction is not launched but returned in *out (see reduce2 below).
-static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const bf16_t* dy, int n, int H, int W,
-                      float* grads, bool with_bias, float alpha, hipStream_t st, bool side = false, int sset = 0,
-                      ReduceSet* defer = nullptr) {
+// filter gradient of conv c into `slab`/`bslab` (capacity cap/bcap floats); the
+// reduction into grads is returned in *red
+static int wgrad_params(srmi_engine* e, const ConvRef& c, const bf16_t* x, const bf16_t* dy, int n, int H, int W,
+                        float* grads, bool with_bias, float alpha, int row_splits, float* slab, float* bslab,
+                        size_t cap, size_t bcap, WgradParams* out, ReduceSet* red) {
   WgradParams p{};
   p.x = x;
   p.dy = dy;
@@ -450,22 +447,40 @@ static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const b
   p.Cout = c.cout;
   p.dy_mode = c.ps ? IN_UNSHUF : IN_PLAIN;
   p.imgs_per_wg = 1;
-  p.row_splits = side ? side_row_splits(e) : choose_row_splits(n, H, c.cout, e->cu_budget);
-  p.slab = side ? (sset ? e->slab_s2 : e->slab_s) : e->slab;
-  p.bslab = side ? (sset ? e->bslab_s2 : e->bslab_s) : e->bslab;
+  p.row_splits = row_splits;
+  p.slab = slab;
+  p.bslab = bslab;
   p.zeros = e->zeros;
   const size_t ns = (size_t)wgrad3x3_nslabs(p);
-  const size_t cap = side ? e->slab_s_floats : e->slab_floats, bcap = side ? e->bslab_s_floats : e->bslab_floats;
   if (ns * c.cout * 576 > cap || ns * c.cout > bcap) return SRMI_ERR_WORKSPACE;
-  int rc = wgrad3x3_launch(p, st);
+  *out = p;
+  *red = ReduceSet{p.slab, p.bslab, (int)ns, c.cout, c.ps, wgrad3x3_slab_layout(p), alpha, grads + c.w,
+                   with_bias ? grads + c.b : nullptr};
+  return 0;
+}
+
+// filter gradient + its reduction, both on st (upsampler / group-tail / body-tail /
+// EDSR convs)
+static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const bf16_t* dy, int n, int H, int W,
+                      float* grads, bool with_bias, float alpha, hipStream_t st) {
+  WgradParams p;
+  ReduceSet r;
+  const int rc = wgrad_params(e, c, x, dy, n, H, W, grads, with_bias, alpha, choose_row_splits(n, H, c.cout, e->cu_budget),
+                              e->slab, e->bslab, e->slab_floats, e->bslab_floats, &p, &r);
   if (rc) return rc;
-  if (defer) {
-    *defer = ReduceSet{p.slab, p.bslab, (int)ns, c.cout, c.ps, wgrad3x3_slab_layout(p), alpha, grads + c.w,
-                       with_bias ? grads + c.b : nullptr};
-    return 0;
-  }
-  return wgrad_reduce_launch(p.slab, p.bslab, (int)ns, c.cout, c.ps, wgrad3x3_slab_layout(p), alpha, grads + c.w,
-                             with_bias ? grads + c.b : nullptr, st);
+  const int rc2 = wgrad3x3_launch(p, st);
+  if (rc2) return rc2;
+  return wgrad_reduce_launch(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb, st);
+}
+
+// a dgrad conv and the filter gradient of the same conv (independent, both reading
+// dy): one fused launch where the shapes allow (bf16, 48-wide tiles), else the two
+// launches one after the other on the same stream
+static int dgrad_with_wgrad(srmi_engine* e, const ConvParams& cp, int epi, const WgradParams& wp, hipStream_t st) {
+  if (rcab_bwd_fusable(cp, wp)) return rcab_bwd_launch(cp, epi, engine_cus(e) / 2, wp, st);
+  const int rc = wgrad3x3_launch(wp, st);
+  if (rc) return rc;
+  return conv3x3_launch(cp, epi, st);
 }
 
 #define RC(x)              \
@@ -579,55 +594,56 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
     RC(conv_wgrad(e, P.body_tail, e->hb(nl, 0), e->dRESb, n, h, w, grads, true, 1.f, st));
     RC(conv_dgrad(e, P.body_tail, e->dRESb, n, h, w, EPI_DG_ACC, gRb, gRf, nullptr, nullptr, nullptr, nullptr, nullptr,
                   1.f, st));
-    int it = 0;  // RCAB counter (buffer ring parity)
+    // One stream, three launches per RCAB:
+    //   [CA backward -> du (+ the slab reductions of the previous RCAB)]
+    //   [dgrad conv2 -> dz  ||  filter gradient conv2 (t, du)]
+    //   [dgrad conv1 -> g (+ CA sums of the next RCAB)  ||  filter gradient conv1 (hb, dz)]
+    // The filter gradients write the slab set of their RCAB's parity; the last
+    // RCAB of a group reduces its own slabs before the group's event.
+    const int rs = rcab_row_splits(e, n);
+    int it = 0;  // RCAB counter (slab-set parity)
     for (int g = nl - 1; g >= 0; --g) {
       const ConvRef& gt = P.group_tail[g];
       RC(conv_wgrad(e, gt, e->hb(g, nb), gRb, n, h, w, grads, true, 1.f, st));
       RC(conv_dgrad(e, gt, gRb, n, h, w, EPI_DG_ACC, nullptr, ghf, nullptr, nullptr, nullptr, e->Um(g, nb), e->pacc,
                     1.f, st));
+      ReduceSet prev2{}, prev1{};
+      bool have_prev = false;
       for (int b = nb; b >= 1; --b) {
         const RCABRef& r = P.groups[g][b - 1];
-        // The two filter gradients of this RCAB run on the side stream, overlapped with
-        // the dgrad chain; DU/DZ rotate through a ring of 4 buffers, and a buffer is
-        // only rewritten after the side stream has finished the wgrads that read it:
-        // the side records its c1 event only after odd RCABs, and main waits only
-        // before even RCAB i >= 4, on the event of RCAB i-3 -- that covers the reuse
-        // of the slots of RCABs i-4 and i-3 (= i and i+1): one record and one wait per
-        // two RCABs.  The side stream waits once per RCAB, on dz, before both filter
-        // gradients (it runs behind main anyway).
-        const int it0 = it++;
-        const int q = it0 & 3, qe = it0 & 1;
-        const bool reuse = it0 >= 4 && !(it0 & 1);
-        bf16_t* du = e->DUr[q];
-        bf16_t* dz = e->DZr[q];
-        if (reuse) HC(hipStreamWaitEvent(st, e->ev_w1[((it0 - 3) >> 1) & 1], 0));
+        const int q = it++ & 1;
+        bf16_t* du = e->DU;
+        bf16_t* dz = e->DZ;
         RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
-                            e->brecp(g, b), e->f32, st));
+                            e->brecp(g, b), e->f32, st, have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
         ReduceSet red2, red1;
-        RC(conv_dgrad(e, r.c2, du, n, h, w, EPI_DG_RELUMASK, dz, nullptr, nullptr, nullptr, nullptr, e->Tm(g, b),
-                      nullptr, 1.f, st));
-        HC(hipEventRecord(e->ev_dz[qe], st));
-        HC(hipStreamWaitEvent(e->side, e->ev_dz[qe], 0));
-        RC(conv_wgrad(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, e->side, true, 0, &red2));
-        RC(conv_wgrad(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, e->side, true, 1, &red1));
-        if (it0 & 1) HC(hipEventRecord(e->ev_w1[(it0 >> 1) & 1], e->side));
-        RC(wgrad_reduce2_launch(red2, red1, e->side));  // both slab sets in one launch
+        WgradParams wp;
+        int epi = EPI_DG_RELUMASK;
+        ConvParams cp = dgrad_params(e, r.c2, du, n, h, w, &epi, dz, nullptr, nullptr, nullptr, nullptr, e->Tm(g, b),
+                                     nullptr, 1.f);
+        RC(wgrad_params(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, rs, e->slab_r[q][0], e->bslab_r[q][0],
+                        e->slab_r_floats, e->bslab_r_floats, &wp, &red2));
+        RC(dgrad_with_wgrad(e, cp, epi, wp, st));
         const bool last = (b == 1);
-        RC(conv_dgrad(e, r.c1, dz, n, h, w, EPI_DG_ACC, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
-                      (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
-                      last ? nullptr : e->pacc, 1.f, st));
+        epi = EPI_DG_ACC;
+        cp = dgrad_params(e, r.c1, dz, n, h, w, &epi, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
+                          (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
+                          last ? nullptr : e->pacc, 1.f);
+        RC(wgrad_params(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, rs, e->slab_r[q][1],
+                        e->bslab_r[q][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red1));
+        RC(dgrad_with_wgrad(e, cp, epi, wp, st));
+        prev2 = red2;
+        prev1 = red1;
+        have_prev = true;
       }
+      RC(wgrad_reduce2_launch(prev2, prev1, st));
       RC(ca_param_grads_batched_launch(e->recp(g, 1), e->brecp(g, 1), nb, n, e->N, 64, R, e->d_caoffs + (size_t)g * nb * 5,
                                        grads, st));
       std::swap(gRf, ghf);
       std::swap(gRb, ghb);
-      if (group_events && group_events[g]) {
-        // the group's gradients are final once main (CA grads, dgrad chain) and the
-        // side stream (filter gradients) are both past it
-        HC(hipEventRecord(e->ev_grp, st));
-        HC(hipStreamWaitEvent(e->side, e->ev_grp, 0));
-        HC(hipEventRecord(reinterpret_cast<hipEvent_t>(group_events[g]), e->side));
-      }
+      // the group's gradients are final here (one stream): the hook for a bucketed
+      // all-reduce overlapped with the rest of backward
+      if (group_events && group_events[g]) HC(hipEventRecord(reinterpret_cast<hipEvent_t>(group_events[g]), st));
     }
   } else {
     const float rsc = P.cfg.res_scale;
@@ -645,10 +661,6 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
       std::swap(gRf, ghf);
       std::swap(gRb, ghb);
     }
-  }
-  if (P.cfg.arch == SRMI_ARCH_RCAN) {  // every side-stream filter gradient is in grads
-    HC(hipEventRecord(e->ev_side, e->side));
-    HC(hipStreamWaitEvent(st, e->ev_side, 0));
   }
   // head: only the weight gradient (the input gradient is never read)
   RC(head_wgrad_launch(lr, gRf, n, e->C, h, w, e->slab, &nsl, st));
@@ -704,24 +716,11 @@ int srmi_engine_create(const srmi_model_config* cfg, void* workspace, size_t ws_
     return SRMI_ERR_WORKSPACE;
   }
   carve(e, base);
-  if (train && e->P.cfg.arch == SRMI_ARCH_RCAN) {
-    HC(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
-    hipEvent_t* evs[] = {&e->ev_dz[0], &e->ev_dz[1], &e->ev_w1[0], &e->ev_w1[1], &e->ev_grp, &e->ev_side};
-    for (hipEvent_t* ev : evs) HC(hipEventCreateWithFlags(ev, hipEventDisableTiming));
-  }
   *out = e;
   return 0;
 }
 
 int srmi_engine_destroy(srmi_engine* e) {
-  if (!e) return 0;
-  hipEvent_t evs[] = {e->ev_dz[0], e->ev_dz[1], e->ev_w1[0], e->ev_w1[1], e->ev_grp, e->ev_side};
-  for (hipEvent_t ev : evs)
-    if (ev) (void)hipEventDestroy(ev);
-  if (e->side) {
-    (void)hipStreamSynchronize(e->side);
-    (void)hipStreamDestroy(e->side);
-  }
   delete e;
   return 0;
 }

@@ -14,6 +14,7 @@
 
 #include "common.hpp"
 #include "srmi_internal.hpp"
+#include "wgrad_reduce.hpp"
 
 namespace srmi {
 
@@ -958,12 +959,27 @@ int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1
 // brec per image: dz2[C] dz1[CR] dbconv2[C]; followed (after all N images) by
 // dm[N][C] = W1^T dz1 (the gradient of the pooled mean).
 // du = g * s + dm / HW  (operand type)
+//
+// Rows blockIdx.y >= N of the grid (nred > 0) carry the fixed-order slab
+// reductions of the previous RCAB's two filter gradients (r0, r1: nred blocks
+// each, 256-thread wgrad_reduce_body): both are memory-bound passes of many small
+// blocks, so the reduction rides in this launch instead of a launch of its own.
 template <typename T>
 __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict__ g, const float* __restrict__ part,
                                                         int nstrips, const float* __restrict__ rec,
                                                         const float* __restrict__ w1, const float* __restrict__ w2,
                                                         int N, int HW, int C, int CR, T* __restrict__ du,
-                                                        float* __restrict__ brec) {
+                                                        float* __restrict__ brec, ReduceSet r0, ReduceSet r1,
+                                                        int nred) {
+  if ((int)blockIdx.y >= N) {
+    const int id = ((int)blockIdx.y - N) * (int)gridDim.x + (int)blockIdx.x;
+    if (id < nred)
+      wgrad_reduce_body<16>(r0.slab, r0.bslab, r0.nslab, r0.Cout, r0.ps, r0.layout, r0.alpha, r0.gw, r0.gb, id);
+    else if (id < 2 * nred)
+      wgrad_reduce_body<16>(r1.slab, r1.bslab, r1.nslab, r1.Cout, r1.ps, r1.layout, r1.alpha, r1.gw, r1.gb,
+                            id - nred);
+    return;
+  }
   __shared__ float red[2][128], s[64], dz2[64], dz1[32], dm[64];
   const int n = blockIdx.y, tid = threadIdx.x;
   const float* r = rec + (size_t)n * (2 * C + CR);
@@ -1054,14 +1070,23 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
 }
 
 int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
-                     const float* w2, int N, int HW, int C, int R, void* du, float* brec, int f32, hipStream_t st) {
+                     const float* w2, int N, int HW, int C, int R, void* du, float* brec, int f32, hipStream_t st,
+                     const ReduceSet* red0, const ReduceSet* red1) {
   if (C != 64 || C % R || (C / R) > 32 || (C / R) % 4 || (HW * C) % 8) return SRMI_ERR_SHAPE;
+  if ((red0 == nullptr) != (red1 == nullptr)) return SRMI_ERR_ARG;
+  if (red0 && (red0->Cout != red1->Cout)) return SRMI_ERR_SHAPE;
+  const int gx = ca_grid_x(HW, C);
+  const ReduceSet none{};
+  const int nred = red0 ? wgrad_reduce_blocks(red0->Cout) : 0;
+  const dim3 grid(gx, N + (2 * nred + gx - 1) / gx);
+  const ReduceSet& a = red0 ? *red0 : none;
+  const ReduceSet& b = red1 ? *red1 : none;
   if (f32)
-    hipLaunchKernelGGL(ca_bwd_du_kernel<float>, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, g, part, nstrips, rec,
-                       w1, w2, N, HW, C, C / R, static_cast<float*>(du), brec);
+    hipLaunchKernelGGL(ca_bwd_du_kernel<float>, grid, dim3(256), 0, st, g, part, nstrips, rec, w1, w2, N, HW, C,
+                       C / R, static_cast<float*>(du), brec, a, b, nred);
   else
-    hipLaunchKernelGGL(ca_bwd_du_kernel<bf16_t>, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st, g, part, nstrips, rec,
-                       w1, w2, N, HW, C, C / R, static_cast<bf16_t*>(du), brec);
+    hipLaunchKernelGGL(ca_bwd_du_kernel<bf16_t>, grid, dim3(256), 0, st, g, part, nstrips, rec, w1, w2, N, HW, C,
+                       C / R, static_cast<bf16_t*>(du), brec, a, b, nred);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

@@ -83,6 +83,10 @@ struct ReduceSet {  // one slab reduction: slabs -> torch-layout dW (and db)
   float* gb;
 };
 int wgrad_reduce2_launch(const ReduceSet& r0, const ReduceSet& r1, hipStream_t st);
+// fused RCAB backward launch: dgrad conv (epi RELUMASK / DG_ACC_CA / DG_ACC, its runs
+// sized for conv_cus CUs) beside the filter gradient wp of the same conv (wgrad48)
+int rcab_bwd_fusable(const ConvParams& cp, const WgradParams& wp);
+int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradParams& wp, hipStream_t st);
 int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, int layout, float alpha,
                         float* gw, float* gb, hipStream_t st);
 
@@ -120,8 +124,10 @@ int charb_partial_launch(const float* y, const float* t, size_t n, float eps, do
 int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1, const float* b1,
                   const float* w2, const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out,
                   void* hb_out, float* rec, int f32, hipStream_t st);
+// red0/red1 (both or neither): two slab reductions carried in the same launch
 int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
-                     const float* w2, int N, int HW, int C, int R, void* du, float* brec, int f32, hipStream_t st);
+                     const float* w2, int N, int HW, int C, int R, void* du, float* brec, int f32, hipStream_t st,
+                     const ReduceSet* red0 = nullptr, const ReduceSet* red1 = nullptr);
 // records of consecutive RCABs Ncap images apart (the engine capacity), N summed
 int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int Ncap, int C, int R,
                                   const long long* offs, float* grads, hipStream_t st);

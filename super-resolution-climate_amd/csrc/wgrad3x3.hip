@@ -22,7 +22,9 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "conv64_body.hpp"
 #include "srmi_internal.hpp"
+#include "wgrad_reduce.hpp"
 
 namespace srmi {
 
@@ -235,11 +237,10 @@ constexpr int NGP = 2 * GD + 2 * GX;                             // groups per p
 // The body is instantiated once per wave (WV = wave index): the wave's DMA groups,
 // taps and tile rotation are compile-time constants (no SGPR pressure, no branches).
 template <int WV>
-__device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
+__device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, int chunk, int cb) {
   using namespace v4;
   const int tid = threadIdx.x, lane = tid & 63;
   constexpr int wave = WV, wave_s = WV;
-  const int chunk = blockIdx.x, cb = blockIdx.y;
   const int Hr = p.H / p.row_splits;
   const int n = chunk / p.row_splits, ybase = (chunk % p.row_splits) * Hr;
   const int np = Hr / 2;
@@ -473,15 +474,81 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem) {
   WSTAMP(63);
 }
 
-__global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void wgrad48_dispatch(const WgradParams& p, char* smem, int chunk, int cb) {
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: wgrad48_body<0>(p, smem); break;
-    case 1: wgrad48_body<1>(p, smem); break;
-    case 2: wgrad48_body<2>(p, smem); break;
-    default: wgrad48_body<3>(p, smem); break;
+    case 0: wgrad48_body<0>(p, smem, chunk, cb); break;
+    case 1: wgrad48_body<1>(p, smem, chunk, cb); break;
+    case 2: wgrad48_body<2>(p, smem, chunk, cb); break;
+    default: wgrad48_body<3>(p, smem, chunk, cb); break;
   }
 }
+
+__global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  wgrad48_dispatch(p, smem, blockIdx.x, blockIdx.y);
+}
+
+// ---------------------------------------------------------------------------
+// Horizontally fused RCAB backward launch: a data-gradient conv (conv64 body:
+// dgrad of conv2 with the ReLU mask, or dgrad of conv1 accumulating into the
+// gradient stream) and the filter gradient of the SAME conv (wgrad48 body) read
+// the same upstream gradient and are independent, so one launch runs both: the
+// conv's runs and the wgrad's row chunks are dealt over the grid evenly
+// (Bresenham interleave), each sized for its share of the CU budget, one
+// workgroup per CU.  This replaces the two-stream overlap of round 1 (a side
+// stream per engine with cross-stream event waits) by co-scheduling inside one
+// launch on one stream: no events, one launch instead of two.
+template <int EPI>
+__global__ void __launch_bounds__(256, 1) rcab_bwd_kernel(ConvParams cp, int run_len, int nconv, WgradParams wp,
+                                                          int nwg) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.x, tot = nconv + nwg;
+  const int c0 = (int)(((long long)b * nconv) / tot), c1 = (int)(((long long)(b + 1) * nconv) / tot);
+  if (c1 > c0) {
+    conv64_body<48, EPI>(cp, run_len, c0, smem);
+    return;
+  }
+  const int w = b - c0, nch = wp.N * wp.row_splits;
+  wgrad48_dispatch(wp, smem, w % nch, w / nch);
+}
+
+int rcab_bwd_fusable(const ConvParams& cp, const WgradParams& wp) {
+  return !cp.f32 && !wp.f32 && cp.Cin == 64 && cp.Cout == 64 && cp.in_mode == IN_PLAIN && cp.W == 48 &&
+         cp.H % 4 == 0 && wp.W == 48 && wp.Cout == 64 && wp.dy_mode == IN_PLAIN && wp.row_splits > 0 &&
+         wp.H % wp.row_splits == 0 && (wp.H / wp.row_splits) % 4 == 0;
+}
+
+int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradParams& wp, hipStream_t st) {
+  if (!rcab_bwd_fusable(cp, wp)) return SRMI_ERR_SHAPE;
+  const int run_len = conv64_run_len(cp, 48, conv_cus);
+  const int nconv = conv64_blocks(cp, 48, run_len);
+  const int nwg = wp.N * wp.row_splits * (wp.Cout / 64);
+  const int lds = Conv2Smem<48>::TOTAL > v4::LDS ? Conv2Smem<48>::TOTAL : v4::LDS;
+  ConvParams c = cp;
+  c.stamps = nullptr;
+  WgradParams w = wp;
+  w.stamps = nullptr;
+  const dim3 grid(nconv + nwg);
+  switch (epi) {
+    case EPI_DG_RELUMASK:
+      if (!c.aux) return SRMI_ERR_ARG;
+      hipLaunchKernelGGL(rcab_bwd_kernel<EPI_DG_RELUMASK>, grid, dim3(256), lds, st, c, run_len, nconv, w, nwg);
+      break;
+    case EPI_DG_ACC_CA:
+      if (!c.r1 || !c.aux || !c.part || c.yb || c.r2 || c.r3 || !c.yf) return SRMI_ERR_ARG;
+      hipLaunchKernelGGL(rcab_bwd_kernel<EPI_DG_ACC_CA>, grid, dim3(256), lds, st, c, run_len, nconv, w, nwg);
+      break;
+    case EPI_DG_ACC:
+      if (!c.yf || (c.part && !c.aux)) return SRMI_ERR_ARG;
+      hipLaunchKernelGGL(rcab_bwd_kernel<EPI_DG_ACC>, grid, dim3(256), lds, st, c, run_len, nconv, w, nwg);
+      break;
+    default:
+      return SRMI_ERR_ARG;
+  }
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
 
 int wgrad3x3_nslabs(const WgradParams& p) { return p.N * p.row_splits; }
 
@@ -512,122 +579,21 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
   return 0;
 }
 
-// -------------------------------------------------------------------- reduce
-// block = kRedQ output quads (4*kRedQ consecutive outputs, float4 loads) x kRedPh
-// slab phases (512 threads); phase q sums slabs q, q+kRedPh, ... with 4
-// independent accumulators (4 loads in flight), then the kRedPh x 4 partials are
-// combined in a fixed 2-level order (deterministic).  64 outputs per block -> 576
-// blocks for a 64->64 conv (the former 256-output blocks left 112 CUs idle).
-// The bias slab ([nslab][Cout]) is handled by the last block(s).
-constexpr int kRedQ = 16, kRedPh = 32;
-__device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab, const float* __restrict__ bslab,
-                                                  int nslab, int Cout, int ps, int layout, float alpha,
-                                                  float* __restrict__ gw, float* __restrict__ gb) {
-  __shared__ float4 red[kRedPh][kRedQ], red2[4][kRedQ];
-  const int per = Cout * 576;
-  const int nwb = per / (4 * kRedQ);  // weight blocks (per % 64 == 0 since Cout % 64 == 0)
-  const int qd = threadIdx.x % kRedQ, ph = threadIdx.x / kRedQ;
-  const bool is_w = (int)blockIdx.x < nwb;
-  const float* src;
-  int stride, o4, valid;
-  if (is_w) {
-    if (!gw) return;
-    o4 = blockIdx.x * (4 * kRedQ) + qd * 4;
-    src = slab + o4;
-    stride = per;
-    valid = 1;
-  } else {
-    if (!gb) return;
-    o4 = (blockIdx.x - nwb) * (4 * kRedQ) + qd * 4;
-    src = bslab + o4;
-    stride = Cout;
-    valid = o4 < Cout;
-  }
-  float4 a[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (valid) {
-    // phase ph sums slabs ph, ph + kRedPh, ... -- U loads in flight per round,
-    // clamped + zeroed past the end (adding 0.f is exact; no divergent branch)
-    constexpr int U = 4;
-    for (int k = ph; k < nslab; k += U * kRedPh) {
-      float4 v[U];
-#pragma unroll
-      for (int j = 0; j < U; ++j) {
-        const int sl = k + j * kRedPh;
-        v[j] = *reinterpret_cast<const float4*>(src + (size_t)min(sl, nslab - 1) * stride);
-        if (sl >= nslab) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int j = 0; j < U; ++j) {
-        a[j].x += v[j].x; a[j].y += v[j].y; a[j].z += v[j].z; a[j].w += v[j].w;
-      }
-    }
-  }
-  red[ph][qd] = make_float4((a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y),
-                            (a[0].z + a[1].z) + (a[2].z + a[3].z), (a[0].w + a[1].w) + (a[2].w + a[3].w));
-  __syncthreads();
-  // fixed-order 2-level combine of the kRedPh phase partials
-  constexpr int L1 = 4, PER = kRedPh / L1;
-  if (ph < L1) {
-    float4 r = red[ph][qd];
-#pragma unroll
-    for (int q = 1; q < PER; ++q) {
-      const float4 t = red[ph + q * L1][qd];
-      r.x += t.x; r.y += t.y; r.z += t.z; r.w += t.w;
-    }
-    red2[ph][qd] = r;
-  }
-  __syncthreads();
-  if (ph != 0 || !valid) return;
-  float4 r = red2[0][qd];
-#pragma unroll
-  for (int q = 1; q < L1; ++q) {
-    const float4 t = red2[q][qd];
-    r.x += t.x; r.y += t.y; r.z += t.z; r.w += t.w;
-  }
-  const float s4[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int o = o4 + e;
-    if (is_w) {
-      int cop, ci, tap;
-      if (layout == 1) {  // wgrad48 native order [cb][wave][t][ct][lane][4]
-        const int cb = o / (64 * 576), l = o - cb * (64 * 576);
-        const int r = l & 3, lane = (l >> 2) & 63, ct = (l >> 8) & 3, wt = l >> 10;
-        const int wave = wt / 9, j = wt;  // j = 9 * wave + t
-        tap = j >> 2;
-        ci = (j & 3) * 16 + (lane & 15);
-        cop = cb * 64 + ((ct + wave) & 3) * 16 + 4 * (lane >> 4) + r;
-      } else {  // [tap][ci][Cout]
-        cop = o % Cout;
-        ci = (o / Cout) & 63;
-        tap = o / (Cout * 64);
-      }
-      const int cot = ps ? (4 * (cop & 63) + (cop >> 6)) : cop;
-      gw[((size_t)cot * 64 + ci) * 9 + tap] = alpha * s4[e];
-    } else if (o < Cout) {
-      const int cot = ps ? (4 * (o & 63) + (o >> 6)) : o;
-      gb[cot] = alpha * s4[e];
-    }
-  }
-}
-
 __global__ void __launch_bounds__(kRedQ * kRedPh) wgrad_reduce_kernel(ReduceSet r) {
-  wgrad_reduce_body(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb);
+  wgrad_reduce_body<kRedPh>(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb, blockIdx.x);
 }
 
 // two independent reductions in one launch (blockIdx.y selects the set): the two
 // filter gradients of an RCAB on the side stream share one launch and one boundary
 __global__ void __launch_bounds__(kRedQ * kRedPh) wgrad_reduce2_kernel(ReduceSet r0, ReduceSet r1) {
   const ReduceSet& r = blockIdx.y ? r1 : r0;
-  wgrad_reduce_body(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb);
+  wgrad_reduce_body<kRedPh>(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb, blockIdx.x);
 }
 
 int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, int layout, float alpha,
                         float* gw, float* gb, hipStream_t st) {
   if (Cout % 64) return SRMI_ERR_SHAPE;
-  const int blocks = Cout * 576 / (4 * kRedQ) + (Cout + 4 * kRedQ - 1) / (4 * kRedQ);
+  const int blocks = wgrad_reduce_blocks(Cout);
   const ReduceSet r{slab, bslab, nslab, Cout, ps, layout, alpha, gw, gb};
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(kRedQ * kRedPh), 0, st, r);
   SRMI_CHECK_LAUNCH();
@@ -636,7 +602,7 @@ int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Co
 
 int wgrad_reduce2_launch(const ReduceSet& r0, const ReduceSet& r1, hipStream_t st) {
   if (r0.Cout % 64 || r1.Cout != r0.Cout) return SRMI_ERR_SHAPE;
-  const int blocks = r0.Cout * 576 / (4 * kRedQ) + (r0.Cout + 4 * kRedQ - 1) / (4 * kRedQ);
+  const int blocks = wgrad_reduce_blocks(r0.Cout);
   hipLaunchKernelGGL(wgrad_reduce2_kernel, dim3(blocks, 2), dim3(kRedQ * kRedPh), 0, st, r0, r1);
   SRMI_CHECK_LAUNCH();
   return 0;
