@@ -13,8 +13,10 @@ bf16 filter repack: exactly dual_trainer.py:310-323.
 Inputs are synthetic lnorm'ed N(0,1) tiles already resident in HBM.
 
 Prints ONE JSON line on rank 0 with the roofline of the dominant kernel
-(the 3x3 filter-gradient kernel, measured with HIP events after the timed
-region; the forward conv alongside) and the CPU baseline
+(the fused conv1 dgrad + filter-gradient launch of the RCAB backward, re-issued
+by the bench's own engines at the in-step configuration and timed with HIP
+events on their streams after the timed region; conv2's fused launch and the
+isolated forward conv alongside; the step-level MFMA fraction) and the CPU baseline
 (the oracle, a PyTorch-CPU restatement of the reference step, timed on this
 host's cores on a bounded sample).
 """
@@ -100,19 +102,87 @@ def _time_launches(launch, stream, n=50, warm=5):
     return e0.elapsed_time(e1) / n
 
 
-def rooflines(dev, batch):
-    """Roofline of the dominant kernel (by rocprofv3 time share: the 3x3 filter-
-    gradient MFMA kernel, ~24 % of a step) plus the forward conv, both at the
-    bench shapes (B tiles of 48x48x64 bf16), average launch duration from HIP events
-    on the launch stream.  Algorithmic bytes = what the op must move at least
-    (inputs once + outputs once); flops = 2 x MACs."""
+ACT_BF16_PER_TILE = 48 * 48 * 64 * 2    # one bf16 48x48x64 activation
+ACT_F32_PER_TILE = 48 * 48 * 64 * 4
+WGRAD_OUT_BYTES = 64 * 577 * 4           # dW (64x64x9) + db, fp32, once per launch
+# Algorithmic bytes per tile of the two fused RCAB-backward launches (SURVEY.md §8(d),
+# DESIGN.md "Kernels"): what each must move at least, every operand once.
+#  F1 = rcab_bwd_kernel<DG_ACC_CA>: conv1's dgrad (reads dz bf16, reads + writes the
+#       fp32 residual-stream gradient g, reads the CA input u bf16 for the CA sums) and
+#       conv1's filter gradient (reads its input hb bf16; dz already counted)
+#  F2 = rcab_bwd_kernel<DG_RELUMASK>: conv2's dgrad (reads du bf16, reads the ReLU
+#       output t bf16 as the mask, writes dz bf16) and conv2's filter gradient (t, du
+#       already counted)
+F1_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE + 2 * ACT_F32_PER_TILE
+F2_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE
+FUSED_FLOP_PER_TILE = 2 * CONV64_FLOP_PER_TILE   # one dgrad conv + one filter-gradient conv
+
+
+def fused_rooflines(tr, step_ms, reps=20):
+    """Roofline of the dominant kernel AT ITS IN-STEP CONFIGURATION: the bench's own
+    trainer engines re-issue their fused backward launch of one RCAB
+    (srmi_engine_probe: same parameters, buffers, grid and CU split as inside the
+    step) `reps` times, every micro-batch engine on its own stream concurrently, as
+    in the step.  HIP events are recorded on each engine's stream; the per-launch
+    average duration is the slowest stream's elapsed / reps (the launches of the
+    engines overlap, so one launch slot moves micro x the per-engine bytes).
+    `achieved` = algorithmic bytes of all launches of one slot / average duration."""
+    from srmi._lib import call
+    main_st = torch.cuda.current_stream()
+    n_eng = len(tr.engines)
+    tiles_per_engine = tr.engines[0].batch
+    out = {}
+    for which, name, bpt in ((1, "rcab_bwd_kernel<EPI_DG_ACC_CA>", F1_BYTES_PER_TILE),
+                             (2, "rcab_bwd_kernel<EPI_DG_RELUMASK>", F2_BYTES_PER_TILE)):
+        streams = [tr.streams[k] or main_st for k in range(n_eng)]
+
+        def issue(r):
+            for k, eng in enumerate(tr.engines):
+                call("srmi_engine_probe", eng._h, which, r, streams[k].cuda_stream)
+
+        issue(3)
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in streams]
+        for k, st in enumerate(streams):
+            ev[k][0].record(st)
+        issue(reps)
+        for k, st in enumerate(streams):
+            ev[k][1].record(st)
+        torch.cuda.synchronize()
+        per_stream = [ev[k][0].elapsed_time(ev[k][1]) / reps for k in range(n_eng)]
+        ms = max(per_stream)
+        bytes_slot = bpt * tiles_per_engine * n_eng + WGRAD_OUT_BYTES * n_eng
+        flop_slot = FUSED_FLOP_PER_TILE * tiles_per_engine * n_eng
+        ach = bytes_slot / (ms * 1e-3) / 1e9
+        tf = flop_slot / (ms * 1e-3) / 1e12
+        tr_ = _pmc_traffic("rcab_bwd_kernel<%d>" % (7 if which == 1 else 4))
+        out[which] = {
+            "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": (tr_["bytes"] * n_eng if tr_ and tr_["bytes"] is not None else None),
+            "traffic_per_launch": tr_["bytes"] if tr_ else None,
+            "traffic_source": tr_["source"] if tr_ else None,
+            "kernel": "srmi::" + name, "in_step": True,
+            "config": f"{n_eng} concurrent launch(es) (one per micro-batch engine), {tiles_per_engine} tiles each, "
+                      "in-step grid and CU split",
+            "avg_launch_ms": round(ms, 4), "per_stream_ms": [round(x, 4) for x in per_stream],
+            "bytes_per_launch": bpt * tiles_per_engine + WGRAD_OUT_BYTES, "launches_per_slot": n_eng,
+            "flop_per_launch": FUSED_FLOP_PER_TILE * tiles_per_engine, "mfma_tflops": round(tf, 1),
+            "mfma_frac": round(tf / PEAK_BF16_TFLOPS, 4),
+            "share_of_step": round(ms * 20 * 10 / step_ms, 3),   # 200 RCABs per step
+        }
+    return out[1], out[2]
+
+
+def conv_fwd_roofline(dev, batch):
+    """The forward conv (fused bias + ReLU epilogue), ISOLATED: one launch over the
+    bench's B tiles on the current stream (in the step it runs at the same shape,
+    once per micro engine)."""
     from srmi._lib import call, ptr
     g = torch.Generator(device="cpu").manual_seed(0)
     N, H, W = batch, 48, 48
     st = torch.cuda.current_stream()
     x = torch.randn(N, H, W, 64, generator=g).to(dev).to(torch.bfloat16)
-    dy = torch.randn(N, H, W, 64, generator=g).to(dev).to(torch.bfloat16)
-    slab = torch.empty(N * 12 * 64 * 577 + 64, dtype=torch.float32, device=dev)
     w = (torch.randn(64, 64, 3, 3, generator=g) * 0.05).to(dev)
     b = torch.zeros(64, device=dev)
     fp = torch.empty(64 * 64 * 9, dtype=torch.bfloat16, device=dev)
@@ -121,31 +191,15 @@ def rooflines(dev, batch):
     call("srmi_pack_conv", ptr(w), ptr(b), 64, 64, 0, ptr(fp), ptr(dp), ptr(pb), 0, st.cuda_stream)
     y = torch.empty_like(x)
     flop = CONV64_FLOP_PER_TILE * N
-    act = N * H * W * 64 * 2  # one bf16 activation tensor
-
-    # dominant: filter gradient (partial slabs; the deterministic slab reduction is a separate launch)
-    ms_w = _time_launches(lambda: call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, 0, ptr(slab),
-                                       slab.numel() * 4, 0, 1.0, None, None, 0, st.cuda_stream), st)
-    bytes_w = 2 * act + 64 * 577 * 4          # x + dY read once, dW + db written once
-    t_hbm, t_mfma = bytes_w / (HBM_PEAK_GBS * 1e9), flop / (PEAK_BF16_TFLOPS * 1e12)
-    tr = _pmc_traffic("wgrad48_kernel")
-    ach = bytes_w / (ms_w * 1e-3) / 1e9
-    dom = {"bound": "hbm" if t_hbm >= t_mfma else "mfma", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr["bytes"] if tr else None,
-           "kernel": "srmi::wgrad48_kernel", "avg_launch_ms": round(ms_w, 4), "bytes_per_launch": bytes_w,
-           "flop_per_launch": flop, "mfma_tflops": round(flop / (ms_w * 1e-3) / 1e12, 1),
-           "mfma_frac": round(flop / (ms_w * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
-           "traffic_source": tr["source"] if tr else None}
-    # secondary: forward conv, fused bias + ReLU epilogue
     ms_c = _time_launches(lambda: call("srmi_conv3x3", ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, 0, ptr(y), None,
                                        None, None, None, None, None, 1.0, 0, st.cuda_stream), st)
     trc = _pmc_traffic("conv64_kernel<48, 0")
     ach_c = flop / (ms_c * 1e-3) / 1e12
-    conv = {"bound": "mfma", "achieved": round(ach_c, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+    return {"bound": "mfma", "achieved": round(ach_c, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach_c / PEAK_BF16_TFLOPS, 4), "traffic": trc["bytes"] if trc else None,
-            "kernel": "srmi::conv64_kernel<48,RELU>", "avg_launch_ms": round(ms_c, 4), "flop_per_launch": flop,
-            "bytes_per_launch": 2 * act + 64 * 576 * 2}
-    return dom, conv
+            "kernel": "srmi::conv64_kernel<48,RELU>", "in_step": False, "config": f"isolated, {N} tiles",
+            "avg_launch_ms": round(ms_c, 4), "flop_per_launch": flop,
+            "bytes_per_launch": 2 * N * ACT_BF16_PER_TILE + 64 * 576 * 2}
 
 
 def inference_bench(dev, side, iters):
@@ -323,12 +377,18 @@ def main():
     loss = float(out["loss"])
     tiles = B * world * args.steps
     value = tiles / dt
+    step_ms = 1000 * dt / args.steps
+    if info.rank == 0:
+        roof, roof_f2 = fused_rooflines(tr, step_ms)
+        step_tf = value / world * TRAIN_GFLOP_PER_TILE_C2 / 1000.0
+        roof["step_mfma_tflops"] = round(step_tf, 1)
+        roof["step_mfma_frac"] = round(step_tf / PEAK_BF16_TFLOPS, 4)
     del tr, hr  # the extra lines below run on their own engines
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     _log(f"timed: {value:.1f} tiles/s")
     if info.rank == 0:
-        roof, roof_conv = rooflines(dev, B)
+        roof_conv = conv_fwd_roofline(dev, B)
         _log("rooflines done")
         edsr = None
         if not args.no_edsr and world == 1:
@@ -355,6 +415,7 @@ def main():
             "model_tflops": round(value * TRAIN_GFLOP_PER_TILE_C2 / 1000.0, 1),
             "loss": round(loss, 6),
             "roofline": roof,
+            "roofline_f2": roof_f2,
             "roofline_conv_fwd": roof_conv,
             "cpu_baseline": cpu,
             "inference": infer,

@@ -116,6 +116,14 @@ int srmi_forward(srmi_engine* e, const float* params, const float* lr, float* sr
 int srmi_backward(srmi_engine* e, const float* params, const float* lr, const float* sr, const float* hr,
                   const float* loss4, const float* dy, float* grads, void** group_events, void* stream);
 
+/* diagnostic (bench roofline): re-issue `reps` times on `stream` the fused backward
+ * launch of RCAB (0, 2) exactly as srmi_backward issues it (same shapes, CU split,
+ * row chunks) -- which = 1: dgrad of conv1 accumulating into the gradient stream
+ * (+ CA sums) beside conv1's filter gradient; which = 2: the ReLU-mask dgrad of
+ * conv2 beside conv2's filter gradient -- on the buffers of the last backward
+ * (their contents are overwritten).  RCAN train engines only. */
+int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream);
+
 /* RMSE (l2loss, squared=False).  loss4[0] = sum of squares (this rank),
  * loss4[1] = global element count; after the optional all-reduce of loss4[0],
  * srmi_rmse_finalize sets loss4[3] = L = sqrt(S/count), loss4[2] = 1/(count L). */

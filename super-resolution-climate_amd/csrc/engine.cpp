@@ -236,7 +236,21 @@ struct srmi_engine {
 // budget: fewer, longer chunks write fewer partial slabs (at C2 2 x 24-row chunks
 // per image instead of 3 x 16).
 static int engine_cus(const srmi_engine* e) { return e->cu_budget > 0 ? e->cu_budget : 256; }
-static int rcab_row_splits(const srmi_engine* e, int n) { return choose_row_splits(n, e->h, 64, engine_cus(e) / 2); }
+// CU shares of the two parts of a fused launch, in percent of the engine budget taken
+// by the filter gradient: after the ReLU-mask dgrad of conv2 (FUSE_WG2) and after the
+// gradient-accumulating dgrad of conv1 (FUSE_WG1, the heavier conv epilogue)
+#ifndef SRMI_FUSE_WG2
+#define SRMI_FUSE_WG2 50
+#endif
+#ifndef SRMI_FUSE_WG1
+#define SRMI_FUSE_WG1 50
+#endif
+static int fuse_wg_cus(const srmi_engine* e, int which) {
+  return engine_cus(e) * (which == 2 ? SRMI_FUSE_WG2 : SRMI_FUSE_WG1) / 100;
+}
+static int rcab_row_splits(const srmi_engine* e, int n, int which) {
+  return choose_row_splits(n, e->h, 64, fuse_wg_cus(e, which));
+}
 
 static size_t carve(srmi_engine* e, char* base) {
   Carver cv;
@@ -303,7 +317,8 @@ static size_t carve(srmi_engine* e, char* base) {
     e->bslab = cv.take<float>(bf);
     if (rcan) {  // the RCAB filter-gradient slab sets (64-channel convs only)
       size_t ns = 0;
-      for (int n = 1; n <= N; ++n) ns = std::max(ns, (size_t)n * rcab_row_splits(e, n));
+      for (int n = 1; n <= N; ++n)
+        ns = std::max(ns, (size_t)n * std::max(rcab_row_splits(e, n, 1), rcab_row_splits(e, n, 2)));
       e->slab_r_floats = ns * 64 * 576;
       e->bslab_r_floats = ns * 64;
       for (int q = 0; q < 2; ++q)
@@ -476,8 +491,9 @@ static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const b
 // a dgrad conv and the filter gradient of the same conv (independent, both reading
 // dy): one fused launch where the shapes allow (bf16, 48-wide tiles), else the two
 // launches one after the other on the same stream
-static int dgrad_with_wgrad(srmi_engine* e, const ConvParams& cp, int epi, const WgradParams& wp, hipStream_t st) {
-  if (rcab_bwd_fusable(cp, wp)) return rcab_bwd_launch(cp, epi, engine_cus(e) / 2, wp, st);
+static int dgrad_with_wgrad(srmi_engine* e, const ConvParams& cp, int epi, const WgradParams& wp, int which,
+                            hipStream_t st) {
+  if (rcab_bwd_fusable(cp, wp)) return rcab_bwd_launch(cp, epi, engine_cus(e) - fuse_wg_cus(e, which), wp, st);
   const int rc = wgrad3x3_launch(wp, st);
   if (rc) return rc;
   return conv3x3_launch(cp, epi, st);
@@ -600,7 +616,7 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
     //   [dgrad conv1 -> g (+ CA sums of the next RCAB)  ||  filter gradient conv1 (hb, dz)]
     // The filter gradients write the slab set of their RCAB's parity; the last
     // RCAB of a group reduces its own slabs before the group's event.
-    const int rs = rcab_row_splits(e, n);
+    const int rs2 = rcab_row_splits(e, n, 2), rs1 = rcab_row_splits(e, n, 1);
     int it = 0;  // RCAB counter (slab-set parity)
     for (int g = nl - 1; g >= 0; --g) {
       const ConvRef& gt = P.group_tail[g];
@@ -621,17 +637,17 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         int epi = EPI_DG_RELUMASK;
         ConvParams cp = dgrad_params(e, r.c2, du, n, h, w, &epi, dz, nullptr, nullptr, nullptr, nullptr, e->Tm(g, b),
                                      nullptr, 1.f);
-        RC(wgrad_params(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, rs, e->slab_r[q][0], e->bslab_r[q][0],
+        RC(wgrad_params(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, rs2, e->slab_r[q][0], e->bslab_r[q][0],
                         e->slab_r_floats, e->bslab_r_floats, &wp, &red2));
-        RC(dgrad_with_wgrad(e, cp, epi, wp, st));
+        RC(dgrad_with_wgrad(e, cp, epi, wp, 2, st));
         const bool last = (b == 1);
         epi = EPI_DG_ACC;
         cp = dgrad_params(e, r.c1, dz, n, h, w, &epi, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
                           (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
                           last ? nullptr : e->pacc, 1.f);
-        RC(wgrad_params(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, rs, e->slab_r[q][1],
+        RC(wgrad_params(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, rs1, e->slab_r[q][1],
                         e->bslab_r[q][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red1));
-        RC(dgrad_with_wgrad(e, cp, epi, wp, st));
+        RC(dgrad_with_wgrad(e, cp, epi, wp, 1, st));
         prev2 = red2;
         prev1 = red1;
         have_prev = true;
@@ -743,6 +759,36 @@ int srmi_backward(srmi_engine* e, const float* params, const float* lr, const fl
   if (!e || !e->train || !params || !lr || !grads || e->last_n < 1) return SRMI_ERR_ARG;
   if (!dy && (!sr || !hr || !loss4)) return SRMI_ERR_ARG;
   return backward_impl(e, params, lr, sr, hr, loss4, dy, grads, group_events, S_(stream));
+}
+
+int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
+  if (!e || !e->train || e->P.cfg.arch != SRMI_ARCH_RCAN || e->last_n < 1 || reps < 1) return SRMI_ERR_ARG;
+  if (which != 1 && which != 2) return SRMI_ERR_ARG;
+  const int n = e->last_n, h = e->h, w = e->w;
+  const int b = e->P.cfg.nblocks >= 2 ? 2 : 1;
+  const RCABRef& r = e->P.groups[0][b - 1];
+  float* ghf = e->GBf;
+  float* grads = e->slab;  // the reductions are not launched: any pointer
+  WgradParams wp;
+  ReduceSet red;
+  ConvParams cp;
+  int epi;
+  if (which == 2) {
+    epi = EPI_DG_RELUMASK;
+    cp = dgrad_params(e, r.c2, e->DU, n, h, w, &epi, e->DZ, nullptr, nullptr, nullptr, nullptr, e->Tm(0, b), nullptr,
+                      1.f);
+    RC(wgrad_params(e, r.c2, e->Tm(0, b), e->DU, n, h, w, grads, false, 1.f, rcab_row_splits(e, n, 2),
+                    e->slab_r[0][0], e->bslab_r[0][0], e->slab_r_floats, e->bslab_r_floats, &wp, &red));
+  } else {
+    const bool last = (b == 1);
+    epi = EPI_DG_ACC;
+    cp = dgrad_params(e, r.c1, e->DZ, n, h, w, &epi, last ? e->GAb : nullptr, ghf, ghf, last ? e->GAf : nullptr,
+                      nullptr, last ? nullptr : e->Um(0, b - 1), last ? nullptr : e->pacc, 1.f);
+    RC(wgrad_params(e, r.c1, e->hb(0, b - 1), e->DZ, n, h, w, grads, true, 1.f, rcab_row_splits(e, n, 1),
+                    e->slab_r[0][1], e->bslab_r[0][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red));
+  }
+  for (int i = 0; i < reps; ++i) RC(dgrad_with_wgrad(e, cp, epi, wp, which, S_(stream)));
+  return 0;
 }
 
 int srmi_rmse_partial(srmi_engine* e, const float* pred, const float* target, size_t n, double count_global,

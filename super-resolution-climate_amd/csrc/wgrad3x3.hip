@@ -504,12 +504,15 @@ __global__ void __launch_bounds__(256, 1) rcab_bwd_kernel(ConvParams cp, int run
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x, tot = nconv + nwg;
   const int c0 = (int)(((long long)b * nconv) / tot), c1 = (int)(((long long)(b + 1) * nconv) / tot);
+#ifndef SRMI_FUSE_DIAG
+#define SRMI_FUSE_DIAG 0  // diagnostic builds only (wrong results): 1 = skip the wgrad part, 2 = skip the conv part
+#endif
   if (c1 > c0) {
-    conv64_body<48, EPI>(cp, run_len, c0, smem);
+    if (!(SRMI_FUSE_DIAG & 2)) conv64_body<48, EPI>(cp, run_len, c0, smem);
     return;
   }
   const int w = b - c0, nch = wp.N * wp.row_splits;
-  wgrad48_dispatch(wp, smem, w % nch, w / nch);
+  if (!(SRMI_FUSE_DIAG & 1)) wgrad48_dispatch(wp, smem, w % nch, w / nch);
 }
 
 int rcab_bwd_fusable(const ConvParams& cp, const WgradParams& wp) {

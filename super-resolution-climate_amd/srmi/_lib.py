@@ -47,6 +47,7 @@ _SIGS = {
     "srmi_pack_weights": ([P, P, P], C.c_int),
     "srmi_forward": ([P, P, P, P, C.c_int, P], C.c_int),
     "srmi_backward": ([P, P, P, P, P, P, P, P, C.POINTER(P), P], C.c_int),
+    "srmi_engine_probe": ([P, C.c_int, C.c_int, P], C.c_int),
     "srmi_rmse_partial": ([P, P, P, C.c_size_t, C.c_double, P, P], C.c_int),
     "srmi_rmse_finalize": ([P, P], C.c_int),
     "srmi_charbonnier_partial": ([P, P, P, C.c_size_t, C.c_double, C.c_float, P, P, P], C.c_int),

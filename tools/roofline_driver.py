@@ -1,11 +1,13 @@
-"""Launch the bench's roofline kernels in isolation (for rocprofv3 --pmc passes).
+"""Run the bench's training step and the in-step roofline probes (for rocprofv3
+--pmc passes and kernel-trace agreement checks).
 
-    python tools/roofline_driver.py [--batch 64] [--iters 20]
+    python tools/roofline_driver.py [--batch 64] [--micro 2] [--steps 2] [--reps 10]
 
-wgrad3x3 (slab-only: the MFMA kernel without its reduction) and the 64->64 conv
-with the fused bias+ReLU epilogue, both at BASELINE config 2 shapes (B tiles of
-48x48x64, bf16).  Inputs are re-used across launches, as in a training step
-where x and dY were just produced.
+The FusedTrainer of bench.py (rcan-10-20-64, 2-var, B tiles of 48x48, micro-batch
+engines) runs `steps` steps, then every engine re-issues its fused backward
+launches (srmi_engine_probe: conv1's dgrad + filter gradient, then conv2's) `reps`
+times on its own stream, concurrently as in the step.  Every dispatch of the
+dominant kernel in this run has the in-step launch configuration.
 """
 import argparse
 import os
@@ -16,34 +18,34 @@ sys.path[:0] = [os.path.join(ROOT, "super-resolution-climate_amd"), ROOT]
 
 import torch  # noqa: E402
 
-from srmi._lib import call, ptr  # noqa: E402
+from srmi._lib import call  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=64)
-    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--micro", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
+    from bench import synthetic_hr
+    from srmi.engine import NetSpec
+    from srmi.trainer import FusedTrainer
     d = torch.device("cuda", 0)
-    N, H, W = a.batch, 48, 48
-    st = torch.cuda.current_stream().cuda_stream
-    g = torch.Generator(device="cpu").manual_seed(0)
-    x = torch.randn(N, H, W, 64, generator=g).to(d).to(torch.bfloat16)
-    dy = torch.randn(N, H, W, 64, generator=g).to(d).to(torch.bfloat16)
-    slab = torch.empty(N * 12 * 64 * 577 + 64, dtype=torch.float32, device=d)
-    w = (torch.randn(64, 64, 3, 3, generator=g) * 0.05).to(d)
-    b = torch.zeros(64, device=d)
-    fp = torch.empty(64 * 64 * 9, dtype=torch.bfloat16, device=d)
-    dp = torch.empty_like(fp)
-    pb = torch.empty(64, device=d)
-    call("srmi_pack_conv", ptr(w), ptr(b), 64, 64, 0, ptr(fp), ptr(dp), ptr(pb), 0, st)
-    y = torch.empty_like(x)
-    for _ in range(a.iters):
-        call("srmi_wgrad3x3", ptr(x), ptr(dy), N, H, W, 64, 0, 0, ptr(slab), slab.numel() * 4, 0, 1.0, None, None,
-             0, st)
-    for _ in range(a.iters):
-        call("srmi_conv3x3", ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, 0, ptr(y), None, None, None, None, None,
-             None, 1.0, 0, st)
+    spec = NetSpec(arch="rcan", nchannels_in=2, nchannels_out=2, nlayers=10, nblocks=20, cbottleneck=2, scale=4)
+    tr = FusedTrainer(spec, a.batch, (48, 48), device=d, micro=a.micro)
+    hr = torch.tensor(synthetic_hr(a.batch, 2, 192, 1234)).to(d)
+    for _ in range(a.steps):
+        tr.step(hr)
+    torch.cuda.synchronize()
+    main_st = torch.cuda.current_stream()
+    for which in (1, 2):
+        for k, eng in enumerate(tr.engines):
+            st = tr.streams[k] or main_st
+            st.wait_stream(main_st)
+            call("srmi_engine_probe", eng._h, which, a.reps, st.cuda_stream)
+        for st in tr.streams[1:]:
+            main_st.wait_stream(st)
     torch.cuda.synchronize()
     print("done")
 
