@@ -1,11 +1,10 @@
 """Summarise a rocprofv3 kernel trace of `bench.py` for profiles/.
 
-The bench's roofline kernels are timed in isolation right after the timed step
-loop (5 warm-up + 50 timed launches each); inside the training step the filter-
-gradient kernels run on a side stream concurrently with the dgrad chain, so
-their in-step durations are stretched by sharing the GPU.  This reports both,
-per kernel: the isolated roofline-phase average (what bench.py's `roofline`
-uses) and the in-step average/total.
+Reports the kernel table of the run (dispatches, average and total duration per
+kernel), and for the two fused RCAB-backward kernels the average duration of the
+roofline-phase dispatches (bench.py fused_rooflines: 3 warm-up + 20 timed launches
+per micro-batch engine, after the timed steps) next to the bench's HIP-event
+average, plus the average over the in-step dispatches.
 
     python tools/prof_summary.py <kernel_trace.csv> <bench_log_with_json_line> <out.json>
 """
@@ -13,6 +12,8 @@ import csv
 import json
 import sys
 from collections import defaultdict
+
+REPS, WARM = 20, 3
 
 
 def main(trace, bench_log, out):
@@ -22,36 +23,32 @@ def main(trace, bench_log, out):
     for ln in open(bench_log):
         if ln.startswith("{") and '"metric"' in ln:
             line = json.loads(ln)
-    res = {"bench": {k: line[k] for k in ("value", "unit", "ms_per_step")} if line else None, "kernels": {}}
-    names = {"wgrad": "wgrad48_kernel", "conv_fwd": "conv64_kernel<48, 0, 2>"}
-    for key, pat in names.items():
+    res = {"bench": {k: line[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup")} if line else None,
+           "fused": {}, "kernels": {}}
+    dur = defaultdict(list)
+    for r in rows:
+        dur[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    tot = sum(sum(v) for v in dur.values())
+    for k, v in sorted(dur.items(), key=lambda kv: -sum(kv[1])):
+        res["kernels"][k[:120]] = {"dispatches": len(v), "avg_us": round(sum(v) / len(v) / 1e3, 3),
+                                   "total_ms": round(sum(v) / 1e6, 3), "share": round(sum(v) / tot, 4)}
+    n_eng = 1
+    if line and line.get("roofline"):
+        n_eng = line["roofline"].get("launches_per_slot", 1)
+    for key, pat, rk in (("F1", "rcab_bwd_kernel<7>", "roofline"), ("F2", "rcab_bwd_kernel<4>", "roofline_f2")):
         d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows if pat in r["Kernel_Name"]]
         if not d:
             continue
-        # the roofline phase is the last 55 launches of the kernel before the inference section:
-        # find the 55-launch run of isolated dispatches (no other srmi kernel in between)
-        idx = [i for i, r in enumerate(rows) if pat in r["Kernel_Name"]]
-        iso = []
-        for j in range(len(idx) - 1, -1, -1):
-            i = idx[j]
-            prev_ok = j > 0 and idx[j - 1] == i - 1
-            if prev_ok or (iso and idx[j + 1] == i + 1):
-                iso.append(i)
-                if len(iso) == 55:
-                    break
-            elif iso:
-                iso = []
-        iso_d = [int(rows[i]["End_Timestamp"]) - int(rows[i]["Start_Timestamp"]) for i in sorted(iso)[5:]]
-        res["kernels"][key] = {
-            "name_contains": pat, "dispatches": len(d), "avg_us_all": round(sum(d) / len(d) / 1e3, 3),
-            "roofline_phase_avg_us": round(sum(iso_d) / len(iso_d) / 1e3, 3) if iso_d else None,
-            "roofline_phase_dispatches": len(iso_d),
-        }
-        if line:
-            rk = "roofline" if key == "wgrad" else "roofline_conv_fwd"
-            res["kernels"][key]["bench_event_avg_us"] = round(line[rk]["avg_launch_ms"] * 1e3, 3)
+        probe = d[-REPS * n_eng:]
+        instep = d[:-(REPS + WARM) * n_eng]
+        rec = {"name_contains": pat, "dispatches": len(d),
+               "roofline_phase_avg_us": round(sum(probe) / len(probe) / 1e3, 3),
+               "in_step_avg_us": round(sum(instep) / len(instep) / 1e3, 3) if instep else None}
+        if line and line.get(rk):
+            rec["bench_event_avg_us"] = round(line[rk]["avg_launch_ms"] * 1e3, 3)
+        res["fused"][key] = rec
     json.dump(res, open(out, "w"), indent=1)
-    print(json.dumps(res, indent=1))
+    print(json.dumps(res["fused"], indent=1))
 
 
 if __name__ == "__main__":
