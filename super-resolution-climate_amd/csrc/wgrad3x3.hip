@@ -498,20 +498,36 @@ __global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
 // workgroup per CU.  This replaces the two-stream overlap of round 1 (a side
 // stream per engine with cross-stream event waits) by co-scheduling inside one
 // launch on one stream: no events, one launch instead of two.
+//
+// Block -> role map.  `paired` (the conv's runs and the wgrad's row chunks cover
+// the same image rows one to one: conv run k <-> chunk k): blocks are dealt in
+// groups of 16, eight conv runs then the eight chunks of the same rows, so run k
+// and chunk k sit 8 blocks apart -- the same XCD under round-robin dispatch -- and
+// the second reader of dY and of the shared operand finds its rows in that XCD's
+// L2 instead of fetching them again.  Otherwise a Bresenham interleave.
 template <int EPI>
 __global__ void __launch_bounds__(256, 1) rcab_bwd_kernel(ConvParams cp, int run_len, int nconv, WgradParams wp,
-                                                          int nwg) {
+                                                          int nwg, int paired) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x, tot = nconv + nwg;
-  const int c0 = (int)(((long long)b * nconv) / tot), c1 = (int)(((long long)(b + 1) * nconv) / tot);
 #ifndef SRMI_FUSE_DIAG
 #define SRMI_FUSE_DIAG 0  // diagnostic builds only (wrong results): 1 = skip the wgrad part, 2 = skip the conv part
 #endif
-  if (c1 > c0) {
-    if (!(SRMI_FUSE_DIAG & 2)) conv64_body<48, EPI>(cp, run_len, c0, smem);
+  int conv = -1, w;
+  if (paired) {
+    const int base = (b >> 4) << 3, i = b & 15, m = min(8, nconv - base);
+    if (i < m) conv = base + i;
+    else w = base + i - m;
+  } else {
+    const int c0 = (int)(((long long)b * nconv) / tot), c1 = (int)(((long long)(b + 1) * nconv) / tot);
+    if (c1 > c0) conv = c0;
+    else w = b - c0;
+  }
+  if (conv >= 0) {
+    if (!(SRMI_FUSE_DIAG & 2)) conv64_body<48, EPI>(cp, run_len, conv, smem);
     return;
   }
-  const int w = b - c0, nch = wp.N * wp.row_splits;
+  const int nch = wp.N * wp.row_splits;
   if (!(SRMI_FUSE_DIAG & 1)) wgrad48_dispatch(wp, smem, w % nch, w / nch);
 }
 
@@ -532,18 +548,26 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
   WgradParams w = wp;
   w.stamps = nullptr;
   const dim3 grid(nconv + nwg);
+#ifndef SRMI_FUSE_PAIR
+#define SRMI_FUSE_PAIR 1
+#endif
+  // conv run k and wgrad chunk k cover the same rows of the same image
+  const int runs_per_col = (cp.H / kTH + run_len - 1) / run_len;
+  const int paired = SRMI_FUSE_PAIR && nconv == nwg && cp.N == wp.N && runs_per_col == wp.row_splits &&
+                     run_len * kTH == wp.H / wp.row_splits;
   switch (epi) {
     case EPI_DG_RELUMASK:
       if (!c.aux) return SRMI_ERR_ARG;
-      hipLaunchKernelGGL(rcab_bwd_kernel<EPI_DG_RELUMASK>, grid, dim3(256), lds, st, c, run_len, nconv, w, nwg);
+      hipLaunchKernelGGL(rcab_bwd_kernel<EPI_DG_RELUMASK>, grid, dim3(256), lds, st, c, run_len, nconv, w, nwg,
+                         paired);
       break;
     case EPI_DG_ACC_CA:
       if (!c.r1 || !c.aux || !c.part || c.yb || c.r2 || c.r3 || !c.yf) return SRMI_ERR_ARG;
-      hipLaunchKernelGGL(rcab_bwd_kernel<EPI_DG_ACC_CA>, grid, dim3(256), lds, st, c, run_len, nconv, w, nwg);
+      hipLaunchKernelGGL(rcab_bwd_kernel<EPI_DG_ACC_CA>, grid, dim3(256), lds, st, c, run_len, nconv, w, nwg, paired);
       break;
     case EPI_DG_ACC:
       if (!c.yf || (c.part && !c.aux)) return SRMI_ERR_ARG;
-      hipLaunchKernelGGL(rcab_bwd_kernel<EPI_DG_ACC>, grid, dim3(256), lds, st, c, run_len, nconv, w, nwg);
+      hipLaunchKernelGGL(rcab_bwd_kernel<EPI_DG_ACC>, grid, dim3(256), lds, st, c, run_len, nconv, w, nwg, paired);
       break;
     default:
       return SRMI_ERR_ARG;
