@@ -11,7 +11,8 @@ import os
 from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("SRMI_LIB") or os.path.join(_HERE, "libsrmi.so")  # SRMI_LIB: diagnostic build
+LIB_PATH_DEFAULT = os.path.join(_HERE, "libsrmi.so")
+LIB_PATH = os.environ.get("SRMI_LIB") or LIB_PATH_DEFAULT  # SRMI_LIB: diagnostic build
 
 SRMI_ARCH_RCAN = 0
 SRMI_ARCH_EDSR = 1
@@ -101,6 +102,8 @@ def load(path: str = LIB_PATH) -> C.CDLL:
                         "there is no CPU fallback")
     lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
     for name, (args, res) in _SIGS.items():
+        if path != LIB_PATH_DEFAULT and not hasattr(lib, name):
+            continue  # a diagnostic build of an older revision (SRMI_LIB): entry points added since stay unbound
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
