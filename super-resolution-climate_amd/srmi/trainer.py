@@ -68,7 +68,8 @@ class FusedTrainer:
     def __init__(self, spec: NetSpec, batch: int, lr_hw=(48, 48), lr: float = 1e-4, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 0.0, interp_loss: bool = True,
                  info: Optional[DistInfo] = None, device: Optional[torch.device] = None, seed: int = 0,
-                 params: Optional[torch.Tensor] = None, micro: Optional[int] = None, loss_fn: str = "l2"):
+                 params: Optional[torch.Tensor] = None, micro: Optional[int] = None, loss_fn: str = "l2",
+                 cu_budget: Optional[int] = None):
         if loss_fn not in LOSS_KINDS:  # single_product_loss, dual_trainer.py:210-211
             raise ValueError(f"Unknown single-product loss function {loss_fn}")
         self.loss_fn = loss_fn
@@ -83,7 +84,8 @@ class FusedTrainer:
             raise ValueError(f"batch {batch} not divisible into {micro} micro-batches")
         self.micro = micro
         self.mb = batch // micro
-        budget = 256 // micro if micro > 1 else 0
+        # CUs each engine's launches are sized for (0 = the whole chip)
+        budget = (256 // micro if micro > 1 else 0) if cu_budget is None else int(cu_budget)
         self.engines = [Engine(spec, self.mb, lr_hw, train=True, device=self.device, cu_budget=budget)
                         for _ in range(micro)]
         self.eng = self.engines[0]
