@@ -3,10 +3,11 @@
  *
  * C ABI: plain pointers, sizes and a hipStream_t (passed as void*).  No torch
  * types.  All device memory is owned by the caller (PyTorch's caching
- * allocator on the Python side) and handed in as workspace; the library's own
- * allocations are host-side: the srmi_engine object (plan, layout, tables) and,
- * for RCAN training engines, one side stream and six events, all created by
- * srmi_engine_create and released by srmi_engine_destroy.  Every entry point returns 0
+ * allocator on the Python side) and handed in as workspace; the library's only
+ * allocation is host-side: the srmi_engine object (plan, workspace layout, pack
+ * tables), created by srmi_engine_create and released by srmi_engine_destroy.
+ * It creates no streams and no events: every launch goes to the caller's stream
+ * (group events for a bucketed all-reduce are the caller's).  Every entry point returns 0
  * on success or a negative status (SRMI_ERR_*, or -hipError_t), which the
  * Python binding raises as RuntimeError (the reference raises Python
  * exceptions; sres/controller/dual_trainer.py:557 @exception_handled).

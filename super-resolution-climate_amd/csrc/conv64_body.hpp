@@ -444,7 +444,11 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
       // group k+2's DMA pieces and the epilogue operands are issued one or two per
       // K-step, so a full memory queue stalls the wave between MFMA groups only
       if (s < NGW && pf && wv_s + 4 * s < NGRP) group_dma_one(k + 2, s);
-      if (s >= 2 && s - 2 < NPT * 4) epi_prefetch_one<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk, s - 2);
+      // the epilogue operands, two per K-step from the first one: a whole strip of
+      // MFMAs to land (spread over K-steps 2..13, the heavy fp32 epilogue of
+      // DG_ACC_CA waited on its last ones at the end of the K-loop: +1.3 % step)
+      if (2 * s < NPT * 4) epi_prefetch_one<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk, 2 * s);
+      if (2 * s + 1 < NPT * 4) epi_prefetch_one<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk, 2 * s + 1);
       __builtin_amdgcn_sched_barrier(0);
       const bool ld = s + LA < 18;
       if (ld) load_step(s + LA, A[(s + LA) % kFragBuf], B[(s + LA) % kFragBuf]);
