@@ -38,25 +38,37 @@ struct ConvSmem {
   static constexpr int TOTAL = HALO_BYTES + 2 * W_BYTES;
 };
 
+// every load of the thread in flight at once (clamped addresses, padding selected
+// to zero afterwards): a load-wait-store loop serialised one memory latency per
+// 16-byte chunk
+template <int NPIX>
 __device__ __forceinline__ void load_halo_chunk(char* halo, const bf16_t* __restrict__ x, int mode, int n, int H,
-                                                int W, int Cin, int cc, int y0, int x0, int TWp2, int npix) {
+                                                int W, int Cin, int cc, int y0, int x0, int TWp2) {
   const int tid = threadIdx.x;
-  const int nch = npix * 8;
-  for (int i = tid; i < nch; i += kThreads) {
+  constexpr int NCH = NPIX * 8, NL = (NCH + kThreads - 1) / kThreads;
+  uint4 hv[NL];
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int i = min(tid + j * kThreads, NCH - 1);
     const int q = i >> 3, c = i & 7;
     const int hy = q / TWp2, hx = q - hy * TWp2;
-    const int y = y0 - 1 + hy, xx = x0 - 1 + hx;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (y >= 0 && y < H && xx >= 0 && xx < W) {
-      const bf16_t* src;
-      if (mode == IN_PLAIN) {
-        src = x + ((size_t)((size_t)n * H + y) * W + xx) * Cin + cc * 64 + c * 8;
-      } else {  // IN_UNSHUF: logical [H][W][4*64] view of a physical [2H][2W][64] map
-        src = x + ((size_t)((size_t)n * 2 * H + 2 * y + (cc >> 1)) * (2 * W) + 2 * xx + (cc & 1)) * 64 + c * 8;
-      }
-      v = *reinterpret_cast<const uint4*>(src);
+    const int y = min(max(y0 - 1 + hy, 0), H - 1), xx = min(max(x0 - 1 + hx, 0), W - 1);
+    const bf16_t* src = mode == IN_PLAIN
+                            ? x + ((size_t)((size_t)n * H + y) * W + xx) * Cin + cc * 64 + c * 8
+                            // IN_UNSHUF: logical [H][W][4*64] view of a physical [2H][2W][64] map
+                            : x + ((size_t)((size_t)n * 2 * H + 2 * y + (cc >> 1)) * (2 * W) + 2 * xx + (cc & 1)) * 64 + c * 8;
+    hv[j] = *reinterpret_cast<const uint4*>(src);
+  }
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int i = tid + j * kThreads;
+    if (i < NCH) {
+      const int q = i >> 3, c = i & 7;
+      const int hy = q / TWp2, hx = q - hy * TWp2;
+      const int y = y0 - 1 + hy, xx = x0 - 1 + hx;
+      const bool ok = y >= 0 && y < H && xx >= 0 && xx < W;
+      *reinterpret_cast<uint4*>(halo + swz128(q, c)) = ok ? hv[j] : make_uint4(0, 0, 0, 0);
     }
-    *reinterpret_cast<uint4*>(halo + swz128(q, c)) = v;
   }
 }
 
@@ -211,7 +223,7 @@ __global__ void __launch_bounds__(kThreads, 2) conv3x3_kernel(ConvParams p) {
 
   for (int cc = 0; cc < nchunks; ++cc) {
     if (cc) __syncthreads();
-    load_halo_chunk(halo, p.x, p.in_mode, n, p.H, p.W, p.Cin, cc, y0, x0, TW + 2, S::HALO_PIX);
+    load_halo_chunk<S::HALO_PIX>(halo, p.x, p.in_mode, n, p.H, p.W, p.Cin, cc, y0, x0, TW + 2);
     // tap 0 filter slice
     {
       const bf16_t* ws = wsrc + ((size_t)(cc * 9 + 0) * p.Cout + cb * 64) * 64;

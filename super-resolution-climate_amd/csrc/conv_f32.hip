@@ -181,22 +181,36 @@ __global__ void __launch_bounds__(256, 1) conv3x3_f32_kernel(ConvParams p) {
 
   for (int cc = 0; cc < nchunks; ++cc) {
     if (cc) __syncthreads();
-    // halo chunk: (TH+2)(TW+2) pixels x 16 float4
-    for (int i = tid; i < S::HALO_PIX * 16; i += 256) {
-      const int q = i >> 4, c = i & 15;
-      const int hy = q / (TW + 2), hx = q - hy * (TW + 2);
-      const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (yy >= 0 && yy < p.H && xx >= 0 && xx < p.W) {
-        const float* src;
-        if (p.in_mode == IN_PLAIN) {
-          src = X + ((size_t)((size_t)n * p.H + yy) * p.W + xx) * p.Cin + cc * 64 + c * 4;
-        } else {  // IN_UNSHUF: logical [H][W][256] view of the PixelShuffle output [2H][2W][64]
-          src = X + ((size_t)((size_t)n * 2 * p.H + 2 * yy + (cc >> 1)) * (2 * p.W) + 2 * xx + (cc & 1)) * 64 + c * 4;
-        }
-        v = *reinterpret_cast<const float4*>(src);
+    // halo chunk: (TH+2)(TW+2) pixels x 16 float4, every load of the thread in
+    // flight at once (clamped addresses, padding selected to zero afterwards): a
+    // load-wait-store loop serialised one memory latency per float4
+    {
+      constexpr int NH = (S::HALO_PIX * 16 + 255) / 256;
+      float4 hv[NH];
+#pragma unroll
+      for (int j = 0; j < NH; ++j) {
+        const int i = min(tid + j * 256, S::HALO_PIX * 16 - 1);
+        const int q = i >> 4, c = i & 15;
+        const int hy = q / (TW + 2), hx = q - hy * (TW + 2);
+        const int yy = min(max(y0 - 1 + hy, 0), p.H - 1), xx = min(max(x0 - 1 + hx, 0), p.W - 1);
+        const float* src = p.in_mode == IN_PLAIN
+                               ? X + ((size_t)((size_t)n * p.H + yy) * p.W + xx) * p.Cin + cc * 64 + c * 4
+                               // IN_UNSHUF: logical [H][W][256] view of the PixelShuffle output [2H][2W][64]
+                               : X + ((size_t)((size_t)n * 2 * p.H + 2 * yy + (cc >> 1)) * (2 * p.W) + 2 * xx + (cc & 1)) * 64 +
+                                     c * 4;
+        hv[j] = *reinterpret_cast<const float4*>(src);
       }
-      *reinterpret_cast<float4*>(halo + swz256(q, c)) = v;
+#pragma unroll
+      for (int j = 0; j < NH; ++j) {
+        const int i = tid + j * 256;
+        if (i < S::HALO_PIX * 16) {
+          const int q = i >> 4, c = i & 15;
+          const int hy = q / (TW + 2), hx = q - hy * (TW + 2);
+          const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
+          const bool ok = yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
+          *reinterpret_cast<float4*>(halo + swz256(q, c)) = ok ? hv[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
     }
     // tap 0 filter slice [64 co][64 ci]
     {

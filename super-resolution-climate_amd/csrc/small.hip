@@ -205,14 +205,28 @@ __global__ void __launch_bounds__(256) tail_fwd_mfma_kernel(const bf16_t* __rest
   char* wl = tsm + HALO * 128;    // [9 taps][16 co rows] x 128 B
   const int n = blockIdx.z, y0 = blockIdx.y * 4, x0 = blockIdx.x * TW, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, fr = lane & 15, fk = lane >> 4;
-  for (int i = tid; i < HALO * 8; i += 256) {
-    const int q = i >> 3, c = i & 7;
-    const int hy = q / WP, hx = q - hy * WP;
-    const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (yy >= 0 && yy < H && xx >= 0 && xx < W)
-      v = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + c * 8);
-    *reinterpret_cast<uint4*>(halo + swz128(q, c)) = v;
+  {  // halo: every load of the thread in flight at once (clamped, padding zeroed after)
+    constexpr int NL = (HALO * 8 + 255) / 256;
+    uint4 hv[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int i = min(tid + j * 256, HALO * 8 - 1);
+      const int q = i >> 3, c = i & 7;
+      const int hy = q / WP, hx = q - hy * WP;
+      const int yy = min(max(y0 - 1 + hy, 0), H - 1), xx = min(max(x0 - 1 + hx, 0), W - 1);
+      hv[j] = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + c * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int i = tid + j * 256;
+      if (i < HALO * 8) {
+        const int q = i >> 3, c = i & 7;
+        const int hy = q / WP, hx = q - hy * WP;
+        const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
+        const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+        *reinterpret_cast<uint4*>(halo + swz128(q, c)) = ok ? hv[j] : make_uint4(0, 0, 0, 0);
+      }
+    }
   }
   // filters w[co][ci][tap] (fp32, torch layout) -> bf16 rows co < C of [tap][co][ci];
   // rows >= C stay unwritten: they only feed output rows that are never stored
@@ -268,17 +282,31 @@ __global__ void __launch_bounds__(256) tail_fwd_f32_kernel(const float* __restri
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   for (int cs = 0; cs < 64; cs += CS) {
     __syncthreads();
-    for (int i = tid; i < 6 * WP * (CS / 4); i += 256) {
-      const int q = i / (CS / 4), c4 = i % (CS / 4);
-      const int hy = q / WP, hx = q % WP;
-      const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (yy >= 0 && yy < H && xx >= 0 && xx < W)
-        v = *reinterpret_cast<const float4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + cs + c4 * 4);
-      hs[c4 * 4 + 0][hy][hx] = v.x;
-      hs[c4 * 4 + 1][hy][hx] = v.y;
-      hs[c4 * 4 + 2][hy][hx] = v.z;
-      hs[c4 * 4 + 3][hy][hx] = v.w;
+    {  // every load of the thread in flight at once (clamped, padding zeroed after)
+      constexpr int NI = 6 * WP * (CS / 4), NL = (NI + 255) / 256;
+      float4 hv[NL];
+#pragma unroll
+      for (int j = 0; j < NL; ++j) {
+        const int i = min(tid + j * 256, NI - 1);
+        const int q = i / (CS / 4), c4 = i % (CS / 4);
+        const int hy = q / WP, hx = q % WP;
+        const int yy = min(max(y0 - 1 + hy, 0), H - 1), xx = min(max(x0 - 1 + hx, 0), W - 1);
+        hv[j] = *reinterpret_cast<const float4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + cs + c4 * 4);
+      }
+#pragma unroll
+      for (int j = 0; j < NL; ++j) {
+        const int i = tid + j * 256;
+        if (i < NI) {
+          const int q = i / (CS / 4), c4 = i % (CS / 4);
+          const int hy = q / WP, hx = q % WP;
+          const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
+          const float4 v = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? hv[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+          hs[c4 * 4 + 0][hy][hx] = v.x;
+          hs[c4 * 4 + 1][hy][hx] = v.y;
+          hs[c4 * 4 + 2][hy][hx] = v.z;
+          hs[c4 * 4 + 3][hy][hx] = v.w;
+        }
+      }
     }
     __syncthreads();
 #pragma unroll 4
@@ -333,15 +361,28 @@ __global__ void __launch_bounds__(256) tail_dgrad_kernel(const float* __restrict
   float* dyl = tds;                   // [C][6][WP]
   float* wl = tds + 4 * 6 * WP;       // [C][9][64]  (tap-major, ci contiguous)
   const float sc = loss ? loss[2] : 1.f;
-  for (int i = tid; i < C * 6 * WP; i += 256) {
-    const int c = i / (6 * WP), r = (i / WP) % 6, xx = i % WP;
-    const int yy = y0 - 1 + r, xg = x0 - 1 + xx;
-    float v = 0.f;
-    if (yy >= 0 && yy < H && xg >= 0 && xg < W) {
+  {  // every load of the thread in flight at once (clamped, padding zeroed after)
+    constexpr int LD = (4 * 6 * WP + 255) / 256;
+    const int nd = C * 6 * WP;
+    float yd[LD], hd[LD];
+#pragma unroll
+    for (int j = 0; j < LD; ++j) {
+      const int i = min(tid + j * 256, nd - 1);
+      const int c = i / (6 * WP), r = (i / WP) % 6, xx = i % WP;
+      const int yy = min(max(y0 - 1 + r, 0), H - 1), xg = min(max(x0 - 1 + xx, 0), W - 1);
       const size_t o = (((size_t)n * C + c) * H + yy) * W + xg;
-      v = hr ? (yv[o] - hr[o]) * sc : yv[o] * sc;
+      yd[j] = yv[o];
+      hd[j] = hr ? hr[o] : 0.f;
     }
-    dyl[i] = v;
+#pragma unroll
+    for (int j = 0; j < LD; ++j) {
+      const int i = tid + j * 256;
+      if (i < nd) {
+        const int r = (i / WP) % 6, xx = i % WP;
+        const int yy = y0 - 1 + r, xg = x0 - 1 + xx;
+        dyl[i] = (yy >= 0 && yy < H && xg >= 0 && xg < W) ? (yd[j] - hd[j]) * sc : 0.f;
+      }
+    }
   }
   for (int i = tid; i < C * 576; i += 256) {
     const int c = i / 576, t = (i / 64) % 9, ci = i % 64;
@@ -437,22 +478,44 @@ __global__ void __launch_bounds__(256) tail_wgrad_lds_kernel(const float* __rest
   for (int x0 = 0; x0 < W; x0 += SEG) {
     const int nx = min(SEG, W - x0);
     __syncthreads();  // previous segment's readers are done
-    for (int i = tid; i < 6 * SP * (64 / VPC); i += 256) {
-      const int q = i / (64 / VPC), ch = i % (64 / VPC), r = q / SP, px = q - r * SP;
-      const int yy = y0 - 1 + r, xx = x0 - 1 + px;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (yy >= 0 && yy < H && xx >= 0 && xx < W && px <= nx + 1)
-        v = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + ch * VPC);
-      *reinterpret_cast<uint4*>(xs + q * 64 + ch * VPC) = v;
-    }
-    for (int i = tid; i < CC * kTailRows * SEG; i += 256) {
-      const int c = i / (kTailRows * SEG), r = (i / SEG) % kTailRows, px = i % SEG;
-      float v = 0.f;
-      if (px < nx) {
-        const size_t o = (((size_t)n * CC + c) * H + y0 + r) * W + x0 + px;
-        v = hr ? (yv[o] - hr[o]) * sc : yv[o] * sc;
+    {  // every load of the thread in flight at once (clamped, padding zeroed after)
+      constexpr int NX = 6 * SP * (64 / VPC), LX = (NX + 255) / 256;
+      constexpr int ND = CC * kTailRows * SEG, LD = (ND + 255) / 256;
+      uint4 xv[LX];
+      float yd[LD], hd[LD];
+#pragma unroll
+      for (int j = 0; j < LX; ++j) {
+        const int i = min(tid + j * 256, NX - 1);
+        const int q = i / (64 / VPC), ch = i % (64 / VPC), r = q / SP, px = q - r * SP;
+        const int yy = min(max(y0 - 1 + r, 0), H - 1), xx = min(max(x0 - 1 + px, 0), W - 1);
+        xv[j] = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + ch * VPC);
       }
-      dyl[c][r][px] = v;
+#pragma unroll
+      for (int j = 0; j < LD; ++j) {
+        const int i = min(tid + j * 256, ND - 1);
+        const int c = i / (kTailRows * SEG), r = (i / SEG) % kTailRows, px = min(i % SEG, nx - 1);
+        const size_t o = (((size_t)n * CC + c) * H + y0 + r) * W + x0 + px;
+        yd[j] = yv[o];
+        hd[j] = hr ? hr[o] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < LX; ++j) {
+        const int i = tid + j * 256;
+        if (i < NX) {
+          const int q = i / (64 / VPC), ch = i % (64 / VPC), r = q / SP, px = q - r * SP;
+          const int yy = y0 - 1 + r, xx = x0 - 1 + px;
+          const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W && px <= nx + 1;
+          *reinterpret_cast<uint4*>(xs + q * 64 + ch * VPC) = ok ? xv[j] : make_uint4(0, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < LD; ++j) {
+        const int i = tid + j * 256;
+        if (i < ND) {
+          const int c = i / (kTailRows * SEG), r = (i / SEG) % kTailRows, px = i % SEG;
+          dyl[c][r][px] = px < nx ? (yd[j] - hd[j]) * sc : 0.f;
+        }
+      }
     }
     __syncthreads();
     float win[3][3];

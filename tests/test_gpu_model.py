@@ -54,7 +54,23 @@ def oracle_grads(model, hr, scale):
     out = model(ro.downsample(h, scale))
     loss = ro.l2loss(out, h)
     loss.backward()
-    return float(loss), out.detach(), {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+    return float(loss), out.detach(), {conv_key(n): p.grad.detach().clone() for n, p in model.named_parameters()}
+
+
+def conv_key(n):
+    return n.replace(".conv.", ".")
+
+
+def drift_bounds(model, hr, scale, g_ref):
+    """Per-tensor gradient bounds DERIVED from the reference's own bf16 drift
+    (SURVEY.md §8(c)): the same fp64 oracle step with bf16-rounded conv operands
+    (tests/gpu_oracle.py, the engine's precision model); the engine may sit at
+    most 3x that drift (+1e-3) from the exact gradient."""
+    import copy
+    from gpu_oracle import bf16_operand_emulation
+    emul = bf16_operand_emulation(copy.deepcopy(model))
+    _, _, g_emu = oracle_grads(emul, hr, scale)
+    return {n: 3.0 * rel_l2(g_emu[n], g_ref[n]) + 1e-3 for n in g_ref}
 
 
 @pytest.mark.parametrize("arch,C,nl,nb,scale,S,B,gname", [
@@ -88,15 +104,15 @@ def test_small_model_step_vs_golden(arch, C, nl, nb, scale, S, B, gname):
     assert abs(iloss0 - float(gd["iloss0"])) / float(gd["iloss0"]) < 1e-5
     # SR output of that forward
     assert rel_l2(tr.sr[:B].cpu()[:, :, ::4, ::4], gd["out_sub"]) < 2e-2
-    # gradients, per tensor
+    # gradients, per tensor, within the bound derived from the bf16-operand drift
     grads = tr.grads.cpu()
-    worst = 0.0
+    bound = drift_bounds(model, hr, scale, g_ref)
     for name, off, n, shape in tr.eng.table:
         r = rel_l2(grads[off:off + n].view(shape), g_ref[name])
-        worst = max(worst, r)
-        assert r < 8e-2, (name, r)
+        assert r <= bound[name], (name, r, bound[name])
     gl2 = np.array([float(grads[off:off + n].norm()) for _, off, n, _ in tr.eng.table])
-    np.testing.assert_allclose(gl2, gd["grad_l2"], rtol=8e-2)
+    rtol = np.array([bound[nm] for nm, _, _, _ in tr.eng.table])
+    assert np.all(np.abs(gl2 - gd["grad_l2"]) <= rtol * np.abs(gd["grad_l2"]))
     # second step: loss after one Adam update
     res = tr.step(hr_d)
     torch.cuda.synchronize()
@@ -194,6 +210,7 @@ def test_plugin_module_reference_style_step():
     d = dev()
     from srmi.config import ConfigContext
     from srmi.model.rcan.network import get_model
+    torch.manual_seed(0)  # the module draws its default init from the global generator, as nn.Conv2d does
     with ConfigContext("sres", dict(model="rcan-10-20-64", task="SSS_SST-tiles-48"), **{"model.nlayers": 2,
                                                                                          "model.nblocks": 2}):
         net = get_model(nchannels_in=2, nchannels_out=2, device=d).to(d)
@@ -212,10 +229,11 @@ def test_plugin_module_reference_style_step():
     loss = torch.sqrt(((out - hr) ** 2).mean())
     loss.backward()
     l_ref, out_ref, g_ref = oracle_grads(oracle, hr.cpu().numpy(), 4)
+    bound = drift_bounds(oracle, hr.cpu().numpy(), 4, g_ref)
     assert abs(loss.item() - l_ref) / l_ref < 2e-3
     for name, p in net.named_parameters():
         assert p.grad is not None
-        assert rel_l2(p.grad, g_ref[name]) < 8e-2, name
+        assert rel_l2(p.grad, g_ref[name]) <= bound[name], (name, rel_l2(p.grad, g_ref[name]), bound[name])
     opt.step()
     # state_dict round trip through the tolerant loader
     sd = {k: v.clone() for k, v in net.state_dict().items()}

@@ -11,7 +11,7 @@ d = torch.device('cuda', 0); torch.cuda.set_device(d)
 print(bench.edsr_bench(d, 64, 5, 2)['value'])
 PY
 for v in new old; do
-  if [ $v = old ]; then export SRMI_LIB=$R/build/alt/libsrmi_prev.so; fi
+  if [ $v = old ]; then [ -f "$R/alt/libsrmi_prev.so" ] || continue; export SRMI_LIB=$R/alt/libsrmi_prev.so; fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/pe_$v -o e -- python3 /tmp/edsr_only.py $R > $R/gpurun_out/pe_$v.log 2>&1 || exit 1
   echo "== $v $(grep -v Warn $R/gpurun_out/pe_$v.log | tail -1)"
   python3 - $R/gpurun_out/pe_$v/e_kernel_stats.csv <<'PY'
