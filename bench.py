@@ -404,7 +404,7 @@ def main():
         _log("rooflines done")
         edsr = None
         if not args.no_edsr and world == 1:
-            edsr = edsr_bench(dev, args.edsr_batch, 6, 2)
+            edsr = edsr_bench(dev, args.edsr_batch, 10, 3)
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
             _log("edsr done")
