@@ -194,6 +194,12 @@ int srmi_wgrad3x3(const void* x, const void* dy, int N, int H, int W, int Cout, 
 int srmi_ca_forward(const void* u, const float* part, int nstrips, const float* w1, const float* b1, const float* w2,
                     const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, void* hb_out,
                     float* rec, int dtype, void* stream);
+/* the same CALayer forward on the bf16 engine's residual-stream pair: h = h_in
+ * (fp32, when non-NULL) or hi_in + lo_in (bf16 pair); out: hi = bf16(h + s*u),
+ * lo = bf16(h + s*u - hi) (in place allowed: lo_out == lo_in) */
+int srmi_ca_forward_pair(const void* u, const float* part, int nstrips, const float* w1, const float* b1,
+                         const float* w2, const float* b2, int N, int HW, int C, int R, const float* h_in,
+                         const void* hi_in, const void* lo_in, void* hi_out, void* lo_out, float* rec, void* stream);
 /* brec: N*(2C + C/R) floats (dz2 | dz1 | conv2 bias grad per image) followed by
  * N*C floats of dm (gradient of the pooled mean) -- N*(3C + C/R) in total */
 int srmi_ca_backward(const float* g, const float* part, int nstrips, const float* rec, const float* w1,

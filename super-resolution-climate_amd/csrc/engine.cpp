@@ -542,8 +542,17 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
         const RCABRef& r = P.groups[g][b - 1];
         RC(conv_fwd(e, r.c1, e->hb(g, b - 1), n, h, w, EPI_RELU_BF16, e->Tm(g, b), nullptr, nullptr, nullptr, 1.f, st));
         RC(conv_fwd(e, r.c2, e->Tm(g, b), n, h, w, EPI_POOL_BF16, e->Um(g, b), nullptr, nullptr, e->ppool, 1.f, st));
-        RC(ca_fwd_launch(e->Um(g, b), e->ppool, nstrips, prm + r.ca_w1, prm + r.ca_b1, prm + r.ca_w2, prm + r.ca_b2, n,
-                         HW, 64, R, b == 1 ? rin : e->Hf, e->Hf, e->hb(g, b), e->recp(g, b), e->f32, st));
+        if (e->f32) {
+          RC(ca_fwd_launch(e->Um(g, b), e->ppool, nstrips, prm + r.ca_w1, prm + r.ca_b1, prm + r.ca_w2, prm + r.ca_b2,
+                           n, HW, 64, R, b == 1 ? rin : e->Hf, e->Hf, e->hb(g, b), e->recp(g, b), 1, st));
+        } else {
+          // the residual stream inside the group as the pair hb (bf16, the next conv's
+          // input) + lo (bf16 remainder, in Hf's memory); the group input rin is fp32
+          bf16_t* lo = reinterpret_cast<bf16_t*>(e->Hf);
+          RC(ca_fwd_launch(e->Um(g, b), e->ppool, nstrips, prm + r.ca_w1, prm + r.ca_b1, prm + r.ca_w2, prm + r.ca_b2,
+                           n, HW, 64, R, b == 1 ? rin : nullptr, nullptr, e->hb(g, b), e->recp(g, b), 0, st,
+                           b == 1 ? nullptr : e->hb(g, b - 1), b == 1 ? nullptr : lo, lo));
+        }
       }
       RC(conv_fwd(e, P.group_tail[g], e->hb(g, nb), n, h, w, EPI_RESID, e->hb(g + 1, 0), e->Rf, rin, nullptr, 1.f,
                   st));
@@ -921,6 +930,14 @@ int srmi_ca_forward(const void* u, const float* part, int nstrips, const float* 
   if (dtype != SRMI_DTYPE_BF16 && dtype != SRMI_DTYPE_F32) return SRMI_ERR_ARG;
   return ca_fwd_launch(u, part, nstrips, w1, b1, w2, b2, N, HW, C, R, h_in, h_out, hb_out, rec,
                        dtype == SRMI_DTYPE_F32, S_(stream));
+}
+
+int srmi_ca_forward_pair(const void* u, const float* part, int nstrips, const float* w1, const float* b1,
+                         const float* w2, const float* b2, int N, int HW, int C, int R, const float* h_in,
+                         const void* hi_in, const void* lo_in, void* hi_out, void* lo_out, float* rec, void* stream) {
+  if (!hi_out || !lo_out || (!h_in && (!hi_in || !lo_in))) return SRMI_ERR_ARG;
+  return ca_fwd_launch(u, part, nstrips, w1, b1, w2, b2, N, HW, C, R, h_in, nullptr, hi_out, rec, 0, S_(stream),
+                       h_in ? nullptr : hi_in, h_in ? nullptr : lo_in, lo_out);
 }
 
 int srmi_ca_backward(const float* g, const float* part, int nstrips, const float* rec, const float* w1,

@@ -896,14 +896,25 @@ struct Unit4<float> {
 #endif
 constexpr int kCaVec = SRMI_CA_VEC;
 
-// h_out = u * s + h_in  (fp32 + operand-type copy); grid (chunks, N)
-template <typename T>
+// h_out = u * s + h_in; grid (chunks, N).  Residual-stream forms (MODE):
+//   CA_F32   fp32 h in, fp32 h + operand-type copy out (the exact-fp32 engine mode)
+//   CA_F32LO fp32 h in (the group input), h out as a bf16 pair hi + lo
+//   CA_LO    bf16 pair in and out
+// The pair: hi = bf16(h) -- the next conv's operand, stored anyway -- and
+// lo = bf16(h - hi), so hi + lo keeps h to ~2^-17 relative (16 significant bits
+// against the 8 of the bf16 operands the convs see) while the pass moves 10 B per
+// element instead of 12 (u 2 + h 4 in, h 4 + hb 2 out).
+enum CaMode { CA_F32 = 0, CA_F32LO = 1, CA_LO = 2 };
+
+template <typename T, int MODE>
 __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, const float* __restrict__ part,
                                                      int nstrips, int HW, const float* __restrict__ w1,
                                                      const float* __restrict__ b1, const float* __restrict__ w2,
                                                      const float* __restrict__ b2, int C, int CR,
-                                                     const float* __restrict__ h_in, float* __restrict__ h_out,
-                                                     T* __restrict__ hb_out, float* __restrict__ rec) {
+                                                     const float* __restrict__ h_in, const bf16_t* __restrict__ hi_in,
+                                                     const bf16_t* __restrict__ lo_in, float* __restrict__ h_out,
+                                                     T* __restrict__ hb_out, bf16_t* __restrict__ lo_out,
+                                                     float* __restrict__ rec) {
   __shared__ float red[4][64], m[64], z1[32], s[64];
   const int n = blockIdx.y, tid = threadIdx.x;
   // 1. the MLP operands (L2 hits), issued first so that waiting for them does not
@@ -938,7 +949,13 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
   for (int k = 0; k < NU; ++k) {  // clamped, unconditional (tail lanes store nothing)
     const size_t e = base + min(q0 + (size_t)k * blockDim.x, nq - 1) * 4;
     uu[k] = Unit4<T>::ld(u + e);
-    hh[k] = *reinterpret_cast<const float4*>(h_in + e);
+    if constexpr (MODE == CA_LO) {
+      const uint2 hi = *reinterpret_cast<const uint2*>(hi_in + e), lo = *reinterpret_cast<const uint2*>(lo_in + e);
+      hh[k] = make_float4(bf2f(hi.x & 0xFFFFu) + bf2f(lo.x & 0xFFFFu), bf2f(hi.x >> 16) + bf2f(lo.x >> 16),
+                          bf2f(hi.y & 0xFFFFu) + bf2f(lo.y & 0xFFFFu), bf2f(hi.y >> 16) + bf2f(lo.y >> 16));
+    } else {
+      hh[k] = *reinterpret_cast<const float4*>(h_in + e);
+    }
   }
   __builtin_amdgcn_sched_barrier(0);
   // 3. the MLP (LDS-only barriers: the stream loads stay in flight)
@@ -976,8 +993,9 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
   }
   // 4. elementwise; lane-contiguous runs written through (common.hpp): the
   //    boundary after this launch then has no dirty residual stream to flush
-  const auto rh = wt_rsrc(h_out, (uint32_t)((size_t)gridDim.y * HW * C * 4));
+  [[maybe_unused]] const auto rh = wt_rsrc(h_out, (uint32_t)((size_t)gridDim.y * HW * C * 4));
   const auto rhb = wt_rsrc(hb_out, (uint32_t)((size_t)gridDim.y * HW * C * sizeof(T)));
+  [[maybe_unused]] const auto rlo = wt_rsrc(lo_out, (uint32_t)((size_t)gridDim.y * HW * C * 2));
 #pragma unroll
   for (int k = 0; k < NU; ++k) {
     const size_t q = q0 + (size_t)k * blockDim.x;
@@ -989,8 +1007,16 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
     o[1] = Unit4<T>::get(uu[k], 1) * s[c0 + 1] + hh[k].y;
     o[2] = Unit4<T>::get(uu[k], 2) * s[c0 + 2] + hh[k].z;
     o[3] = Unit4<T>::get(uu[k], 3) * s[c0 + 3] + hh[k].w;
-    st_wt16(rh, h_out, (uint32_t)(e * 4), make_float4(o[0], o[1], o[2], o[3]));
-    Unit4<T>::st(rhb, hb_out, e, o);
+    if constexpr (MODE == CA_F32) {
+      st_wt16(rh, h_out, (uint32_t)(e * 4), make_float4(o[0], o[1], o[2], o[3]));
+      Unit4<T>::st(rhb, hb_out, e, o);
+    } else {
+      const uint2 hi = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+      const uint2 lo = make_uint2(pack2(o[0] - bf2f(hi.x & 0xFFFFu), o[1] - bf2f(hi.x >> 16)),
+                                  pack2(o[2] - bf2f(hi.y & 0xFFFFu), o[3] - bf2f(hi.y >> 16)));
+      st_wt8(rhb, hb_out, (uint32_t)(e * 2), hi);
+      st_wt8(rlo, lo_out, (uint32_t)(e * 2), lo);
+    }
   }
 }
 
@@ -1002,16 +1028,31 @@ static int ca_grid_x(int HW, int C) {
 
 int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1, const float* b1, const float* w2,
                   const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, void* hb_out,
-                  float* rec, int f32, hipStream_t st) {
+                  float* rec, int f32, hipStream_t st, const void* hi_in, const void* lo_in, void* lo_out) {
   if (C != 64 || C % R || (C / R) > 32 || (C / R) % 4 || (HW * C) % 8) return SRMI_ERR_SHAPE;
-  if (f32)
-    hipLaunchKernelGGL(ca_fwd_kernel<float>, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st,
-                       static_cast<const float*>(u), part, nstrips, HW, w1, b1, w2, b2, C, C / R, h_in, h_out,
-                       static_cast<float*>(hb_out), rec);
-  else
-    hipLaunchKernelGGL(ca_fwd_kernel<bf16_t>, dim3(ca_grid_x(HW, C), N), dim3(256), 0, st,
-                       static_cast<const bf16_t*>(u), part, nstrips, HW, w1, b1, w2, b2, C, C / R, h_in, h_out,
-                       static_cast<bf16_t*>(hb_out), rec);
+  const dim3 grid(ca_grid_x(HW, C), N);
+  const bf16_t *hi = static_cast<const bf16_t*>(hi_in), *lo = static_cast<const bf16_t*>(lo_in);
+  bf16_t* lout = static_cast<bf16_t*>(lo_out);
+  if (f32) {
+    if (!h_in || !h_out || lo_out || hi_in) return SRMI_ERR_ARG;
+    hipLaunchKernelGGL((ca_fwd_kernel<float, CA_F32>), grid, dim3(256), 0, st, static_cast<const float*>(u), part,
+                       nstrips, HW, w1, b1, w2, b2, C, C / R, h_in, hi, lo, h_out, static_cast<float*>(hb_out), lout,
+                       rec);
+  } else if (!lo_out) {
+    if (!h_in || !h_out) return SRMI_ERR_ARG;
+    hipLaunchKernelGGL((ca_fwd_kernel<bf16_t, CA_F32>), grid, dim3(256), 0, st, static_cast<const bf16_t*>(u), part,
+                       nstrips, HW, w1, b1, w2, b2, C, C / R, h_in, hi, lo, h_out, static_cast<bf16_t*>(hb_out), lout,
+                       rec);
+  } else if (h_in) {
+    hipLaunchKernelGGL((ca_fwd_kernel<bf16_t, CA_F32LO>), grid, dim3(256), 0, st, static_cast<const bf16_t*>(u),
+                       part, nstrips, HW, w1, b1, w2, b2, C, C / R, h_in, hi, lo, h_out,
+                       static_cast<bf16_t*>(hb_out), lout, rec);
+  } else {
+    if (!hi || !lo) return SRMI_ERR_ARG;
+    hipLaunchKernelGGL((ca_fwd_kernel<bf16_t, CA_LO>), grid, dim3(256), 0, st, static_cast<const bf16_t*>(u), part,
+                       nstrips, HW, w1, b1, w2, b2, C, C / R, h_in, hi, lo, h_out, static_cast<bf16_t*>(hb_out), lout,
+                       rec);
+  }
   SRMI_CHECK_LAUNCH();
   return 0;
 }

@@ -121,9 +121,13 @@ int charb_partial_launch(const float* y, const float* t, size_t n, float eps, do
                          float* partial, int nblk, hipStream_t st);
 
 // channel attention
+// residual stream: fp32 h_in / h_out, or (bf16 engine) as a bf16 hi + lo pair: lo_out
+// non-null -> hi goes to hb_out, lo to lo_out; input from h_in (fp32) or, h_in null,
+// from the pair hi_in + lo_in
 int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1, const float* b1,
                   const float* w2, const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out,
-                  void* hb_out, float* rec, int f32, hipStream_t st);
+                  void* hb_out, float* rec, int f32, hipStream_t st, const void* hi_in = nullptr,
+                  const void* lo_in = nullptr, void* lo_out = nullptr);
 // red0/red1 (both or neither): two slab reductions carried in the same launch
 int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
                      const float* w2, int N, int HW, int C, int R, void* du, float* brec, int f32, hipStream_t st,

@@ -69,6 +69,8 @@ _SIGS = {
                        P, P, C.c_int, P], C.c_int),
     "srmi_ca_forward": ([P, P, C.c_int, P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, C.c_int, P],
                         C.c_int),
+    "srmi_ca_forward_pair": ([P, P, C.c_int, P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P],
+                             C.c_int),
     "srmi_ca_backward": ([P, P, C.c_int, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, C.c_int, P], C.c_int),
     "srmi_head_forward": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, C.c_int, P], C.c_int),
     "srmi_tail_forward": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int, P], C.c_int),

@@ -260,6 +260,44 @@ def test_channel_attention_fwd_bwd(dt):
     np.testing.assert_allclose(brec[:N * 160].view(N, 160)[:, 96:].double().cpu().numpy(), U.grad.sum((1, 2)).numpy(), rtol=1e-4, atol=1e-3)
 
 
+def test_channel_attention_forward_residual_pair():
+    """The bf16 engine's residual stream as a (hi, lo) bf16 pair: the group's first
+    CALayer add takes the fp32 group input, the next ones the pair, in place.  hi is
+    h to bf16 precision and hi + lo keeps h to 2^-16 (rel-L2) over a chain of adds."""
+    d = dev()
+    N, H, W, Cc, R = 2, 48, 48, 64, 2
+    g = torch.Generator(device="cpu").manual_seed(8)
+    w1 = (torch.randn(Cc // R, Cc, generator=g) * 0.1).to(d)
+    b1 = (torch.randn(Cc // R, generator=g) * 0.1).to(d)
+    w2 = (torch.randn(Cc, Cc // R, generator=g) * 0.1).to(d)
+    b2 = (torch.randn(Cc, generator=g) * 0.1).to(d)
+    ns = call("srmi_conv3x3_nstrips", H, W)
+    h_in = torch.randn(N, H, W, Cc, generator=g).to(d)
+    h_ref = h_in.double().cpu()
+    hi = [torch.empty(N, H, W, Cc, dtype=torch.bfloat16, device=d) for _ in range(2)]
+    lo = torch.empty(N, H, W, Cc, dtype=torch.bfloat16, device=d)
+    rec = torch.empty(N, 160, device=d)
+    for step in range(6):
+        u = bf(torch.randn(N, H, W, Cc, generator=g)).to(d)
+        part = torch.zeros(N, ns, Cc, device=d)
+        part[:, 0, :] = u.float().sum((1, 2))
+        first = step == 0
+        call("srmi_ca_forward_pair", ptr(u), ptr(part), ns, ptr(w1), ptr(b1), ptr(w2), ptr(b2), N, H * W, Cc, R,
+             ptr(h_in if first else None), ptr(None if first else hi[(step + 1) % 2]), ptr(None if first else lo),
+             ptr(hi[step % 2]), ptr(lo), ptr(rec), S())
+        torch.cuda.synchronize()
+        m = u.double().cpu().mean((1, 2))
+        s = torch.sigmoid(torch.relu(m @ w1.double().cpu().T + b1.double().cpu()) @ w2.double().cpu().T + b2.double().cpu())
+        h_ref = h_ref + u.double().cpu() * s[:, None, None, :]
+        got = hi[step % 2].double().cpu() + lo.double().cpu()
+        # the pair's rounding error is relative to the stream's magnitude (lo carries
+        # bf16 precision of a remainder below hi's half ulp), not to each element
+        assert rel_l2(got, h_ref) < 2 ** -16
+        assert float((got - h_ref).abs().max()) <= 2 ** -14 * float(h_ref.abs().max())
+        # hi is within half a bf16 ulp (plus lo's rounding) of h: the conv operand
+        assert rel_l2(hi[step % 2], h_ref) < 2 ** -8
+
+
 def test_downsample_upsample_match_reference():
     import os
     d = dev()
