@@ -343,14 +343,14 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   constexpr int NGW = (NGRP + 3) / 4;            // pieces per wave (upper bound)
   // Per-lane parts of the DMA source, computed once: piece i = wv_s + 4m covers ring
   // pixels q = 8i + lane/8, i.e. row rr and halo column hx of the group; the chunk
-  // swizzle of ring slot 1 differs from slots 0 and 2 by bit 2 (200 px per slot).
+  // swizzle (q & 7) is the same in all three ring slots (4 (TW + 2) px apart).
   int loff[NGW], lrr[NGW];
   uint32_t okx = 0;
 #pragma unroll
   for (int m = 0; m < NGW; ++m) {
     const int i = wv_s + 4 * m;
     const int q = 8 * i + (lane >> 3);
-    const int c = (lane & 7) ^ ((q >> 1) & 7);
+    const int c = (lane & 7) ^ (q & 7);
     const int rr = q / (TW + 2), hx = q - rr * (TW + 2);
     const int xx = x0 - 1 + hx;
     okx |= (i < NGRP && xx >= 0 && xx < p.W) ? (1u << m) : 0u;
@@ -360,7 +360,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   auto group_dma_one = [&](int gidx, int m) __attribute__((always_inline)) {
     const int slot = gidx % 3, y0 = 4 * gidx - 3;
     const char* base = reinterpret_cast<const char*>(xn + ((ptrdiff_t)y0 * p.W + x0) * 64);
-    const int o = loff[m] ^ (slot == 1 ? 64 : 0);  // chunk c ^ 4 (8 bf16 = 16 B per chunk)
+    const int o = loff[m];  // ring slots are 4 (TW + 2) px apart, a multiple of 8: same swizzle
     const bool ok = ((okx >> m) & 1u) && y0 + lrr[m] >= 0 && y0 + lrr[m] < p.H;
     const void* src = ok ? (const void*)(base + o) : zpage;
     glds16(src, rbase + (uint32_t)(slot * 4 * (TW + 2)) * 128u + (uint32_t)(wv_s + 4 * m) * 1024u);
@@ -376,7 +376,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   {
     const uint32_t wbase = lds_u32(wl);
     for (int i = wv_s; i < 72; i += 4) {
-      const int tap = i >> 3, row = 8 * (i & 7) + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+      const int tap = i >> 3, row = 8 * (i & 7) + (lane >> 3), c = (lane & 7) ^ (row & 7);
       glds16(p.w + ((size_t)(tap * p.Cout + cb * 64 + row)) * 64 + c * 8, wbase + (uint32_t)i * 1024u);
     }
     group_dma(k0);
