@@ -308,8 +308,12 @@ constexpr int kFragBuf = SRMI_CONV_FRAGBUF;
 // The kernel body as a device function of a virtual block index `bid` and the
 // workgroup's LDS (>= Conv2Smem<TW>::TOTAL bytes), so that a horizontally fused
 // launch (wgrad3x3.hip, rcab_bwd_kernel) can run it beside other work.
+// tail > 0 splits each run: the workgroup of run `bid` does its strips except the
+// last `tail` ones (tail_part = false), or only those (tail_part = true; the fused
+// backward hands them to the filter-gradient workgroup of the same rows)
 template <int TW, int EPI>
-__device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, int bid, char* smem) {
+__device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, int bid, char* smem, int tail = 0,
+                                            bool tail_part = false) {
   using S = Conv2Smem<TW>;
   constexpr int NPT = TW / 16;
   char* wl = smem;
@@ -327,7 +331,12 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   r /= nsx;
   const int n = r % p.N;
   const int cb = r / p.N;
-  const int k0 = ry * run_len, k1 = min(nsy, k0 + run_len);
+  int k0 = ry * run_len, k1 = min(nsy, k0 + run_len);
+  if (tail > 0) {
+    if (tail_part) k0 = max(k0, k1 - tail);
+    else k1 = max(k0, k1 - tail);
+  }
+  if (k0 >= k1) return;
   const int x0 = sx * TW;
   STAMP(0);
 
@@ -371,8 +380,19 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
       if (wv_s + 4 * m < NGRP) group_dma_one(gidx, m);
   };
 
+  // bias first (read only by the epilogue): its latency hides under the prologue wait
+  // instead of following it (~650 cycles per workgroup)
+  float4 bias[4];
+  {
+    const float* bp = p.bias ? p.bias : reinterpret_cast<const float*>(kZeros);  // pointer select, no branch
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) bias[ct] = *reinterpret_cast<const float4*>(bp + cb * 64 + ct * 16 + fk * 4);
+  }
   // prologue: filters (all 9 taps, 72 KiB) and input groups k0, k0+1, all by LDS-DMA
-  // (swizzle on the source side), everything in flight before the one wait.
+  // (swizzle on the source side), everything in flight before the one wait.  (Waiting
+  // only for the groups and the first taps, the rest landing under the first strip's
+  // K-steps, measured slower: the prologue is latency-, not byte-bound, -300 cycles,
+  // while the first strip's MFMA phase grew by 500.)
   {
     const uint32_t wbase = lds_u32(wl);
     for (int i = wv_s; i < 72; i += 4) {
@@ -380,16 +400,10 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
       glds16(p.w + ((size_t)(tap * p.Cout + cb * 64 + row)) * 64 + c * 8, wbase + (uint32_t)i * 1024u);
     }
     group_dma(k0);
-    group_dma(k0 + 1);  // strip k0 reads groups k0 and k0+1 (issuing these first measured the same)
+    group_dma(k0 + 1);
     wait_vm<0>();
   }
   STAMP(1);
-  float4 bias[4];
-  {
-    const float* bp = p.bias ? p.bias : reinterpret_cast<const float*>(kZeros);  // pointer select, no branch
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) bias[ct] = *reinterpret_cast<const float4*>(bp + cb * 64 + ct * 16 + fk * 4);
-  }
   // lane-constant A-fragment byte offsets (tap adds 8192)
   uint32_t aoff[2][4];
 #pragma unroll
