@@ -48,57 +48,33 @@ struct Conv2Smem {
 };
 
 // Epilogue operands that live in global memory are prefetched into registers
-// before the MFMA phase (one wave per SIMD: nothing else would hide their latency).
-template <int NPT, int EPI>
+// before the MFMA phase.  NCT = output-channel tiles (16 wide) per wave: 4 when a
+// wave owns the whole 64-channel block of its row, 2 in the 8-wave form (a wave
+// per row and channel half), whose tiles start at ct0.
+template <int NPT, int EPI, int NCT = 4>
 struct EpiPre {
-  float4 r1[NPT][4];
-  uint2 aux[NPT][4];
+  float4 r1[NPT][NCT];
+  uint2 aux[NPT][NCT];
 };
 
-template <int NPT, int EPI>
-__device__ __forceinline__ void epi_prefetch(const ConvParams& p, EpiPre<NPT, EPI>& e, int n, int cb, int y, int x0,
-                                             int fr, int fk) {
+// one (pt, c) element (idx = pt * NCT + c), issued one or two per K-step
+template <int NPT, int EPI, int NCT>
+__device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT, EPI, NCT>& e, int n, int cb, int y,
+                                                 int x0, int fr, int fk, int ct0, int idx) {
   if constexpr (EPI == EPI_RESID || EPI == EPI_DG_ACC || EPI == EPI_DG_RELUMASK || EPI == EPI_DG_ACC_CA) {
-    const size_t HW = (size_t)p.H * p.W;
-#pragma unroll
-    for (int pt = 0; pt < NPT; ++pt) {
-      const size_t pix = (size_t)n * HW + (size_t)y * p.W + x0 + pt * 16 + fr;
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        const size_t o = pix * p.Cout + cb * 64 + ct * 16 + fk * 4;
-        if constexpr (EPI == EPI_RESID) e.r1[pt][ct] = *reinterpret_cast<const float4*>(p.r1 + o);
-        if constexpr (EPI == EPI_DG_ACC) {
-          e.r1[pt][ct] = p.r1 ? *reinterpret_cast<const float4*>(p.r1 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
-          e.aux[pt][ct] = p.part ? *reinterpret_cast<const uint2*>(p.aux + o) : make_uint2(0, 0);
-        }
-        if constexpr (EPI == EPI_DG_RELUMASK) e.aux[pt][ct] = *reinterpret_cast<const uint2*>(p.aux + o);
-        if constexpr (EPI == EPI_DG_ACC_CA) {
-          e.r1[pt][ct] = *reinterpret_cast<const float4*>(p.r1 + o);
-          e.aux[pt][ct] = *reinterpret_cast<const uint2*>(p.aux + o);
-        }
-      }
-    }
-  }
-}
-
-// one (pt, ct) element of epi_prefetch (e = pt * 4 + ct), for interleaving
-template <int NPT, int EPI>
-__device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT, EPI>& e, int n, int cb, int y,
-                                                 int x0, int fr, int fk, int idx) {
-  if constexpr (EPI == EPI_RESID || EPI == EPI_DG_ACC || EPI == EPI_DG_RELUMASK || EPI == EPI_DG_ACC_CA) {
-    const int pt = idx >> 2, ct = idx & 3;
+    const int pt = idx / NCT, c = idx % NCT;
     const size_t HW = (size_t)p.H * p.W;
     const size_t pix = (size_t)n * HW + (size_t)y * p.W + x0 + pt * 16 + fr;
-    const size_t o = pix * p.Cout + cb * 64 + ct * 16 + fk * 4;
-    if constexpr (EPI == EPI_RESID) e.r1[pt][ct] = *reinterpret_cast<const float4*>(p.r1 + o);
+    const size_t o = pix * p.Cout + cb * 64 + (ct0 + c) * 16 + fk * 4;
+    if constexpr (EPI == EPI_RESID) e.r1[pt][c] = *reinterpret_cast<const float4*>(p.r1 + o);
     if constexpr (EPI == EPI_DG_ACC) {
-      e.r1[pt][ct] = p.r1 ? *reinterpret_cast<const float4*>(p.r1 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
-      e.aux[pt][ct] = p.part ? *reinterpret_cast<const uint2*>(p.aux + o) : make_uint2(0, 0);
+      e.r1[pt][c] = p.r1 ? *reinterpret_cast<const float4*>(p.r1 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+      e.aux[pt][c] = p.part ? *reinterpret_cast<const uint2*>(p.aux + o) : make_uint2(0, 0);
     }
-    if constexpr (EPI == EPI_DG_RELUMASK) e.aux[pt][ct] = *reinterpret_cast<const uint2*>(p.aux + o);
+    if constexpr (EPI == EPI_DG_RELUMASK) e.aux[pt][c] = *reinterpret_cast<const uint2*>(p.aux + o);
     if constexpr (EPI == EPI_DG_ACC_CA) {
-      e.r1[pt][ct] = *reinterpret_cast<const float4*>(p.r1 + o);
-      e.aux[pt][ct] = *reinterpret_cast<const uint2*>(p.aux + o);
+      e.r1[pt][c] = *reinterpret_cast<const float4*>(p.r1 + o);
+      e.aux[pt][c] = *reinterpret_cast<const uint2*>(p.aux + o);
     }
   }
 }
@@ -112,59 +88,74 @@ __device__ __forceinline__ float relu_mask(uint32_t bits16, float v) {
 // lane's read of another lane's staged data above that lane's write.
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
-// Fused epilogue of the v2 kernel (same semantics as conv_epilogue).
-template <int NPT, int EPI>
-__device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)[NPT][4], const EpiPre<NPT, EPI>& e,
-                                               const float4 (&bias)[4], int n, int cb, int y, int x0, int strip,
-                                               int nstrips, float* red, int fr, int fk, int wave, int tid,
-                                               char* stage) {
+// Fused epilogue of the v2 kernel (same semantics as conv_epilogue).  A wave holds
+// row `row` of the strip, channel tiles ct0 .. ct0+NCT-1.  NCT < 4: two waves (the
+// channel halves) share the row's LDS staging, so their writes and the full-line
+// stores that read them are separated by workgroup barriers and each wave stores
+// every other 1 KiB run.
+template <int NPT, int EPI, int NCT = 4>
+__device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)[NPT][NCT],
+                                               const EpiPre<NPT, EPI, NCT>& e, const float4 (&bias)[NCT], int n,
+                                               int cb, int y, int x0, int strip, int nstrips, float* red, int fr,
+                                               int fk, int row, int ct0, int tid, char* stage) {
+  constexpr bool kShared = NCT < 4;
+  const int half_id = ct0 >> 1;  // shared form: which of the two waves of the row
+  auto stage_sync = [&]() __attribute__((always_inline)) {
+    if constexpr (kShared) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      lds_order();
+    }
+  };
   const size_t HW = (size_t)p.H * p.W;
   [[maybe_unused]] const auto rfa = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
   constexpr bool kPart1 = (EPI == EPI_POOL_BF16);
   constexpr bool kPart2 = (EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_CA);
-  float ps0[4][4], ps1[4][4];
+  float ps0[NCT][4], ps1[NCT][4];
   // fp32 output staged through LDS (DG_ACC, whose epilogue also reads r2/r3 from
   // global memory, measured faster with direct stores)
   constexpr bool kF = (EPI == EPI_RESID || EPI == EPI_DG_ACC_CA);
-  float4 fv[NPT][4];  // fp32 outputs, written back through LDS after the loop
-  uint2 bv[NPT][4];   // bf16 outputs, likewise
+  float4 fv[NPT][NCT];  // fp32 outputs, written back through LDS after the loop
+  uint2 bv[NPT][NCT];   // bf16 outputs, likewise
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct)
+  for (int c = 0; c < NCT; ++c)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) ps0[ct][r] = ps1[ct][r] = 0.f;
+    for (int r = 0; r < 4; ++r) ps0[c][r] = ps1[c][r] = 0.f;
 #pragma unroll
   for (int pt = 0; pt < NPT; ++pt) {
     const int xx = x0 + pt * 16 + fr;
     const size_t pix = (size_t)n * HW + (size_t)y * p.W + xx;
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      const int col = ct * 16 + fk * 4;
+    for (int c = 0; c < NCT; ++c) {
+      const int col = (ct0 + c) * 16 + fk * 4;
       const int co = cb * 64 + col;
       const size_t o = pix * p.Cout + co;
-      f32x4 v = acc[pt][ct];
+      f32x4 v = acc[pt][c];
       if constexpr (EPI == EPI_RELU_BF16 || EPI == EPI_POOL_BF16 || EPI == EPI_RESID || EPI == EPI_PS_BF16 ||
                     EPI == EPI_PLAIN_BF16) {
-        v[0] += bias[ct].x; v[1] += bias[ct].y; v[2] += bias[ct].z; v[3] += bias[ct].w;
+        v[0] += bias[c].x; v[1] += bias[c].y; v[2] += bias[c].z; v[3] += bias[c].w;
       }
       if constexpr (EPI == EPI_RELU_BF16) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
       }
       if constexpr (EPI == EPI_RESID) {
-        const float4 rr = e.r1[pt][ct];
+        const float4 rr = e.r1[pt][c];
         v[0] = p.alpha * v[0] + rr.x; v[1] = p.alpha * v[1] + rr.y;
         v[2] = p.alpha * v[2] + rr.z; v[3] = p.alpha * v[3] + rr.w;
-        fv[pt][ct] = make_float4(v[0], v[1], v[2], v[3]);
+        fv[pt][c] = make_float4(v[0], v[1], v[2], v[3]);
       }
       if constexpr (EPI == EPI_DG_RELUMASK) {
-        const uint2 tt = e.aux[pt][ct];
+        const uint2 tt = e.aux[pt][c];
         v[0] = p.alpha * relu_mask(tt.x & 0xFFFFu, v[0]);
         v[1] = p.alpha * relu_mask(tt.x >> 16, v[1]);
         v[2] = p.alpha * relu_mask(tt.y & 0xFFFFu, v[2]);
         v[3] = p.alpha * relu_mask(tt.y >> 16, v[3]);
       }
       if constexpr (EPI == EPI_DG_ACC) {
-        const float4 rr = e.r1[pt][ct];
+        const float4 rr = e.r1[pt][c];
         v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
         if (p.r2) {
           const float4 q = *reinterpret_cast<const float4*>(p.r2 + o);
@@ -176,38 +167,39 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
         }
         st_wt16(rfa, p.yf, (uint32_t)(o * 4), make_float4(v[0], v[1], v[2], v[3]));
         if (p.part) {
-          const uint2 uu = e.aux[pt][ct];
-          ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
-          ps1[ct][0] += v[0] * bf2f(uu.x & 0xFFFFu);
-          ps1[ct][1] += v[1] * bf2f(uu.x >> 16);
-          ps1[ct][2] += v[2] * bf2f(uu.y & 0xFFFFu);
-          ps1[ct][3] += v[3] * bf2f(uu.y >> 16);
+          const uint2 uu = e.aux[pt][c];
+          ps0[c][0] += v[0]; ps0[c][1] += v[1]; ps0[c][2] += v[2]; ps0[c][3] += v[3];
+          ps1[c][0] += v[0] * bf2f(uu.x & 0xFFFFu);
+          ps1[c][1] += v[1] * bf2f(uu.x >> 16);
+          ps1[c][2] += v[2] * bf2f(uu.y & 0xFFFFu);
+          ps1[c][3] += v[3] * bf2f(uu.y >> 16);
         }
       }
       if constexpr (EPI == EPI_DG_ACC_CA) {
-        const float4 rr = e.r1[pt][ct];
+        const float4 rr = e.r1[pt][c];
         v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
-        fv[pt][ct] = make_float4(v[0], v[1], v[2], v[3]);
-        const uint2 uu = e.aux[pt][ct];
-        ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
-        ps1[ct][0] += v[0] * bf2f(uu.x & 0xFFFFu);
-        ps1[ct][1] += v[1] * bf2f(uu.x >> 16);
-        ps1[ct][2] += v[2] * bf2f(uu.y & 0xFFFFu);
-        ps1[ct][3] += v[3] * bf2f(uu.y >> 16);
+        fv[pt][c] = make_float4(v[0], v[1], v[2], v[3]);
+        const uint2 uu = e.aux[pt][c];
+        ps0[c][0] += v[0]; ps0[c][1] += v[1]; ps0[c][2] += v[2]; ps0[c][3] += v[3];
+        ps1[c][0] += v[0] * bf2f(uu.x & 0xFFFFu);
+        ps1[c][1] += v[1] * bf2f(uu.x >> 16);
+        ps1[c][2] += v[2] * bf2f(uu.y & 0xFFFFu);
+        ps1[c][3] += v[3] * bf2f(uu.y >> 16);
         continue;  // no bf16 copy
       }
       if constexpr (kPart1) {
-        ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
+        ps0[c][0] += v[0]; ps0[c][1] += v[1]; ps0[c][2] += v[2]; ps0[c][3] += v[3];
       }
-      bv[pt][ct] = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      bv[pt][c] = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
     }
   }
   const int lane = tid & 63;
-  // fp32 output: staged in LDS in two halves of the wave's row (256 B per pixel,
+  // fp32 output: staged in LDS in two halves of the row (256 B per pixel,
   // chunk-swizzled) and written back as 1 KiB contiguous runs (full lines)
   if constexpr (kF) {
     if (p.yf) {
       constexpr int HALF = NPT * 8;  // pixels per half
+      constexpr int RUNS = HALF / 4;  // 1 KiB runs per half
       const auto rf = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
       const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
 #pragma unroll
@@ -215,37 +207,38 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
 #pragma unroll
         for (int pt = 0; pt < NPT; ++pt)
 #pragma unroll
-          for (int ct = 0; ct < 4; ++ct) {
+          for (int c = 0; c < NCT; ++c) {
             const int px = pt * 16 + fr;
             if ((px >= HALF) == (h == 1)) {
-              const int lpx = px - h * HALF, c16 = ct * 4 + fk;
-              *reinterpret_cast<float4*>(stage + lpx * 256 + ((c16 ^ (lpx & 15)) << 4)) = fv[pt][ct];
+              const int lpx = px - h * HALF, c16 = (ct0 + c) * 4 + fk;
+              *reinterpret_cast<float4*>(stage + lpx * 256 + ((c16 ^ (lpx & 15)) << 4)) = fv[pt][c];
             }
           }
-        lds_order();
+        stage_sync();
 #pragma unroll
-        for (int i = 0; i < HALF / 4; ++i) {
+        for (int j = 0; j < (kShared ? RUNS / 2 : RUNS); ++j) {
+          const int i = kShared ? 2 * j + half_id : j;
           const int lin = i * 1024 + lane * 16, lpx = lin >> 8, c = (lin >> 4) & 15;
           const float4 val = *reinterpret_cast<const float4*>(stage + lpx * 256 + ((c ^ (lpx & 15)) << 4));
           st_wt16(rf, p.yf, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 4), val);
         }
-        lds_order();
+        stage_sync();
       }
     }
   }
-  // bf16 output staged in LDS (this wave's row, 128 B per pixel, chunk-swizzled)
+  // bf16 output staged in LDS (the row, 128 B per pixel, chunk-swizzled)
   if constexpr (EPI != EPI_DG_ACC_CA) {
     if (p.yb) {
 #pragma unroll
       for (int pt = 0; pt < NPT; ++pt)
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-          const int px = pt * 16 + fr, c16 = ct * 2 + (fk >> 1);
-          *reinterpret_cast<uint2*>(stage + px * 128 + ((c16 ^ (px & 7)) << 4) + (fk & 1) * 8) = bv[pt][ct];
+        for (int c = 0; c < NCT; ++c) {
+          const int px = pt * 16 + fr, c16 = (ct0 + c) * 2 + (fk >> 1);
+          *reinterpret_cast<uint2*>(stage + px * 128 + ((c16 ^ (px & 7)) << 4) + (fk & 1) * 8) = bv[pt][c];
         }
     }
   }
-  lds_order();
+  stage_sync();
   // ... and written back as full 128-byte lines: one 1 KiB contiguous run per
   // instruction (the per-lane 8-byte stores of the MFMA layout touched 32-byte
   // pieces of 16 lines each and stalled the store path for ~2 K cycles per strip).
@@ -253,7 +246,8 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
   if (EPI != EPI_DG_ACC_CA && p.yb) {
     const auto rb = wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
 #pragma unroll
-    for (int i = 0; i < NPT * 2; ++i) {
+    for (int j = 0; j < (kShared ? NPT : NPT * 2); ++j) {
+      const int i = kShared ? 2 * j + half_id : j;
       const int lin = i * 1024 + lane * 16, px = lin >> 7, c = (lin >> 4) & 7;
       const uint4 val = *reinterpret_cast<const uint4*>(stage + px * 128 + ((c ^ (px & 7)) << 4));
       size_t line;
@@ -269,15 +263,16 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
     const bool on = EPI != EPI_DG_ACC || p.part;
     if (on) {
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
+      for (int c = 0; c < NCT; ++c)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float s0 = sum16(ps0[ct][r]);
+          const int ct = ct0 + c;
+          const float s0 = sum16(ps0[c][r]);
           float s1 = 0.f;
-          if constexpr (kPart2) s1 = sum16(ps1[ct][r]);
+          if constexpr (kPart2) s1 = sum16(ps1[c][r]);
           if (fr == 0) {
-            red[(wave * 2 + 0) * 64 + ct * 16 + fk * 4 + r] = s0;
-            if constexpr (kPart2) red[(wave * 2 + 1) * 64 + ct * 16 + fk * 4 + r] = s1;
+            red[(row * 2 + 0) * 64 + ct * 16 + fk * 4 + r] = s0;
+            if constexpr (kPart2) red[(row * 2 + 1) * 64 + ct * 16 + fk * 4 + r] = s1;
           }
         }
     }
@@ -311,9 +306,15 @@ constexpr int kFragBuf = SRMI_CONV_FRAGBUF;
 // tail > 0 splits each run: the workgroup of run `bid` does its strips except the
 // last `tail` ones (tail_part = false), or only those (tail_part = true; the fused
 // backward hands them to the filter-gradient workgroup of the same rows)
-template <int TW, int EPI>
+//
+// NW = waves per workgroup: 4 (one per output row of the strip, all 64 output
+// channels) or 8 (a wave per row and channel half: two waves per SIMD, so one wave's
+// LDS / memory waits overlap the other's MFMAs; same LDS footprint)
+template <int TW, int EPI, int NW = 4>
 __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, int bid, char* smem, int tail = 0,
                                             bool tail_part = false) {
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  constexpr int NCT = NW == 8 ? 2 : 4;  // 16-wide output-channel tiles per wave
   using S = Conv2Smem<TW>;
   constexpr int NPT = TW / 16;
   char* wl = smem;
@@ -321,6 +322,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   float* red = reinterpret_cast<float*>(smem + S::WB + S::RING);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = wave & 3, ct0 = NCT * (wave >> 2);  // strip row, first channel tile
   const int fr = lane & 15, fk = lane >> 4;
   const int nsx = p.W / TW, nsy = p.H / kTH;
   const int runs_per_col = (nsy + run_len - 1) / run_len;
@@ -349,7 +351,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   const uint32_t rbase = lds_u32(ring);
   const void* const zpage = uniform_ptr(kZeros);
   constexpr int NGRP = S::GROUPB / 1024;         // 1 KiB DMA pieces per group
-  constexpr int NGW = (NGRP + 3) / 4;            // pieces per wave (upper bound)
+  constexpr int NGW = (NGRP + NW - 1) / NW;      // pieces per wave (upper bound)
   // Per-lane parts of the DMA source, computed once: piece i = wv_s + 4m covers ring
   // pixels q = 8i + lane/8, i.e. row rr and halo column hx of the group; the chunk
   // swizzle (q & 7) is the same in all three ring slots (4 (TW + 2) px apart).
@@ -357,7 +359,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   uint32_t okx = 0;
 #pragma unroll
   for (int m = 0; m < NGW; ++m) {
-    const int i = wv_s + 4 * m;
+    const int i = wv_s + NW * m;
     const int q = 8 * i + (lane >> 3);
     const int c = (lane & 7) ^ (q & 7);
     const int rr = q / (TW + 2), hx = q - rr * (TW + 2);
@@ -372,21 +374,21 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     const int o = loff[m];  // ring slots are 4 (TW + 2) px apart, a multiple of 8: same swizzle
     const bool ok = ((okx >> m) & 1u) && y0 + lrr[m] >= 0 && y0 + lrr[m] < p.H;
     const void* src = ok ? (const void*)(base + o) : zpage;
-    glds16(src, rbase + (uint32_t)(slot * 4 * (TW + 2)) * 128u + (uint32_t)(wv_s + 4 * m) * 1024u);
+    glds16(src, rbase + (uint32_t)(slot * 4 * (TW + 2)) * 128u + (uint32_t)(wv_s + NW * m) * 1024u);
   };
   auto group_dma = [&](int gidx) __attribute__((always_inline)) {
 #pragma unroll
     for (int m = 0; m < NGW; ++m)
-      if (wv_s + 4 * m < NGRP) group_dma_one(gidx, m);
+      if (wv_s + NW * m < NGRP) group_dma_one(gidx, m);
   };
 
   // bias first (read only by the epilogue): its latency hides under the prologue wait
   // instead of following it (~650 cycles per workgroup)
-  float4 bias[4];
+  float4 bias[NCT];
   {
     const float* bp = p.bias ? p.bias : reinterpret_cast<const float*>(kZeros);  // pointer select, no branch
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) bias[ct] = *reinterpret_cast<const float4*>(bp + cb * 64 + ct * 16 + fk * 4);
+    for (int c = 0; c < NCT; ++c) bias[c] = *reinterpret_cast<const float4*>(bp + cb * 64 + (ct0 + c) * 16 + fk * 4);
   }
   // prologue: filters (all 9 taps, 72 KiB) and input groups k0, k0+1, all by LDS-DMA
   // (swizzle on the source side), everything in flight before the one wait.  (Waiting
@@ -395,7 +397,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   // while the first strip's MFMA phase grew by 500.)
   {
     const uint32_t wbase = lds_u32(wl);
-    for (int i = wv_s; i < 72; i += 4) {
+    for (int i = wv_s; i < 72; i += NW) {
       const int tap = i >> 3, row = 8 * (i & 7) + (lane >> 3), c = (lane & 7) ^ (row & 7);
       glds16(p.w + ((size_t)(tap * p.Cout + cb * 64 + row)) * 64 + c * 8, wbase + (uint32_t)i * 1024u);
     }
@@ -405,20 +407,20 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   }
   STAMP(1);
   // lane-constant A-fragment byte offsets (tap adds 8192)
-  uint32_t aoff[2][4];
+  uint32_t aoff[2][NCT];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) aoff[kk][ct] = swz128(ct * 16 + fr, kk * 4 + fk);
+    for (int c = 0; c < NCT; ++c) aoff[kk][c] = swz128((ct0 + c) * 16 + fr, kk * 4 + fk);
   __syncthreads();
 
 #pragma unroll 1
   for (int k = k0; k < k1; ++k) {
-    const int y = 4 * k + wave;
+    const int y = 4 * k + row;
     const bool pf = (k + 1 < k1);
     // group k+2 -> ring slot (k+2)%3, which held group k-1 (last read by strip k-1,
     // released by the barrier that ended it)
-    EpiPre<NPT, EPI> ep;
+    EpiPre<NPT, EPI, NCT> ep;
     [[maybe_unused]] const int sj = 2 + 5 * min(k - k0, 11);
     STAMP(sj);
 
@@ -434,19 +436,19 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
         for (int kk = 0; kk < 2; ++kk) boff[ky][kx][kk] = swz128(slot * (TW + 2) + fr + kx, kk * 4 + fk);
     }
 
-    f32x4 acc[NPT][4];
+    f32x4 acc[NPT][NCT];
 #pragma unroll
     for (int i = 0; i < NPT; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NCT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // 18 K-steps (9 taps x 2 halves of 32 ci), fragments triple-buffered in
     // registers: steps s+1 and s+2's ds_reads are in flight while step s's MFMAs run.
-    bf16x8 A[kFragBuf][4], B[kFragBuf][NPT];
-    auto load_step = [&](int s, bf16x8 (&a)[4], bf16x8 (&b)[NPT]) __attribute__((always_inline)) {
+    bf16x8 A[kFragBuf][NCT], B[kFragBuf][NPT];
+    auto load_step = [&](int s, bf16x8 (&a)[NCT], bf16x8 (&b)[NPT]) __attribute__((always_inline)) {
       const int tap = s >> 1, kk = s & 1, ky = tap / 3, kx = tap % 3;
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) a[ct] = lds_frag(wl, tap * 8192 + aoff[kk][ct]);
+      for (int c = 0; c < NCT; ++c) a[c] = lds_frag(wl, tap * 8192 + aoff[kk][c]);
 #pragma unroll
       for (int pt = 0; pt < NPT; ++pt) b[pt] = lds_frag(ring, boff[ky][kx][kk] + pt * 2048);
     };
@@ -457,30 +459,30 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     for (int s = 0; s < 18; ++s) {
       // group k+2's DMA pieces and the epilogue operands are issued one or two per
       // K-step, so a full memory queue stalls the wave between MFMA groups only
-      if (s < NGW && pf && wv_s + 4 * s < NGRP) group_dma_one(k + 2, s);
+      if (s < NGW && pf && wv_s + NW * s < NGRP) group_dma_one(k + 2, s);
       // the epilogue operands, two per K-step from the first one: a whole strip of
       // MFMAs to land (spread over K-steps 2..13, the heavy fp32 epilogue of
       // DG_ACC_CA waited on its last ones at the end of the K-loop: +1.3 % step)
-      if (2 * s < NPT * 4) epi_prefetch_one<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk, 2 * s);
-      if (2 * s + 1 < NPT * 4) epi_prefetch_one<NPT, EPI>(p, ep, n, cb, y, x0, fr, fk, 2 * s + 1);
+      if (2 * s < NPT * NCT) epi_prefetch_one<NPT, EPI, NCT>(p, ep, n, cb, y, x0, fr, fk, ct0, 2 * s);
+      if (2 * s + 1 < NPT * NCT) epi_prefetch_one<NPT, EPI, NCT>(p, ep, n, cb, y, x0, fr, fk, ct0, 2 * s + 1);
       __builtin_amdgcn_sched_barrier(0);
       const bool ld = s + LA < 18;
       if (ld) load_step(s + LA, A[(s + LA) % kFragBuf], B[(s + LA) % kFragBuf]);
 #pragma unroll
       for (int pt = 0; pt < NPT; ++pt)
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct)
-          acc[pt][ct] = mfma16(A[s % kFragBuf][ct], B[s % kFragBuf][pt], acc[pt][ct]);
+        for (int c = 0; c < NCT; ++c)
+          acc[pt][c] = mfma16(A[s % kFragBuf][c], B[s % kFragBuf][pt], acc[pt][c]);
 #if SRMI_CONV_ILV
       // one fragment read issued behind each MFMA: the reads' issue time hides under
       // the MFMA pipe instead of stalling it between K-steps
       if (ld) {
 #pragma unroll
-        for (int j = 0; j < 4 + NPT; ++j) {
+        for (int j = 0; j < NCT + NPT; ++j) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 4 * NPT - (4 + NPT), 0);
+        if constexpr (NCT * NPT > NCT + NPT) __builtin_amdgcn_sched_group_barrier(0x008, NCT * NPT - (NCT + NPT), 0);
       }
 #endif
       __builtin_amdgcn_sched_barrier(0);
@@ -497,8 +499,8 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    conv_epilogue2<NPT, EPI>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx, nsy * nsx, red, fr, fk, wave, tid,
-                             ring + (k % 3) * S::GROUPB + wave * TW * 128);
+    conv_epilogue2<NPT, EPI, NCT>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx, nsy * nsx, red, fr, fk, row, ct0,
+                                  tid, ring + (k % 3) * S::GROUPB + row * TW * 128);
     STAMP(sj + 3);
     // LDS-only barrier: this strip's global stores stay in flight into the next strip
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -509,10 +511,10 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   STAMP(61);
 }
 
-template <int TW, int EPI>
-__global__ void __launch_bounds__(kThreads, 1) conv64_kernel(ConvParams p, int run_len) {
+template <int TW, int EPI, int NW>
+__global__ void __launch_bounds__(NW * 64, 1) conv64_kernel(ConvParams p, int run_len) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv64_body<TW, EPI>(p, run_len, blockIdx.x, smem);
+  conv64_body<TW, EPI, NW>(p, run_len, blockIdx.x, smem);
 }
 
 // runs of the v2 kernel for a CU budget: ~one workgroup per CU of the budget
