@@ -237,11 +237,21 @@ constexpr int NGP = 2 * GD + 2 * GX;                             // groups per p
 
 // The body is instantiated once per wave (WV = wave index): the wave's DMA groups,
 // taps and tile rotation are compile-time constants (no SGPR pressure, no branches).
-template <int WV>
+//
+// NW = 8 (two waves per SIMD): the 36 N tiles are split 4 / 5 between waves WV and
+// WV + 4 (the same SIMD: 17 + 20 MFMAs per K-step, as one 4-wave wave's 37); waves
+// 0-3 also issue the DMA (the 4-wave schedule) and the bias gradient; every wave
+// keeps all four output-channel tiles and writes its partial slab in the 4-wave
+// layout, so wgrad_reduce is unchanged.
+template <int WV, int NW = 4>
 __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, int chunk, int cb) {
   using namespace v4;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  constexpr int NT = NW == 4 ? 9 : (WV < 4 ? 4 : 5);                     // N tiles of this wave
+  constexpr int J0 = NW == 4 ? 9 * WV : (WV < 4 ? 4 * WV : 16 + 5 * (WV - 4));  // its first N tile
+  constexpr bool kMain = WV < 4;  // DMA + bias gradient
   const int tid = threadIdx.x, lane = tid & 63;
-  constexpr int wave = WV, wave_s = WV;
+  constexpr int wave = WV & 3, wave_s = WV & 3;
   const int Hr = p.H / p.row_splits;
   const int n = chunk / p.row_splits, ybase = (chunk % p.row_splits) * Hr;
   const int np = Hr / 2;
@@ -323,11 +333,11 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
     }
   };
 
-  f32x4 acc[4][9];
+  f32x4 acc[4][NT];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 bacc = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 ones;
 #pragma unroll
@@ -337,15 +347,15 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   const int g4 = lane >> 4, li = lane & 15, lq = li >> 2, lp = li & 3;
   const int prow = g4 >> 1, pcol = 8 * (g4 & 1) + lq;
   const uint32_t half = (lp & 1) * 8;
-  uint32_t acol[4][2], bcol[9][2];
-  int bky[9];
+  uint32_t acol[4][2], bcol[NT][2];
+  int bky[NT];
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
     for (int h = 0; h < 2; ++h) acol[ct][h] = swz128t(pcol + 4 * h, 2 * ((ct + wave) & 3) + (lp >> 1)) + half;
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int j = 9 * wave + t, tap = j >> 2, it = j & 3, kx = tap % 3;
+  for (int t = 0; t < NT; ++t) {
+    const int j = J0 + t, tap = j >> 2, it = j & 3, kx = tap % 3;
     bky[t] = tap / 3;
 #pragma unroll
     for (int h = 0; h < 2; ++h) bcol[t][h] = DY_RING + swz128t(pcol + kx + 4 * h, 2 * it + (lp >> 1)) + half;
@@ -353,26 +363,36 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
 
   // slot offsets: dY row r -> slot r & (RD-1); input row r -> slot (r + 1) % RX.
   // Per pair the lane's A row is 2j + prow, its B rows 2j + prow + ky (ky of tap t).
-  int boffr[9];
+  int boffr[NT];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) boffr[t] = prow + bky[t];  // 0..3
-  auto slots = [&](int j, uint32_t& ra, uint32_t (&rb)[9]) __attribute__((always_inline)) {
+  for (int t = 0; t < NT; ++t) boffr[t] = prow + bky[t];  // 0..3
+  auto slots = [&](int j, uint32_t& ra, uint32_t (&rb)[NT]) __attribute__((always_inline)) {
     ra = (uint32_t)(((2 * j + prow) & (RD - 1)) * DSLOT);
     int sb = (2 * j) % RX;  // uniform
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
+    for (int t = 0; t < NT; ++t) {
       int sl = sb + boffr[t];
       sl = sl >= RX ? sl - RX : sl;
       rb[t] = (uint32_t)(sl * XSLOT);
     }
   };
-  auto load_step = [&](uint32_t ra, const uint32_t (&rb)[9], int kc, bf16x8 (&a)[4], bf16x8 (&b)[9])
+  auto load_a = [&](uint32_t ra, int kc, bf16x8 (&a)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+      a[ct] = cat_tr(lds_tr(smem, ra + acol[ct][0] + kc * 2048), lds_tr(smem, ra + acol[ct][1] + kc * 2048));
+  };
+  auto load_b = [&](const uint32_t (&rb)[NT], int kc, bf16x8 (&b)[NT]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      b[t] = cat_tr(lds_tr(smem, rb[t] + bcol[t][0] + kc * 2048), lds_tr(smem, rb[t] + bcol[t][1] + kc * 2048));
+  };
+  auto load_step = [&](uint32_t ra, const uint32_t (&rb)[NT], int kc, bf16x8 (&a)[4], bf16x8 (&b)[NT])
       __attribute__((always_inline)) {
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct)
       a[ct] = cat_tr(lds_tr(smem, ra + acol[ct][0] + kc * 2048), lds_tr(smem, ra + acol[ct][1] + kc * 2048));
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
+    for (int t = 0; t < NT; ++t)
       b[t] = cat_tr(lds_tr(smem, rb[t] + bcol[t][0] + kc * 2048), lds_tr(smem, rb[t] + bcol[t][1] + kc * 2048));
   };
   // vmcnt helper: this wave owns 7 (waves 0,1) or 6 (waves 2,3) groups of a pair
@@ -389,18 +409,23 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   };
 
   // prologue: input rows -1, 0 and pairs 0 .. PF-1; wait for the rows and pair 0
+  if constexpr (kMain) {
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
-    if (wave_s + 4 * m < 2 * GX) dma(0, wave_s + 4 * m, true);
-  for (int P = 0; P < PF && P < np; ++P) dma_pair_part(P, 0, 7);
+    for (int m = 0; m < 4; ++m)
+      if (wave_s + 4 * m < 2 * GX) dma(0, wave_s + 4 * m, true);
+    for (int P = 0; P < PF && P < np; ++P) dma_pair_part(P, 0, 7);
+  }
   wait_groups(min(PF, np) - 1, 0);
   __syncthreads();
   WSTAMP(1);
 
   // fragments double-buffered across K-steps; a pair has 3 K-steps, so the pair loop
-  // is unrolled by two (np is even) to keep the buffer parity compile-time
-  bf16x8 A[2][4], B[2][9];
-  uint32_t ra, rb[9];
+  // is unrolled by two (np is even) to keep the buffer parity compile-time.  8 waves
+  // (256 registers a wave): B single-buffered, each tile reloaded right behind its
+  // MFMAs (the partner wave on the SIMD covers the read latency).
+  constexpr int NB = NW == 8 ? 1 : 2;
+  bf16x8 A[2][4], B[NB][NT];
+  uint32_t ra, rb[NT];
   slots(0, ra, rb);
   load_step(ra, rb, 0, A[0], B[0]);
 
@@ -412,30 +437,42 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
       WSTAMP(2 + min(j, 59));
       const bool pf = j + PF < np;
       const bool more = j + 1 < np;
-      uint32_t ran, rbn[9];
+      uint32_t ran, rbn[NT];
       slots(j + 1, ran, rbn);
 #pragma unroll
       for (int kc = 0; kc < 3; ++kc) {
         const int cur = (3 * q + kc) & 1, nxt = cur ^ 1;
-        if (pf)
+        if (kMain && pf)
           dma_pair_part(j + PF, kc == 0 ? 0 : (kc == 1 ? 3 : 5), kc == 0 ? 3 : (kc == 1 ? 5 : 7));
         __builtin_amdgcn_sched_barrier(0);
         const bool ld = kc < 2 || more;
-        if (kc < 2) load_step(ra, rb, kc + 1, A[nxt], B[nxt]);
-        else if (more) load_step(ran, rbn, 0, A[nxt], B[nxt]);  // next pair's first K-step
+        if constexpr (NB == 2) {
+          if (kc < 2) load_step(ra, rb, kc + 1, A[nxt], B[nxt]);
+          else if (more) load_step(ran, rbn, 0, A[nxt], B[nxt]);  // next pair's first K-step
+        } else {
+          if (kc < 2) load_a(ra, kc + 1, A[nxt]);
+          else if (more) load_a(ran, 0, A[nxt]);
+        }
 #pragma unroll
-        for (int t = 0; t < 9; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
-          for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(A[cur][ct], B[cur][t], acc[ct][t]);
-        bacc = mfma16(A[cur][0], ones, bacc);  // slot 0 = this wave's own co tile
-        // the next K-step's 26 transposed reads issued behind the MFMAs, one per MFMA
+          for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(A[cur][ct], B[cur % NB][t], acc[ct][t]);
+        if constexpr (kMain) bacc = mfma16(A[cur][0], ones, bacc);  // slot 0 = this wave's own co tile
+        if constexpr (NB == 1) {
+          if (kc < 2) load_b(rb, kc + 1, B[0]);
+          else if (more) load_b(rbn, 0, B[0]);
+        }
+        // the next K-step's transposed reads issued behind the MFMAs, one per MFMA
+        constexpr int NRD = 2 * (4 + NT), NMF = 4 * NT + (kMain ? 1 : 0);
+        constexpr int NPAIR = NRD < NMF ? NRD : NMF;
         if (ld) {
 #pragma unroll
-          for (int i = 0; i < 26; ++i) {
+          for (int i = 0; i < NPAIR; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
           }
-          __builtin_amdgcn_sched_group_barrier(0x008, 11, 0);
+          if constexpr (NMF > NPAIR) __builtin_amdgcn_sched_group_barrier(0x008, NMF - NPAIR, 0);
+          if constexpr (NRD > NPAIR) __builtin_amdgcn_sched_group_barrier(0x100, NRD - NPAIR, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
         if (kc == 1) {
@@ -450,7 +487,7 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
       }
       ra = ran;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) rb[t] = rbn[t];
+      for (int t = 0; t < NT; ++t) rb[t] = rbn[t];
     }
   }
 
@@ -458,16 +495,19 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   // writes 1 KiB contiguous; wgrad_reduce_kernel maps it back to (co, ci, tap)
   // (plain stores: written through, the wgrad launch was 0.9 us shorter but the
   // reduce that re-reads the slabs right after it 1.9 us longer)
-  const size_t soff = (size_t)chunk * Cout * 576 + (size_t)cb * (64 * 576) + (size_t)wave * (9 * 4 * 256);
+  // (N tile J, slot ct of rotation `wave`) -> the 4-wave position (wave J / 9, tile
+  // J % 9, the slot of the same output-channel tile under that wave's rotation)
+  const size_t soff = (size_t)chunk * Cout * 576 + (size_t)cb * (64 * 576);
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {
+      const int J = J0 + t, w4 = J / 9, t4 = J % 9, s4 = (ct + wave - w4) & 3;
       const float4 v = make_float4(acc[ct][t][0], acc[ct][t][1], acc[ct][t][2], acc[ct][t][3]);
-      const size_t o = soff + ((t * 4 + ct) * 64 + lane) * 4;
+      const size_t o = soff + (size_t)w4 * (9 * 4 * 256) + ((t4 * 4 + s4) * 64 + lane) * 4;
       *reinterpret_cast<float4*>(p.slab + o) = v;
     }
-  if ((lane & 15) == 0) {
+  if (kMain && (lane & 15) == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       p.bslab[(size_t)chunk * Cout + cb * 64 + wave * 16 + 4 * (lane >> 4) + r] = bacc[r];
@@ -475,18 +515,29 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   WSTAMP(63);
 }
 
+template <int NW = 4>
 __device__ __forceinline__ void wgrad48_dispatch(const WgradParams& p, char* smem, int chunk, int cb) {
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: wgrad48_body<0>(p, smem, chunk, cb); break;
-    case 1: wgrad48_body<1>(p, smem, chunk, cb); break;
-    case 2: wgrad48_body<2>(p, smem, chunk, cb); break;
-    default: wgrad48_body<3>(p, smem, chunk, cb); break;
+    case 0: wgrad48_body<0, NW>(p, smem, chunk, cb); break;
+    case 1: wgrad48_body<1, NW>(p, smem, chunk, cb); break;
+    case 2: wgrad48_body<2, NW>(p, smem, chunk, cb); break;
+    case 3: wgrad48_body<3, NW>(p, smem, chunk, cb); break;
+    default:
+      if constexpr (NW == 8) {
+        switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+          case 4: wgrad48_body<4, NW>(p, smem, chunk, cb); break;
+          case 5: wgrad48_body<5, NW>(p, smem, chunk, cb); break;
+          case 6: wgrad48_body<6, NW>(p, smem, chunk, cb); break;
+          default: wgrad48_body<7, NW>(p, smem, chunk, cb); break;
+        }
+      }
+      break;
   }
 }
 
 __global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  wgrad48_dispatch(p, smem, blockIdx.x, blockIdx.y);
+  wgrad48_dispatch<4>(p, smem, blockIdx.x, blockIdx.y);
 }
 
 // ---------------------------------------------------------------------------
@@ -511,9 +562,9 @@ __global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
 // dgrad half (F1: 24.7 vs 36.9 us at C2), so the last `tail` strips of dgrad run k
 // move to the workgroup of chunk k, which runs them after its chunk (same rows, same
 // XCD), with its own filter prologue.
-template <int EPI>
-__global__ void __launch_bounds__(256, 1) rcab_bwd_kernel(ConvParams cp, int run_len, int nconv, WgradParams wp,
-                                                          int nwg, int paired, int tail) {
+template <int EPI, int NW>
+__global__ void __launch_bounds__(NW * 64, 1) rcab_bwd_kernel(ConvParams cp, int run_len, int nconv, WgradParams wp,
+                                                              int nwg, int paired, int tail) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x, tot = nconv + nwg;
 #ifndef SRMI_FUSE_DIAG
@@ -530,14 +581,14 @@ __global__ void __launch_bounds__(256, 1) rcab_bwd_kernel(ConvParams cp, int run
     else w = b - c0;
   }
   if (conv >= 0) {
-    if (!(SRMI_FUSE_DIAG & 2)) conv64_body<48, EPI>(cp, run_len, conv, smem, tail, false);
+    if (!(SRMI_FUSE_DIAG & 2)) conv64_body<48, EPI, NW>(cp, run_len, conv, smem, tail, false);
     return;
   }
   const int nch = wp.N * wp.row_splits;
-  if (!(SRMI_FUSE_DIAG & 1)) wgrad48_dispatch(wp, smem, w % nch, w / nch);
+  if (!(SRMI_FUSE_DIAG & 1)) wgrad48_dispatch<NW>(wp, smem, w % nch, w / nch);
   if (tail > 0 && !(SRMI_FUSE_DIAG & 2)) {
     __syncthreads();  // every wave is past its last LDS read of the chunk
-    conv64_body<48, EPI>(cp, run_len, w, smem, tail, true);
+    conv64_body<48, EPI, NW>(cp, run_len, w, smem, tail, true);
   }
 }
 
@@ -546,6 +597,12 @@ int rcab_bwd_fusable(const ConvParams& cp, const WgradParams& wp) {
          cp.H % 4 == 0 && wp.W == 48 && wp.Cout == 64 && wp.dy_mode == IN_PLAIN && wp.row_splits > 0 &&
          wp.H % wp.row_splits == 0 && (wp.H / wp.row_splits) % 4 == 0;
 }
+
+// waves per workgroup of the fused launch (8: two per SIMD in both roles)
+#ifndef SRMI_FUSE_NW
+#define SRMI_FUSE_NW 8
+#endif
+constexpr int kFuseNW = SRMI_FUSE_NW;
 
 int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradParams& wp, hipStream_t st) {
   if (!rcab_bwd_fusable(cp, wp)) return SRMI_ERR_SHAPE;
@@ -576,16 +633,16 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
   switch (epi) {
     case EPI_DG_RELUMASK:
       if (!c.aux) return SRMI_ERR_ARG;
-      hipLaunchKernelGGL(rcab_bwd_kernel<EPI_DG_RELUMASK>, grid, dim3(256), lds, st, c, run_len, nconv, w, nwg,
+      hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_RELUMASK, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len, nconv, w, nwg,
                          paired, tail);
       break;
     case EPI_DG_ACC_CA:
       if (!c.r1 || !c.aux || !c.part || c.yb || c.r2 || c.r3 || !c.yf) return SRMI_ERR_ARG;
-      hipLaunchKernelGGL(rcab_bwd_kernel<EPI_DG_ACC_CA>, grid, dim3(256), lds, st, c, run_len, nconv, w, nwg, paired, tail);
+      hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len, nconv, w, nwg, paired, tail);
       break;
     case EPI_DG_ACC:
       if (!c.yf || (c.part && !c.aux)) return SRMI_ERR_ARG;
-      hipLaunchKernelGGL(rcab_bwd_kernel<EPI_DG_ACC>, grid, dim3(256), lds, st, c, run_len, nconv, w, nwg, paired, tail);
+      hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len, nconv, w, nwg, paired, tail);
       break;
     default:
       return SRMI_ERR_ARG;
