@@ -283,6 +283,9 @@ __global__ void __launch_bounds__(kThreads, 2) conv3x3_kernel(ConvParams p) {
 #ifndef SRMI_CONV_NW8
 #define SRMI_CONV_NW8 1
 #endif
+#ifndef SRMI_DGRAD_NW8
+#define SRMI_DGRAD_NW8 1
+#endif
 template <int TW, int EPI>
 static int launch_tw(const ConvParams& p, hipStream_t st) {
   if (p.Cin == 64 && p.in_mode == IN_PLAIN) {
@@ -291,10 +294,10 @@ static int launch_tw(const ConvParams& p, hipStream_t st) {
     dim3 grid(conv64_blocks(p, TW, run_len));
     ConvParams q = p;
     q.stamps = g_debug_stamps;
-    // forward epilogues: 8 waves (two per SIMD, a wave per row and channel half)
-    constexpr int NW = (SRMI_CONV_NW8 && TW == 48 && (EPI == EPI_RELU_BF16 || EPI == EPI_POOL_BF16 ||
-                                                       EPI == EPI_RESID || EPI == EPI_PS_BF16 ||
-                                                       EPI == EPI_PLAIN_BF16)) ? 8 : 4;
+    // 8 waves (two per SIMD, a wave per row and channel half) at TW = 48
+    constexpr bool kFwd = EPI == EPI_RELU_BF16 || EPI == EPI_POOL_BF16 || EPI == EPI_RESID || EPI == EPI_PS_BF16 ||
+                          EPI == EPI_PLAIN_BF16;
+    constexpr int NW = (TW == 48 && (kFwd ? SRMI_CONV_NW8 : SRMI_DGRAD_NW8)) ? 8 : 4;
     hipLaunchKernelGGL((conv64_kernel<TW, EPI, NW>), grid, dim3(NW * 64), Conv2Smem<TW>::TOTAL, st, q, run_len);
   } else {
     constexpr int E1 = EPI == EPI_DG_ACC_CA ? EPI_DG_ACC : EPI;  // v1 handles the general form

@@ -535,9 +535,13 @@ __device__ __forceinline__ void wgrad48_dispatch(const WgradParams& p, char* sme
   }
 }
 
-__global__ void __launch_bounds__(256, 1) wgrad48_kernel(WgradParams p) {
+#ifndef SRMI_WGRAD_NW
+#define SRMI_WGRAD_NW 8
+#endif
+constexpr int kWgradNW = SRMI_WGRAD_NW;  // waves per workgroup of the standalone filter gradient
+__global__ void __launch_bounds__(kWgradNW * 64, 1) wgrad48_kernel(WgradParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  wgrad48_dispatch<4>(p, smem, blockIdx.x, blockIdx.y);
+  wgrad48_dispatch<kWgradNW>(p, smem, blockIdx.x, blockIdx.y);
 }
 
 // ---------------------------------------------------------------------------
@@ -669,7 +673,7 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
   WgradParams q = p;
   q.stamps = g_wg_stamps;
   if (use_wgrad48(p)) {
-    hipLaunchKernelGGL(wgrad48_kernel, grid, dim3(256), v4::LDS, st, q);
+    hipLaunchKernelGGL(wgrad48_kernel, grid, dim3(kWgradNW * 64), v4::LDS, st, q);
   } else if (p.W % 48 == 0) {
     hipLaunchKernelGGL(wgrad3x3_kernel<48>, grid, dim3(256), Wg3<48>::TOTAL, st, q);
   } else if (p.W % 32 == 0) {
