@@ -156,7 +156,7 @@ def fused_rooflines(tr, step_ms, reps=20):
         flop_slot = FUSED_FLOP_PER_TILE * tiles_per_engine * n_eng
         ach = bytes_slot / (ms * 1e-3) / 1e9
         tf = flop_slot / (ms * 1e-3) / 1e12
-        tr_ = _pmc_traffic("rcab_bwd_kernel<%d>" % (7 if which == 1 else 4))
+        tr_ = _pmc_traffic("rcab_bwd_kernel<%d" % (7 if which == 1 else 4))
         out[which] = {
             "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4),

@@ -210,7 +210,7 @@ struct srmi_engine {
   long long* d_caoffs;
   std::vector<PackEntry> h_entries;
   std::vector<long long> h_caoffs;
-  long long max_pack_elems = 0;
+  int max_cob = 0, max_cib = 0;  // largest Cout / 64, Cin / 64 of the packed convs
   bool tables_uploaded = false;
   int last_n = 0;
 
@@ -357,7 +357,7 @@ static int init_engine(srmi_engine* e, const srmi_model_config* cfg, int train) 
 
 static void build_tables(srmi_engine* e) {
   e->h_entries.clear();
-  e->max_pack_elems = 0;
+  e->max_cob = e->max_cib = 0;
   for (ConvRef* c : e->P.mfma_convs) {
     PackEntry pe{};
     pe.w_off = c->w;
@@ -369,7 +369,8 @@ static void build_tables(srmi_engine* e) {
     pe.Cin = c->cin;
     pe.ps = c->ps;
     e->h_entries.push_back(pe);
-    e->max_pack_elems = std::max(e->max_pack_elems, (long long)c->cout * c->cin * 9);
+    e->max_cob = std::max(e->max_cob, (c->cout + 63) / 64);
+    e->max_cib = std::max(e->max_cib, (c->cin + 63) / 64);
   }
   e->h_caoffs.clear();
   for (auto& grp : e->P.groups)
@@ -753,8 +754,8 @@ int srmi_engine_destroy(srmi_engine* e) {
 int srmi_pack_weights(srmi_engine* e, const float* params, void* stream) {
   if (!e || !params) return SRMI_ERR_ARG;
   RC(upload_tables(e, S_(stream)));
-  return pack_launch(params, e->d_entries, (int)e->h_entries.size(), e->max_pack_elems, e->packs, e->pbias, e->f32,
-                     S_(stream));
+  return pack_launch(params, e->d_entries, (int)e->h_entries.size(), e->max_cob, e->max_cib, e->packs, e->pbias,
+                     e->f32, S_(stream));
 }
 
 int srmi_forward(srmi_engine* e, const float* params, const float* lr, float* sr, int n, void* stream) {

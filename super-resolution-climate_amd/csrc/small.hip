@@ -1322,31 +1322,66 @@ __device__ __forceinline__ void pack_elem(const float* __restrict__ W, const flo
   }
 }
 
+// One workgroup per (64-output-channel block, 64-input-channel block, conv): the
+// block's filters W[cot][cc*64 .. +63][9] (64 contiguous 2304-byte rows, cot the
+// torch channel of packed channel cop) are read coalesced into LDS in the pack's
+// element type, then both packs are written as full 128-byte rows (forward: 64 ci
+// of one (tap, cop); dgrad: 64 co of one (tap, ci)).  The element-wise form read W
+// with a 36 B (forward) / 2.3 KB (dgrad) lane stride: 262 us per step.
 template <typename T>
-__global__ void pack_kernel(const float* __restrict__ params, const PackEntry* __restrict__ ents,
-                            T* __restrict__ packs, float* __restrict__ pbias) {
-  const PackEntry e = ents[blockIdx.y];
-  const long long total = (long long)e.Cout * e.Cin * 9;
-  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x)
-    pack_elem(params + e.w_off, params + e.b_off, e.Cout, e.Cin, e.ps, blockIdx.z, idx, packs + e.f_off,
-              packs + e.d_off, pbias + e.pb_off);
+__global__ void __launch_bounds__(256) pack_tile_kernel(const float* __restrict__ params,
+                                                        const PackEntry* __restrict__ ents, T* __restrict__ packs,
+                                                        float* __restrict__ pbias) {
+  extern __shared__ __attribute__((aligned(16))) char smem_pack[];
+  T* wl = reinterpret_cast<T*>(smem_pack);  // [64 l][64 ci_l][9]
+  const PackEntry e = ents[blockIdx.z];
+  const int cb = blockIdx.x, cc = blockIdx.y;
+  if (cb * 64 >= e.Cout || cc * 64 >= e.Cin) return;
+  const int Cout = e.Cout, Cin = e.Cin, tid = threadIdx.x;
+  const float* W = params + e.w_off;
+  auto cot_of = [&](int cop) { return e.ps ? 4 * (cop & 63) + (cop >> 6) : cop; };
+  // 1. 64 rows x 576 floats (144 float4 each)
+  for (int i = tid; i < 64 * 144; i += 256) {
+    const int l = i / 144, q = i - l * 144;
+    const float4 v = *reinterpret_cast<const float4*>(W + ((size_t)cot_of(cb * 64 + l) * Cin + cc * 64) * 9 + q * 4);
+    T* d = wl + l * 576 + q * 4;
+    d[0] = from_f32<T>(v.x); d[1] = from_f32<T>(v.y); d[2] = from_f32<T>(v.z); d[3] = from_f32<T>(v.w);
+  }
+  __syncthreads();
+  // 2. forward pack rows (tap, cop): [cc][tap][cop][ci_l]; 8 lanes per row, 8 ci each
+  T* fp = packs + e.f_off;
+  for (int i = tid; i < 9 * 64 * 8; i += 256) {
+    const int seg = i & 7, r = i >> 3, l = r & 63, tap = r >> 6;
+    T v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = wl[l * 576 + (seg * 8 + k) * 9 + tap];
+    T* d = fp + (((size_t)cc * 9 + tap) * Cout + cb * 64 + l) * 64 + seg * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = v[k];
+  }
+  // 3. dgrad pack rows (tapd, ci): [cb][tapd][ci][co_l] = W[cot][ci][8 - tapd]
+  T* dp = packs + e.d_off;
+  for (int i = tid; i < 9 * 64 * 8; i += 256) {
+    const int seg = i & 7, r = i >> 3, ci_l = r & 63, tapd = r >> 6;
+    T v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = wl[(seg * 8 + k) * 576 + ci_l * 9 + (8 - tapd)];
+    T* d = dp + (((size_t)cb * 9 + tapd) * Cin + cc * 64 + ci_l) * 64 + seg * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = v[k];
+  }
+  if (cc == 0 && tid < 64) pbias[e.pb_off + cb * 64 + tid] = params[e.b_off + cot_of(cb * 64 + tid)];
 }
 
-// grid (kPackSlices, entries, 3): a few blocks per conv that stride over its
-// elements.  (A grid sized for the largest conv left ~3/4 of ~700 K blocks empty
-// for the 400 64->64 convs: 188 us of block dispatch per step.)
-constexpr int kPackSlices = 4;
-int pack_launch(const float* params, const PackEntry* dev_entries, int nentries, long long max_elems, void* packs,
+int pack_launch(const float* params, const PackEntry* dev_entries, int nentries, int max_cob, int max_cib, void* packs,
                 float* pbias, int f32, hipStream_t st) {
-  (void)max_elems;
-  const long long bx = kPackSlices;
+  const dim3 grid((unsigned)max_cob, (unsigned)max_cib, (unsigned)nentries);
   if (f32)
-    hipLaunchKernelGGL(pack_kernel<float>, dim3((unsigned)bx, nentries, 3), dim3(256), 0, st, params, dev_entries,
+    hipLaunchKernelGGL(pack_tile_kernel<float>, grid, dim3(256), 64 * 576 * sizeof(float), st, params, dev_entries,
                        static_cast<float*>(packs), pbias);
   else
-    hipLaunchKernelGGL(pack_kernel<bf16_t>, dim3((unsigned)bx, nentries, 3), dim3(256), 0, st, params, dev_entries,
-                       static_cast<bf16_t*>(packs), pbias);
+    hipLaunchKernelGGL(pack_tile_kernel<bf16_t>, grid, dim3(256), 64 * 576 * sizeof(bf16_t), st, params,
+                       dev_entries, static_cast<bf16_t*>(packs), pbias);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

@@ -147,7 +147,8 @@ struct PackEntry {
   long long pb_off;  // offset of the packed bias in the fp32 packed-bias buffer
   int Cout, Cin, ps, pad;
 };
-int pack_launch(const float* params, const PackEntry* dev_entries, int nentries, long long max_elems,
+// max_cob / max_cib: the largest Cout / 64 and Cin / 64 over the entries
+int pack_launch(const float* params, const PackEntry* dev_entries, int nentries, int max_cob, int max_cib,
                 void* packs, float* pbias, int f32, hipStream_t st);
 
 int pack_one_launch(const float* w, const float* b, int Cout, int Cin, int ps, void* fpack, void* dpack,
