@@ -300,7 +300,7 @@ static size_t carve(srmi_engine* e, char* base) {
       // a call may pass fewer tiles than the capacity (a short last batch), and
       // fewer tiles get more row splits: size for the largest n * rs(n)
       for (int n = 1; n <= N; ++n) {
-        const size_t ns = (size_t)n * choose_row_splits(n, H, Cout, e->cu_budget);
+        const size_t ns = (size_t)n * choose_row_splits(n, H, Cout, e->cu_budget) * (W % 48 == 0 ? W / 48 : 1);
         sf = std::max(sf, ns * Cout * 576);
         bf = std::max(bf, ns * Cout);
       }

@@ -252,14 +252,18 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   constexpr bool kMain = WV < 4;  // DMA + bias gradient
   const int tid = threadIdx.x, lane = tid & 63;
   constexpr int wave = WV & 3, wave_s = WV & 3;
-  const int Hr = p.H / p.row_splits;
-  const int n = chunk / p.row_splits, ybase = (chunk % p.row_splits) * Hr;
+  // chunk = (image, row band, 48-column block): W may be any multiple of 48 (the
+  // upsampler's second stage runs at 96); Wd = the row stride in pixels
+  const int Hr = p.H / p.row_splits, Wd = p.W, nxb = Wd / TW;
+  const int xb = chunk % nxb, cr = chunk / nxb, x0 = xb * TW;
+  const int n = cr / p.row_splits, ybase = (cr % p.row_splits) * Hr;
   const int np = Hr / 2;
   const int H = p.H, Cout = p.Cout;
   const bool plain = p.dy_mode == IN_PLAIN;
   WSTAMP(0);
-  const bf16_t* dyn = plain ? p.dy + (size_t)n * H * TW * Cout + cb * 64 : p.dy + (size_t)n * 4 * H * TW * 64;
-  const bf16_t* xn = p.x + (size_t)n * H * TW * 64;
+  const bf16_t* dyn = plain ? p.dy + ((size_t)n * H * Wd + x0) * Cout + cb * 64
+                            : p.dy + ((size_t)n * 4 * H * Wd + 2 * x0) * 64;
+  const bf16_t* xn = p.x + ((size_t)n * H * Wd + x0) * 64;
   const uint32_t lds0 = lds_u32(smem);
   const void* const zpage = uniform_ptr(kZerosW);
   const int dq = lane >> 3, ls = lane & 7;
@@ -276,16 +280,16 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
       const int r = 2 * P + rr, y = ybase + r, xx = 8 * g + dq;
       const int c = (g & 1) ? cl1 : cl0;
       const bf16_t* src = plain
-                              ? dyn + ((size_t)y * TW + xx) * Cout + c * 8
-                              : dyn + ((size_t)(2 * y + (cb >> 1)) * (2 * TW) + 2 * xx + (cb & 1)) * 64 + c * 8;
+                              ? dyn + ((size_t)y * Wd + xx) * Cout + c * 8
+                              : dyn + ((size_t)(2 * y + (cb >> 1)) * (2 * Wd) + 2 * xx + (cb & 1)) * 64 + c * 8;
       glds16(src, lds0 + (uint32_t)((r % RD) * DSLOT + g * 1024));
     } else {
       const int kk = pre ? k : k - 2 * GD, rr = kk / GX, g = kk - rr * GX;
       const int r = pre ? rr - 1 : 2 * P + 1 + rr;  // chunk-relative input row
       const int y = ybase + r, hx = 8 * g + dq, xx = hx - 1;
-      const bool ok = hx < TW + 2 && y >= 0 && y < H && xx >= 0 && xx < TW;
+      const bool ok = hx < TW + 2 && y >= 0 && y < H && x0 + xx >= 0 && x0 + xx < Wd;
       const int c = (g & 1) ? cl1 : cl0;
-      const void* src = ok ? (const void*)(xn + ((size_t)y * TW + xx) * 64 + c * 8) : zpage;
+      const void* src = ok ? (const void*)(xn + ((ptrdiff_t)y * Wd + xx) * 64 + c * 8) : zpage;
       glds16(src, lds0 + (uint32_t)(DY_RING + ((r + 1) % RX) * XSLOT + g * 1024));
     }
   };
@@ -302,19 +306,19 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
     if (k < 2 * GD) {
       const int rr = k / GD, g = k - rr * GD, xx = 8 * g + dq;
       const int c = (g & 1) ? cl1 : cl0;
-      loff[m] = plain ? (rr * TW + xx) * Cout + c * 8 : (2 * rr * (2 * TW) + 2 * xx) * 64 + c * 8;
+      loff[m] = plain ? (rr * Wd + xx) * Cout + c * 8 : (2 * rr * (2 * Wd) + 2 * xx) * 64 + c * 8;
     } else if (k < NGP) {
       const int kk = k - 2 * GD, rr = kk / GX, g = kk - rr * GX, hx = 8 * g + dq, xx = hx - 1;
       const int c = (g & 1) ? cl1 : cl0;
-      const bool ok = hx < TW + 2 && xx >= 0 && xx < TW;
+      const bool ok = hx < TW + 2 && x0 + xx >= 0 && x0 + xx < Wd;
       okx |= ok ? (1u << m) : 0u;
-      loff[m] = (rr * TW + (ok ? xx : 0)) * 64 + c * 8;
+      loff[m] = (rr * Wd + (ok ? xx : 0)) * 64 + c * 8;
     }
   }
   auto dma_pair_part = [&](int P, int m0, int m1) __attribute__((always_inline)) {
-    const bf16_t* dyb = plain ? dyn + (size_t)(ybase + 2 * P) * TW * Cout
-                              : dyn + ((size_t)(2 * (ybase + 2 * P) + (cb >> 1)) * (2 * TW) + (cb & 1)) * 64;
-    const bf16_t* xb = xn + (ptrdiff_t)(ybase + 2 * P + 1) * TW * 64;
+    const bf16_t* dyb = plain ? dyn + (size_t)(ybase + 2 * P) * Wd * Cout
+                              : dyn + ((size_t)(2 * (ybase + 2 * P) + (cb >> 1)) * (2 * Wd) + (cb & 1)) * 64;
+    const bf16_t* xb = xn + (ptrdiff_t)(ybase + 2 * P + 1) * Wd * 64;
     const bool yv0 = ybase + 2 * P + 1 < H, yv1 = ybase + 2 * P + 2 < H;
 #pragma unroll
     for (int m = m0; m < m1; ++m) {
@@ -656,14 +660,15 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
 }
 
 
-int wgrad3x3_nslabs(const WgradParams& p) { return p.N * p.row_splits; }
-
 static bool use_wgrad48(const WgradParams& p) {
-  // v4 (row-pair rings, per-wave specialised) for W == 48
-  return p.W == 48 && p.row_splits > 0 && (p.H / p.row_splits) % 2 == 0;
+  // v4 (row-pair rings, per-wave specialised) for W a multiple of 48: one chunk per
+  // (image, row band, 48-column block)
+  return !p.f32 && p.W % 48 == 0 && p.row_splits > 0 && (p.H / p.row_splits) % 2 == 0;
 }
 
-int wgrad3x3_slab_layout(const WgradParams& p) { return !p.f32 && use_wgrad48(p) ? 1 : 0; }
+int wgrad3x3_nslabs(const WgradParams& p) { return p.N * p.row_splits * (use_wgrad48(p) ? p.W / 48 : 1); }
+
+int wgrad3x3_slab_layout(const WgradParams& p) { return use_wgrad48(p) ? 1 : 0; }
 
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
   if (p.f32) return wgrad_f32_launch(p, st);

@@ -181,7 +181,8 @@ def test_conv_dgrad_unshuffle(N, H, W, dt):
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("N,H,W,rs", [(2, 48, 48, 0), (2, 48, 48, 1), (1, 8, 96, 0), (1, 4, 32, 0), (3, 12, 64, 3),
                                        (64, 48, 48, 0), (4, 96, 96, 0), (3, 12, 48, 3), (2, 48, 48, 12), (1, 8, 48, 2),
-                                       (2, 24, 48, 2), (4, 32, 32, 4), (2, 16, 128, 2)])
+                                       (2, 24, 48, 2), (4, 32, 32, 4), (2, 16, 128, 2), (2, 8, 144, 1),
+                                       (32, 96, 96, 1)])
 def test_wgrad(N, H, W, rs, dt):
     d = dev()
     g = torch.Generator(device="cpu").manual_seed(5)
@@ -199,7 +200,7 @@ def test_wgrad(N, H, W, rs, dt):
 
 
 @pytest.mark.parametrize("dt", DTS)
-@pytest.mark.parametrize("N,H,W", [(2, 48, 48), (1, 4, 96), (2, 8, 32)])
+@pytest.mark.parametrize("N,H,W", [(2, 48, 48), (1, 4, 96), (2, 8, 32), (2, 96, 96)])
 def test_wgrad_pixelshuffle(N, H, W, dt):
     d = dev()
     g = torch.Generator(device="cpu").manual_seed(6)
