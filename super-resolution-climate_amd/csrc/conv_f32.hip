@@ -41,29 +41,32 @@ struct CF32Smem {
 };
 
 // fused epilogue (same semantics as the bf16 kernels' conv_epilogue, fp32 outputs)
-template <int NPT, int EPI>
-__device__ __forceinline__ void epilogue_f32(const ConvParams& p, f32x4 (&acc)[NPT][4], int n, int cb, int y, int x0,
-                                             int strip, int nstrips, float* red, int fr, int fk, int wave, int tid) {
+// (a wave holds row `row` of the strip, output-channel tiles ct0 .. ct0+NCT-1)
+template <int NPT, int EPI, int NCT = 4>
+__device__ __forceinline__ void epilogue_f32(const ConvParams& p, f32x4 (&acc)[NPT][NCT], int n, int cb, int y, int x0,
+                                             int strip, int nstrips, float* red, int fr, int fk, int row, int ct0,
+                                             int tid) {
   const size_t HW = (size_t)p.H * p.W;
   float* yb = reinterpret_cast<float*>(p.yb);
   const float* aux = reinterpret_cast<const float*>(p.aux);
   constexpr bool kPart1 = (EPI == EPI_POOL_BF16);
   constexpr bool kPart2 = (EPI == EPI_DG_ACC);
-  float ps0[4][4], ps1[4][4];
+  float ps0[NCT][4], ps1[NCT][4];
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct)
+  for (int c = 0; c < NCT; ++c)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) ps0[ct][r] = ps1[ct][r] = 0.f;
+    for (int r = 0; r < 4; ++r) ps0[c][r] = ps1[c][r] = 0.f;
 #pragma unroll
   for (int pt = 0; pt < NPT; ++pt) {
     const int xx = x0 + pt * 16 + fr;
     const size_t pix = (size_t)n * HW + (size_t)y * p.W + xx;
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
+    for (int c = 0; c < NCT; ++c) {
+      const int ct = ct0 + c;
       const int col = ct * 16 + fk * 4;
       const int co = cb * 64 + col;
       const size_t o = pix * p.Cout + co;
-      f32x4 v = acc[pt][ct];
+      f32x4 v = acc[pt][c];
       if constexpr (EPI == EPI_RELU_BF16 || EPI == EPI_POOL_BF16 || EPI == EPI_RESID || EPI == EPI_PS_BF16 ||
                     EPI == EPI_PLAIN_BF16) {
         if (EPI != EPI_PLAIN_BF16 || p.bias) {
@@ -99,13 +102,13 @@ __device__ __forceinline__ void epilogue_f32(const ConvParams& p, f32x4 (&acc)[N
         *reinterpret_cast<float4*>(p.yf + o) = make_float4(v[0], v[1], v[2], v[3]);
         if (p.part) {
           const float4 uu = *reinterpret_cast<const float4*>(aux + o);
-          ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
-          ps1[ct][0] += v[0] * uu.x; ps1[ct][1] += v[1] * uu.y;
-          ps1[ct][2] += v[2] * uu.z; ps1[ct][3] += v[3] * uu.w;
+          ps0[c][0] += v[0]; ps0[c][1] += v[1]; ps0[c][2] += v[2]; ps0[c][3] += v[3];
+          ps1[c][0] += v[0] * uu.x; ps1[c][1] += v[1] * uu.y;
+          ps1[c][2] += v[2] * uu.z; ps1[c][3] += v[3] * uu.w;
         }
       }
       if constexpr (kPart1) {
-        ps0[ct][0] += v[0]; ps0[ct][1] += v[1]; ps0[ct][2] += v[2]; ps0[ct][3] += v[3];
+        ps0[c][0] += v[0]; ps0[c][1] += v[1]; ps0[c][2] += v[2]; ps0[c][3] += v[3];
       }
       const float4 ov = make_float4(v[0], v[1], v[2], v[3]);
       if constexpr (EPI == EPI_PS_BF16) {
@@ -123,15 +126,16 @@ __device__ __forceinline__ void epilogue_f32(const ConvParams& p, f32x4 (&acc)[N
     const bool on = !kPart2 || p.part;
     if (on) {
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
+      for (int c = 0; c < NCT; ++c)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float s0 = sum16(ps0[ct][r]);
+          const int ct = ct0 + c;
+          const float s0 = sum16(ps0[c][r]);
           float s1 = 0.f;
-          if constexpr (kPart2) s1 = sum16(ps1[ct][r]);
+          if constexpr (kPart2) s1 = sum16(ps1[c][r]);
           if (fr == 0) {
-            red[(wave * 2 + 0) * 64 + ct * 16 + fk * 4 + r] = s0;
-            if constexpr (kPart2) red[(wave * 2 + 1) * 64 + ct * 16 + fk * 4 + r] = s1;
+            red[(row * 2 + 0) * 64 + ct * 16 + fk * 4 + r] = s0;
+            if constexpr (kPart2) red[(row * 2 + 1) * 64 + ct * 16 + fk * 4 + r] = s1;
           }
         }
     }
@@ -156,16 +160,21 @@ __device__ __forceinline__ void epilogue_f32(const ConvParams& p, f32x4 (&acc)[N
 // MFMAs).  Wave w computes output row w; per tap and 16-channel group g a lane reads
 // ONE float4 per A tile (filter row) and per B tile (pixel) -- K index k of MFMA s
 // is channel 16g + 4k + s -- and issues 16 x NPT MFMAs with them.
-template <int TW, int EPI>
-__global__ void __launch_bounds__(256, 1) conv3x3_f32_kernel(ConvParams p) {
+//
+// NW = 8: two waves per SIMD, a wave per row and output-channel half (the 16x16x4
+// f32 MFMA's 32-cycle issue interval leaves one wave's LDS reads and waits exposed).
+template <int TW, int EPI, int NW>
+__global__ void __launch_bounds__(NW * 64, 1) conv3x3_f32_kernel(ConvParams p) {
   using S = CF32Smem<TW>;
   constexpr int NPT = TW / 16;
+  constexpr int NT = NW * 64, NCT = NW == 8 ? 2 : 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* halo = smem;
   char* wbuf = smem + S::HALO_BYTES;
   const float* X = reinterpret_cast<const float*>(p.x);
   const float* Wp = reinterpret_cast<const float*>(p.w);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = wave & 3, ct0 = NCT * (wave >> 2);
   const int fr = lane & 15, fk = lane >> 4;
   const int strips_x = p.W / TW;
   const int sy = blockIdx.x / strips_x, sx = blockIdx.x - sy * strips_x;
@@ -173,11 +182,11 @@ __global__ void __launch_bounds__(256, 1) conv3x3_f32_kernel(ConvParams p) {
   const int cb = blockIdx.y, n = blockIdx.z;
   const int nchunks = p.Cin >> 6;
 
-  f32x4 acc[NPT][4];
+  f32x4 acc[NPT][NCT];
 #pragma unroll
   for (int i = 0; i < NPT; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NCT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   for (int cc = 0; cc < nchunks; ++cc) {
     if (cc) __syncthreads();
@@ -185,11 +194,11 @@ __global__ void __launch_bounds__(256, 1) conv3x3_f32_kernel(ConvParams p) {
     // flight at once (clamped addresses, padding selected to zero afterwards): a
     // load-wait-store loop serialised one memory latency per float4
     {
-      constexpr int NH = (S::HALO_PIX * 16 + 255) / 256;
+      constexpr int NH = (S::HALO_PIX * 16 + NT - 1) / NT;
       float4 hv[NH];
 #pragma unroll
       for (int j = 0; j < NH; ++j) {
-        const int i = min(tid + j * 256, S::HALO_PIX * 16 - 1);
+        const int i = min(tid + j * NT, S::HALO_PIX * 16 - 1);
         const int q = i >> 4, c = i & 15;
         const int hy = q / (TW + 2), hx = q - hy * (TW + 2);
         const int yy = min(max(y0 - 1 + hy, 0), p.H - 1), xx = min(max(x0 - 1 + hx, 0), p.W - 1);
@@ -202,7 +211,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3_f32_kernel(ConvParams p) {
       }
 #pragma unroll
       for (int j = 0; j < NH; ++j) {
-        const int i = tid + j * 256;
+        const int i = tid + j * NT;
         if (i < S::HALO_PIX * 16) {
           const int q = i >> 4, c = i & 15;
           const int hy = q / (TW + 2), hx = q - hy * (TW + 2);
@@ -216,33 +225,33 @@ __global__ void __launch_bounds__(256, 1) conv3x3_f32_kernel(ConvParams p) {
     {
       const float* ws = Wp + ((size_t)(cc * 9 + 0) * p.Cout + cb * 64) * 64;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = tid + r * 256, row = i >> 4, c = i & 15;
-        *reinterpret_cast<float4*>(wbuf + swz256(row, c)) = *reinterpret_cast<const float4*>(ws + row * 64 + c * 4);
+      for (int r = 0; r < 1024 / NT; ++r) {
+        const int i = tid + r * NT, wr = i >> 4, c = i & 15;
+        *reinterpret_cast<float4*>(wbuf + swz256(wr, c)) = *reinterpret_cast<const float4*>(ws + wr * 64 + c * 4);
       }
     }
     __syncthreads();
 #pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
       // next tap's slice into registers (unconditional, clamped: keeps them in VGPRs)
-      float4 nxt[4];
+      float4 nxt[1024 / NT];
       {
         const float* ws = Wp + ((size_t)(cc * 9 + min(tap + 1, 8)) * p.Cout + cb * 64) * 64;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = tid + r * 256;
+        for (int r = 0; r < 1024 / NT; ++r) {
+          const int i = tid + r * NT;
           nxt[r] = *reinterpret_cast<const float4*>(ws + (i >> 4) * 64 + (i & 15) * 4);
         }
       }
       const char* wb = wbuf + (tap & 1) * S::W_BYTES;
       const int ky = tap / 3, kx = tap - ky * 3;
-      const int qrow = (wave + ky) * (TW + 2) + fr + kx;
+      const int qrow = (row + ky) * (TW + 2) + fr + kx;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int chunk = 4 * g + fk;
-        f32x4 a[4], b[NPT];
+        f32x4 a[NCT], b[NPT];
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) a[ct] = *reinterpret_cast<const f32x4*>(wb + swz256(ct * 16 + fr, chunk));
+        for (int c = 0; c < NCT; ++c) a[c] = *reinterpret_cast<const f32x4*>(wb + swz256((ct0 + c) * 16 + fr, chunk));
 #pragma unroll
         for (int pt = 0; pt < NPT; ++pt) b[pt] = *reinterpret_cast<const f32x4*>(halo + swz256(qrow + pt * 16, chunk));
         // s outermost: consecutive MFMAs update different accumulators (16x16x4 f32 has
@@ -252,27 +261,32 @@ __global__ void __launch_bounds__(256, 1) conv3x3_f32_kernel(ConvParams p) {
 #pragma unroll
           for (int pt = 0; pt < NPT; ++pt)
 #pragma unroll
-            for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = mfma4(a[ct][s], b[pt][s], acc[pt][ct]);
+            for (int c = 0; c < NCT; ++c) acc[pt][c] = mfma4(a[c][s], b[pt][s], acc[pt][c]);
       }
       if (tap < 8) {
         char* wn = wbuf + ((tap + 1) & 1) * S::W_BYTES;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = tid + r * 256;
+        for (int r = 0; r < 1024 / NT; ++r) {
+          const int i = tid + r * NT;
           *reinterpret_cast<float4*>(wn + swz256(i >> 4, i & 15)) = nxt[r];
         }
       }
       __syncthreads();
     }
   }
-  epilogue_f32<NPT, EPI>(p, acc, n, cb, y0 + wave, x0, blockIdx.x, gridDim.x, reinterpret_cast<float*>(smem), fr, fk,
-                         wave, tid);
+  epilogue_f32<NPT, EPI, NCT>(p, acc, n, cb, y0 + row, x0, blockIdx.x, gridDim.x, reinterpret_cast<float*>(smem), fr,
+                              fk, row, ct0, tid);
 }
+
+#ifndef SRMI_F32_NW
+#define SRMI_F32_NW 8
+#endif
+constexpr int kF32NW = SRMI_F32_NW;  // waves per workgroup of the fp32 conv
 
 template <int TW, int EPI>
 int launch_f32(const ConvParams& p, hipStream_t st) {
   dim3 grid((p.H / kTH) * (p.W / TW), p.Cout / 64, p.N);
-  hipLaunchKernelGGL((conv3x3_f32_kernel<TW, EPI>), grid, dim3(256), CF32Smem<TW>::TOTAL, st, p);
+  hipLaunchKernelGGL((conv3x3_f32_kernel<TW, EPI, kF32NW>), grid, dim3(kF32NW * 64), CF32Smem<TW>::TOTAL, st, p);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
@@ -304,12 +318,18 @@ struct WgF32 {
   static constexpr int KSTEPS = DYPIX / 4;
 };
 
-template <int TW>
-__global__ void __launch_bounds__(256, 1) wgrad_f32_kernel(WgradParams p) {
+//
+// NW = 8 (two waves per SIMD): the 36 N tiles split 4 / 5 between waves WV and
+// WV + 4 (the same SIMD: 16 + 20 MFMAs per K-step, as one 4-wave wave's 36); the
+// DMA groups are dealt over all 8 waves.  The body is instantiated per wave (WV):
+// its N tiles are compile-time.
+template <int TW, int NW, int WV>
+__device__ __forceinline__ void wgrad_f32_body(const WgradParams& p, char* smem) {
   using S = WgF32<TW>;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  constexpr int NT = NW == 4 ? 9 : (WV < 4 ? 4 : 5);                       // N tiles of this wave
+  constexpr int J0 = NW == 4 ? 9 * WV : (WV < 4 ? 4 * WV : 16 + 5 * (WV - 4));  // its first N tile
+  const int tid = threadIdx.x, lane = tid & 63;
+  constexpr int wave = WV, wave_s = WV;
   const int chunk = blockIdx.x, cb = blockIdx.y;
   const int Hr = p.H / p.row_splits;
   const int n = chunk / p.row_splits, ybase = (chunk % p.row_splits) * Hr;
@@ -345,29 +365,29 @@ __global__ void __launch_bounds__(256, 1) wgrad_f32_kernel(WgradParams p) {
     }
     glds16(src, dst);
   };
-  constexpr int NGW = (S::NG + 3) / 4;  // groups per wave
+  constexpr int NGW = (S::NG + NW - 1) / NW;  // groups per wave
   auto dma_stage = [&](int st, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int m = 0; m < NGW; ++m) {
-      const int k = wave_s + 4 * m;
+      const int k = wave_s + NW * m;
       if (k < S::NG) dma_group(st, buf, k);
     }
   };
 
-  f32x4 acc[4][9];
+  f32x4 acc[4][NT];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bsum[4] = {0.f, 0.f, 0.f, 0.f};
 
   // lane-constant read offsets: A = dY[pixel k][co = 16 ct + (l & 15)],
   // B = X[pixel k + kx (row + ky)][ci = 16 it + (l & 15)] for the wave's 9 N tiles
   const int lk = lane >> 4, li = lane & 15;
-  int bky[9], bkx[9], bci[9];
+  int bky[NT], bkx[NT], bci[NT];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int j = 9 * wave + t, tap = j >> 2, it = j & 3;
+  for (int t = 0; t < NT; ++t) {
+    const int j = J0 + t, tap = j >> 2, it = j & 3;
     bky[t] = tap / 3;
     bkx[t] = tap % 3;
     bci[t] = it * 16 + li;
@@ -385,17 +405,17 @@ __global__ void __launch_bounds__(256, 1) wgrad_f32_kernel(WgradParams p) {
     for (int ks = 0; ks < S::KSTEPS; ++ks) {
       const int r = ks / (TW / 4), px = 4 * (ks % (TW / 4)) + lk;  // this lane's K pixel
       const int qa = r * TW + px;
-      float a[4], b[9];
+      float a[4], b[NT];
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) a[ct] = *reinterpret_cast<const float*>(sb + wofs(qa, ct * 16 + li));
 #pragma unroll
-      for (int t = 0; t < 9; ++t)
+      for (int t = 0; t < NT; ++t)
         b[t] = *reinterpret_cast<const float*>(sb + S::DYPIX * 256 + wofs((r + bky[t]) * S::XP + px + bkx[t], bci[t]));
 #pragma unroll
-      for (int t = 0; t < 9; ++t)
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma4(a[ct], b[t], acc[ct][t]);
-      if (wave == 0) {
+      if constexpr (wave == 0) {
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) bsum[ct] += a[ct];
       }
@@ -408,8 +428,8 @@ __global__ void __launch_bounds__(256, 1) wgrad_f32_kernel(WgradParams p) {
   // ci column l & 15 of N tile j
   float* slab = p.slab + (size_t)chunk * p.Cout * 576;
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int j = 9 * wave + t, tap = j >> 2, it = j & 3;
+  for (int t = 0; t < NT; ++t) {
+    const int j = J0 + t, tap = j >> 2, it = j & 3;
     const int ci = it * 16 + li;
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {
@@ -418,7 +438,7 @@ __global__ void __launch_bounds__(256, 1) wgrad_f32_kernel(WgradParams p) {
           make_float4(acc[ct][t][0], acc[ct][t][1], acc[ct][t][2], acc[ct][t][3]);
     }
   }
-  if (wave == 0) {
+  if constexpr (wave == 0) {
     // lanes l, l+16, l+32, l+48 hold partial sums of co 16 ct + (l & 15)
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {
@@ -427,6 +447,27 @@ __global__ void __launch_bounds__(256, 1) wgrad_f32_kernel(WgradParams p) {
       v += __shfl_xor(v, 32, 64);
       if (lane < 16) p.bslab[(size_t)chunk * p.Cout + cb * 64 + ct * 16 + lane] = v;
     }
+  }
+}
+
+template <int TW, int NW>
+__global__ void __launch_bounds__(NW * 64, 1) wgrad_f32_kernel(WgradParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+    case 0: wgrad_f32_body<TW, NW, 0>(p, smem); break;
+    case 1: wgrad_f32_body<TW, NW, 1>(p, smem); break;
+    case 2: wgrad_f32_body<TW, NW, 2>(p, smem); break;
+    case 3: wgrad_f32_body<TW, NW, 3>(p, smem); break;
+    default:
+      if constexpr (NW == 8) {
+        switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+          case 4: wgrad_f32_body<TW, NW, 4>(p, smem); break;
+          case 5: wgrad_f32_body<TW, NW, 5>(p, smem); break;
+          case 6: wgrad_f32_body<TW, NW, 6>(p, smem); break;
+          default: wgrad_f32_body<TW, NW, 7>(p, smem); break;
+        }
+      }
+      break;
   }
 }
 
@@ -452,9 +493,9 @@ int wgrad_f32_launch(const WgradParams& p, hipStream_t st) {
   if (p.dy_mode == IN_UNSHUF && p.Cout != 256) return SRMI_ERR_SHAPE;
   dim3 grid(p.N * p.row_splits, p.Cout / 64);
   if (p.W % 48 == 0) {
-    hipLaunchKernelGGL(wgrad_f32_kernel<48>, grid, dim3(256), 2 * WgF32<48>::STAGE, st, p);
+    hipLaunchKernelGGL((wgrad_f32_kernel<48, kF32NW>), grid, dim3(kF32NW * 64), 2 * WgF32<48>::STAGE, st, p);
   } else if (p.W % 32 == 0) {
-    hipLaunchKernelGGL(wgrad_f32_kernel<32>, grid, dim3(256), 2 * WgF32<32>::STAGE, st, p);
+    hipLaunchKernelGGL((wgrad_f32_kernel<32, kF32NW>), grid, dim3(kF32NW * 64), 2 * WgF32<32>::STAGE, st, p);
   } else {
     return SRMI_ERR_SHAPE;
   }
