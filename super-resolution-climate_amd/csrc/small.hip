@@ -262,34 +262,43 @@ __global__ void __launch_bounds__(256) tail_fwd_mfma_kernel(const bf16_t* __rest
   }
 }
 
-// Exact-fp32 form (fp32 engine mode) on the VALU: one output pixel per thread, 4 rows
-// x 64 px per workgroup; per 16-channel slice the 6 x 66 halo is staged channel-major
-// in LDS ([c][row][px]: a wave reads 64 consecutive floats), the filters [C][9][64] in
-// LDS (broadcast reads).  C <= 4 outputs per pixel: an MFMA form would waste 12 of its
-// 16 output rows at 1/16 of the bf16 rate.
+// Exact-fp32 form (fp32 engine mode) on the VALU (C <= 4 outputs per pixel: an MFMA
+// form would waste 12 of its 16 output rows at 1/16 of the bf16 rate).  Register-
+// blocked: a thread owns 4 consecutive pixels of one row, a workgroup 4 rows x 256 px.
+// Per 8-channel slice the 6 x 258 halo is staged channel-major in LDS; per (channel,
+// filter row) a thread reads its 6-pixel window with one ds_read_b128 + one b64 and the
+// 3 taps' filters for all C outputs as float4 broadcasts, then issues 4 px x 3 kx x 4 co
+// FMAs (the one-pixel-per-thread form read LDS once per 0.8 FMA: 1.27 ms at EDSR x8).
+constexpr int kTfTX = 256, kTfCS = 8, kTfWP = kTfTX + 4;  // px per row, channels per slice, LDS row pitch
 __global__ void __launch_bounds__(256) tail_fwd_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                            const float* __restrict__ b, int C, int H, int W,
                                                            float* __restrict__ y) {
-  constexpr int TX = 64, WP = TX + 2, CS = 16;
-  __shared__ float hs[CS][6][WP];
-  __shared__ float wl[4][9][64];
-  const int n = blockIdx.z, y0 = blockIdx.y * 4, x0 = blockIdx.x * TX, tid = threadIdx.x;
-  for (int i = tid; i < C * 576; i += 256) {
-    const int co = i / 576, ci = (i / 9) % 64, tap = i % 9;
-    wl[co][tap][ci] = w[i];
+  __shared__ __attribute__((aligned(16))) float hs[kTfCS][6][kTfWP];
+  __shared__ float4 wl[64][9];  // [ci][tap] -> co 0..3 (zero beyond C)
+  const int n = blockIdx.z, y0 = blockIdx.y * 4, x0 = blockIdx.x * kTfTX, tid = threadIdx.x;
+  for (int i = tid; i < 64 * 9; i += 256) {
+    const int ci = i / 9, tap = i % 9;
+    float v[4];
+#pragma unroll
+    for (int co = 0; co < 4; ++co) v[co] = co < C ? w[((size_t)co * 64 + ci) * 9 + tap] : 0.f;
+    wl[ci][tap] = make_float4(v[0], v[1], v[2], v[3]);
   }
-  const int r = tid / TX, px = tid % TX;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int cs = 0; cs < 64; cs += CS) {
+  const int r = tid >> 6, t = tid & 63;  // row r, pixels 4t .. 4t+3 of the block
+  float acc[4][4];                       // [co][px]
+#pragma unroll
+  for (int co = 0; co < 4; ++co)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[co][j] = 0.f;
+  for (int cs = 0; cs < 64; cs += kTfCS) {
     __syncthreads();
     {  // every load of the thread in flight at once (clamped, padding zeroed after)
-      constexpr int NI = 6 * WP * (CS / 4), NL = (NI + 255) / 256;
+      constexpr int NI = 6 * (kTfTX + 2) * (kTfCS / 4), NL = (NI + 255) / 256;
       float4 hv[NL];
 #pragma unroll
       for (int j = 0; j < NL; ++j) {
         const int i = min(tid + j * 256, NI - 1);
-        const int q = i / (CS / 4), c4 = i % (CS / 4);
-        const int hy = q / WP, hx = q % WP;
+        const int q = i / (kTfCS / 4), c4 = i % (kTfCS / 4);
+        const int hy = q / (kTfTX + 2), hx = q % (kTfTX + 2);
         const int yy = min(max(y0 - 1 + hy, 0), H - 1), xx = min(max(x0 - 1 + hx, 0), W - 1);
         hv[j] = *reinterpret_cast<const float4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + cs + c4 * 4);
       }
@@ -297,8 +306,8 @@ __global__ void __launch_bounds__(256) tail_fwd_f32_kernel(const float* __restri
       for (int j = 0; j < NL; ++j) {
         const int i = tid + j * 256;
         if (i < NI) {
-          const int q = i / (CS / 4), c4 = i % (CS / 4);
-          const int hy = q / WP, hx = q % WP;
+          const int q = i / (kTfCS / 4), c4 = i % (kTfCS / 4);
+          const int hy = q / (kTfTX + 2), hx = q % (kTfTX + 2);
           const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
           const float4 v = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? hv[j] : make_float4(0.f, 0.f, 0.f, 0.f);
           hs[c4 * 4 + 0][hy][hx] = v.x;
@@ -309,20 +318,38 @@ __global__ void __launch_bounds__(256) tail_fwd_f32_kernel(const float* __restri
       }
     }
     __syncthreads();
-#pragma unroll 4
-    for (int c = 0; c < CS; ++c)
+#pragma unroll 2
+    for (int c = 0; c < kTfCS; ++c)
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const float v = hs[c][r + tap / 3][px + tap % 3];
+      for (int ky = 0; ky < 3; ++ky) {
+        const float4 v0 = *reinterpret_cast<const float4*>(&hs[c][r + ky][4 * t]);
+        const float2 v1 = *reinterpret_cast<const float2*>(&hs[c][r + ky][4 * t + 4]);
+        const float xv[6] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y};
 #pragma unroll
-        for (int co = 0; co < 4; ++co)
-          if (co < C) acc[co] = fmaf(v, wl[co][tap][cs + c], acc[co]);
+        for (int kx = 0; kx < 3; ++kx) {
+          const float4 wv = wl[cs + c][ky * 3 + kx];
+          const float wc[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+          for (int co = 0; co < 4; ++co)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[co][j] = fmaf(xv[j + kx], wc[co], acc[co][j]);
+        }
       }
   }
-  if (x0 + px < W) {
+  const int xo = x0 + 4 * t;
 #pragma unroll
-    for (int co = 0; co < 4; ++co)
-      if (co < C) y[(((size_t)n * C + co) * H + y0 + r) * W + x0 + px] = acc[co] + b[co];
+  for (int co = 0; co < 4; ++co) {
+    if (co < C) {
+      const float bb = b[co];
+      float* dst = y + (((size_t)n * C + co) * H + y0 + r) * W + xo;
+      if (xo + 3 < W && (W & 3) == 0) {
+        *reinterpret_cast<float4*>(dst) = make_float4(acc[co][0] + bb, acc[co][1] + bb, acc[co][2] + bb, acc[co][3] + bb);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (xo + j < W) dst[j] = acc[co][j] + bb;
+      }
+    }
   }
 }
 
@@ -330,7 +357,7 @@ int tail_fwd_launch(const void* xv, const float* w, const float* b, int N, int C
                     hipStream_t st) {
   if (C < 1 || C > 4 || H % 4) return SRMI_ERR_SHAPE;
   if (f32) {
-    hipLaunchKernelGGL(tail_fwd_f32_kernel, dim3((W + 63) / 64, H / 4, N), dim3(256), 0, st,
+    hipLaunchKernelGGL(tail_fwd_f32_kernel, dim3((W + kTfTX - 1) / kTfTX, H / 4, N), dim3(256), 0, st,
                        static_cast<const float*>(xv), w, b, C, H, W, y);
     SRMI_CHECK_LAUNCH();
     return 0;
