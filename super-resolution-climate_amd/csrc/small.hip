@@ -416,34 +416,55 @@ __global__ void __launch_bounds__(256) tail_dgrad_kernel(const float* __restrict
     wl[i] = w[((size_t)c * 64 + ci) * 9 + t];
   }
   __syncthreads();
+  // a thread: 8 input channels (ck) of 4 consecutive pixels of one row; per (c, ky)
+  // the 6-pixel dy window is read once and each tap's 8 filters once (96 FMAs per 8
+  // LDS reads; one pixel per thread read 3 per 8 FMAs)
   const int ck = tid & 7;
   const auto rdx = wt_rsrc(dx, (uint32_t)((size_t)gridDim.z * H * W * 64 * sizeof(T)));
-  for (int px = tid >> 3; px < 4 * TWT; px += 32) {
-    const int r = px / TWT, xx = px - r * TWT;
-    float acc[8];
+  constexpr int QPR = TWT / 4;  // 4-pixel groups per row
+  for (int pg = tid >> 3; pg < 4 * QPR; pg += 32) {
+    const int r = pg / QPR, xq = 4 * (pg - r * QPR);
+    float acc[4][8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[j][e] = 0.f;
     for (int c = 0; c < C; ++c) {
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int ky = t / 3, kx = t % 3;
-        const float d = dyl[(c * 6 + r + 2 - ky) * WP + xx + 2 - kx];
-        const float4 w0 = *reinterpret_cast<const float4*>(wl + (c * 9 + t) * 64 + ck * 8);
-        const float4 w1 = *reinterpret_cast<const float4*>(wl + (c * 9 + t) * 64 + ck * 8 + 4);
-        acc[0] += d * w0.x; acc[1] += d * w0.y; acc[2] += d * w0.z; acc[3] += d * w0.w;
-        acc[4] += d * w1.x; acc[5] += d * w1.y; acc[6] += d * w1.z; acc[7] += d * w1.w;
+      for (int ky = 0; ky < 3; ++ky) {
+        // output px xq + j, tap (ky, kx) reads dy at column xq + j + 2 - kx (halo-relative)
+        const float* drow = dyl + (c * 6 + r + 2 - ky) * WP + xq;
+        float dv[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) dv[i] = drow[i];
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int t = ky * 3 + kx;
+          const float4 w0 = *reinterpret_cast<const float4*>(wl + (c * 9 + t) * 64 + ck * 8);
+          const float4 w1 = *reinterpret_cast<const float4*>(wl + (c * 9 + t) * 64 + ck * 8 + 4);
+          const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float d = dv[j + 2 - kx];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[j][e] += d * wv[e];
+          }
+        }
       }
     }
-    const size_t e = (((size_t)n * H + y0 + r) * W + x0 + xx) * 64 + ck * 8;
-    if constexpr (sizeof(T) == 2) {
-      uint4 o;
-      o.x = pack2(acc[0], acc[1]); o.y = pack2(acc[2], acc[3]);
-      o.z = pack2(acc[4], acc[5]); o.w = pack2(acc[6], acc[7]);
-      // 8 lanes per pixel: 128-byte lines, written through (common.hpp)
-      st_wt16(rdx, dx, (uint32_t)(e * 2), o);
-    } else {
-      st_wt16(rdx, dx, (uint32_t)(e * 4), make_float4(acc[0], acc[1], acc[2], acc[3]));
-      st_wt16(rdx, dx, (uint32_t)(e * 4 + 16), make_float4(acc[4], acc[5], acc[6], acc[7]));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const size_t e = (((size_t)n * H + y0 + r) * W + x0 + xq + j) * 64 + ck * 8;
+      if constexpr (sizeof(T) == 2) {
+        uint4 o;
+        o.x = pack2(acc[j][0], acc[j][1]); o.y = pack2(acc[j][2], acc[j][3]);
+        o.z = pack2(acc[j][4], acc[j][5]); o.w = pack2(acc[j][6], acc[j][7]);
+        // 8 lanes per pixel: 128-byte lines, written through (common.hpp)
+        st_wt16(rdx, dx, (uint32_t)(e * 2), o);
+      } else {
+        st_wt16(rdx, dx, (uint32_t)(e * 4), make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]));
+        st_wt16(rdx, dx, (uint32_t)(e * 4 + 16), make_float4(acc[j][4], acc[j][5], acc[j][6], acc[j][7]));
+      }
     }
   }
 }
