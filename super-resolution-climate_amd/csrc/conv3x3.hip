@@ -42,11 +42,18 @@ struct ConvSmem {
 // to zero afterwards): a load-wait-store loop serialised one memory latency per
 // 16-byte chunk
 template <int NPIX>
-__device__ __forceinline__ void load_halo_chunk(char* halo, const bf16_t* __restrict__ x, int mode, int n, int H,
-                                                int W, int Cin, int cc, int y0, int x0, int TWp2) {
+struct HaloRegs {
+  static constexpr int NCH = NPIX * 8, NL = (NCH + kThreads - 1) / kThreads;
+  uint4 v[NL];
+};
+
+// issue: every 16-B chunk of this thread's share of the chunk-cc halo into registers
+template <int NPIX>
+__device__ __forceinline__ void halo_issue(HaloRegs<NPIX>& hr, const bf16_t* __restrict__ x, int mode, int n, int H,
+                                           int W, int Cin, int cc, int y0, int x0, int TWp2) {
   const int tid = threadIdx.x;
-  constexpr int NCH = NPIX * 8, NL = (NCH + kThreads - 1) / kThreads;
-  uint4 hv[NL];
+  constexpr int NCH = HaloRegs<NPIX>::NCH, NL = HaloRegs<NPIX>::NL;
+  uint4* hv = hr.v;
 #pragma unroll
   for (int j = 0; j < NL; ++j) {
     const int i = min(tid + j * kThreads, NCH - 1);
@@ -59,6 +66,22 @@ __device__ __forceinline__ void load_halo_chunk(char* halo, const bf16_t* __rest
                             : x + ((size_t)((size_t)n * 2 * H + 2 * y + (cc >> 1)) * (2 * W) + 2 * xx + (cc & 1)) * 64 + c * 8;
     hv[j] = *reinterpret_cast<const uint4*>(src);
   }
+}
+
+// workgroup barrier ordering LDS only (__syncthreads' release fence drains vmcnt,
+// which would wait for the prefetched slices and halo)
+__device__ __forceinline__ void lds_only_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// commit: the registers into the swizzled LDS halo, padding zeroed
+template <int NPIX>
+__device__ __forceinline__ void halo_commit(char* halo, const HaloRegs<NPIX>& hr, int H, int W, int y0, int x0,
+                                            int TWp2) {
+  const int tid = threadIdx.x;
+  constexpr int NCH = HaloRegs<NPIX>::NCH, NL = HaloRegs<NPIX>::NL;
+  const uint4* hv = hr.v;
 #pragma unroll
   for (int j = 0; j < NL; ++j) {
     const int i = tid + j * kThreads;
@@ -221,58 +244,83 @@ __global__ void __launch_bounds__(kThreads, 2) conv3x3_kernel(ConvParams p) {
   const int fr = lane & 15;   // A row (co within tile) / B column (pixel within tile)
   const int fk = lane >> 4;   // 8-wide k group
 
-  for (int cc = 0; cc < nchunks; ++cc) {
-    if (cc) __syncthreads();
-    load_halo_chunk<S::HALO_PIX>(halo, p.x, p.in_mode, n, p.H, p.W, p.Cin, cc, y0, x0, TW + 2);
-    // tap 0 filter slice
-    {
-      const bf16_t* ws = wsrc + ((size_t)(cc * 9 + 0) * p.Cout + cb * 64) * 64;
+  // The K dimension as one stream of nchunks*9 filter slices s = (cc, tap), each
+  // [64 co][64 ci] = 8 KiB.  A slice's global load is issued three slices before
+  // its use (register ring of 3, stored to the LDS double buffer one slice
+  // ahead), and the next chunk's halo is loaded into registers while the current
+  // chunk's nine taps run: a slice's compute (24 MFMAs per wave) is far shorter
+  // than one global latency, so loading one slice ahead left every tap waiting.
+  const int nslices = nchunks * 9;
+  auto slice_src = [&](int s) {
+    return wsrc + ((size_t)s * p.Cout + cb * 64) * 64;  // (cc*9 + tap) slices are consecutive
+  };
+  auto slice_issue = [&](uint4& r0, uint4& r1, int s) {
+    const bf16_t* ws = slice_src(min(s, nslices - 1));  // clamped, unconditional
+    r0 = *reinterpret_cast<const uint4*>(ws + (tid >> 3) * 64 + (tid & 7) * 8);
+    r1 = *reinterpret_cast<const uint4*>(ws + ((tid + kThreads) >> 3) * 64 + (tid & 7) * 8);
+  };
+  auto slice_commit = [&](const uint4& r0, const uint4& r1, int buf) {
+    char* wn = wbuf + buf * S::W_BYTES;
+    *reinterpret_cast<uint4*>(wn + swz128(tid >> 3, tid & 7)) = r0;
+    *reinterpret_cast<uint4*>(wn + swz128((tid + kThreads) >> 3, tid & 7)) = r1;
+  };
+
+  // register ring of three slices (named, so that it stays in registers)
+  HaloRegs<S::HALO_PIX> hr;
+  uint4 ra0, ra1, rb0, rb1, rc0, rc1;
+  halo_issue<S::HALO_PIX>(hr, p.x, p.in_mode, n, p.H, p.W, p.Cin, 0, y0, x0, TW + 2);
+  slice_issue(ra0, ra1, 0);
+  slice_issue(rb0, rb1, 1);
+  slice_issue(rc0, rc1, 2);
+  halo_commit<S::HALO_PIX>(halo, hr, p.H, p.W, y0, x0, TW + 2);
+  slice_commit(ra0, ra1, 0);
+  lds_only_barrier();
+
+  // one slice: reload slot (q0, q1) (slice s, committed at the end of slice s - 1)
+  // with s + 3, run the 24 MFMAs, commit slot (n0, n1) = slice s + 1
+  auto step = [&](const int cc, const int tap, uint4& q0, uint4& q1, const uint4& n0, const uint4& n1) {
+    const int s = cc * 9 + tap;
+    slice_issue(q0, q1, s + 3);
+    const char* wb = wbuf + (s & 1) * S::W_BYTES;
+    const int ky = tap / 3, kx = tap - ky * 3;
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        const int i = tid + r * kThreads;
-        const int row = i >> 3, c = i & 7;
-        *reinterpret_cast<uint4*>(wbuf + swz128(row, c)) =
-            *reinterpret_cast<const uint4*>(ws + row * 64 + c * 8);
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + fk;
+      bf16x8 a[4];
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) a[ct] = lds_frag(wb, swz128(ct * 16 + fr, chunk));
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt) {
+        const int q = (wave + ky) * (TW + 2) + pt * 16 + fr + kx;
+        const bf16x8 b = lds_frag(halo, swz128(q, chunk));
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = mfma16(a[ct], b, acc[pt][ct]);
       }
     }
-    __syncthreads();
+    if (s + 1 < nslices) {
+      // buffer (s+1)&1 was last read by slice s-1, behind the previous barrier
+      slice_commit(n0, n1, (s + 1) & 1);
+      if (tap == 8) {  // the next chunk's halo, issued before the barrier that frees the LDS halo
+        halo_issue<S::HALO_PIX>(hr, p.x, p.in_mode, n, p.H, p.W, p.Cin, cc + 1, y0, x0, TW + 2);
+        lds_only_barrier();
+        halo_commit<S::HALO_PIX>(halo, hr, p.H, p.W, y0, x0, TW + 2);
+      }
+    }
+    // LDS-only barrier: the prefetched slices and halo stay in flight across it
+    lds_only_barrier();
+  };
+
 #pragma unroll 1
-    for (int tap = 0; tap < 9; ++tap) {
-      uint4 nxt[2];
-      if (tap < 8) {
-        const bf16_t* ws = wsrc + ((size_t)(cc * 9 + tap + 1) * p.Cout + cb * 64) * 64;
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-          const int i = tid + r * kThreads;
-          nxt[r] = *reinterpret_cast<const uint4*>(ws + (i >> 3) * 64 + (i & 7) * 8);
-        }
-      }
-      const char* wb = wbuf + (tap & 1) * S::W_BYTES;
-      const int ky = tap / 3, kx = tap - ky * 3;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int chunk = kk * 4 + fk;
-        bf16x8 a[4];
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) a[ct] = lds_frag(wb, swz128(ct * 16 + fr, chunk));
-#pragma unroll
-        for (int pt = 0; pt < NPT; ++pt) {
-          const int q = (wave + ky) * (TW + 2) + pt * 16 + fr + kx;
-          const bf16x8 b = lds_frag(halo, swz128(q, chunk));
-#pragma unroll
-          for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = mfma16(a[ct], b, acc[pt][ct]);
-        }
-      }
-      if (tap < 8) {
-        char* wn = wbuf + ((tap + 1) & 1) * S::W_BYTES;
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-          const int i = tid + r * kThreads;
-          *reinterpret_cast<uint4*>(wn + swz128(i >> 3, i & 7)) = nxt[r];
-        }
-      }
-      __syncthreads();
-    }
+  for (int cc = 0; cc < nchunks; ++cc) {
+    step(cc, 0, ra0, ra1, rb0, rb1);
+    step(cc, 1, rb0, rb1, rc0, rc1);
+    step(cc, 2, rc0, rc1, ra0, ra1);
+    step(cc, 3, ra0, ra1, rb0, rb1);
+    step(cc, 4, rb0, rb1, rc0, rc1);
+    step(cc, 5, rc0, rc1, ra0, ra1);
+    step(cc, 6, ra0, ra1, rb0, rb1);
+    step(cc, 7, rb0, rb1, rc0, rc1);
+    step(cc, 8, rc0, rc1, ra0, ra1);
   }
 
   // ------------------------------------------------------------------ epilogue

@@ -1446,6 +1446,7 @@ __global__ void pack_one_kernel(const float* __restrict__ W, const float* __rest
 int pack_one_launch(const float* w, const float* b, int Cout, int Cin, int ps, void* fpack, void* dpack,
                     float* pbias, int f32, hipStream_t st) {
   if (Cout % 64 || Cin % 64) return SRMI_ERR_SHAPE;
+  if (ps && Cout != 256) return SRMI_ERR_SHAPE;  // the PixelShuffle(2) permutation spans 4 x 64 channels
   long long bx = ((long long)Cout * Cin * 9 + 255) / 256;
   if (bx > 1024) bx = 1024;
   if (f32)

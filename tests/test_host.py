@@ -217,6 +217,10 @@ def test_conv_abi_rejects_missing_operands():
     # an unknown dtype is refused too
     args = [dummy, dummy, dummy, 1, 4, 48, 64, 64, 0, 0, dummy, None, None, None, None, None, None, 1.0, 7, None]
     assert lib.srmi_conv3x3(*args) == -10001
+    # a PixelShuffle pack needs Cout = 256 (its channel permutation spans 4 x 64 outputs):
+    # Cout/Cin swapped is refused (SRMI_ERR_SHAPE) instead of reading past the filter
+    for dtype in (0, 1):
+        assert lib.srmi_pack_conv(dummy, dummy, 64, 256, 1, dummy, dummy, dummy, dtype, None) == -10002
 
 
 def _force_dp_rank(port, q):
