@@ -188,6 +188,11 @@ int head_wgrad_reduce_launch(const float* slab, int nslab, int C, float* gw, flo
 }
 
 // =========================================================================== tail
+// workgroup barrier ordering LDS only: prefetched global loads stay in flight
+__device__ __forceinline__ void tail_fwd_lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
 // y[n][c][yy][xx] = b[c] + sum_{tap,ci} x[n][yy+ky-1][xx+kx-1][ci] * w[c][ci][tap]
 // As an MFMA implicit GEMM with A = filters (16 output-channel
 // rows, only the C < 16 real ones ever written or stored), B = halo pixels,
@@ -195,19 +200,26 @@ int head_wgrad_reduce_launch(const float* slab, int nslab, int C, float* gw, flo
 // pixels (wave w = row w), halo and bf16 filters staged in LDS with the conv
 // kernels' chunk swizzle.  The VALU form above spent ~1 K FMAs per pixel with
 // per-FMA weight loads; this one is bound by reading the 64-channel input once.
+//
+// Persistent: a workgroup converts the filters once and walks strips s = blockIdx.x,
+// + gridDim.x, ...; the next strip's halo is loaded into registers while the current
+// strip's MFMAs and stores run and committed to LDS behind LDS-only barriers (one
+// strip per workgroup waited one memory latency per 24 KiB of output work).
 template <int TW>
 __global__ void __launch_bounds__(256) tail_fwd_mfma_kernel(const bf16_t* __restrict__ x, const float* __restrict__ w,
-                                                            const float* __restrict__ b, int C, int H, int W,
+                                                            const float* __restrict__ b, int C, int H, int W, int N,
                                                             float* __restrict__ y) {
   constexpr int NPT = TW / 16, WP = TW + 2, HALO = 6 * WP;
+  constexpr int NL = (HALO * 8 + 255) / 256;
   extern __shared__ __attribute__((aligned(16))) char tsm[];
   char* halo = tsm;               // [6][WP] px x 128 B
   char* wl = tsm + HALO * 128;    // [9 taps][16 co rows] x 128 B
-  const int n = blockIdx.z, y0 = blockIdx.y * 4, x0 = blockIdx.x * TW, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, fr = lane & 15, fk = lane >> 4;
-  {  // halo: every load of the thread in flight at once (clamped, padding zeroed after)
-    constexpr int NL = (HALO * 8 + 255) / 256;
-    uint4 hv[NL];
+  const int sx = W / TW, sy = H / 4, nstrips = sx * sy * N;
+  uint4 hv[NL];
+  auto issue = [&](int st) {  // every load of the thread in flight at once (clamped)
+    const int n = st / (sx * sy), rem = st - n * sx * sy, y0 = (rem / sx) * 4, x0 = (rem % sx) * TW;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int i = min(tid + j * 256, HALO * 8 - 1);
@@ -216,8 +228,24 @@ __global__ void __launch_bounds__(256) tail_fwd_mfma_kernel(const bf16_t* __rest
       const int yy = min(max(y0 - 1 + hy, 0), H - 1), xx = min(max(x0 - 1 + hx, 0), W - 1);
       hv[j] = *reinterpret_cast<const uint4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + c * 8);
     }
+  };
+  int s = blockIdx.x;
+  if (s >= nstrips) return;
+  issue(s);
+  // filters w[co][ci][tap] (fp32, torch layout) -> bf16 rows co < C of [tap][co][ci];
+  // rows >= C stay unwritten: they only feed output rows that are never stored
+  for (int i = tid; i < C * 576; i += 256) {
+    const int co = i / 576, ci = (i / 9) % 64, tap = i % 9;
+    *reinterpret_cast<bf16_t*>(wl + tap * 2048 + swz128(co, ci >> 3) + (ci & 7) * 2) = f2bf(w[i]);
+  }
+  float bias[4];
 #pragma unroll
-    for (int j = 0; j < NL; ++j) {
+  for (int i = 0; i < 4; ++i) bias[i] = i < C ? b[i] : 0.f;
+  for (; s < nstrips; s += gridDim.x) {
+    const int n = s / (sx * sy), rem = s - n * sx * sy, y0 = (rem / sx) * 4, x0 = (rem % sx) * TW;
+    tail_fwd_lds_barrier();  // the previous strip's halo readers are done
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {  // commit (padding zeroed)
       const int i = tid + j * 256;
       if (i < HALO * 8) {
         const int q = i >> 3, c = i & 7;
@@ -227,38 +255,32 @@ __global__ void __launch_bounds__(256) tail_fwd_mfma_kernel(const bf16_t* __rest
         *reinterpret_cast<uint4*>(halo + swz128(q, c)) = ok ? hv[j] : make_uint4(0, 0, 0, 0);
       }
     }
-  }
-  // filters w[co][ci][tap] (fp32, torch layout) -> bf16 rows co < C of [tap][co][ci];
-  // rows >= C stay unwritten: they only feed output rows that are never stored
-  for (int i = tid; i < C * 576; i += 256) {
-    const int co = i / 576, ci = (i / 9) % 64, tap = i % 9;
-    *reinterpret_cast<bf16_t*>(wl + tap * 2048 + swz128(co, ci >> 3) + (ci & 7) * 2) = f2bf(w[i]);
-  }
-  __syncthreads();
-  f32x4 acc[NPT];
+    tail_fwd_lds_barrier();
+    if (s + (int)gridDim.x < nstrips) issue(s + gridDim.x);
+    f32x4 acc[NPT];
 #pragma unroll
-  for (int pt = 0; pt < NPT; ++pt) acc[pt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int pt = 0; pt < NPT; ++pt) acc[pt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int tap = 0; tap < 9; ++tap) {
-    const int ky = tap / 3, kx = tap % 3;
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap % 3;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 a = lds_frag(wl, tap * 2048 + swz128(fr, kk * 4 + fk));
-#pragma unroll
-      for (int pt = 0; pt < NPT; ++pt)
-        acc[pt] = mfma16(a, lds_frag(halo, swz128((wave + ky) * WP + pt * 16 + fr + kx, kk * 4 + fk)), acc[pt]);
-    }
-  }
-  // lane (fr, fk) holds output channels 4 fk + i of pixel pt * 16 + fr
-  if (fk == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (i < C) {
-        const float bb = b[i];
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 a = lds_frag(wl, tap * 2048 + swz128(fr, kk * 4 + fk));
 #pragma unroll
         for (int pt = 0; pt < NPT; ++pt)
-          y[(((size_t)n * C + i) * H + y0 + wave) * W + x0 + pt * 16 + fr] = acc[pt][i] + bb;
+          acc[pt] = mfma16(a, lds_frag(halo, swz128((wave + ky) * WP + pt * 16 + fr + kx, kk * 4 + fk)), acc[pt]);
       }
+    }
+    // lane (fr, fk) holds output channels 4 fk + i of pixel pt * 16 + fr
+    if (fk == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (i < C) {
+#pragma unroll
+          for (int pt = 0; pt < NPT; ++pt)
+            y[(((size_t)n * C + i) * H + y0 + wave) * W + x0 + pt * 16 + fr] = acc[pt][i] + bias[i];
+        }
+    }
   }
 }
 
@@ -353,6 +375,11 @@ __global__ void __launch_bounds__(256) tail_fwd_f32_kernel(const float* __restri
   }
 }
 
+#ifndef SRMI_TAIL_FWD_BLOCKS
+#define SRMI_TAIL_FWD_BLOCKS 512
+#endif
+constexpr int kTailFwdBlocks = SRMI_TAIL_FWD_BLOCKS;
+
 int tail_fwd_launch(const void* xv, const float* w, const float* b, int N, int C, int H, int W, float* y, int f32,
                     hipStream_t st) {
   if (C < 1 || C > 4 || H % 4) return SRMI_ERR_SHAPE;
@@ -363,12 +390,15 @@ int tail_fwd_launch(const void* xv, const float* w, const float* b, int N, int C
     return 0;
   }
   const bf16_t* x = static_cast<const bf16_t*>(xv);
+  // persistent grid: two workgroups per CU (the LDS image + filters take 57 KiB)
   if (W % 48 == 0) {
-    hipLaunchKernelGGL(tail_fwd_mfma_kernel<48>, dim3(W / 48, H / 4, N), dim3(256), 6 * 50 * 128 + 9 * 2048, st, x,
-                       w, b, C, H, W, y);
+    const int ns = (W / 48) * (H / 4) * N;
+    hipLaunchKernelGGL(tail_fwd_mfma_kernel<48>, dim3(std::min(ns, kTailFwdBlocks)), dim3(256),
+                       6 * 50 * 128 + 9 * 2048, st, x, w, b, C, H, W, N, y);
   } else if (W % 32 == 0) {
-    hipLaunchKernelGGL(tail_fwd_mfma_kernel<32>, dim3(W / 32, H / 4, N), dim3(256), 6 * 34 * 128 + 9 * 2048, st, x,
-                       w, b, C, H, W, y);
+    const int ns = (W / 32) * (H / 4) * N;
+    hipLaunchKernelGGL(tail_fwd_mfma_kernel<32>, dim3(std::min(ns, kTailFwdBlocks)), dim3(256),
+                       6 * 34 * 128 + 9 * 2048, st, x, w, b, C, H, W, N, y);
   } else {
     return SRMI_ERR_SHAPE;
   }
@@ -1376,6 +1406,21 @@ __device__ __forceinline__ void pack_elem(const float* __restrict__ W, const flo
 // element type, then both packs are written as full 128-byte rows (forward: 64 ci
 // of one (tap, cop); dgrad: 64 co of one (tap, ci)).  The element-wise form read W
 // with a 36 B (forward) / 2.3 KB (dgrad) lane stride: 262 us per step.
+// 8 consecutive pack elements (16-byte aligned: seg * 8 elements into a 64-element row)
+// as one 16-byte store (bf16) or two (fp32) instead of 8 element stores
+template <typename T>
+__device__ __forceinline__ void store8(T* d, const T (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = (uint32_t)v[2 * k] | ((uint32_t)v[2 * k + 1] << 16);
+    *reinterpret_cast<uint4*>(d) = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) pack_tile_kernel(const float* __restrict__ params,
                                                         const PackEntry* __restrict__ ents, T* __restrict__ packs,
@@ -1388,12 +1433,26 @@ __global__ void __launch_bounds__(256) pack_tile_kernel(const float* __restrict_
   const int Cout = e.Cout, Cin = e.Cin, tid = threadIdx.x;
   const float* W = params + e.w_off;
   auto cot_of = [&](int cop) { return e.ps ? 4 * (cop & 63) + (cop >> 6) : cop; };
-  // 1. 64 rows x 576 floats (144 float4 each)
-  for (int i = tid; i < 64 * 144; i += 256) {
-    const int l = i / 144, q = i - l * 144;
-    const float4 v = *reinterpret_cast<const float4*>(W + ((size_t)cot_of(cb * 64 + l) * Cin + cc * 64) * 9 + q * 4);
-    T* d = wl + l * 576 + q * 4;
-    d[0] = from_f32<T>(v.x); d[1] = from_f32<T>(v.y); d[2] = from_f32<T>(v.z); d[3] = from_f32<T>(v.w);
+  // 1. 64 rows x 576 floats (144 float4 each = 36 per thread), in batches of 12 loads
+  //    in flight (a load-then-store loop waited one memory latency per float4: 88 us)
+  static_assert(64 * 144 == 36 * 256, "36 float4 per thread");
+#pragma unroll
+  for (int b0 = 0; b0 < 36; b0 += 12) {
+    float4 v[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      const int i = tid + (b0 + j) * 256, l = i / 144, q = i - l * 144;
+      v[j] = *reinterpret_cast<const float4*>(W + ((size_t)cot_of(cb * 64 + l) * Cin + cc * 64) * 9 + q * 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      const int i = tid + (b0 + j) * 256, l = i / 144, q = i - l * 144;
+      T* d = wl + l * 576 + q * 4;
+      if constexpr (sizeof(T) == 2)  // one ds_write_b64 (a bf16 element at a time: four ds_write_b16)
+        *reinterpret_cast<uint2*>(d) = make_uint2(pack2(v[j].x, v[j].y), pack2(v[j].z, v[j].w));
+      else
+        *reinterpret_cast<float4*>(d) = v[j];
+    }
   }
   __syncthreads();
   // 2. forward pack rows (tap, cop): [cc][tap][cop][ci_l]; 8 lanes per row, 8 ci each
@@ -1403,9 +1462,7 @@ __global__ void __launch_bounds__(256) pack_tile_kernel(const float* __restrict_
     T v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = wl[l * 576 + (seg * 8 + k) * 9 + tap];
-    T* d = fp + (((size_t)cc * 9 + tap) * Cout + cb * 64 + l) * 64 + seg * 8;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) d[k] = v[k];
+    store8(fp + (((size_t)cc * 9 + tap) * Cout + cb * 64 + l) * 64 + seg * 8, v);
   }
   // 3. dgrad pack rows (tapd, ci): [cb][tapd][ci][co_l] = W[cot][ci][8 - tapd]
   T* dp = packs + e.d_off;
@@ -1414,9 +1471,7 @@ __global__ void __launch_bounds__(256) pack_tile_kernel(const float* __restrict_
     T v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = wl[(seg * 8 + k) * 576 + ci_l * 9 + (8 - tapd)];
-    T* d = dp + (((size_t)cb * 9 + tapd) * Cin + cc * 64 + ci_l) * 64 + seg * 8;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) d[k] = v[k];
+    store8(dp + (((size_t)cb * 9 + tapd) * Cin + cc * 64 + ci_l) * 64 + seg * 8, v);
   }
   if (cc == 0 && tid < 64) pbias[e.pb_off + cb * 64 + tid] = params[e.b_off + cot_of(cb * 64 + tid)];
 }

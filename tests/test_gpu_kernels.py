@@ -178,6 +178,26 @@ def test_conv_dgrad_unshuffle(N, H, W, dt):
     assert rel_l2(out.float(), ref) < TOL[dt]
 
 
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 48, 48, 128, 128), (1, 8, 96, 192, 64), (2, 8, 32, 128, 64),
+                                             (3, 12, 48, 256, 128)])
+def test_conv_generic_multichunk(N, H, W, Cin, Cout):
+    """The generic conv (Cin > 64, plain input): the K stream of Cin/64 chunks x 9
+    filter slices with its three-slice register prefetch and the chunk-boundary
+    halo reload, at 2, 3 and 4 chunks and one or two output-channel blocks."""
+    d = dev()
+    g = torch.Generator(device="cpu").manual_seed(9)
+    x = bf(torch.randn(N, H, W, Cin, generator=g)).to(d)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.04).to(d)
+    b = (torch.randn(Cout, generator=g) * 0.1).to(d)
+    fp, dp, pb = pack(w, b)
+    ref = nhwc(Fn.conv2d(nchw(x).double().cpu(), wref(w, "bf16"), b.double().cpu(), padding=1))
+    y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=d)
+    conv(x, fp, pb, N, H, W, Cin, Cout, 6, yb=y)
+    assert rel_l2(y.float(), ref) < TOL["bf16"]
+    conv(x, fp, pb, N, H, W, Cin, Cout, 0, yb=y)
+    assert rel_l2(y.float(), ref.clamp_min(0)) < TOL["bf16"]
+
+
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("N,H,W,rs", [(2, 48, 48, 0), (2, 48, 48, 1), (1, 8, 96, 0), (1, 4, 32, 0), (3, 12, 64, 3),
                                        (64, 48, 48, 0), (4, 96, 96, 0), (3, 12, 48, 3), (2, 48, 48, 12), (1, 8, 48, 2),
@@ -331,11 +351,13 @@ def test_adam_matches_reference():
 
 
 @pytest.mark.parametrize("dt", DTS)
-@pytest.mark.parametrize("C,H,W", [(1, 8, 192), (2, 12, 192), (4, 8, 256), (3, 4, 96)])
+@pytest.mark.parametrize("C,H,W", [(1, 8, 192), (2, 12, 192), (4, 8, 256), (3, 4, 96), (2, 192, 288), (3, 192, 256)])
 def test_tail_forward(C, H, W, dt):
     """Tail conv 64 -> C (network.py:16 / EDSR tail) through srmi_tail_forward: bf16 =
     MFMA implicit GEMM with bf16 operands (and bf16 filters) vs an fp64 conv of the
-    same bf16 input; fp32 = the exact fp32 form."""
+    same bf16 input; fp32 = the exact fp32 form.  The two large shapes have more
+    strips (576, 768) than the persistent bf16 grid has workgroups (512), so each
+    workgroup walks several strips with the next strip's halo prefetched."""
     d = dev()
     g = torch.Generator(device="cpu").manual_seed(12)
     N = 2
