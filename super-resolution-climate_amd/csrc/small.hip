@@ -20,27 +20,32 @@ namespace srmi {
 
 // =========================================================================== head
 // x0[n][y][x][co] = b[co] + sum_{c,tap} lr[n][c][y+ky-1][x+kx-1] * w[co][c][tap]
+// One workgroup per (image, row): lane = co, the 4 waves split the row's pixels.
+// (Four rows per workgroup gave 384 workgroups at C2 -- 1.5 waves per SIMD for a
+// store-bound pass: 31 us for 28 MB.)
+constexpr int kHeadFwdRows = 1;
 template <typename T>
 __global__ void __launch_bounds__(256) head_fwd_kernel(const float* __restrict__ lr, const float* __restrict__ w,
                                                        const float* __restrict__ b, int C, int H, int W,
                                                        float* __restrict__ x0f, T* __restrict__ x0b) {
-  extern __shared__ float hs[];  // [C][6][W+2] halo, then [64][9C] weights
-  const int n = blockIdx.y, y0 = blockIdx.x * 4, tid = threadIdx.x;
+  constexpr int RB = kHeadFwdRows, HR = RB + 2;
+  extern __shared__ float hs[];  // [C][HR][W+2] halo
+  const int n = blockIdx.y, y0 = blockIdx.x * RB, tid = threadIdx.x;
   const int Wp = W + 2;
   float* halo = hs;
-  const int hsz = C * 6 * Wp;
+  const int hsz = C * HR * Wp;
   for (int i = tid; i < hsz; i += 256) {
-    const int c = i / (6 * Wp), r = (i / Wp) % 6, xx = i % Wp;
+    const int c = i / (HR * Wp), r = (i / Wp) % HR, xx = i % Wp;
     const int y = y0 - 1 + r, x = xx - 1;
     halo[i] = (y >= 0 && y < H && x >= 0 && x < W) ? lr[(((size_t)n * C + c) * H + y) * W + x] : 0.f;
   }
-  __syncthreads();
   const int co = tid & 63, grp = tid >> 6;
   float wr[36];
 #pragma unroll
   for (int k = 0; k < 36; ++k) wr[k] = (k < 9 * C) ? w[co * 9 * C + k] : 0.f;
   const float bb = b[co];
-  for (int px = grp; px < 4 * W; px += 4) {
+  __syncthreads();
+  for (int px = grp; px < RB * W; px += 4) {
     const int r = px / W, x = px - r * W;
     float s = bb;
 #pragma unroll
@@ -48,7 +53,7 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const float* __restrict__
       if (c < C) {
 #pragma unroll
         for (int t = 0; t < 9; ++t)
-          s += halo[(c * 6 + r + t / 3) * Wp + x + t % 3] * wr[c * 9 + t];
+          s += halo[(c * HR + r + t / 3) * Wp + x + t % 3] * wr[c * 9 + t];
       }
     }
     const size_t o = (((size_t)n * H + y0 + r) * W + x) * 64 + co;
@@ -60,12 +65,13 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const float* __restrict__
 int head_fwd_launch(const float* lr, const float* w, const float* b, int N, int C, int H, int W, float* x0f,
                     void* x0b, int f32, hipStream_t st) {
   if (C < 1 || C > 4 || H % 4) return SRMI_ERR_SHAPE;
-  const int smem = C * 6 * (W + 2) * 4;
+  const int smem = C * (kHeadFwdRows + 2) * (W + 2) * 4;
+  const dim3 grid(H / kHeadFwdRows, N);
   if (f32)
-    hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(H / 4, N), dim3(256), smem, st, lr, w, b, C, H, W, x0f,
+    hipLaunchKernelGGL(head_fwd_kernel<float>, grid, dim3(256), smem, st, lr, w, b, C, H, W, x0f,
                        static_cast<float*>(x0b));
   else
-    hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, dim3(H / 4, N), dim3(256), smem, st, lr, w, b, C, H, W, x0f,
+    hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, grid, dim3(256), smem, st, lr, w, b, C, H, W, x0f,
                        static_cast<bf16_t*>(x0b));
   SRMI_CHECK_LAUNCH();
   return 0;
