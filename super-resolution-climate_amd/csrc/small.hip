@@ -298,19 +298,32 @@ __global__ void __launch_bounds__(256) tail_fwd_mfma_kernel(const bf16_t* __rest
 }
 
 // Exact-fp32 form (fp32 engine mode) on the VALU (C <= 4 outputs per pixel: an MFMA
-// form would waste 12 of its 16 output rows at 1/16 of the bf16 rate).  Register-
-// blocked: a thread owns 4 consecutive pixels of one row, a workgroup 4 rows x 256 px.
-// Per 8-channel slice the 6 x 258 halo is staged channel-major in LDS; per (channel,
-// filter row) a thread reads its 6-pixel window with one ds_read_b128 + one b64 and the
-// 3 taps' filters for all C outputs as float4 broadcasts, then issues 4 px x 3 kx x 4 co
-// FMAs (the one-pixel-per-thread form read LDS once per 0.8 FMA: 1.27 ms at EDSR x8).
-constexpr int kTfTX = 256, kTfCS = 8, kTfWP = kTfTX + 4;  // px per row, channels per slice, LDS row pitch
+// form would waste 12 of its 16 output rows at 1/16 of the bf16 rate).  A workgroup
+// = 4 rows x 32 px of one image with ALL 64 channels of its 6 x 34 halo staged once,
+// pixel-major (whole 256-byte pixel rows per load; pitch 68 floats).  Thread = (row,
+// 4-pixel group, 8-channel group): per filter row it reads its 6-pixel x 8-channel
+// window (12 ds_read_b128) and the taps' filters for all C outputs as float4
+// broadcasts, issues 8 ch x 3 kx x 4 px x 4 co FMAs, and the 8 channel groups (8
+// consecutive lanes) are summed by xor shuffles in a fixed order.  (The former form
+// staged 8-channel slices of 256-px rows: every 128-byte line of x was fetched for 4
+// slices at different times -- 731 us at EDSR x8 for a 1.07 GB input.)
+constexpr int kTfTX = 32, kTfP = 68;  // px per row per workgroup, LDS pixel pitch (floats)
 __global__ void __launch_bounds__(256) tail_fwd_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                            const float* __restrict__ b, int C, int H, int W,
                                                            float* __restrict__ y) {
-  __shared__ __attribute__((aligned(16))) float hs[kTfCS][6][kTfWP];
+  __shared__ __attribute__((aligned(16))) float hs[6][kTfTX + 2][kTfP];
   __shared__ float4 wl[64][9];  // [ci][tap] -> co 0..3 (zero beyond C)
   const int n = blockIdx.z, y0 = blockIdx.y * 4, x0 = blockIdx.x * kTfTX, tid = threadIdx.x;
+  constexpr int NI = 6 * (kTfTX + 2) * 16, NL = (NI + 255) / 256;  // float4 chunks of the halo
+  float4 hv[NL];
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {  // every load of the thread in flight at once (clamped)
+    const int i = min(tid + j * 256, NI - 1);
+    const int q = i >> 4, c4 = i & 15;
+    const int hy = q / (kTfTX + 2), hx = q - hy * (kTfTX + 2);
+    const int yy = min(max(y0 - 1 + hy, 0), H - 1), xx = min(max(x0 - 1 + hx, 0), W - 1);
+    hv[j] = *reinterpret_cast<const float4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + c4 * 4);
+  }
   for (int i = tid; i < 64 * 9; i += 256) {
     const int ci = i / 9, tap = i % 9;
     float v[4];
@@ -318,60 +331,59 @@ __global__ void __launch_bounds__(256) tail_fwd_f32_kernel(const float* __restri
     for (int co = 0; co < 4; ++co) v[co] = co < C ? w[((size_t)co * 64 + ci) * 9 + tap] : 0.f;
     wl[ci][tap] = make_float4(v[0], v[1], v[2], v[3]);
   }
-  const int r = tid >> 6, t = tid & 63;  // row r, pixels 4t .. 4t+3 of the block
-  float acc[4][4];                       // [co][px]
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {  // padding zeroed
+    const int i = tid + j * 256;
+    if (i < NI) {
+      const int q = i >> 4, c4 = i & 15;
+      const int hy = q / (kTfTX + 2), hx = q - hy * (kTfTX + 2);
+      const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
+      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      *reinterpret_cast<float4*>(&hs[hy][hx][c4 * 4]) = ok ? hv[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __syncthreads();
+  const int cg = tid & 7, pg = (tid >> 3) & 7, r = tid >> 6;  // channels 8cg.., pixels 4pg.., row r
+  float acc[4][4];                                            // [co][px]
 #pragma unroll
   for (int co = 0; co < 4; ++co)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[co][j] = 0.f;
-  for (int cs = 0; cs < 64; cs += kTfCS) {
-    __syncthreads();
-    {  // every load of the thread in flight at once (clamped, padding zeroed after)
-      constexpr int NI = 6 * (kTfTX + 2) * (kTfCS / 4), NL = (NI + 255) / 256;
-      float4 hv[NL];
 #pragma unroll
-      for (int j = 0; j < NL; ++j) {
-        const int i = min(tid + j * 256, NI - 1);
-        const int q = i / (kTfCS / 4), c4 = i % (kTfCS / 4);
-        const int hy = q / (kTfTX + 2), hx = q % (kTfTX + 2);
-        const int yy = min(max(y0 - 1 + hy, 0), H - 1), xx = min(max(x0 - 1 + hx, 0), W - 1);
-        hv[j] = *reinterpret_cast<const float4*>(x + (((size_t)n * H + yy) * W + xx) * 64 + cs + c4 * 4);
-      }
+  for (int ky = 0; ky < 3; ++ky) {
+    float xw[6][8];
 #pragma unroll
-      for (int j = 0; j < NL; ++j) {
-        const int i = tid + j * 256;
-        if (i < NI) {
-          const int q = i / (kTfCS / 4), c4 = i % (kTfCS / 4);
-          const int hy = q / (kTfTX + 2), hx = q % (kTfTX + 2);
-          const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
-          const float4 v = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? hv[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-          hs[c4 * 4 + 0][hy][hx] = v.x;
-          hs[c4 * 4 + 1][hy][hx] = v.y;
-          hs[c4 * 4 + 2][hy][hx] = v.z;
-          hs[c4 * 4 + 3][hy][hx] = v.w;
-        }
-      }
+    for (int p = 0; p < 6; ++p) {
+      const float4 u0 = *reinterpret_cast<const float4*>(&hs[r + ky][4 * pg + p][8 * cg]);
+      const float4 u1 = *reinterpret_cast<const float4*>(&hs[r + ky][4 * pg + p][8 * cg + 4]);
+      xw[p][0] = u0.x; xw[p][1] = u0.y; xw[p][2] = u0.z; xw[p][3] = u0.w;
+      xw[p][4] = u1.x; xw[p][5] = u1.y; xw[p][6] = u1.z; xw[p][7] = u1.w;
     }
-    __syncthreads();
-#pragma unroll 2
-    for (int c = 0; c < kTfCS; ++c)
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {
-        const float4 v0 = *reinterpret_cast<const float4*>(&hs[c][r + ky][4 * t]);
-        const float2 v1 = *reinterpret_cast<const float2*>(&hs[c][r + ky][4 * t + 4]);
-        const float xv[6] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y};
+    for (int k = 0; k < 8; ++k)
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const float4 wv = wl[cs + c][ky * 3 + kx];
-          const float wc[4] = {wv.x, wv.y, wv.z, wv.w};
+      for (int kx = 0; kx < 3; ++kx) {
+        const float4 wv = wl[8 * cg + k][ky * 3 + kx];
+        const float wc[4] = {wv.x, wv.y, wv.z, wv.w};
 #pragma unroll
-          for (int co = 0; co < 4; ++co)
+        for (int co = 0; co < 4; ++co)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[co][j] = fmaf(xv[j + kx], wc[co], acc[co][j]);
-        }
+          for (int j = 0; j < 4; ++j) acc[co][j] = fmaf(xw[j + kx][k], wc[co], acc[co][j]);
       }
   }
-  const int xo = x0 + 4 * t;
+  // sum over the 8 channel groups (lanes 8m .. 8m+7), fixed order
+#pragma unroll
+  for (int co = 0; co < 4; ++co)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = acc[co][j];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      acc[co][j] = v;
+    }
+  if (cg != 0) return;
+  const int xo = x0 + 4 * pg;
 #pragma unroll
   for (int co = 0; co < 4; ++co) {
     if (co < C) {
