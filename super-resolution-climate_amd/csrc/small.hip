@@ -475,6 +475,11 @@ __global__ void __launch_bounds__(256) tail_dgrad_kernel(const float* __restrict
   // the 6-pixel dy window is read once and each tap's 8 filters once (96 FMAs per 8
   // LDS reads; one pixel per thread read 3 per 8 FMAs)
   const int ck = tid & 7;
+  // the thread's channels: bf16 8ck .. 8ck+7 (one 16-byte store; 8 lanes = a 128-byte
+  // pixel row); fp32 4ck .. 4ck+3 and 32+4ck .. 32+4ck+3, so that each of the two
+  // 16-byte stores of the 8 lanes covers one contiguous 128-byte half of the pixel
+  // row (8ck .. 8ck+7 left every store instruction writing 16 B pieces 16 B apart)
+  const int c_lo = sizeof(T) == 2 ? 8 * ck : 4 * ck, c_hi = sizeof(T) == 2 ? 8 * ck + 4 : 32 + 4 * ck;
   const auto rdx = wt_rsrc(dx, (uint32_t)((size_t)gridDim.z * H * W * 64 * sizeof(T)));
   constexpr int QPR = TWT / 4;  // 4-pixel groups per row
   for (int pg = tid >> 3; pg < 4 * QPR; pg += 32) {
@@ -495,8 +500,8 @@ __global__ void __launch_bounds__(256) tail_dgrad_kernel(const float* __restrict
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
           const int t = ky * 3 + kx;
-          const float4 w0 = *reinterpret_cast<const float4*>(wl + (c * 9 + t) * 64 + ck * 8);
-          const float4 w1 = *reinterpret_cast<const float4*>(wl + (c * 9 + t) * 64 + ck * 8 + 4);
+          const float4 w0 = *reinterpret_cast<const float4*>(wl + (c * 9 + t) * 64 + c_lo);
+          const float4 w1 = *reinterpret_cast<const float4*>(wl + (c * 9 + t) * 64 + c_hi);
           const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -509,16 +514,16 @@ __global__ void __launch_bounds__(256) tail_dgrad_kernel(const float* __restrict
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const size_t e = (((size_t)n * H + y0 + r) * W + x0 + xq + j) * 64 + ck * 8;
+      const size_t e = (((size_t)n * H + y0 + r) * W + x0 + xq + j) * 64;
       if constexpr (sizeof(T) == 2) {
         uint4 o;
         o.x = pack2(acc[j][0], acc[j][1]); o.y = pack2(acc[j][2], acc[j][3]);
         o.z = pack2(acc[j][4], acc[j][5]); o.w = pack2(acc[j][6], acc[j][7]);
         // 8 lanes per pixel: 128-byte lines, written through (common.hpp)
-        st_wt16(rdx, dx, (uint32_t)(e * 2), o);
+        st_wt16(rdx, dx, (uint32_t)((e + c_lo) * 2), o);
       } else {
-        st_wt16(rdx, dx, (uint32_t)(e * 4), make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]));
-        st_wt16(rdx, dx, (uint32_t)(e * 4 + 16), make_float4(acc[j][4], acc[j][5], acc[j][6], acc[j][7]));
+        st_wt16(rdx, dx, (uint32_t)((e + c_lo) * 4), make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]));
+        st_wt16(rdx, dx, (uint32_t)((e + c_hi) * 4), make_float4(acc[j][4], acc[j][5], acc[j][6], acc[j][7]));
       }
     }
   }
