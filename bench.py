@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--cu-budget", type=int, default=None, help="CUs each engine sizes its launches for")
     ap.add_argument("--infer-region", type=int, default=4096, help="C5 HR region side (BASELINE: 4096)")
     ap.add_argument("--infer-iters", type=int, default=5)
+    ap.add_argument("--no-dp-probe", action="store_true", help="skip the dp_overhead_1rank measurement")
     ap.add_argument("--force-dp", action="store_true",
                     help="diagnostic: the DP path (RCCL group, reducer stream, bucketed all-reduce) at one rank")
     return ap.parse_args()
@@ -120,6 +121,10 @@ FUSED_FLOP_PER_TILE = 2 * CONV64_FLOP_PER_TILE   # one dgrad conv + one filter-g
 
 
 def fused_rooflines(tr, step_ms, reps=20):
+    # per engine and step: conv2's fused launch (F2) runs once per RCAB; conv1's
+    # (F1, EPI_DG_ACC_CA) once per RCAB except the first of each residual group, whose
+    # conv1 dgrad accumulates into the group-input gradient instead (EPI_DG_ACC, a
+    # different kernel: engine.cpp backward_impl)
     """Roofline of the dominant kernel AT ITS IN-STEP CONFIGURATION: the bench's own
     trainer engines re-issue their fused backward launch of one RCAB
     (srmi_engine_probe: same parameters, buffers, grid and CU split as inside the
@@ -133,6 +138,8 @@ def fused_rooflines(tr, step_ms, reps=20):
     n_eng = len(tr.engines)
     tiles_per_engine = tr.engines[0].batch
     out = {}
+    nl, nb = tr.spec.nlayers, tr.spec.nblocks
+    per_step = {1: nl * (nb - 1), 2: nl * nb}
     for which, name, bpt in ((1, "rcab_bwd_kernel<EPI_DG_ACC_CA>", F1_BYTES_PER_TILE),
                              (2, "rcab_bwd_kernel<EPI_DG_RELUMASK>", F2_BYTES_PER_TILE)):
         streams = [tr.streams[k] or main_st for k in range(n_eng)]
@@ -170,7 +177,8 @@ def fused_rooflines(tr, step_ms, reps=20):
             "bytes_per_launch": bpt * tiles_per_engine + WGRAD_OUT_BYTES, "launches_per_slot": n_eng,
             "flop_per_launch": FUSED_FLOP_PER_TILE * tiles_per_engine, "mfma_tflops": round(tf, 1),
             "mfma_frac": round(tf / PEAK_BF16_TFLOPS, 4),
-            "share_of_step": round(ms * 20 * 10 / step_ms, 3),   # 200 RCABs per step
+            "launches_per_engine_per_step": per_step[which],
+            "share_of_step": round(ms * per_step[which] / step_ms, 3),
         }
     return out[1], out[2]
 
@@ -267,6 +275,39 @@ def edsr_bench(dev, batch, steps, warmup):
                               "frac": round(tf / PEAK_FP32_TFLOPS, 4)},
             "config": {"workload": "edsr-16-64 x8 train step (down8 + fwd + RMSE + interp RMSE + bwd + Adam), "
                                    "4-var 32x32->256x256 tiles, exact fp32", "batch": batch}}
+
+
+def dp_overhead_probe(tr, spec, hr, args, reps=2):
+    """dp_overhead_1rank: the data-parallel machinery's own cost on one GPU -- a
+    one-rank RCCL process group (backend "nccl"), the reducer's comm stream, the
+    per-residual-group events and the 11 bucketed all-reduces of the N>1 path
+    (bench --force-dp) -- against the plain step, interleaved on this GPU (K steps of
+    each, `reps` rounds, best of each).  Streams per rank: one per micro-batch
+    engine + the reducer's comm stream (+ RCCL's internal stream)."""
+    from srmi.dist import init_from_env
+    from srmi.trainer import FusedTrainer
+    info = init_from_env(None, force=True)
+    dp = FusedTrainer(spec, args.batch, (48, 48), lr=1e-4, interp_loss=not args.no_interp_loss, info=info,
+                      device=hr.device, seed=0, micro=args.micro, cu_budget=args.cu_budget)
+    for _ in range(args.warmup):
+        dp.step(hr)
+    torch.cuda.synchronize()
+    best = {"plain": 0.0, "dp": 0.0}
+    for _ in range(reps):
+        for name, t in (("plain", tr), ("dp", dp)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                t.step(hr)
+            torch.cuda.synchronize()
+            best[name] = max(best[name], args.batch * args.steps / (time.perf_counter() - t0))
+    del dp
+    torch.distributed.destroy_process_group()
+    return {"tiles_per_s_plain": round(best["plain"], 2), "tiles_per_s_dp": round(best["dp"], 2),
+            "overhead_frac": round(1.0 - best["dp"] / best["plain"], 4),
+            "streams_per_rank": f"{tr.micro} engine stream(s) + 1 reducer comm stream (+ RCCL internal)",
+            "config": f"1-rank RCCL group, {tr.micro} micro-batch engine(s), same B={args.batch}, "
+                      f"best of {reps} interleaved rounds of {args.steps} steps"}
 
 
 def _log(msg):
@@ -395,6 +436,10 @@ def main():
         step_tf = value / world * TRAIN_GFLOP_PER_TILE_C2 / 1000.0
         roof["step_mfma_tflops"] = round(step_tf, 1)
         roof["step_mfma_frac"] = round(step_tf / PEAK_BF16_TFLOPS, 4)
+    dp_probe = None
+    if world == 1 and not info.enabled and not args.no_dp_probe:
+        dp_probe = dp_overhead_probe(tr, spec, hr, args)
+        _log(f"dp probe: {dp_probe}")
     del tr, hr  # the extra lines below run on their own engines
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -430,6 +475,7 @@ def main():
             "roofline": roof,
             "roofline_f2": roof_f2,
             "roofline_conv_fwd": roof_conv,
+            "dp_overhead_1rank": dp_probe,
             "cpu_baseline": cpu,
             "inference": infer,
             "edsr_x8": edsr,

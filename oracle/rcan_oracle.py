@@ -370,9 +370,11 @@ def process_region(model, region: np.ndarray, ty: int, tx: int, scale: int, batc
 def evaluate(model, regions: Sequence[np.ndarray], ty: int, tx: int, scale: int, batch_size: int,
              loss_fn: str = "l2"):
     """ModelTrainer.evaluate (dual_trainer.py:482-543) over the time slices of a
-    tset (no flips): losses = mean over all batches of all regions; results = the
-    normalised tiles concatenated along the tile axis (merge_results_tiles, :38-42)."""
-    bm, bi, res = [], [], {k: [] for k in ("input", "target", "model", "interpolated")}
+    tset (no flips): losses = mean over all batches of all regions (:532, :541);
+    results = the normalised tiles of the LAST region only: clear_results at the
+    start of every time slice (:505, :545-549), then that slice's batches
+    concatenated along the tile axis (merge_results_tiles, :38-42, :551-555)."""
+    bm, bi, results = [], [], {}
     for region in regions:
         tiles, _, _, _, _ = region_to_tiles(region, ty, tx)
         dt = torch.float64 if tiles.dtype == np.float64 else torch.float32
@@ -383,9 +385,8 @@ def evaluate(model, regions: Sequence[np.ndarray], ty: int, tx: int, scale: int,
         interp = upsample(lr, scale)
         bm += batch_losses(sr, target, batch_size, loss_fn)
         bi += batch_losses(interp, target, batch_size, loss_fn)
-        for k, v in (("input", lr), ("target", target), ("model", sr), ("interpolated", interp)):
-            res[k].append(v.numpy())
-    results = {k: np.concatenate(v, axis=0) for k, v in res.items()}
+        results = {k: v.numpy() for k, v in (("input", lr), ("target", target), ("model", sr),
+                                               ("interpolated", interp))}
     return results, {"model": float(np.array(bm).mean()), "interpolated": float(np.array(bi).mean())}
 
 

@@ -352,6 +352,14 @@ static int init_engine(srmi_engine* e, const srmi_model_config* cfg, int train) 
   if (e->h % 4 || (e->w % 32 && e->w % 48)) return SRMI_ERR_SHAPE;
   const int Hs = e->h * e->S;
   if (Hs % 16 || ((e->w * e->S) % 32)) return SRMI_ERR_SHAPE;
+  // the kernels store activation / gradient maps through buffer resources with a
+  // 32-bit byte range: refuse any map of 2^32 bytes or more (the largest is the
+  // last pixel-shuffle output, mapn << 2 nups elements, and the fp32 streams)
+  const size_t lim = (size_t)1 << 32;
+  const size_t ps_bytes = (e->mapn << (2 * e->P.nups)) * e->esz;
+  const size_t f32_bytes = e->mapn * 4;
+  const size_t hr_bytes = (size_t)e->N * std::max(e->C, e->Co) * Hs * (e->w * e->S) * 4;
+  if (ps_bytes >= lim || f32_bytes >= lim || hr_bytes >= lim) return SRMI_ERR_SHAPE;
   return 0;
 }
 

@@ -83,13 +83,43 @@ def cfg() -> _Cfg:
     return _CURRENT
 
 
+def _resolve_root(sec: Section) -> Section:
+    """The platform yaml's relative interpolations (``${.root}/results``,
+    ``{root}/results``; config/platform/*.yaml) resolved against its own root."""
+    root = sec.get("root")
+    if root is None:
+        return sec
+    for k, v in list(sec.items()):
+        if isinstance(v, str) and k != "root":
+            sec[k] = v.replace("${.root}", str(root)).replace("{root}", str(root))
+    return sec
+
+
 class ConfigContext:
-    """with ConfigContext('sres', dict(task='SST-tiles-48', model='rcan-10-20-64'), **{'task.lr': 1e-4}):"""
+    """with ConfigContext('sres', dict(task='SST-tiles-48', model='rcan-10-20-64', dataset='swot'), **{'task.lr': 1e-4}):
+
+    Identity keys as the reference's ConfigContext.activate sets them
+    (sres/base/util/config.py:51, :82-84): ``task.name`` = the task config name,
+    ``task.dataset`` = the dataset config name and ``task.training_version`` =
+    ``'-'.join([name, model, dataset, task])`` -- the stem of the checkpoint files
+    (checkpoints.py:62) -- plus ``.model/.task/.dataset/.cid`` attributes on the
+    context (ResultsAccumulator reads cc.dataset / cc.task / cc.model,
+    manager.py:185-191)."""
 
     def __init__(self, cname: str, configuration: Dict[str, str], **overrides):
         self.cname = cname
+        self.name = cname
         self.configuration = dict(configuration)
         self.overrides = overrides
+        self.model = self.configuration.get("model")
+        self.task = self.configuration.get("task")
+        self.dataset = self.configuration.get("dataset")
+        self.pipeline = self.configuration.get("pipeline")
+        self.platform = self.configuration.get("platform")
+        # config.py:51 joins the four names (the reference raises on a missing one;
+        # here the id is formed from the names present, as a partial context still
+        # has to name its checkpoints)
+        self.cid = "-".join(str(v) for v in (cname, self.model, self.dataset, self.task) if v is not None)
         self._prev = None
 
     def load(self) -> _Cfg:
@@ -102,13 +132,20 @@ class ConfigContext:
         c.setdefault("pipeline", Section(gpu=0))
         c.setdefault("task", Section())
         c.setdefault("model", Section())
+        if "platform" in c:
+            _resolve_root(c["platform"])
         for k, v in self.overrides.items():
             sec, key = k.split(".", 1)
             c.setdefault(sec, Section())[key] = v
         if "FMOD_GPU" in os.environ:  # sres/base/util/config.py:79
             c["pipeline"]["gpu"] = int(os.environ["FMOD_GPU"])
-        if "model" in self.configuration:
-            c["task"]["training_version"] = f"{self.cname}-{self.configuration['model']}"
+        # activate(), config.py:82-84
+        if self.task is not None:
+            c["task"]["name"] = self.task
+        if self.dataset is not None:
+            c["task"]["dataset"] = self.dataset
+        if self.model is not None:
+            c["task"]["training_version"] = self.cid
         return c
 
     def __enter__(self):
@@ -146,6 +183,24 @@ def init_parms(model: str, custom: Dict[str, Any], model_cfg: Optional[Any] = No
         for k, v in pd.items():
             parms[k] = get(k, v)
     return parms
+
+
+def check_fused_task(task, nchannels_in: int, nchannels_out: int) -> None:
+    """Refuse what the fused trainer does not implement from apply_network
+    (dual_trainer.py:557-571): an extra ``task.data_downsample`` > 1 before the
+    model's own bicubic 1/s, and a target that is a channel subset of the input
+    (``index_select`` of task.target_variables).  Every in-scope task yaml has
+    input == target variables and data_downsample 1."""
+    ds = float(task.get("data_downsample", 1.0) or 1.0) if task is not None else 1.0
+    if ds != 1.0:
+        raise NotImplementedError(f"task.data_downsample={ds}: the fused trainer implements data_downsample == 1 only")
+    if nchannels_in != nchannels_out:
+        raise NotImplementedError(f"target channel subset ({nchannels_out} of {nchannels_in} input variables): "
+                                  "the fused trainer needs input_variables == target_variables")
+    if task is not None and "input_variables" in task and "target_variables" in task:
+        if list(task["input_variables"]) != list(task["target_variables"]):
+            raise NotImplementedError(f"target_variables {list(task['target_variables'])} != input_variables "
+                                      f"{list(task['input_variables'])}: not implemented by the fused trainer")
 
 
 def tile_sizes(task) -> tuple:

@@ -45,6 +45,15 @@ class CheckpointStore:
         self.results_dir = results_dir
         self.training_version = training_version
 
+    @classmethod
+    def from_config(cls, c=None) -> "CheckpointStore":
+        """checkpoint_path's inputs (checkpoints.py:60-66): ``cfg().platform.results``
+        and ``cfg().task.training_version`` (set by ConfigContext, config.py:84)."""
+        if c is None:
+            from .config import cfg
+            c = cfg()
+        return cls(str(c["platform"]["results"]), str(c["task"]["training_version"]))
+
     def path(self, tset: str, backup: bool = False) -> str:
         v = _tset(tset)
         v = "valid" if v == "test" else v  # checkpoint_path: Test -> Validation (:63)
@@ -90,6 +99,15 @@ class LossRecords:
     def __init__(self, save_dir: str, dataset: str, task: str, model: str):
         self.save_dir, self.dataset, self.task, self.model = save_dir, dataset, task, model
         self.results: List[List[str]] = []
+
+    @classmethod
+    def from_context(cls, cc, save_dir: Optional[str] = None) -> "LossRecords":
+        """ResultsAccumulator(cc) (manager.py:185-191): cc.dataset / cc.task /
+        cc.model, save_dir defaulting to ``cfg().platform.processed``."""
+        if save_dir is None:
+            from .config import cfg
+            save_dir = str(cfg()["platform"]["processed"])
+        return cls(save_dir, cc.dataset, cc.task, cc.model)
 
     def result_file_path(self) -> str:
         d = os.path.join(self.save_dir, f"{self.task}_result_recs")
@@ -172,7 +190,12 @@ def train_timeslices(trainer, timeslices: Sequence[Callable[[], torch.Tensor]], 
         if records is not None:
             records.refresh_state()
     elif store is not None:
-        state = store.load(trainer, "train", update_model=True) or {}
+        state = store.load(trainer, "train", update_model=True)
+        if state is None:
+            # the reference fails here too (train_state.get on None, dual_trainer.py:287-290);
+            # never train from scratch over -- and then back up over -- an unreadable checkpoint
+            raise RuntimeError(f"cannot resume: the train checkpoint {store.path('train')} exists but could not be "
+                               "loaded into this trainer (refresh_state=True starts over)")
         epoch0 = state.get("epoch", 1)
         itime0 = state.get("itime", 0)
         epoch_loss = state.get("loss", float("inf"))

@@ -159,6 +159,10 @@ class TiledInference:
         self.region.copy_(region)
         self._tile()
         self.n_kept = self.n
+        # every path below scores self.tiles except the compacted one, which resets
+        # this to its compacted copy (a graph replay after a compacted region must
+        # not leave the previous region's tiles here)
+        self._kept_tiles = self.tiles
         if bool(self.bad.any()):  # rare: drop non-finite tiles (reference get_tiles mask)
             self._run_compacted()
         elif self._use_graph:
@@ -186,29 +190,29 @@ class TiledInference:
     def evaluate(self, regions: Sequence[torch.Tensor]) -> Tuple[Dict[str, torch.Tensor], Dict[str, float]]:
         """ModelTrainer.evaluate (dual_trainer.py:482-543) over the time slices of a
         tset: every region is tiled, normalised and scored batch by batch; the loss
-        is the mean over ALL batches of all regions (:532, :541) and the results are
-        the normalised tiles of every batch concatenated along the tile axis
-        (merge_results / merge_results_tiles, :551-555, :38-42): input [n, C, ty/s,
-        tx/s], target / model / interpolated [n, C, ty, tx] (device tensors).  The
+        is the mean over ALL batches of all regions (:532, :541), while the results
+        are those of the LAST evaluated region only -- the reference clears them at
+        the start of every time slice (clear_results, :505, :545-549) and then
+        concatenates that slice's batches (merge_results / merge_results_tiles,
+        :551-555, :38-42): input [n, C, ty/s, tx/s], target / model / interpolated
+        [n, C, ty, tx] (device tensors, normalised tiles).  The
         validation-checkpoint policy applied to the returned loss is
         ValidationCheckpoint.update (srmi.harness)."""
         bm: List[torch.Tensor] = []
         bi: List[torch.Tensor] = []
-        merged: Dict[str, List[torch.Tensor]] = {k: [] for k in ("input", "target", "model", "interpolated")}
+        results: Dict[str, torch.Tensor] = {k: torch.empty(0, device=self.device)
+                                            for k in ("input", "target", "model", "interpolated")}
         for region in regions:
             self.process_region(region)
             nt = self.n_kept
             b = self.batch_losses()
             bm.append(b["model"].clone())
             bi.append(b["interpolated"].clone())
-            if nt:
-                merged["input"].append(self.lr[:nt].clone())
-                merged["target"].append(self._kept_tiles[:nt].clone())
-                merged["model"].append(self.sr[:nt].clone())
-                merged["interpolated"].append(self.interp[:nt].clone())
-        results = {k: torch.cat(v, 0) if v else torch.empty(0, device=self.device) for k, v in merged.items()}
-        m = torch.cat(bm).double().cpu()
-        i = torch.cat(bi).double().cpu()
+            # clear_results(tset) per time slice, then this slice's tiles
+            results = {"input": self.lr[:nt].clone(), "target": self._kept_tiles[:nt].clone(),
+                       "model": self.sr[:nt].clone(), "interpolated": self.interp[:nt].clone()}
+        m = torch.cat(bm).double().cpu() if bm else torch.empty(0, dtype=torch.float64)
+        i = torch.cat(bi).double().cpu() if bi else torch.empty(0, dtype=torch.float64)
         losses = {"model": float(m.mean()) if m.numel() else float("nan"),
                   "interpolated": float(i.mean()) if i.numel() else float("nan")}
         return results, losses

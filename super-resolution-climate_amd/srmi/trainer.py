@@ -25,6 +25,7 @@ import torch
 
 from . import checkpoint as ckpt
 from ._lib import SRMI_LOSS_MEAN, SRMI_LOSS_RMSE
+from .config import check_fused_task
 from .dist import DistInfo, GradReducer, allreduce_sum_
 from .engine import Engine, NetSpec, adam_step, axpy, downsample, upsample
 
@@ -69,9 +70,16 @@ class FusedTrainer:
                  eps: float = 1e-8, weight_decay: float = 0.0, interp_loss: bool = True,
                  info: Optional[DistInfo] = None, device: Optional[torch.device] = None, seed: int = 0,
                  params: Optional[torch.Tensor] = None, micro: Optional[int] = None, loss_fn: str = "l2",
-                 cu_budget: Optional[int] = None):
+                 cu_budget: Optional[int] = None, task=None):
+        """task: the task config section (default: the active srmi ConfigContext's,
+        if any); apply_network features the fused step does not implement
+        (data_downsample > 1, target channel subsets) raise NotImplementedError."""
         if loss_fn not in LOSS_KINDS:  # single_product_loss, dual_trainer.py:210-211
             raise ValueError(f"Unknown single-product loss function {loss_fn}")
+        if task is None:
+            from . import config as _config
+            task = _config._CURRENT.get("task") if _config._CURRENT is not None else None
+        check_fused_task(task, spec.nchannels_in, spec.nchannels_out)
         self.loss_fn = loss_fn
         self.loss_kind = LOSS_KINDS[loss_fn]
         self.info = info or DistInfo()

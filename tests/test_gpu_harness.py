@@ -142,7 +142,8 @@ def test_evaluate_vs_oracle_and_validation_policy(tmp_path):
     ti = TiledInference(spec, flat.to(d), regions[0].shape, (192, 192), device=d, graph=True, batch_size=4)
     res, losses = ti.evaluate([torch.tensor(r, device=d) for r in regions])
     ref_res, ref = ro.evaluate(model, [r.astype(np.float64) for r in regions], 192, 192, 4, batch_size=4)
-    assert res["model"].shape == (12, 1, 192, 192) and res["input"].shape == (12, 1, 48, 48)
+    # results: the last time slice's 6 tiles (clear_results per slice, dual_trainer.py:505, :545-549)
+    assert res["model"].shape == (6, 1, 192, 192) and res["input"].shape == (6, 1, 48, 48)
     assert rel_l2(res["target"], ref_res["target"]) < 1e-5
     assert rel_l2(res["interpolated"], ref_res["interpolated"]) < 1e-5
     assert rel_l2(res["model"], ref_res["model"]) < 2e-2
@@ -160,6 +161,29 @@ def test_evaluate_vs_oracle_and_validation_policy(tmp_path):
     state = torch.load(store.path("valid"), weights_only=True)
     assert abs(state["loss"] - losses["model"]) < 1e-12
     ti.set_params(tr.params)
+
+
+def test_evaluate_graph_replay_after_compacted_region():
+    """[clean, one NaN tile, clean] with the graph path: the middle region takes the
+    compacted (tile-dropping) path, the last one replays the graph; the results
+    are the last region's full tile set (target as long as model), and the losses
+    average every batch of all three regions, as the oracle computes them."""
+    from srmi.inference import TiledInference
+    d = dev()
+    spec, model, flat = _flat1()
+    rng = np.random.RandomState(17)
+    regions = [rng.randn(1, 2 * 192, 3 * 192).astype(np.float32) for _ in range(3)]
+    regions[1][0, 200, 5] = np.nan  # tile (1, 0) of the middle region is dropped
+    ti = TiledInference(spec, flat.to(d), regions[0].shape, (192, 192), device=d, graph=True, batch_size=4)
+    res, losses = ti.evaluate([torch.tensor(r, device=d) for r in regions])
+    ref_res, ref = ro.evaluate(model, [r.astype(np.float64) for r in regions], 192, 192, 4, batch_size=4)
+    for k in ("input", "target", "model", "interpolated"):
+        assert res[k].shape[0] == 6 == ref_res[k].shape[0], k
+    assert rel_l2(res["target"], ref_res["target"]) < 1e-6
+    assert rel_l2(res["interpolated"], ref_res["interpolated"]) < 1e-5
+    assert rel_l2(res["model"], ref_res["model"]) < 2e-2
+    assert abs(losses["interpolated"] - ref["interpolated"]) < 1e-5 * ref["interpolated"]
+    assert abs(losses["model"] - ref["model"]) < 2e-3 * ref["model"]
 
 
 def test_train_timeslices_checkpoints_csv_and_resume(tmp_path):

@@ -103,8 +103,12 @@ def test_oracle_batch_loss_mean_and_evaluate():
     imgs, l = ro.process_region(model, region, 32, 32, 4, batch_size=4)
     assert len(l["batch_model"]) == 2
     assert abs(l["model"] - np.mean(l["batch_model"])) < 1e-15
+    region2 = rng.randn(1, 2 * 32, 3 * 32)
+    res, le = ro.evaluate(model, [region2, region], 32, 32, 4, batch_size=4)
+    # results = the last time slice's tiles only (clear_results per slice, dual_trainer.py:505)
+    assert res["model"].shape == (6, 1, 32, 32)
+    np.testing.assert_array_equal(res["model"], ro.evaluate(model, [region], 32, 32, 4, batch_size=4)[0]["model"])
     res, le = ro.evaluate(model, [region, region], 32, 32, 4, batch_size=4)
-    assert res["model"].shape == (12, 1, 32, 32)
     assert abs(le["model"] - l["model"]) < 1e-12  # same batches twice: same mean
     # charbonnier (dual_trainer.py:196-198)
     p, t = torch.zeros(2, 3), torch.ones(2, 3)

@@ -68,6 +68,25 @@ def test_workspace_sizes_are_sane():
         _lib.call("srmi_workspace_size", C.byref(bad), 1, C.byref(tb))
 
 
+def test_engine_refuses_maps_past_the_32bit_buffer_range():
+    """Maps are stored through buffer resources with 32-bit byte ranges: EDSR x8
+    fp32 at 256 tiles makes the last pixel-shuffle map exactly 2^32 bytes and must be
+    refused (SRMI_ERR_SHAPE), not run with silently dropped stores; 255 tiles fit."""
+    import ctypes as C
+    from srmi import _lib
+    from srmi.engine import NetSpec
+    spec = NetSpec(arch="edsr", nchannels_in=4, nchannels_out=4, nlayers=16, scale=8, dtype="fp32")
+    b = C.c_size_t()
+    ok = spec.cstruct(255, 32, 32)
+    _lib.call("srmi_workspace_size", C.byref(ok), 1, C.byref(b))
+    assert (255 * 32 * 32 * 64 << 6) * 4 < 2 ** 32
+    big = spec.cstruct(256, 32, 32)
+    with pytest.raises(_lib.SrmiError):
+        _lib.call("srmi_workspace_size", C.byref(big), 1, C.byref(b))
+    bf = NetSpec(arch="edsr", nchannels_in=4, nchannels_out=4, nlayers=16, scale=8)
+    _lib.call("srmi_workspace_size", C.byref(bf.cstruct(256, 32, 32)), 1, C.byref(b))  # bf16: 2^31
+
+
 def test_config_context_and_init_parms():
     from srmi.config import ConfigContext, cfg, init_parms
     with ConfigContext("sres", dict(model="rcan-10-20-64", task="SSS_SST-tiles-48"), **{"task.lr": 1e-4}):
