@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--cu-budget", type=int, default=None, help="CUs each engine sizes its launches for")
     ap.add_argument("--infer-region", type=int, default=4096, help="C5 HR region side (BASELINE: 4096)")
     ap.add_argument("--infer-iters", type=int, default=5)
+    ap.add_argument("--stagger-us", type=int, default=None, help="phase offset between micro-batch engines")
     ap.add_argument("--no-dp-probe", action="store_true", help="skip the dp_overhead_1rank measurement")
     ap.add_argument("--force-dp", action="store_true",
                     help="diagnostic: the DP path (RCCL group, reducer stream, bucketed all-reduce) at one rank")
@@ -242,7 +243,9 @@ def inference_bench(dev, side, iters):
     mpix = ti.n * 192 * 192 / 1e6
     return {"metric": "inference MPix/sec (HR pixels produced)", "value": round(mpix / (ms * 1e-3), 2),
             "unit": "MPix/s", "ms_per_region": round(ms, 3), "tiles": ti.n, "hr_mpix_per_region": round(mpix, 3),
-            "model_tflops": round(ti.n * 73.26e9 / (ms * 1e-3) / 1e12, 1), "dtype": "bf16", "data": "synthetic",
+            "model_tflops": round(ti.n * 73.26e9 / (ms * 1e-3) / 1e12, 1),
+            "mfma_frac": round(ti.n * 73.26e9 / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+            "dtype": "bf16", "data": "synthetic",
             "config": {"workload": f"rcan-10-20-64 tiled inference, 1 var, {side}x{side} HR region, 192^2 tiles "
                                    "(floor), graph-replayed", "graph": True}}
 
@@ -391,8 +394,9 @@ def main():
     C, B = args.channels, args.batch
     spec = NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=10, nblocks=20,
                    cbottleneck=2, scale=4)
+    kw = {} if args.stagger_us is None else {"stagger_us": args.stagger_us}
     tr = FusedTrainer(spec, B, (48, 48), lr=1e-4, interp_loss=not args.no_interp_loss, info=info, device=dev, seed=0,
-                      micro=args.micro, cu_budget=args.cu_budget)
+                      micro=args.micro, cu_budget=args.cu_budget, **kw)
     hr = torch.tensor(synthetic_hr(B, C, 192, 1234 + info.rank)).to(dev)
 
     micro = tr.micro
@@ -471,7 +475,7 @@ def main():
                        "global_batch": B * world, "per_gpu_batch": B, "tile": "48->192",
                        "parallelism": f"dp{world}"},
             "model_tflops": round(value * TRAIN_GFLOP_PER_TILE_C2 / 1000.0, 1),
-            "loss": round(loss, 6),
+            "loss": loss,
             "roofline": roof,
             "roofline_f2": roof_f2,
             "roofline_conv_fwd": roof_conv,

@@ -165,6 +165,11 @@ int srmi_adam_step(float* p, const float* g, float* m, float* v, size_t n, int s
 /* y += a * x (flat fp32; sums micro-batch gradients) */
 int srmi_axpy(float* y, const float* x, float a, size_t n, void* stream);
 
+/* hold `stream` for `us` microseconds (1..1000) with one sleeping wave: the phase
+ * offset between micro-batch engines (no reference counterpart: a scheduling
+ * primitive of the MI355X engine) */
+int srmi_stream_delay(int us, void* stream);
+
 /* ---- op-level entry points (kernel parity tests, custom graphs) ---------- */
 /* dtype: SRMI_DTYPE_BF16 (x / yb / aux / packs bf16) or SRMI_DTYPE_F32 (fp32) */
 /* forward conv: x NHWC [N][H][W][Cin], packed filters (srmi_pack_conv),

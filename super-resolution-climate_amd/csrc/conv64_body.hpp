@@ -2,6 +2,8 @@
 // with the horizontally fused backward launch of wgrad3x3.hip.  Included by those
 // two translation units only (its zero page and stamp buffer are per-TU statics).
 #pragma once
+#include <type_traits>
+
 #include "common.hpp"
 #include "srmi_internal.hpp"
 
@@ -41,7 +43,7 @@ struct Conv2Smem {
   static constexpr int GROUPB = 4 * ROWB;
   static constexpr int WB = 9 * 64 * 128;          // resident filters
   static constexpr int RING = 3 * GROUPB;
-  static constexpr int RED = 4 * 128 * 4;          // cross-wave channel sums
+  static constexpr int RED = 2 * 4 * 128 * 4;      // cross-wave channel sums (two buffers: deferred form)
   static constexpr int TOTAL = WB + RING + RED;
   static constexpr int GCH = GROUPB / 16;          // 16-B chunks per group
   static constexpr int GPT = (GCH + kThreads - 1) / kThreads;
@@ -300,6 +302,18 @@ constexpr int kFragBuf = SRMI_CONV_FRAGBUF;
 #define SRMI_CONV_ILV 1
 #endif  // register buffers of A/B fragments (K-steps)
 
+#ifndef SRMI_DEFER
+#define SRMI_DEFER 4  // bit mask: 1 RELU, 2 POOL, 4 DG_RELUMASK, 8 DG_ACC_CA (in-step A/B: only 4 gains)
+#endif
+template <int EPI>
+constexpr bool conv64_defers() {
+  return ((SRMI_DEFER & 1) && EPI == EPI_RELU_BF16) || ((SRMI_DEFER & 2) && EPI == EPI_POOL_BF16) ||
+         ((SRMI_DEFER & 4) && EPI == EPI_DG_RELUMASK) || ((SRMI_DEFER & 8) && EPI == EPI_DG_ACC_CA);
+}
+template <int TW, int EPI>
+__device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_len, int bid, char* smem, int tail,
+                                                  bool tail_part);
+
 // The kernel body as a device function of a virtual block index `bid` and the
 // workgroup's LDS (>= Conv2Smem<TW>::TOTAL bytes), so that a horizontally fused
 // launch (wgrad3x3.hip, rcab_bwd_kernel) can run it beside other work.
@@ -314,6 +328,10 @@ template <int TW, int EPI, int NW = 4>
 __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, int bid, char* smem, int tail = 0,
                                             bool tail_part = false) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  if constexpr (NW == 8 && conv64_defers<EPI>()) {
+    conv64_body_defer<TW, EPI>(p, run_len, bid, smem, tail, tail_part);
+    return;
+  }
   constexpr int NCT = NW == 8 ? 2 : 4;  // 16-wide output-channel tiles per wave
   using S = Conv2Smem<TW>;
   constexpr int NPT = TW / 16;
@@ -507,6 +525,424 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     STAMP(sj + 4);
+  }
+  STAMP(61);
+}
+
+// ============================================================================
+// Deferred-epilogue form of the 8-wave body (the four hot epilogues: conv1 RELU and
+// conv2 POOL forward, the ReLU-mask dgrad of conv2 and the gradient-stream dgrad of
+// conv1).  In the form above every strip ends with its epilogue behind a barrier:
+// the MFMA pipe idles for ~2.6 K cycles per strip (bias / mask, packing, LDS
+// staging, two more barriers, the stores) against ~3.5 K cycles of MFMA
+// (profiles/r02_conv_stamps_8wave.txt).  Here the epilogue of strip k-1 runs
+// inside strip k's K-loop, one pixel tile per K-step behind that step's MFMAs, from
+// the previous strip's accumulators held in registers; its operands (ReLU output t,
+// gradient stream g, CA input u) are loaded at the first K-steps of strip k; strip
+// k ends with ONE barrier (ring-slot release + group k+2's DMA published).  Only
+// the last strip of a run keeps an exposed epilogue.
+//
+// No LDS staging: each wave stores its own results straight from registers.  For
+// the bf16 outputs the filter rows are read permuted -- accumulator row 4fk + r of
+// tile c is output channel ct0*16 + 8fk + 4c + r -- so a lane holds 8 contiguous
+// channels of its pixel and one 16-byte store per pixel tile writes, per pixel, the
+// wave's whole 64-byte channel half (16 such runs per instruction).  The fp32
+// gradient stream keeps the natural rows: a lane's 4 channels of a tile are 16
+// contiguous bytes, 64 contiguous bytes per pixel per store.  Channel sums (POOL,
+// DG_ACC_CA) go through two LDS buffers: strip k-1's per-row sums are written
+// during strip k, summed over the 4 rows and stored during strip k+1.  Results are
+// bit-identical to the form above (same MFMA order per output element, same sum
+// order).
+
+// opaque to the IR passes (a value "redefined" here cannot be computed with earlier)
+__device__ __forceinline__ void pin(float& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(uint32_t& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin4(f32x4& v) {
+  float a = v[0], b = v[1], c = v[2], d = v[3];
+  pin(a); pin(b); pin(c); pin(d);
+  v = f32x4{a, b, c, d};
+}
+__device__ __forceinline__ void pin4f(float4& v) { pin(v.x); pin(v.y); pin(v.z); pin(v.w); }
+__device__ __forceinline__ void pin4u(uint4& v) { pin(v.x); pin(v.y); pin(v.z); pin(v.w); }
+
+#ifndef SRMI_DEFER_WT
+#define SRMI_DEFER_WT 1  // deferred epilogue stores: 1 write-through (sc1), 0 plain
+#endif
+#ifndef SRMI_DEFER_PRIO
+#define SRMI_DEFER_PRIO 0
+#endif
+template <typename V>
+__device__ __forceinline__ void st_defer(__amdgpu_buffer_rsrc_t r, void* base, uint32_t off, const V& v) {
+#if SRMI_DEFER_WT
+  st_wt16(r, base, off, v);
+#else
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+  (void)base;
+#endif
+}
+
+template <int NPT>
+struct DeferOps {
+  uint4 t[NPT];      // DG_RELUMASK: the ReLU output t, 8 bf16 (permuted rows)
+  float4 g[NPT][2];  // DG_ACC_CA: gradient stream in (natural rows)
+  uint2 u[NPT][2];   // DG_ACC_CA: the CA input u
+};
+
+template <int TW, int EPI>
+__device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_len, int bid, char* smem, int tail,
+                                                  bool tail_part) {
+  constexpr int NW = 8, NCT = 2;
+  using S = Conv2Smem<TW>;
+  constexpr int NPT = TW / 16;
+  constexpr bool kPerm = EPI != EPI_DG_ACC_CA;  // bf16 output: permuted filter rows
+  constexpr bool kPart = EPI == EPI_POOL_BF16 || EPI == EPI_DG_ACC_CA;
+  constexpr bool kCA = EPI == EPI_DG_ACC_CA;
+  constexpr int ES = 10;  // K-step of the first deferred epilogue tile
+  char* wl = smem;
+  char* ring = smem + S::WB;
+  float* red = reinterpret_cast<float*>(smem + S::WB + S::RING);  // [2 buffers][4 rows][2][64]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = wave & 3, ct0 = NCT * (wave >> 2);
+  const int fr = lane & 15, fk = lane >> 4;
+  const int nsx = p.W / TW, nsy = p.H / kTH;
+  const int runs_per_col = (nsy + run_len - 1) / run_len;
+  int r = bid;
+  const int ry = r % runs_per_col;
+  r /= runs_per_col;
+  const int sx = r % nsx;
+  r /= nsx;
+  const int n = r % p.N;
+  const int cb = r / p.N;
+  int k0 = ry * run_len, k1 = min(nsy, k0 + run_len);
+  if (tail > 0) {
+    if (tail_part) k0 = max(k0, k1 - tail);
+    else k1 = max(k0, k1 - tail);
+  }
+  if (k0 >= k1) return;
+  const int x0 = sx * TW;
+  STAMP(0);
+  const bf16_t* xn = p.x + (size_t)n * p.H * p.W * 64;
+  const size_t HW = (size_t)p.H * p.W;
+
+  // input-group DMA (as conv64_body)
+  const int wv_s = __builtin_amdgcn_readfirstlane(wave);
+  const uint32_t rbase = lds_u32(ring);
+  const void* const zpage = uniform_ptr(kZeros);
+  constexpr int NGRP = S::GROUPB / 1024;
+  constexpr int NGW = (NGRP + NW - 1) / NW;
+  int loff[NGW], lrr[NGW];
+  uint32_t okx = 0;
+#pragma unroll
+  for (int m = 0; m < NGW; ++m) {
+    const int i = wv_s + NW * m;
+    const int q = 8 * i + (lane >> 3);
+    const int c = (lane & 7) ^ (q & 7);
+    const int rr = q / (TW + 2), hx = q - rr * (TW + 2);
+    const int xx = x0 - 1 + hx;
+    okx |= (i < NGRP && xx >= 0 && xx < p.W) ? (1u << m) : 0u;
+    loff[m] = ((rr * p.W + hx - 1) * 64 + c * 8) * (int)sizeof(bf16_t);
+    lrr[m] = rr;
+  }
+  auto group_dma_one = [&](int gidx, int m) __attribute__((always_inline)) {
+    const int slot = gidx % 3, y0 = 4 * gidx - 3;
+    const char* base = reinterpret_cast<const char*>(xn + ((ptrdiff_t)y0 * p.W + x0) * 64);
+    const bool ok = ((okx >> m) & 1u) && y0 + lrr[m] >= 0 && y0 + lrr[m] < p.H;
+    const void* src = ok ? (const void*)(base + loff[m]) : zpage;
+    glds16(src, rbase + (uint32_t)(slot * 4 * (TW + 2)) * 128u + (uint32_t)(wv_s + NW * m) * 1024u);
+  };
+  auto group_dma = [&](int gidx) __attribute__((always_inline)) {
+#pragma unroll
+    for (int m = 0; m < NGW; ++m)
+      if (wv_s + NW * m < NGRP) group_dma_one(gidx, m);
+  };
+
+  // channel of accumulator row (c, r) of this lane, and the lane's channel bases
+  auto chan = [&](int c, int rr) -> int { return kPerm ? ct0 * 16 + 8 * fk + 4 * c + rr : (ct0 + c) * 16 + 4 * fk + rr; };
+  float4 bias[NCT];
+  {
+    const float* bp = p.bias ? p.bias : reinterpret_cast<const float*>(kZeros);
+#pragma unroll
+    for (int c = 0; c < NCT; ++c) bias[c] = *reinterpret_cast<const float4*>(bp + cb * 64 + chan(c, 0));
+  }
+  {
+    const uint32_t wbase = lds_u32(wl);
+    // the filter image uses the swz128t chunk swizzle (c ^ (bit1, bit3 of the row)):
+    // conflict-free for the permuted A rows (8 (fr >> 2) + 4c + (fr & 3)) as well as
+    // the natural ones, where swz128 would collide 2-way on the permuted rows and make
+    // the K-loop LDS-bound (20 -> 28 LDS cycles per wave and K-step against 24 of MFMA)
+    for (int i = wv_s; i < 72; i += NW) {
+      const int tap = i >> 3, rw = 8 * (i & 7) + (lane >> 3);
+      const int c = (lane & 7) ^ ((((rw >> 1) & 1) << 1) | (((rw >> 3) & 1) << 2));
+      glds16(p.w + ((size_t)(tap * p.Cout + cb * 64 + rw)) * 64 + c * 8, wbase + (uint32_t)i * 1024u);
+    }
+    group_dma(k0);
+    group_dma(k0 + 1);
+    wait_vm<0>();
+  }
+  STAMP(1);
+  // A-fragment rows: lane fr of tile c reads the filter row of the channel its
+  // accumulator row fr will hold (permuted for bf16 outputs)
+  uint32_t aoff[2][NCT];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int c = 0; c < NCT; ++c) {
+      const int arow = kPerm ? ct0 * 16 + 8 * (fr >> 2) + 4 * c + (fr & 3) : (ct0 + c) * 16 + fr;
+      aoff[kk][c] = swz128t(arow, kk * 4 + fk);
+    }
+  __syncthreads();
+
+  const auto rout = kPerm ? wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2))
+                          : wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
+  const int nstrips_all = nsy * nsx;
+  f32x4 accp[NPT][NCT];  // the previous strip's accumulators
+  DeferOps<NPT> ops;     // operands of the pending epilogue
+
+  // operand loads of the epilogue of strip kp (pixel row 4 kp + row), load slot i
+  constexpr int NLD = EPI == EPI_DG_RELUMASK ? NPT : (kCA ? NPT * NCT : 0);
+  auto op_load = [&](int kp, int i) __attribute__((always_inline)) {
+    const int yy = 4 * kp + row;
+    if constexpr (EPI == EPI_DG_RELUMASK) {
+      const size_t pix = (size_t)n * HW + (size_t)yy * p.W + x0 + i * 16 + fr;
+      ops.t[i] = *reinterpret_cast<const uint4*>(p.aux + pix * p.Cout + cb * 64 + chan(0, 0));
+    } else if constexpr (kCA) {
+      const int pt = i / NCT, c = i % NCT;
+      const size_t pix = (size_t)n * HW + (size_t)yy * p.W + x0 + pt * 16 + fr;
+      const size_t o = pix * p.Cout + cb * 64 + chan(c, 0);
+      ops.g[pt][c] = *reinterpret_cast<const float4*>(p.r1 + o);
+      ops.u[pt][c] = *reinterpret_cast<const uint2*>(p.aux + o);
+    }
+  };
+  // epilogue of pixel tile pt of strip kp from accp
+  float ps0[NCT][4], ps1[NCT][4];
+  auto epi_tile = [&](int kp, int pt) __attribute__((always_inline)) {
+    // pin the tile's work to this K-step: without these the IR passes hoist the
+    // arithmetic (and the operand waits with it) up to the loads at K-step 0
+#pragma unroll
+    for (int c = 0; c < NCT; ++c) pin4(accp[pt][c]);
+    if constexpr (EPI == EPI_DG_RELUMASK) pin4u(ops.t[pt]);
+    if constexpr (kCA) {
+#pragma unroll
+      for (int c = 0; c < NCT; ++c) {
+        pin4f(ops.g[pt][c]);
+        pin(ops.u[pt][c].x);
+        pin(ops.u[pt][c].y);
+      }
+    }
+    const int yy = 4 * kp + row;
+    const size_t pix = (size_t)n * HW + (size_t)yy * p.W + x0 + pt * 16 + fr;
+    if constexpr (kPerm) {
+      float o[8];
+#pragma unroll
+      for (int c = 0; c < NCT; ++c) {
+        const f32x4 v = accp[pt][c];
+        const float b[4] = {bias[c].x, bias[c].y, bias[c].z, bias[c].w};
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          float x = v[rr];
+          if constexpr (EPI == EPI_RELU_BF16) x = fmaxf(x + b[rr], 0.f);
+          if constexpr (EPI == EPI_POOL_BF16) {
+            x += b[rr];
+            ps0[c][rr] += x;
+          }
+          if constexpr (EPI == EPI_DG_RELUMASK) {
+            const uint32_t w = (c ? (rr < 2 ? ops.t[pt].z : ops.t[pt].w) : (rr < 2 ? ops.t[pt].x : ops.t[pt].y));
+            x = p.alpha * relu_mask((rr & 1) ? (w >> 16) : (w & 0xFFFFu), x);
+          }
+          o[4 * c + rr] = x;
+        }
+      }
+      const uint4 val = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+      st_defer(rout, p.yb, (uint32_t)((pix * p.Cout + cb * 64 + chan(0, 0)) * 2), val);
+    } else {
+#pragma unroll
+      for (int c = 0; c < NCT; ++c) {
+        const f32x4 a = accp[pt][c];
+        const float4 gg = ops.g[pt][c];
+        const uint2 uu = ops.u[pt][c];
+        const float v[4] = {a[0] + gg.x, a[1] + gg.y, a[2] + gg.z, a[3] + gg.w};
+        st_defer(rout, p.yf, (uint32_t)((pix * p.Cout + cb * 64 + chan(c, 0)) * 4), make_float4(v[0], v[1], v[2], v[3]));
+        ps0[c][0] += v[0]; ps0[c][1] += v[1]; ps0[c][2] += v[2]; ps0[c][3] += v[3];
+        ps1[c][0] += v[0] * bf2f(uu.x & 0xFFFFu);
+        ps1[c][1] += v[1] * bf2f(uu.x >> 16);
+        ps1[c][2] += v[2] * bf2f(uu.y & 0xFFFFu);
+        ps1[c][3] += v[3] * bf2f(uu.y >> 16);
+      }
+    }
+  };
+  // this wave's row sums of strip kp -> red buffer kp & 1
+  auto part_rows = [&](int kp) __attribute__((always_inline)) {
+    float* rb = red + (kp & 1) * 512;
+#pragma unroll
+    for (int c = 0; c < NCT; ++c)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const float s0 = sum16(ps0[c][rr]);
+        float s1 = 0.f;
+        if constexpr (kCA) s1 = sum16(ps1[c][rr]);
+        if (fr == 0) {
+          rb[(row * 2 + 0) * 64 + chan(c, rr)] = s0;
+          if constexpr (kCA) rb[(row * 2 + 1) * 64 + chan(c, rr)] = s1;
+        }
+      }
+  };
+  // the 4 rows' sums of strip kp -> the per-strip partial record (published by a barrier)
+  auto part_store = [&](int kp) __attribute__((always_inline)) {
+    const float* rb = red + (kp & 1) * 512;
+    const size_t rec = ((size_t)n * nstrips_all + kp * nsx + sx) * p.part_stride;
+    if (tid < 64) {
+      p.part[rec + cb * 64 + tid] = rb[tid] + rb[128 + tid] + rb[256 + tid] + rb[384 + tid];
+    } else if (kCA && tid < 128) {
+      const int c = tid - 64;
+      p.part[rec + 64 + c] = rb[64 + c] + rb[192 + c] + rb[320 + c] + rb[448 + c];
+    }
+  };
+  auto zero_ps = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < NCT; ++c)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) ps0[c][rr] = ps1[c][rr] = 0.f;
+  };
+
+  // one strip; PREV: run strip k-1's epilogue inside it; LAST: prefetch strip k's
+  // own epilogue operands at its end (the exposed epilogue after the loop reads them)
+  auto strip = [&](int k, auto prev_tag, auto last_tag) __attribute__((always_inline)) {
+    constexpr bool PREV = decltype(prev_tag)::value;
+    constexpr bool LAST = decltype(last_tag)::value;
+    const int y = 4 * k + row;
+    const bool pf = (k + 1 < k1);
+    const bool red_store = kPart && (k - 2 >= k0) && tid < (kCA ? 128 : 64);
+    [[maybe_unused]] const int sj = 2 + 5 * min(k - k0, 11);
+    STAMP(sj);
+    uint32_t boff[3][3][2];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int rr = y + ky - 1 + 3;
+      const int slot = ((rr >> 2) % 3) * 4 + (rr & 3);
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) boff[ky][kx][kk] = swz128(slot * (TW + 2) + fr + kx, kk * 4 + fk);
+    }
+    f32x4 acc[NPT][NCT];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i)
+#pragma unroll
+      for (int j = 0; j < NCT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (PREV) zero_ps();
+    bf16x8 A[kFragBuf][NCT], B[kFragBuf][NPT];
+    auto load_step = [&](int st, bf16x8 (&a)[NCT], bf16x8 (&b)[NPT]) __attribute__((always_inline)) {
+      const int tap = st >> 1, kk = st & 1, ky = tap / 3, kx = tap % 3;
+#pragma unroll
+      for (int c = 0; c < NCT; ++c) a[c] = lds_frag(wl, tap * 8192 + aoff[kk][c]);
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt) b[pt] = lds_frag(ring, boff[ky][kx][kk] + pt * 2048);
+    };
+    constexpr int LA = kFragBuf - 1;
+#pragma unroll
+    for (int st = 0; st < LA; ++st) load_step(st, A[st], B[st]);
+#pragma unroll
+    for (int st = 0; st < 18; ++st) {
+      // VMEM issue order in a strip: the deferred epilogue's operand loads (K-steps
+      // 0-2), group k+2's DMA (0-3), the deferred stores (K-steps ES..), the
+      // previous-but-one strip's partial record (17): the DMA is waited for at the
+      // end with a count of the stores behind it
+      if constexpr (PREV && NLD > 0) {
+        constexpr int PER = (NLD + 2) / 3;
+#pragma unroll
+        for (int i = 0; i < PER; ++i)
+          if (st < 3 && st * PER + i < NLD) op_load(k - 1, st * PER + i);
+      }
+      if (st < NGW && pf && wv_s + NW * st < NGRP) group_dma_one(k + 2, st);
+      __builtin_amdgcn_sched_barrier(0);
+      const bool ld = st + LA < 18;
+      if (ld) load_step(st + LA, A[(st + LA) % kFragBuf], B[(st + LA) % kFragBuf]);
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt)
+#pragma unroll
+        for (int c = 0; c < NCT; ++c) acc[pt][c] = mfma16(A[st % kFragBuf][c], B[st % kFragBuf][pt], acc[pt][c]);
+      if (ld) {
+#pragma unroll
+        for (int j = 0; j < NCT + NPT; ++j) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        if constexpr (NCT * NPT > NCT + NPT) __builtin_amdgcn_sched_group_barrier(0x008, NCT * NPT - (NCT + NPT), 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (PREV) {
+        if (st >= ES && st < ES + NPT) epi_tile(k - 1, st - ES);
+        if constexpr (kPart)
+          if (st == ES + NPT) part_rows(k - 1);
+      }
+      if constexpr (kPart)
+        if (st == 17 && red_store) part_store(k - 2);
+      if constexpr (LAST && NLD > 0) {
+        // the exposed epilogue's operands, behind this strip's last MFMAs
+        constexpr int PER = (NLD + 1) / 2;
+#pragma unroll
+        for (int i = 0; i < PER; ++i)
+          if (st >= 16 && (st - 16) * PER + i < NLD) op_load(k, (st - 16) * PER + i);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    STAMP(sj + 1);
+    // group k+2 has landed once only this strip's deferred stores (and the partial
+    // record) may still be in flight behind it
+    constexpr int NST = PREV ? (kPerm ? NPT : NPT * NCT) : 0;
+    if (!pf) {
+      // no DMA in this strip: nothing to wait for (the loads of the exposed
+      // epilogue are waited for where they are used)
+    } else if (red_store) {
+      wait_vm<NST + 1>();
+    } else {
+      wait_vm<NST>();
+    }
+    STAMP(sj + 2);
+#ifdef SRMI_STAMPS
+    // diagnostic: every wave's arrival at the strip barrier (slots 40 + 8 j + wave, j < 3)
+    if (p.stamps && lane == 0 && k - k0 < 3) p.stamps[blockIdx.x * 64 + 40 + 8 * (k - k0) + wave] = __builtin_amdgcn_s_memtime();
+#endif
+    // every wave is past its reads of group k (ring slot released) and its red[]
+    // writes; group k+2 is published
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    STAMP(sj + 3);
+    STAMP(sj + 4);
+#pragma unroll
+    for (int i = 0; i < NPT; ++i)
+#pragma unroll
+      for (int j = 0; j < NCT; ++j) accp[i][j] = acc[i][j];
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+#if SRMI_DEFER_PRIO
+  // the second-dispatched half (waves 4-7) loses every MFMA arbitration to its older
+  // partner and reaches the strip barrier ~1.2 K cycles later: static priority
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+  if (k1 - k0 == 1) {
+    strip(k0, F{}, T{});
+  } else {
+    strip(k0, F{}, F{});
+#pragma unroll 1
+    for (int k = k0 + 1; k < k1 - 1; ++k) strip(k, T{}, F{});
+    strip(k1 - 1, T{}, T{});
+  }
+  // the last strip's epilogue, exposed
+  if constexpr (kPart)
+    if (k1 - 2 >= k0) part_store(k1 - 2);
+  zero_ps();
+#pragma unroll
+  for (int pt = 0; pt < NPT; ++pt) epi_tile(k1 - 1, pt);
+  if constexpr (kPart) {
+    part_rows(k1 - 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    part_store(k1 - 1);
   }
   STAMP(61);
 }

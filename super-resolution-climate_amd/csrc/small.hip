@@ -1570,4 +1570,21 @@ int scale_add_launch(float* y, const float* x, float a, size_t n, hipStream_t st
   return 0;
 }
 
+// One wave that holds its stream for `ticks` of the 100 MHz constant clock
+// (s_memrealtime): a phase offset between the two micro-batch engines' streams, so
+// that one engine's memory-bound passes meet the other's MFMA-bound convs instead of
+// their own twins (srmi.trainer.FusedTrainer stagger).  Bounded: it always ends.
+__global__ void __launch_bounds__(64) stream_delay_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+int stream_delay_launch(int us, hipStream_t st) {
+  if (us <= 0) return 0;
+  if (us > 1000) return SRMI_ERR_ARG;
+  hipLaunchKernelGGL(stream_delay_kernel, dim3(1), dim3(64), 0, st, (unsigned long long)us * 100ull);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace srmi

@@ -149,6 +149,8 @@ def stamps():
     for epi in [int(v) for v in os.environ.get("KBENCH_EPI", "0").split(",")]:
         if epi == 5:
             args = (ptr(x), ptr(dp), None, N, H, W, 64, 64, 0, 5, None, ptr(r1), ptr(r1), None, None, ptr(t), ptr(part))
+        elif epi == 7:
+            args = (ptr(x), ptr(dp), None, N, H, W, 64, 64, 0, 7, None, ptr(r1), ptr(r1), None, None, ptr(t), ptr(part))
         elif epi == 1:
             args = (ptr(x), ptr(fp), ptr(pb), N, H, W, 64, 64, 0, 1, ptr(yb), None, None, None, None, None, ptr(part))
         elif epi == 4:
@@ -173,6 +175,14 @@ def stamps():
         print(f"conv epi={epi} workgroups {len(st)} clock {clk:.0f} MHz  WG span median {np.median(span_us):.2f} us "
               f"max {span_us.max():.2f} us; WG start spread {(rt[:, 0].max() - rt[:, 0].min()) / 100.0:.2f} us, "
               f"first start -> last end {(rt[:, 1].max() - rt[:, 0].min()) / 100.0:.2f} us")
+        if os.environ.get("KBENCH_WAVES"):  # per-wave barrier arrival (deferred body diagnostic)
+            for j in range(3):
+                arr = st[:, 40 + 8 * j:48 + 8 * j].astype(np.int64)
+                if not np.all(arr):
+                    break
+                rel_w = arr - arr[:, :1]
+                print(f"strip {j} barrier arrival vs wave 0, median per wave: "
+                      + " ".join(f"{int(np.median(rel_w[:, w])):6d}" for w in range(8)))
         names = ["prologue"] + [f"s{j}:{k}" for j in range(3) for k in ("issue", "mfma", "gstore", "epi", "barrier")]
         prev = np.zeros(len(st))
         for i, nm in enumerate(names, start=1):
