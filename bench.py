@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--cu-budget", type=int, default=None, help="CUs each engine sizes its launches for")
     ap.add_argument("--infer-region", type=int, default=4096, help="C5 HR region side (BASELINE: 4096)")
     ap.add_argument("--infer-iters", type=int, default=5)
-    ap.add_argument("--stagger-us", type=int, default=None, help="phase offset between micro-batch engines")
+    ap.add_argument("--no-train", action="store_true", help="skip the training leg (C4 / C5 lines only)")
     ap.add_argument("--no-dp-probe", action="store_true", help="skip the dp_overhead_1rank measurement")
     ap.add_argument("--force-dp", action="store_true",
                     help="diagnostic: the DP path (RCCL group, reducer stream, bucketed all-reduce) at one rank")
@@ -392,11 +392,15 @@ def main():
     dev = torch.device("cuda", info.local_rank)
     torch.cuda.set_device(dev)
     C, B = args.channels, args.batch
+    if args.no_train:  # diagnostic: the C4 / C5 lines alone
+        rec = {"edsr_x8": None if args.no_edsr else edsr_bench(dev, args.edsr_batch, 10, 3),
+               "inference": None if args.no_inference else inference_bench(dev, args.infer_region, args.infer_iters)}
+        print(json.dumps(rec), flush=True)
+        return
     spec = NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=10, nblocks=20,
                    cbottleneck=2, scale=4)
-    kw = {} if args.stagger_us is None else {"stagger_us": args.stagger_us}
     tr = FusedTrainer(spec, B, (48, 48), lr=1e-4, interp_loss=not args.no_interp_loss, info=info, device=dev, seed=0,
-                      micro=args.micro, cu_budget=args.cu_budget, **kw)
+                      micro=args.micro, cu_budget=args.cu_budget)
     hr = torch.tensor(synthetic_hr(B, C, 192, 1234 + info.rank)).to(dev)
 
     micro = tr.micro

@@ -165,11 +165,6 @@ int srmi_adam_step(float* p, const float* g, float* m, float* v, size_t n, int s
 /* y += a * x (flat fp32; sums micro-batch gradients) */
 int srmi_axpy(float* y, const float* x, float a, size_t n, void* stream);
 
-/* hold `stream` for `us` microseconds (1..1000) with one sleeping wave: the phase
- * offset between micro-batch engines (no reference counterpart: a scheduling
- * primitive of the MI355X engine) */
-int srmi_stream_delay(int us, void* stream);
-
 /* ---- op-level entry points (kernel parity tests, custom graphs) ---------- */
 /* dtype: SRMI_DTYPE_BF16 (x / yb / aux / packs bf16) or SRMI_DTYPE_F32 (fp32) */
 /* forward conv: x NHWC [N][H][W][Cin], packed filters (srmi_pack_conv),
@@ -200,8 +195,10 @@ int srmi_ca_forward(const void* u, const float* part, int nstrips, const float* 
                     const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, void* hb_out,
                     float* rec, int dtype, void* stream);
 /* the same CALayer forward on the bf16 engine's residual-stream pair: h = h_in
- * (fp32, when non-NULL) or hi_in + lo_in (bf16 pair); out: hi = bf16(h + s*u),
- * lo = bf16(h + s*u - hi) (in place allowed: lo_out == lo_in) */
+ * (fp32, when non-NULL) or the pair hi_in (bf16) + lo_in (int8 remainder); out:
+ * hi = bf16(h + s*u), lo = rint((h + s*u - hi) * 2^(15 - E(hi))) in [-127, 127]
+ * (E = hi's binary exponent; 0 for |hi| < 2^-111, inf, nan), i.e. 16 significant
+ * bits (in place allowed: lo_out == lo_in) */
 int srmi_ca_forward_pair(const void* u, const float* part, int nstrips, const float* w1, const float* b1,
                          const float* w2, const float* b2, int N, int HW, int C, int R, const float* h_in,
                          const void* hi_in, const void* lo_in, void* hi_out, void* lo_out, float* rec, void* stream);

@@ -1009,8 +1009,6 @@ int srmi_tiles_to_region(const float* tiles, const float* mean, const float* std
   return tiles_to_region_launch(tiles, mean, std, inv, C, ty, tx, gy, gx, out, S_(stream));
 }
 
-int srmi_stream_delay(int us, void* stream) { return stream_delay_launch(us, S_(stream)); }
-
 int srmi_axpy(float* y, const float* x, float a, size_t n, void* stream) {
   if (!y || !x) return SRMI_ERR_ARG;
   return scale_add_launch(y, x, a, n, S_(stream));

@@ -1006,13 +1006,31 @@ constexpr int kCaVec = SRMI_CA_VEC;
 
 // h_out = u * s + h_in; grid (chunks, N).  Residual-stream forms (MODE):
 //   CA_F32   fp32 h in, fp32 h + operand-type copy out (the exact-fp32 engine mode)
-//   CA_F32LO fp32 h in (the group input), h out as a bf16 pair hi + lo
-//   CA_LO    bf16 pair in and out
-// The pair: hi = bf16(h) -- the next conv's operand, stored anyway -- and
-// lo = bf16(h - hi), so hi + lo keeps h to ~2^-17 relative (16 significant bits
-// against the 8 of the bf16 operands the convs see) while the pass moves 10 B per
-// element instead of 12 (u 2 + h 4 in, h 4 + hb 2 out).
+//   CA_F32LO fp32 h in (the group input), h out as a pair hi + lo
+//   CA_LO    pair in and out
+// The pair: hi = bf16(h) -- the next conv's operand, stored anyway -- and an 8-bit
+// remainder lo = rint((h - hi) * 256 / ulp(hi)) (ulp of hi's binade, |h - hi| <=
+// ulp / 2, so |lo| <= 128, clamped to 127), so hi + lo * ulp / 256 keeps h to 16
+// significant bits (8 of hi + 8 of lo; the bf16 operands the convs see carry 8)
+// while the pass moves 8 B per element (u 2 + hi 2 + lo 1 in, hi 2 + lo 1 out)
+// instead of 12 with an fp32 stream (10 with a bf16 lo).
 enum CaMode { CA_F32 = 0, CA_F32LO = 1, CA_LO = 2 };
+
+// lo8 codec: s = 2^(15 - E) for hi = m * 2^E (1 <= |m| < 2), biased exponent e =
+// E + 127; 2^(E - 15) has biased exponent e - 15.  hi that is zero, subnormal, tiny
+// (e <= 15), inf or nan carries no remainder.
+__device__ __forceinline__ uint32_t lo8_encode(float h, float hi) {
+  const uint32_t e = (__float_as_uint(hi) >> 23) & 0xFFu;
+  const float s = __uint_as_float((269u - e) << 23);
+  float q = rintf((h - hi) * s);
+  q = fminf(fmaxf(q, -127.f), 127.f);
+  return (e > 15u && e < 255u) ? ((uint32_t)(int)q & 0xFFu) : 0u;
+}
+__device__ __forceinline__ float lo8_decode(float hi, uint32_t byte) {
+  const uint32_t e = (__float_as_uint(hi) >> 23) & 0xFFu;
+  const float q = (float)(int)(int8_t)(uint8_t)byte;
+  return (e > 15u && e < 255u) ? fmaf(q, __uint_as_float((e - 15u) << 23), hi) : hi;
+}
 
 template <typename T, int MODE>
 __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, const float* __restrict__ part,
@@ -1020,8 +1038,8 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
                                                      const float* __restrict__ b1, const float* __restrict__ w2,
                                                      const float* __restrict__ b2, int C, int CR,
                                                      const float* __restrict__ h_in, const bf16_t* __restrict__ hi_in,
-                                                     const bf16_t* __restrict__ lo_in, float* __restrict__ h_out,
-                                                     T* __restrict__ hb_out, bf16_t* __restrict__ lo_out,
+                                                     const uint8_t* __restrict__ lo_in, float* __restrict__ h_out,
+                                                     T* __restrict__ hb_out, uint8_t* __restrict__ lo_out,
                                                      float* __restrict__ rec) {
   __shared__ float red[4][64], m[64], z1[32], s[64];
   const int n = blockIdx.y, tid = threadIdx.x;
@@ -1058,9 +1076,10 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
     const size_t e = base + min(q0 + (size_t)k * blockDim.x, nq - 1) * 4;
     uu[k] = Unit4<T>::ld(u + e);
     if constexpr (MODE == CA_LO) {
-      const uint2 hi = *reinterpret_cast<const uint2*>(hi_in + e), lo = *reinterpret_cast<const uint2*>(lo_in + e);
-      hh[k] = make_float4(bf2f(hi.x & 0xFFFFu) + bf2f(lo.x & 0xFFFFu), bf2f(hi.x >> 16) + bf2f(lo.x >> 16),
-                          bf2f(hi.y & 0xFFFFu) + bf2f(lo.y & 0xFFFFu), bf2f(hi.y >> 16) + bf2f(lo.y >> 16));
+      const uint2 hi = *reinterpret_cast<const uint2*>(hi_in + e);
+      const uint32_t lo = *reinterpret_cast<const uint32_t*>(lo_in + e);
+      hh[k] = make_float4(lo8_decode(bf2f(hi.x & 0xFFFFu), lo & 0xFFu), lo8_decode(bf2f(hi.x >> 16), (lo >> 8) & 0xFFu),
+                          lo8_decode(bf2f(hi.y & 0xFFFFu), (lo >> 16) & 0xFFu), lo8_decode(bf2f(hi.y >> 16), lo >> 24));
     } else {
       hh[k] = *reinterpret_cast<const float4*>(h_in + e);
     }
@@ -1103,7 +1122,7 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
   //    boundary after this launch then has no dirty residual stream to flush
   [[maybe_unused]] const auto rh = wt_rsrc(h_out, (uint32_t)((size_t)gridDim.y * HW * C * 4));
   const auto rhb = wt_rsrc(hb_out, (uint32_t)((size_t)gridDim.y * HW * C * sizeof(T)));
-  [[maybe_unused]] const auto rlo = wt_rsrc(lo_out, (uint32_t)((size_t)gridDim.y * HW * C * 2));
+  [[maybe_unused]] const auto rlo = wt_rsrc(lo_out, (uint32_t)((size_t)gridDim.y * HW * C));
 #pragma unroll
   for (int k = 0; k < NU; ++k) {
     const size_t q = q0 + (size_t)k * blockDim.x;
@@ -1120,10 +1139,10 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
       Unit4<T>::st(rhb, hb_out, e, o);
     } else {
       const uint2 hi = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-      const uint2 lo = make_uint2(pack2(o[0] - bf2f(hi.x & 0xFFFFu), o[1] - bf2f(hi.x >> 16)),
-                                  pack2(o[2] - bf2f(hi.y & 0xFFFFu), o[3] - bf2f(hi.y >> 16)));
+      const uint32_t lo = lo8_encode(o[0], bf2f(hi.x & 0xFFFFu)) | (lo8_encode(o[1], bf2f(hi.x >> 16)) << 8) |
+                          (lo8_encode(o[2], bf2f(hi.y & 0xFFFFu)) << 16) | (lo8_encode(o[3], bf2f(hi.y >> 16)) << 24);
       st_wt8(rhb, hb_out, (uint32_t)(e * 2), hi);
-      st_wt8(rlo, lo_out, (uint32_t)(e * 2), lo);
+      __builtin_amdgcn_raw_buffer_store_b32(lo, rlo, (uint32_t)e, 0, 16);
     }
   }
 }
@@ -1139,8 +1158,9 @@ int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1
                   float* rec, int f32, hipStream_t st, const void* hi_in, const void* lo_in, void* lo_out) {
   if (C != 64 || C % R || (C / R) > 32 || (C / R) % 4 || (HW * C) % 8) return SRMI_ERR_SHAPE;
   const dim3 grid(ca_grid_x(HW, C), N);
-  const bf16_t *hi = static_cast<const bf16_t*>(hi_in), *lo = static_cast<const bf16_t*>(lo_in);
-  bf16_t* lout = static_cast<bf16_t*>(lo_out);
+  const bf16_t* hi = static_cast<const bf16_t*>(hi_in);
+  const uint8_t* lo = static_cast<const uint8_t*>(lo_in);
+  uint8_t* lout = static_cast<uint8_t*>(lo_out);
   if (f32) {
     if (!h_in || !h_out || lo_out || hi_in) return SRMI_ERR_ARG;
     hipLaunchKernelGGL((ca_fwd_kernel<float, CA_F32>), grid, dim3(256), 0, st, static_cast<const float*>(u), part,
@@ -1566,23 +1586,6 @@ int scale_add_launch(float* y, const float* x, float a, size_t n, hipStream_t st
   size_t blocks = (n + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(scale_add_kernel, dim3(blocks), dim3(256), 0, st, y, x, a, n);
-  SRMI_CHECK_LAUNCH();
-  return 0;
-}
-
-// One wave that holds its stream for `ticks` of the 100 MHz constant clock
-// (s_memrealtime): a phase offset between the two micro-batch engines' streams, so
-// that one engine's memory-bound passes meet the other's MFMA-bound convs instead of
-// their own twins (srmi.trainer.FusedTrainer stagger).  Bounded: it always ends.
-__global__ void __launch_bounds__(64) stream_delay_kernel(unsigned long long ticks) {
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
-}
-
-int stream_delay_launch(int us, hipStream_t st) {
-  if (us <= 0) return 0;
-  if (us > 1000) return SRMI_ERR_ARG;
-  hipLaunchKernelGGL(stream_delay_kernel, dim3(1), dim3(64), 0, st, (unsigned long long)us * 100ull);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

@@ -155,7 +155,6 @@ int pack_one_launch(const float* w, const float* b, int Cout, int Cin, int ps, v
                     float* pbias, int f32, hipStream_t st);
 
 int scale_add_launch(float* y, const float* x, float a, size_t n, hipStream_t st);
-int stream_delay_launch(int us, hipStream_t st);
 
 // tiled-region data path (tiles.hip)
 int region_to_tiles_launch(const float* region, int C, int H, int W, int ty, int tx, float* tiles, float* mean,

@@ -247,8 +247,13 @@ template <int WV, int NW = 4>
 __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, int chunk, int cb) {
   using namespace v4;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  constexpr int NT = NW == 4 ? 9 : (WV < 4 ? 4 : 5);                     // N tiles of this wave
-  constexpr int J0 = NW == 4 ? 9 * WV : (WV < 4 ? 4 * WV : 16 + 5 * (WV - 4));  // its first N tile
+#ifndef SRMI_WG_OLD5
+#define SRMI_WG_OLD5 0  // 1: the older half (waves 0-3, the MFMA-arbitration winners) takes 5 tiles
+#endif
+  constexpr int NT = NW == 4 ? 9 : ((WV < 4) == (SRMI_WG_OLD5 != 0) ? 5 : 4);  // N tiles of this wave
+  constexpr int J0 = NW == 4 ? 9 * WV
+                             : (SRMI_WG_OLD5 ? (WV < 4 ? 5 * WV : 20 + 4 * (WV - 4))
+                                             : (WV < 4 ? 4 * WV : 16 + 5 * (WV - 4)));  // its first N tile
   constexpr bool kMain = WV < 4;  // DMA + bias gradient
   const int tid = threadIdx.x, lane = tid & 63;
   constexpr int wave = WV & 3, wave_s = WV & 3;
@@ -422,6 +427,9 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   wait_groups(min(PF, np) - 1, 0);
   __syncthreads();
   WSTAMP(1);
+#ifdef SRMI_WG_PRIO
+  if constexpr (NW == 8 && WV >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
 
   // fragments double-buffered across K-steps; a pair has 3 K-steps, so the pair loop
   // is unrolled by two (np is even) to keep the buffer parity compile-time.  8 waves

@@ -75,7 +75,6 @@ _SIGS = {
     "srmi_head_forward": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, C.c_int, P], C.c_int),
     "srmi_tail_forward": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int, P], C.c_int),
     "srmi_axpy": ([P, P, C.c_float, C.c_size_t, P], C.c_int),
-    "srmi_stream_delay": ([C.c_int, P], C.c_int),
     "srmi_region_to_tiles": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P], C.c_int),
     "srmi_tiles_to_region": ([P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),
     "srmi_batch_prep": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P], C.c_int),

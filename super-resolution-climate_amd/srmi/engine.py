@@ -201,12 +201,6 @@ def axpy(y: torch.Tensor, x: torch.Tensor, a: float = 1.0, stream=None):
     return y
 
 
-def stream_delay(us: int, stream=None):
-    """Hold `stream` for `us` microseconds (one sleeping wave; srmi_stream_delay)."""
-    if us > 0:
-        call("srmi_stream_delay", int(us), stream_handle(stream))
-
-
 def adam_step(p, g, m, v, step: int, lr: float, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, stream=None):
     call("srmi_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), int(step), float(lr), float(betas[0]),
          float(betas[1]), float(eps), float(weight_decay), stream_handle(stream))

@@ -27,7 +27,7 @@ from . import checkpoint as ckpt
 from ._lib import SRMI_LOSS_MEAN, SRMI_LOSS_RMSE
 from .config import check_fused_task
 from .dist import DistInfo, GradReducer, allreduce_sum_
-from .engine import Engine, NetSpec, adam_step, axpy, downsample, stream_delay, upsample
+from .engine import Engine, NetSpec, adam_step, axpy, downsample, upsample
 
 LOSS_KINDS = {"l2": SRMI_LOSS_RMSE, "charbonnier": SRMI_LOSS_MEAN}
 CHARBONNIER_EPS = 1e-6  # ModelTrainer.eps, sres/controller/dual_trainer.py:122
@@ -70,7 +70,7 @@ class FusedTrainer:
                  eps: float = 1e-8, weight_decay: float = 0.0, interp_loss: bool = True,
                  info: Optional[DistInfo] = None, device: Optional[torch.device] = None, seed: int = 0,
                  params: Optional[torch.Tensor] = None, micro: Optional[int] = None, loss_fn: str = "l2",
-                 cu_budget: Optional[int] = None, task=None, stagger_us: int = 0):
+                 cu_budget: Optional[int] = None, task=None):
         """task: the task config section (default: the active srmi ConfigContext's,
         if any); apply_network features the fused step does not implement
         (data_downsample > 1, target channel subsets) raise NotImplementedError."""
@@ -92,10 +92,6 @@ class FusedTrainer:
             raise ValueError(f"batch {batch} not divisible into {micro} micro-batches")
         self.micro = micro
         self.mb = batch // micro
-        # phase offset of engine k's forward and backward (k * stagger_us): the
-        # engines run the same kernel sequence and would otherwise meet their own
-        # memory-bound CA passes at the same time
-        self.stagger_us = int(stagger_us)
         # CUs each engine's launches are sized for (0 = the whole chip)
         budget = (256 // micro if micro > 1 else 0) if cu_budget is None else int(cu_budget)
         self.engines = [Engine(spec, self.mb, lr_hw, train=True, device=self.device, cu_budget=budget)
@@ -176,8 +172,6 @@ class FusedTrainer:
                 self.miloss4[k].zero_()
                 continue
             with self._ctx(k):
-                if k and self.stagger_us:
-                    stream_delay(k * self.stagger_us)
                 downsample(hr[sl], s, out=self.lrbuf[sl])
                 eng.forward(self.params, self.lrbuf[sl], out=self.sr[sl])
                 self._loss_partial(eng, self.sr[sl], hr[sl], self.mloss4[k], count,
@@ -207,8 +201,6 @@ class FusedTrainer:
                         for ev in evs[k]:
                             ev.record()
                     continue
-                if k and self.stagger_us:
-                    stream_delay(k * self.stagger_us)
                 if self.dy is not None:
                     eng.backward(self.params, self.lrbuf[sl], self.mgrads[k], dy=self.dy[sl], events=evs[k])
                 else:

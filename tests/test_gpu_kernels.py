@@ -281,10 +281,21 @@ def test_channel_attention_fwd_bwd(dt):
     np.testing.assert_allclose(brec[:N * 160].view(N, 160)[:, 96:].double().cpu().numpy(), U.grad.sum((1, 2)).numpy(), rtol=1e-4, atol=1e-3)
 
 
+def lo8_decode(hi: torch.Tensor, lo: torch.Tensor) -> torch.Tensor:
+    """The residual pair's value hi + lo * 2^(E - 15) (E = hi's binary exponent;
+    no remainder for |hi| < 2^-111, inf, nan) -- include/srmi.h srmi_ca_forward_pair."""
+    h = hi.double().cpu()
+    q = lo.cpu().view(torch.int8).double()
+    e = torch.frexp(h.float())[1].double() - 1  # hi = m * 2^e, 1 <= |m| < 2
+    ok = torch.isfinite(h) & (h.abs() >= 2.0 ** -111)
+    return torch.where(ok, h + q * torch.pow(2.0, e - 15), h)
+
+
 def test_channel_attention_forward_residual_pair():
-    """The bf16 engine's residual stream as a (hi, lo) bf16 pair: the group's first
-    CALayer add takes the fp32 group input, the next ones the pair, in place.  hi is
-    h to bf16 precision and hi + lo keeps h to 2^-16 (rel-L2) over a chain of adds."""
+    """The bf16 engine's residual stream as a pair (hi bf16, lo int8 remainder): the
+    group's first CALayer add takes the fp32 group input, the next ones the pair, in
+    place.  hi is h to bf16 precision and the pair keeps h to 16 significant bits
+    (2^-16 rel-L2) over a chain of adds."""
     d = dev()
     N, H, W, Cc, R = 2, 48, 48, 64, 2
     g = torch.Generator(device="cpu").manual_seed(8)
@@ -296,7 +307,7 @@ def test_channel_attention_forward_residual_pair():
     h_in = torch.randn(N, H, W, Cc, generator=g).to(d)
     h_ref = h_in.double().cpu()
     hi = [torch.empty(N, H, W, Cc, dtype=torch.bfloat16, device=d) for _ in range(2)]
-    lo = torch.empty(N, H, W, Cc, dtype=torch.bfloat16, device=d)
+    lo = torch.empty(N, H, W, Cc, dtype=torch.uint8, device=d)
     rec = torch.empty(N, 160, device=d)
     for step in range(6):
         u = bf(torch.randn(N, H, W, Cc, generator=g)).to(d)
@@ -310,9 +321,9 @@ def test_channel_attention_forward_residual_pair():
         m = u.double().cpu().mean((1, 2))
         s = torch.sigmoid(torch.relu(m @ w1.double().cpu().T + b1.double().cpu()) @ w2.double().cpu().T + b2.double().cpu())
         h_ref = h_ref + u.double().cpu() * s[:, None, None, :]
-        got = hi[step % 2].double().cpu() + lo.double().cpu()
-        # the pair's rounding error is relative to the stream's magnitude (lo carries
-        # bf16 precision of a remainder below hi's half ulp), not to each element
+        got = lo8_decode(hi[step % 2], lo)
+        # lo resolves 1/256 of hi's ulp: the pair's rounding error is 2^-16 of each
+        # element (the fp32 arithmetic of the adds is in the same range)
         assert rel_l2(got, h_ref) < 2 ** -16
         assert float((got - h_ref).abs().max()) <= 2 ** -14 * float(h_ref.abs().max())
         # hi is within half a bf16 ulp (plus lo's rounding) of h: the conv operand
