@@ -55,9 +55,20 @@ struct Conv2Smem {
 // per row and channel half), whose tiles start at ct0.
 template <int NPT, int EPI, int NCT = 4>
 struct EpiPre {
-  float4 r1[NPT][NCT];
-  uint2 aux[NPT][NCT];
+  float4 r1[NPT][NCT];     // (DG_ACC_CA, DG_ACC: the gradient streams' 16-byte chunks of the
+  uint2 aux[NPT][NCT];     //  wave's 1 KiB store runs, and u's 8 bytes beside them -- see
+  float4 r2[NPT][NCT];     //  conv_epilogue2)
 };
+
+// the gradient-stream epilogues (DG_ACC_CA, DG_ACC) add their fp32 operands to the
+// staged dgrad in the 1 KiB run layout of the stores instead of the MFMA layout
+#ifndef SRMI_DGACC_RUN
+#define SRMI_DGACC_RUN 1
+#endif
+template <int EPI>
+constexpr bool epi_run() {
+  return EPI == EPI_DG_ACC_CA || (SRMI_DGACC_RUN && EPI == EPI_DG_ACC);
+}
 
 // one (pt, c) element (idx = pt * NCT + c), issued one or two per K-step
 template <int NPT, int EPI, int NCT>
@@ -69,14 +80,31 @@ __device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT
     const size_t pix = (size_t)n * HW + (size_t)y * p.W + x0 + pt * 16 + fr;
     const size_t o = pix * p.Cout + cb * 64 + (ct0 + c) * 16 + fk * 4;
     if constexpr (EPI == EPI_RESID) e.r1[pt][c] = *reinterpret_cast<const float4*>(p.r1 + o);
-    if constexpr (EPI == EPI_DG_ACC) {
+    if constexpr (EPI == EPI_DG_ACC && !epi_run<EPI>()) {
       e.r1[pt][c] = p.r1 ? *reinterpret_cast<const float4*>(p.r1 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
       e.aux[pt][c] = p.part ? *reinterpret_cast<const uint2*>(p.aux + o) : make_uint2(0, 0);
     }
     if constexpr (EPI == EPI_DG_RELUMASK) e.aux[pt][c] = *reinterpret_cast<const uint2*>(p.aux + o);
-    if constexpr (EPI == EPI_DG_ACC_CA) {
-      e.r1[pt][c] = *reinterpret_cast<const float4*>(p.r1 + o);
-      e.aux[pt][c] = *reinterpret_cast<const uint2*>(p.aux + o);
+    if constexpr (epi_run<EPI>()) {
+      // load q of the wave = 16-byte chunk `lane` of its q-th 1 KiB output run (the
+      // layout of the fp32 store loop of conv_epilogue2): full 128-byte lines, half
+      // the requests of the MFMA layout's 64-byte pieces (and a quarter for u)
+      constexpr bool kSh = NCT < 4;
+      constexpr int HALF = NPT * 8, JW = kSh ? NPT : 2 * NPT;  // runs per half-row per wave
+      const int h = idx / JW, j = idx % JW, lane = fk * 16 + fr;
+      const int i = kSh ? 2 * j + (ct0 >> 1) : j;
+      const int lin = i * 1024 + lane * 16, lpx = lin >> 8, ch = (lin >> 4) & 15;
+      const size_t oc = ((size_t)n * HW + (size_t)y * p.W + x0 + h * HALF + lpx) * p.Cout + cb * 64 + ch * 4;
+      if constexpr (EPI == EPI_DG_ACC_CA) {
+        e.r1[pt][c] = *reinterpret_cast<const float4*>(p.r1 + oc);  // (load q = idx at [q / NCT][q % NCT])
+        e.aux[pt][c] = *reinterpret_cast<const uint2*>(p.aux + oc);
+      } else {  // DG_ACC: every operand optional (uniform branches)
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        e.r1[pt][c] = p.r1 ? *reinterpret_cast<const float4*>(p.r1 + oc) : z;
+        e.r2[pt][c] = p.r2 ? *reinterpret_cast<const float4*>(p.r2 + oc) : z;
+        e.aux[pt][c] = p.part ? *reinterpret_cast<const uint2*>(p.aux + oc) : make_uint2(0, 0);
+      }
+      (void)o;
     }
   }
 }
@@ -118,7 +146,8 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
   float ps0[NCT][4], ps1[NCT][4];
   // fp32 output staged through LDS (DG_ACC, whose epilogue also reads r2/r3 from
   // global memory, measured faster with direct stores)
-  constexpr bool kF = (EPI == EPI_RESID || EPI == EPI_DG_ACC_CA);
+  constexpr bool kRun = epi_run<EPI>();  // g added in the run layout
+  constexpr bool kF = (EPI == EPI_RESID || kRun);
   float4 fv[NPT][NCT];  // fp32 outputs, written back through LDS after the loop
   uint2 bv[NPT][NCT];   // bf16 outputs, likewise
 #pragma unroll
@@ -156,7 +185,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
         v[2] = p.alpha * relu_mask(tt.y & 0xFFFFu, v[2]);
         v[3] = p.alpha * relu_mask(tt.y >> 16, v[3]);
       }
-      if constexpr (EPI == EPI_DG_ACC) {
+      if constexpr (EPI == EPI_DG_ACC && !kRun) {
         const float4 rr = e.r1[pt][c];
         v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
         if (p.r2) {
@@ -177,16 +206,8 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
           ps1[c][3] += v[3] * bf2f(uu.y >> 16);
         }
       }
-      if constexpr (EPI == EPI_DG_ACC_CA) {
-        const float4 rr = e.r1[pt][c];
-        v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
-        fv[pt][c] = make_float4(v[0], v[1], v[2], v[3]);
-        const uint2 uu = e.aux[pt][c];
-        ps0[c][0] += v[0]; ps0[c][1] += v[1]; ps0[c][2] += v[2]; ps0[c][3] += v[3];
-        ps1[c][0] += v[0] * bf2f(uu.x & 0xFFFFu);
-        ps1[c][1] += v[1] * bf2f(uu.x >> 16);
-        ps1[c][2] += v[2] * bf2f(uu.y & 0xFFFFu);
-        ps1[c][3] += v[3] * bf2f(uu.y >> 16);
+      if constexpr (kRun) {
+        fv[pt][c] = make_float4(v[0], v[1], v[2], v[3]);  // dx; g is added in the store loop
         continue;  // no bf16 copy
       }
       if constexpr (kPart1) {
@@ -199,10 +220,11 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
   // fp32 output: staged in LDS in two halves of the row (256 B per pixel,
   // chunk-swizzled) and written back as 1 KiB contiguous runs (full lines)
   if constexpr (kF) {
-    if (p.yf) {
+    if (kRun || p.yf) {
       constexpr int HALF = NPT * 8;  // pixels per half
       constexpr int RUNS = HALF / 4;  // 1 KiB runs per half
       const auto rf = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
+      [[maybe_unused]] const auto rbb = wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
       const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -221,15 +243,42 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
         for (int j = 0; j < (kShared ? RUNS / 2 : RUNS); ++j) {
           const int i = kShared ? 2 * j + half_id : j;
           const int lin = i * 1024 + lane * 16, lpx = lin >> 8, c = (lin >> 4) & 15;
-          const float4 val = *reinterpret_cast<const float4*>(stage + lpx * 256 + ((c ^ (lpx & 15)) << 4));
+          float4 val = *reinterpret_cast<const float4*>(stage + lpx * 256 + ((c ^ (lpx & 15)) << 4));
+          if constexpr (kRun) {
+            // g += dx in the run layout; the lane's channels 4c..4c+3 (c = lane & 15)
+            // are the same in every run, so its sums accumulate in registers
+            const int q = h * (kShared ? RUNS / 2 : RUNS) + j;
+            const float4 gg = e.r1[q / NCT][q % NCT];
+            const uint2 uu = e.aux[q / NCT][q % NCT];
+            val.x += gg.x; val.y += gg.y; val.z += gg.z; val.w += gg.w;
+            if constexpr (EPI == EPI_DG_ACC) {
+              const float4 g2 = e.r2[q / NCT][q % NCT];
+              val.x += g2.x; val.y += g2.y; val.z += g2.z; val.w += g2.w;
+              if (p.r3) {
+                const float4 g3 = *reinterpret_cast<const float4*>(
+                    p.r3 + (pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4);
+                val.x += g3.x; val.y += g3.y; val.z += g3.z; val.w += g3.w;
+              }
+            }
+            ps0[0][0] += val.x; ps0[0][1] += val.y; ps0[0][2] += val.z; ps0[0][3] += val.w;
+            ps1[0][0] += val.x * bf2f(uu.x & 0xFFFFu);
+            ps1[0][1] += val.y * bf2f(uu.x >> 16);
+            ps1[0][2] += val.z * bf2f(uu.y & 0xFFFFu);
+            ps1[0][3] += val.w * bf2f(uu.y >> 16);
+          }
           st_wt16(rf, p.yf, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 4), val);
+          if constexpr (EPI == EPI_DG_ACC) {
+            if (p.yb)  // its bf16 copy: 512 contiguous bytes per instruction
+              st_wt8(rbb, p.yb, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 2),
+                     make_uint2(pack2(val.x, val.y), pack2(val.z, val.w)));
+          }
         }
         stage_sync();
       }
     }
   }
   // bf16 output staged in LDS (the row, 128 B per pixel, chunk-swizzled)
-  if constexpr (EPI != EPI_DG_ACC_CA) {
+  if constexpr (!kRun) {
     if (p.yb) {
 #pragma unroll
       for (int pt = 0; pt < NPT; ++pt)
@@ -240,12 +289,12 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
         }
     }
   }
-  stage_sync();
+  if constexpr (!kRun) stage_sync();  // (kRun: the staging loop above ended with one)
   // ... and written back as full 128-byte lines: one 1 KiB contiguous run per
   // instruction (the per-lane 8-byte stores of the MFMA layout touched 32-byte
   // pieces of 16 lines each and stalled the store path for ~2 K cycles per strip).
   // The wave's own LDS writes precede its reads (in-order LDS per wave).
-  if (EPI != EPI_DG_ACC_CA && p.yb) {
+  if (!kRun && p.yb) {
     const auto rb = wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
 #pragma unroll
     for (int j = 0; j < (kShared ? NPT : NPT * 2); ++j) {
@@ -261,7 +310,37 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       st_wt16(rb, p.yb, (uint32_t)((line + c * 8) * 2), val);
     }
   }
-  if constexpr (kPart1 || kPart2) {
+  if constexpr (kRun) {
+   if (EPI == EPI_DG_ACC_CA || p.part) {  // (uniform)
+    // lanes l, l ^ 16, l ^ 32, l ^ 48 hold the same 4 channels: fixed-order xor
+    // sums, then one 64-channel partial per wave in red[wave][2][64], summed over
+    // the waves in wave order
+    const int wave = tid >> 6;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a = ps0[0][r], b = ps1[0][r];
+      a += __shfl_xor(a, 16, 64);
+      b += __shfl_xor(b, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      b += __shfl_xor(b, 32, 64);
+      if (lane < 16) {
+        red[(wave * 2 + 0) * 64 + lane * 4 + r] = a;
+        red[(wave * 2 + 1) * 64 + lane * 4 + r] = b;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    constexpr int NWV = kShared ? 8 : 4;
+    if (tid < 128) {
+      const int s = tid >> 6, c = tid & 63;
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) sum += red[(w * 2 + s) * 64 + c];
+      p.part[((size_t)n * nstrips + strip) * p.part_stride + s * 64 + c] = sum;
+    }
+   }
+  } else if constexpr (kPart1 || kPart2) {
     const bool on = EPI != EPI_DG_ACC || p.part;
     if (on) {
 #pragma unroll

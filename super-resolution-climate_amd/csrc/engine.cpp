@@ -885,7 +885,7 @@ int srmi_conv3x3(const void* x, const void* wpack, const float* bias, int N, int
   p.r3 = r3;
   p.aux = (const bf16_t*)aux;
   p.part = part;
-  p.part_stride = (epi == EPI_DG_ACC) ? 128 : Cout;
+  p.part_stride = (epi == EPI_DG_ACC || epi == EPI_DG_ACC_CA) ? 128 : Cout;
   p.alpha = alpha;
   return conv3x3_launch(p, epi, S_(stream));
 }

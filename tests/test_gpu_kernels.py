@@ -160,6 +160,16 @@ def test_conv_dgrad_epilogues(N, H, W, dt):
     ds = part[:, :, 64:].sum(1).double().cpu()
     np.testing.assert_allclose(Gs.numpy(), exp.sum((1, 2)).numpy(), rtol=1e-4, atol=2e-3)
     np.testing.assert_allclose(ds.numpy(), (exp * u.double().cpu()).sum((1, 2)).numpy(), rtol=1e-4, atol=2e-3)
+    # the RCAB form (epi 7): g += dx in place, sums of g and g*u, nothing else
+    yf = r1.clone()
+    part.zero_()
+    conv(dy, dp, None, N, H, W, 64, 64, 7, yf=yf, r1=yf, aux=u, part=part, dt=dt)
+    exp = ref + r1.double().cpu()
+    np.testing.assert_allclose(yf.double().cpu().numpy(), exp.numpy(), rtol=1e-5, atol=5e-5)
+    Gs = part[:, :, :64].sum(1).double().cpu()
+    ds = part[:, :, 64:].sum(1).double().cpu()
+    np.testing.assert_allclose(Gs.numpy(), exp.sum((1, 2)).numpy(), rtol=1e-4, atol=2e-3)
+    np.testing.assert_allclose(ds.numpy(), (exp * u.double().cpu()).sum((1, 2)).numpy(), rtol=1e-4, atol=2e-3)
 
 
 @pytest.mark.parametrize("dt", DTS)
