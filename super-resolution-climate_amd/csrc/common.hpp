@@ -36,6 +36,36 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
 }
 
+// The pair: a value as hi = bf16(h) plus an 8-bit remainder lo in units of 1/256 of
+// hi's ulp -- 16 significant bits in 3 bytes (the bf16 engine's residual stream and
+// its filter-gradient partial slabs).
+// lo8 codec: s = 2^(15 - E) for hi = m * 2^E (1 <= |m| < 2), biased exponent e =
+// E + 127; 2^(E - 15) has biased exponent e - 15.  hi that is zero, subnormal, tiny
+// (e <= 15), inf or nan carries no remainder.
+__device__ __forceinline__ uint32_t lo8_encode(float h, float hi) {
+  const uint32_t e = (__float_as_uint(hi) >> 23) & 0xFFu;
+  const float s = __uint_as_float((269u - e) << 23);
+  float q = rintf((h - hi) * s);
+  q = fminf(fmaxf(q, -127.f), 127.f);
+  return (e > 15u && e < 255u) ? ((uint32_t)(int)q & 0xFFu) : 0u;
+}
+__device__ __forceinline__ float lo8_decode(float hi, uint32_t byte) {
+  const uint32_t e = (__float_as_uint(hi) >> 23) & 0xFFu;
+  const float q = (float)(int)(int8_t)(uint8_t)byte;
+  return (e > 15u && e < 255u) ? fmaf(q, __uint_as_float((e - 15u) << 23), hi) : hi;
+}
+
+// four elements: hi as 4 bf16 (uint2), lo as 4 bytes (uint32, element 0 lowest)
+__device__ __forceinline__ float4 pair_decode4(uint2 hi, uint32_t lo) {
+  return make_float4(lo8_decode(bf2f(hi.x & 0xFFFFu), lo & 0xFFu), lo8_decode(bf2f(hi.x >> 16), (lo >> 8) & 0xFFu),
+                     lo8_decode(bf2f(hi.y & 0xFFFFu), (lo >> 16) & 0xFFu), lo8_decode(bf2f(hi.y >> 16), lo >> 24));
+}
+__device__ __forceinline__ uint32_t pair_encode4(float a, float b, float c, float d, uint2& hi) {
+  hi = make_uint2(pack2(a, b), pack2(c, d));
+  return lo8_encode(a, bf2f(hi.x & 0xFFFFu)) | (lo8_encode(b, bf2f(hi.x >> 16)) << 8) |
+         (lo8_encode(c, bf2f(hi.y & 0xFFFFu)) << 16) | (lo8_encode(d, bf2f(hi.y >> 16)) << 24);
+}
+
 // Write-through (sc1) 16-byte stores.  A kernel's end-of-launch release writes
 // back every dirty L2 line before the next dependent kernel starts (MI355X
 // kernel boundary: ~1.8 us + dirty bytes / 6 TB/s); stores that write through

@@ -1016,22 +1016,7 @@ constexpr int kCaVec = SRMI_CA_VEC;
 // instead of 12 with an fp32 stream (10 with a bf16 lo).
 enum CaMode { CA_F32 = 0, CA_F32LO = 1, CA_LO = 2 };
 
-// lo8 codec: s = 2^(15 - E) for hi = m * 2^E (1 <= |m| < 2), biased exponent e =
-// E + 127; 2^(E - 15) has biased exponent e - 15.  hi that is zero, subnormal, tiny
-// (e <= 15), inf or nan carries no remainder.
-__device__ __forceinline__ uint32_t lo8_encode(float h, float hi) {
-  const uint32_t e = (__float_as_uint(hi) >> 23) & 0xFFu;
-  const float s = __uint_as_float((269u - e) << 23);
-  float q = rintf((h - hi) * s);
-  q = fminf(fmaxf(q, -127.f), 127.f);
-  return (e > 15u && e < 255u) ? ((uint32_t)(int)q & 0xFFu) : 0u;
-}
-__device__ __forceinline__ float lo8_decode(float hi, uint32_t byte) {
-  const uint32_t e = (__float_as_uint(hi) >> 23) & 0xFFu;
-  const float q = (float)(int)(int8_t)(uint8_t)byte;
-  return (e > 15u && e < 255u) ? fmaf(q, __uint_as_float((e - 15u) << 23), hi) : hi;
-}
-
+// (lo8_encode / lo8_decode, the pair codec: common.hpp)
 template <typename T, int MODE>
 __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, const float* __restrict__ part,
                                                      int nstrips, int HW, const float* __restrict__ w1,
@@ -1076,10 +1061,7 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
     const size_t e = base + min(q0 + (size_t)k * blockDim.x, nq - 1) * 4;
     uu[k] = Unit4<T>::ld(u + e);
     if constexpr (MODE == CA_LO) {
-      const uint2 hi = *reinterpret_cast<const uint2*>(hi_in + e);
-      const uint32_t lo = *reinterpret_cast<const uint32_t*>(lo_in + e);
-      hh[k] = make_float4(lo8_decode(bf2f(hi.x & 0xFFFFu), lo & 0xFFu), lo8_decode(bf2f(hi.x >> 16), (lo >> 8) & 0xFFu),
-                          lo8_decode(bf2f(hi.y & 0xFFFFu), (lo >> 16) & 0xFFu), lo8_decode(bf2f(hi.y >> 16), lo >> 24));
+      hh[k] = pair_decode4(*reinterpret_cast<const uint2*>(hi_in + e), *reinterpret_cast<const uint32_t*>(lo_in + e));
     } else {
       hh[k] = *reinterpret_cast<const float4*>(h_in + e);
     }
@@ -1138,9 +1120,8 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
       st_wt16(rh, h_out, (uint32_t)(e * 4), make_float4(o[0], o[1], o[2], o[3]));
       Unit4<T>::st(rhb, hb_out, e, o);
     } else {
-      const uint2 hi = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-      const uint32_t lo = lo8_encode(o[0], bf2f(hi.x & 0xFFFFu)) | (lo8_encode(o[1], bf2f(hi.x >> 16)) << 8) |
-                          (lo8_encode(o[2], bf2f(hi.y & 0xFFFFu)) << 16) | (lo8_encode(o[3], bf2f(hi.y >> 16)) << 24);
+      uint2 hi;
+      const uint32_t lo = pair_encode4(o[0], o[1], o[2], o[3], hi);
       st_wt8(rhb, hb_out, (uint32_t)(e * 2), hi);
       __builtin_amdgcn_raw_buffer_store_b32(lo, rlo, (uint32_t)e, 0, 16);
     }

@@ -235,6 +235,10 @@ constexpr int NGP = 2 * GD + 2 * GX;                             // groups per p
 }  // namespace v4
 
 
+#ifndef SRMI_SLAB_WT
+#define SRMI_SLAB_WT 0  // 1: partial slabs stored write-through
+#endif
+
 // The body is instantiated once per wave (WV = wave index): the wave's DMA groups,
 // taps and tile rotation are compile-time constants (no SGPR pressure, no branches).
 //
@@ -510,6 +514,9 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   // (N tile J, slot ct of rotation `wave`) -> the 4-wave position (wave J / 9, tile
   // J % 9, the slot of the same output-channel tile under that wave's rotation)
   const size_t soff = (size_t)chunk * Cout * 576 + (size_t)cb * (64 * 576);
+  // (write-through: the slab leaves the XCD's L2 while the other waves still
+  //  compute, instead of in the dirty-line flush at the end of the launch)
+  [[maybe_unused]] const auto rsl = wt_rsrc(p.slab, (uint32_t)((size_t)(chunk + 1) * Cout * 576 * 4));
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -517,7 +524,11 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
       const int J = J0 + t, w4 = J / 9, t4 = J % 9, s4 = (ct + wave - w4) & 3;
       const float4 v = make_float4(acc[ct][t][0], acc[ct][t][1], acc[ct][t][2], acc[ct][t][3]);
       const size_t o = soff + (size_t)w4 * (9 * 4 * 256) + ((t4 * 4 + s4) * 64 + lane) * 4;
+#if SRMI_SLAB_WT
+      st_wt16(rsl, p.slab, (uint32_t)(o * 4), v);
+#else
       *reinterpret_cast<float4*>(p.slab + o) = v;
+#endif
     }
   if (kMain && (lane & 15) == 0) {
 #pragma unroll
