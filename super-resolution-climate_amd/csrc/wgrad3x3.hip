@@ -236,7 +236,7 @@ constexpr int NGP = 2 * GD + 2 * GX;                             // groups per p
 
 
 #ifndef SRMI_SLAB_WT
-#define SRMI_SLAB_WT 0  // 1: partial slabs stored write-through
+#define SRMI_SLAB_WT 1  // partial slabs stored write-through (in-step A/B +1.1 %)
 #endif
 
 // The body is instantiated once per wave (WV = wave index): the wave's DMA groups,
@@ -508,9 +508,11 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   }
 
   // partial slab in the MFMA-native order (slab layout 1): every store instruction
-  // writes 1 KiB contiguous; wgrad_reduce_kernel maps it back to (co, ci, tap)
-  // (plain stores: written through, the wgrad launch was 0.9 us shorter but the
-  // reduce that re-reads the slabs right after it 1.9 us longer)
+  // writes 1 KiB contiguous; wgrad_reduce_kernel maps it back to (co, ci, tap).
+  // Write-through: in the step (two engines, the reduction one or two launches
+  // later) +1.1 % over plain stores, whose 9.4 MB of dirty lines per fused launch
+  // left in the flush at its end (a standalone wgrad + reduce pair measured the
+  // other way round in round 2: the launch 0.9 us shorter, the reduce 1.9 us longer)
   // (N tile J, slot ct of rotation `wave`) -> the 4-wave position (wave J / 9, tile
   // J % 9, the slot of the same output-channel tile under that wave's rotation)
   const size_t soff = (size_t)chunk * Cout * 576 + (size_t)cb * (64 * 576);
