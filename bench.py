@@ -280,37 +280,39 @@ def edsr_bench(dev, batch, steps, warmup):
                                    "4-var 32x32->256x256 tiles, exact fp32", "batch": batch}}
 
 
-def dp_overhead_probe(tr, spec, hr, args, reps=2):
+def dp_overhead_probe(args, reps=2):
     """dp_overhead_1rank: the data-parallel machinery's own cost on one GPU -- a
     one-rank RCCL process group (backend "nccl"), the reducer's comm stream, the
     per-residual-group events and the 11 bucketed all-reduces of the N>1 path
-    (bench --force-dp) -- against the plain step, interleaved on this GPU (K steps of
-    each, `reps` rounds, best of each).  Streams per rank: one per micro-batch
-    engine + the reducer's comm stream (+ RCCL's internal stream)."""
-    from srmi.dist import init_from_env
-    from srmi.trainer import FusedTrainer
-    info = init_from_env(None, force=True)
-    dp = FusedTrainer(spec, args.batch, (48, 48), lr=1e-4, interp_loss=not args.no_interp_loss, info=info,
-                      device=hr.device, seed=0, micro=args.micro, cu_budget=args.cu_budget)
-    for _ in range(args.warmup):
-        dp.step(hr)
-    torch.cuda.synchronize()
+    (bench --force-dp) -- against the plain step.  Each leg runs as a CHILD process
+    with one trainer, as a real rank does: a second trainer in this process would
+    add its streams to this one's and oversubscribe the 4 hardware queues a process
+    gets (GPU_MAX_HW_QUEUES), which measured -42 % for reasons that are not the DP
+    path's.  `reps` interleaved rounds of plain / DP children, best of each.
+    Streams per rank: one per micro-batch engine + the reducer's comm stream (+ RCCL's
+    internal stream)."""
+    import subprocess
+    base = [sys.executable, os.path.abspath(__file__), "--no-cpu-baseline", "--no-inference", "--no-edsr",
+            "--no-dp-probe", "--steps", str(args.steps), "--warmup", str(args.warmup), "--batch", str(args.batch)]
+    if args.micro is not None:
+        base += ["--micro", str(args.micro)]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
     best = {"plain": 0.0, "dp": 0.0}
+    micro = None
     for _ in range(reps):
-        for name, t in (("plain", tr), ("dp", dp)):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(args.steps):
-                t.step(hr)
-            torch.cuda.synchronize()
-            best[name] = max(best[name], args.batch * args.steps / (time.perf_counter() - t0))
-    del dp
-    torch.distributed.destroy_process_group()
+        for name, extra in (("plain", []), ("dp", ["--force-dp"])):
+            r = subprocess.run(base + extra, env=env, capture_output=True, text=True, timeout=240)
+            if r.returncode != 0:
+                return {"error": f"{name} child exited {r.returncode}: {r.stderr.strip().splitlines()[-1:]}"}
+            line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+            best[name] = max(best[name], line["value"])
+            micro = line.get("micro", micro)
     return {"tiles_per_s_plain": round(best["plain"], 2), "tiles_per_s_dp": round(best["dp"], 2),
             "overhead_frac": round(1.0 - best["dp"] / best["plain"], 4),
-            "streams_per_rank": f"{tr.micro} engine stream(s) + 1 reducer comm stream (+ RCCL internal)",
-            "config": f"1-rank RCCL group, {tr.micro} micro-batch engine(s), same B={args.batch}, "
-                      f"best of {reps} interleaved rounds of {args.steps} steps"}
+            "streams_per_rank": f"{micro} engine stream(s) + 1 reducer comm stream (+ RCCL internal)",
+            "config": f"1-rank RCCL group, {micro} micro-batch engine(s), same B={args.batch}, child process per "
+                      f"leg (one trainer per process, as a rank), best of {reps} interleaved rounds of "
+                      f"{args.steps} steps"}
 
 
 def _log(msg):
@@ -444,13 +446,13 @@ def main():
         step_tf = value / world * TRAIN_GFLOP_PER_TILE_C2 / 1000.0
         roof["step_mfma_tflops"] = round(step_tf, 1)
         roof["step_mfma_frac"] = round(step_tf / PEAK_BF16_TFLOPS, 4)
-    dp_probe = None
-    if world == 1 and not info.enabled and not args.no_dp_probe:
-        dp_probe = dp_overhead_probe(tr, spec, hr, args)
-        _log(f"dp probe: {dp_probe}")
     del tr, hr  # the extra lines below run on their own engines
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
+    dp_probe = None
+    if world == 1 and not info.enabled and not args.no_dp_probe:
+        dp_probe = dp_overhead_probe(args)
+        _log(f"dp probe: {dp_probe}")
     _log(f"timed: {value:.1f} tiles/s")
     if info.rank == 0:
         roof_conv = conv_fwd_roofline(dev, B)
