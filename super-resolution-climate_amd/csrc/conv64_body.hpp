@@ -150,7 +150,6 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
   constexpr bool kF = (EPI == EPI_RESID || kRun);
   float4 fv[NPT][NCT];  // fp32 outputs, written back through LDS after the loop
   uint2 bv[NPT][NCT];   // bf16 outputs, likewise
-  [[maybe_unused]] float c0v[NCT][4], cLv[NCT][4];  // RELU statistics: first / last column
 #pragma unroll
   for (int c = 0; c < NCT; ++c)
 #pragma unroll
@@ -171,15 +170,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       }
       if constexpr (EPI == EPI_RELU_BF16) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = fmaxf(v[r], 0.f);
-          // CA-backward fold statistics (stored only when p.part): the row's sum, the
-          // same for an edge row, and the first / last column's pixel
-          ps0[c][r] += v[r];
-          ps1[c][r] += v[r];
-          if (pt == 0) c0v[c][r] = v[r];
-          if (pt == NPT - 1) cLv[c][r] = v[r];
-        }
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
       }
       if constexpr (EPI == EPI_RESID) {
         const float4 rr = e.r1[pt][c];
@@ -234,10 +225,6 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       constexpr int RUNS = HALF / 4;  // 1 KiB runs per half
       const auto rf = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
       [[maybe_unused]] const auto rbb = wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
-      [[maybe_unused]] const auto rdu = wt_rsrc(p.du_out, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
-      // the lane's 4 channels are 4 (lane & 15) .. + 3 in every run: their CA scales
-      [[maybe_unused]] float4 sdu = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (kRun && p.du_out) sdu = *reinterpret_cast<const float4*>(p.s_rec + (size_t)n * 160 + 96 + 4 * (lane & 15));
       const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -280,10 +267,6 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             ps1[0][3] += val.w * bf2f(uu.y >> 16);
           }
           st_wt16(rf, p.yf, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 4), val);
-          if (p.du_out) {  // CA-backward fold: du' = g * s of the RCAB before (bf16, 512 B per instruction)
-            st_wt8(rdu, p.du_out, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 2),
-                   make_uint2(pack2(val.x * sdu.x, val.y * sdu.y), pack2(val.z * sdu.z, val.w * sdu.w)));
-          }
           if constexpr (EPI == EPI_DG_ACC) {
             if (p.yb)  // its bf16 copy: 512 contiguous bytes per instruction
               st_wt8(rbb, p.yb, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 2),
@@ -325,56 +308,6 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
         line = ((size_t)n * HW + (size_t)y * p.W + x0 + px) * p.Cout + cb * 64;
       }
       st_wt16(rb, p.yb, (uint32_t)((line + c * 8) * 2), val);
-    }
-  }
-  if constexpr (EPI == EPI_RELU_BF16) {
-    if (p.part) {  // CA-backward fold: the per-strip statistics of t (uniform branch)
-      const int nsx = p.W / (NPT * 16), nsy = p.H / kTH, k = strip / nsx;
-      const bool edge_strip = (k == 0) || (k == nsy - 1);
-      const bool edge_row = (y == 0) || (y == p.H - 1);  // (one row of an edge strip: H >= 8)
-      const bool first_x = (x0 == 0), last_x = (x0 + NPT * 16 == p.W);
-#pragma unroll
-      for (int c = 0; c < NCT; ++c)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ch = (ct0 + c) * 16 + fk * 4 + r;
-          const float s0 = sum16(ps0[c][r]);
-          float s1 = 0.f;
-          if (edge_row) s1 = sum16(ps1[c][r]);
-          if (fr == 0) {
-            red[(row * 3 + 0) * 64 + ch] = s0;
-            red[(row * 3 + 1) * 64 + ch] = first_x ? c0v[c][r] : 0.f;
-            if (edge_row) {
-              red[768 + ch] = s1;
-              red[832 + ch] = first_x ? c0v[c][r] : 0.f;
-            }
-          }
-          if (fr == 15) {
-            red[(row * 3 + 2) * 64 + ch] = last_x ? cLv[c][r] : 0.f;
-            if (edge_row) red[896 + ch] = last_x ? cLv[c][r] : 0.f;
-          }
-        }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      float* rec = p.part + ((size_t)n * nstrips + strip) * p.part_stride;
-      if (tid < 64) {
-        float S = 0.f, C0 = 0.f, CL = 0.f;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          S += red[(rr * 3 + 0) * 64 + tid];
-          C0 += red[(rr * 3 + 1) * 64 + tid];
-          CL += red[(rr * 3 + 2) * 64 + tid];
-        }
-        rec[tid] = S;
-        rec[64 + tid] = C0;
-        rec[128 + tid] = CL;
-      } else if (tid < 128) {
-        const int c = tid - 64;
-        rec[192 + c] = edge_strip ? red[768 + c] : 0.f;
-        rec[256 + c] = edge_strip ? red[832 + c] : 0.f;
-        rec[320 + c] = edge_strip ? red[896 + c] : 0.f;
-      }
     }
   }
   if constexpr (kRun) {
@@ -827,13 +760,6 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     wait_vm<0>();
   }
   STAMP(1);
-  if constexpr (EPI == EPI_DG_RELUMASK) {
-    // CA-backward fold: the dgrad of the constant dm / HW per border class ([9][64],
-    // the red buffer is free in this epilogue), published by the barrier below
-    if (p.corr)
-      for (int i = tid; i < 144; i += NW * 64)
-        reinterpret_cast<float4*>(red)[i] = reinterpret_cast<const float4*>(p.corr + (size_t)n * 576)[i];
-  }
   // A-fragment rows: lane fr of tile c reads the filter row of the channel its
   // accumulator row fr will hold (permuted for bf16 outputs)
   uint32_t aoff[2][NCT];
@@ -887,17 +813,6 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     const size_t pix = (size_t)n * HW + (size_t)yy * p.W + x0 + pt * 16 + fr;
     if constexpr (kPerm) {
       float o[8];
-      [[maybe_unused]] float cr[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if constexpr (EPI == EPI_DG_RELUMASK) {
-        if (p.corr) {  // the lane's 8 channels of its pixel's border class
-          const int xx = x0 + pt * 16 + fr;
-          const int cls = (yy == 0 ? 0 : yy == p.H - 1 ? 6 : 3) + (xx == 0 ? 0 : xx == p.W - 1 ? 2 : 1);
-          const float4 a = *reinterpret_cast<const float4*>(red + cls * 64 + chan(0, 0));
-          const float4 b = *reinterpret_cast<const float4*>(red + cls * 64 + chan(0, 0) + 4);
-          cr[0] = a.x; cr[1] = a.y; cr[2] = a.z; cr[3] = a.w;
-          cr[4] = b.x; cr[5] = b.y; cr[6] = b.z; cr[7] = b.w;
-        }
-      }
 #pragma unroll
       for (int c = 0; c < NCT; ++c) {
         const f32x4 v = accp[pt][c];
@@ -912,7 +827,7 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
           }
           if constexpr (EPI == EPI_DG_RELUMASK) {
             const uint32_t w = (c ? (rr < 2 ? ops.t[pt].z : ops.t[pt].w) : (rr < 2 ? ops.t[pt].x : ops.t[pt].y));
-            x = p.alpha * relu_mask((rr & 1) ? (w >> 16) : (w & 0xFFFFu), x + cr[4 * c + rr]);
+            x = p.alpha * relu_mask((rr & 1) ? (w >> 16) : (w & 0xFFFFu), x);
           }
           o[4 * c + rr] = x;
         }

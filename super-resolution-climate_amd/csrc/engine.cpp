@@ -213,15 +213,6 @@ struct srmi_engine {
   int max_cob = 0, max_cib = 0;  // largest Cout / 64, Cin / 64 of the packed convs
   bool tables_uploaded = false;
   int last_n = 0;
-  // CA-backward fold (no du pass; srmi_internal.hpp CaFold): conv1's per-strip
-  // statistics of t per RCAB, T per RCAB parity, the conv2-dgrad correction
-  bool fold = false;
-  float* stats = nullptr;   // [nl * nb][N][nstrips][384]
-  float* foldT[2] = {};     // [N][576]
-  float* fcorr = nullptr;   // [N][9][64]
-  float* statsp(int g, int b) const {
-    return stats + (size_t)(g * P.cfg.nblocks + (b - 1)) * N * conv3x3_nstrips(h, w) * 384;
-  }
 
   bf16_t* at(bf16_t* base, size_t elems) const {
     return reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(base) + elems * esz);
@@ -303,11 +294,6 @@ static size_t carve(srmi_engine* e, char* base) {
     e->dRESb = act(m);
     for (int k = 0; k < 3; ++k) e->dPS[k] = nullptr;
     for (int k = 0; k < P.nups; ++k) e->dPS[k] = act(m << (2 * (k + 1)));
-    if (e->fold) {
-      e->stats = cv.take<float>((size_t)nl * nb * N * nstrips * 384);
-      for (int q = 0; q < 2; ++q) e->foldT[q] = cv.take<float>((size_t)N * 576);
-      e->fcorr = cv.take<float>((size_t)N * 576);
-    }
     // slab: max over all wgrads
     size_t sf = 0, bf = 0;
     auto upd = [&](int H, int W, int Cout) {
@@ -349,11 +335,6 @@ static size_t carve(srmi_engine* e, char* base) {
   return cv.off + 256;
 }
 
-// CA-backward fold (see srmi_internal.hpp CaFold): the bf16 RCAN engine at 48-wide
-// tiles skips the du pass of every RCAB
-#ifndef SRMI_FOLD_CA
-#define SRMI_FOLD_CA 0
-#endif
 static int init_engine(srmi_engine* e, const srmi_model_config* cfg, int train) {
   int rc = build_plan(cfg, e->P);
   if (rc) return rc;
@@ -379,7 +360,6 @@ static int init_engine(srmi_engine* e, const srmi_model_config* cfg, int train) 
   const size_t f32_bytes = e->mapn * 4;
   const size_t hr_bytes = (size_t)e->N * std::max(e->C, e->Co) * Hs * (e->w * e->S) * 4;
   if (ps_bytes >= lim || f32_bytes >= lim || hr_bytes >= lim) return SRMI_ERR_SHAPE;
-  e->fold = SRMI_FOLD_CA && train && !e->f32 && e->P.cfg.arch == SRMI_ARCH_RCAN && e->w == 48 && e->h >= 8;
   return 0;
 }
 
@@ -431,7 +411,7 @@ static int conv_fwd(srmi_engine* e, const ConvRef& c, const bf16_t* x, int n, in
   p.yf = yf;
   p.r1 = r1;
   p.part = part;
-  p.part_stride = epi == EPI_RELU_BF16 ? 384 : 64;  // (RELU + part: the fold statistics)
+  p.part_stride = 64;
   p.alpha = alpha;
   p.zeros = e->zeros;
   p.cu_budget = e->cu_budget;
@@ -569,8 +549,7 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
       const float* rin = g == 0 ? e->X0f : e->Rf;
       for (int b = 1; b <= nb; ++b) {
         const RCABRef& r = P.groups[g][b - 1];
-        RC(conv_fwd(e, r.c1, e->hb(g, b - 1), n, h, w, EPI_RELU_BF16, e->Tm(g, b), nullptr, nullptr,
-                    e->fold ? e->statsp(g, b) : nullptr, 1.f, st));
+        RC(conv_fwd(e, r.c1, e->hb(g, b - 1), n, h, w, EPI_RELU_BF16, e->Tm(g, b), nullptr, nullptr, nullptr, 1.f, st));
         RC(conv_fwd(e, r.c2, e->Tm(g, b), n, h, w, EPI_POOL_BF16, e->Um(g, b), nullptr, nullptr, e->ppool, 1.f, st));
         if (e->f32) {
           RC(ca_fwd_launch(e->Um(g, b), e->ppool, nstrips, prm + r.ca_w1, prm + r.ca_b1, prm + r.ca_w2, prm + r.ca_b2,
@@ -660,16 +639,8 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
     for (int g = nl - 1; g >= 0; --g) {
       const ConvRef& gt = P.group_tail[g];
       RC(conv_wgrad(e, gt, e->hb(g, nb), gRb, n, h, w, grads, true, 1.f, st));
-      {
-        int epi = EPI_DG_ACC;
-        ConvParams tp = dgrad_params(e, gt, gRb, n, h, w, &epi, nullptr, ghf, nullptr, nullptr, nullptr, e->Um(g, nb),
-                                     e->pacc, 1.f);
-        if (e->fold) {  // du' of the group's last RCAB
-          tp.du_out = e->DU;
-          tp.s_rec = e->recp(g, nb);
-        }
-        RC(conv3x3_launch(tp, epi, st));
-      }
+      RC(conv_dgrad(e, gt, gRb, n, h, w, EPI_DG_ACC, nullptr, ghf, nullptr, nullptr, nullptr, e->Um(g, nb), e->pacc,
+                    1.f, st));
       ReduceSet prev2{}, prev1{};
       bool have_prev = false;
       for (int b = nb; b >= 1; --b) {
@@ -677,18 +648,8 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         const int q = it++ & 1;
         bf16_t* du = e->DU;
         bf16_t* dz = e->DZ;
-        if (e->fold) {
-          // the CA backward without a du pass: du' = bf16(g s) is in DU already (F1 of
-          // the RCAB after, or the group tail); this launch writes brec, T and the
-          // conv2-dgrad correction, and reduces the previous RCAB's slabs
-          const CaFold f{e->statsp(g, b), e->foldT[q], e->at(e->packs, r.c2.d_off), e->fcorr, h, w};
-          RC(ca_bwd_fold_launch(e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R,
-                                e->brecp(g, b), f, st, have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
-        } else {
-          RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
-                              e->brecp(g, b), e->f32, st, have_prev ? &prev2 : nullptr,
-                              have_prev ? &prev1 : nullptr));
-        }
+        RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
+                            e->brecp(g, b), e->f32, st, have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
         ReduceSet red2, red1;
         WgradParams wp;
         int epi = EPI_DG_RELUMASK;
@@ -696,23 +657,12 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
                                      nullptr, 1.f);
         RC(wgrad_params(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, rs2, e->slab_r[q][0], e->bslab_r[q][0],
                         e->slab_r_floats, e->bslab_r_floats, &wp, &red2));
-        if (e->fold) {  // du = du' + dm / HW: the constant's share of dz and of conv2's filter gradient
-          cp.corr = e->fcorr;
-          red2.cdm = e->brecp(g, b) + (size_t)n * 160;
-          red2.cT = e->foldT[q];
-          red2.cN = n;
-          red2.cinvHW = 1.f / (float)HW;
-        }
         RC(dgrad_with_wgrad(e, cp, epi, wp, 2, st));
         const bool last = (b == 1);
         epi = EPI_DG_ACC;
         cp = dgrad_params(e, r.c1, dz, n, h, w, &epi, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
                           (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
                           last ? nullptr : e->pacc, 1.f);
-        if (e->fold && !last) {  // du' of RCAB b - 1 (DU was last read by F2 above)
-          cp.du_out = e->DU;
-          cp.s_rec = e->recp(g, b - 1);
-        }
         RC(wgrad_params(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, rs1, e->slab_r[q][1],
                         e->bslab_r[q][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red1));
         RC(dgrad_with_wgrad(e, cp, epi, wp, 1, st));
@@ -845,7 +795,6 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
     epi = EPI_DG_RELUMASK;
     cp = dgrad_params(e, r.c2, e->DU, n, h, w, &epi, e->DZ, nullptr, nullptr, nullptr, nullptr, e->Tm(0, b), nullptr,
                       1.f);
-    if (e->fold) cp.corr = e->fcorr;
     RC(wgrad_params(e, r.c2, e->Tm(0, b), e->DU, n, h, w, grads, false, 1.f, rcab_row_splits(e, n, 2),
                     e->slab_r[0][0], e->bslab_r[0][0], e->slab_r_floats, e->bslab_r_floats, &wp, &red));
   } else {
@@ -853,10 +802,6 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
     epi = EPI_DG_ACC;
     cp = dgrad_params(e, r.c1, e->DZ, n, h, w, &epi, last ? e->GAb : nullptr, ghf, ghf, last ? e->GAf : nullptr,
                       nullptr, last ? nullptr : e->Um(0, b - 1), last ? nullptr : e->pacc, 1.f);
-    if (e->fold && !last) {
-      cp.du_out = e->DU;
-      cp.s_rec = e->recp(0, b - 1);
-    }
     RC(wgrad_params(e, r.c1, e->hb(0, b - 1), e->DZ, n, h, w, grads, true, 1.f, rcab_row_splits(e, n, 1),
                     e->slab_r[0][1], e->bslab_r[0][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red));
   }

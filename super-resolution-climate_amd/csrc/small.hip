@@ -1187,11 +1187,10 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
   if ((int)blockIdx.y >= N) {
     const int id = ((int)blockIdx.y - N) * (int)gridDim.x + (int)blockIdx.x;
     if (id < nred)
-      wgrad_reduce_body<16>(r0.slab, r0.bslab, r0.nslab, r0.Cout, r0.ps, r0.layout, r0.alpha, r0.gw, r0.gb, id,
-                            r0.cdm, r0.cT, r0.cN, r0.cinvHW);
+      wgrad_reduce_body<16>(r0.slab, r0.bslab, r0.nslab, r0.Cout, r0.ps, r0.layout, r0.alpha, r0.gw, r0.gb, id);
     else if (id < 2 * nred)
       wgrad_reduce_body<16>(r1.slab, r1.bslab, r1.nslab, r1.Cout, r1.ps, r1.layout, r1.alpha, r1.gw, r1.gb,
-                            id - nred, r1.cdm, r1.cT, r1.cN, r1.cinvHW);
+                            id - nred);
     return;
   }
   __shared__ float red[2][128], s[64], dz2[64], dz1[32], dm[64];
@@ -1301,158 +1300,6 @@ int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float
   else
     hipLaunchKernelGGL(ca_bwd_du_kernel<bf16_t>, grid, dim3(256), 0, st, g, part, nstrips, rec, w1, w2, N, HW, C,
                        C / R, static_cast<bf16_t*>(du), brec, a, b, nred);
-  SRMI_CHECK_LAUNCH();
-  return 0;
-}
-
-// CA-backward fold (srmi_internal.hpp CaFold): no du pass.  du = g * s + dm / HW is
-// never materialised: F1 writes du' = bf16(g * s), F2's dgrad adds the dgrad of the
-// constant dm / HW (corr, per border class), F2's filter-gradient reduction adds
-// dm / HW (x) T, T[ci][tap] = the sum of t over tap's valid window.  One block per
-// image: the MLP backward of ca_bwd_du_kernel (same operands, same order), T from
-// conv1's per-strip statistics, corr from the conv2 dgrad pack; blocks >= N carry the
-// previous RCAB's two slab reductions.
-__global__ void __launch_bounds__(256) ca_bwd_fold_kernel(const float* __restrict__ part, int nstrips,
-                                                          const float* __restrict__ rec, const float* __restrict__ w1,
-                                                          const float* __restrict__ w2, int N, int HW, int C, int CR,
-                                                          float* __restrict__ brec, CaFold f, ReduceSet r0,
-                                                          ReduceSet r1, int nred) {
-  if ((int)blockIdx.x >= N) {
-    const int id = (int)blockIdx.x - N;
-    if (id < nred)
-      wgrad_reduce_body<16>(r0.slab, r0.bslab, r0.nslab, r0.Cout, r0.ps, r0.layout, r0.alpha, r0.gw, r0.gb, id,
-                            r0.cdm, r0.cT, r0.cN, r0.cinvHW);
-    else if (id < 2 * nred)
-      wgrad_reduce_body<16>(r1.slab, r1.bslab, r1.nslab, r1.Cout, r1.ps, r1.layout, r1.alpha, r1.gw, r1.gb,
-                            id - nred, r1.cdm, r1.cT, r1.cN, r1.cinvHW);
-    return;
-  }
-  __shared__ float red[2][128], s[64], dz2[64], dz1[32], dm[64], P[9][64];
-  const int n = blockIdx.x, tid = threadIdx.x;
-  const float* r = rec + (size_t)n * (2 * C + CR);
-  const int j = tid >> 3, pj = tid & 7;
-  const int c4 = tid >> 2, p4 = tid & 3, per = CR / 4;
-  float pa = 0.f;  // G[c] = sum_p g, ds[c] = sum_p g*u
-  for (int k = tid >> 7; k < nstrips; k += 2) pa += part[((size_t)n * nstrips + k) * (2 * C) + (tid & 127)];
-  const int jc = min(j, CR - 1);
-  float wa[8], wb[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) wa[i] = w2[(pj * 8 + i) * CR + jc];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) wb[i] = w1[(p4 * per + min(i, per - 1)) * C + c4];
-  const float zj = r[C + jc];
-  const float svl = r[C + CR + (tid & 63)];
-  red[tid >> 7][tid & 127] = pa;
-  s[tid & 63] = svl;
-  __syncthreads();
-  float G = 0.f, sv = 0.f;
-  if (tid < C) {
-    G = red[0][tid] + red[1][tid];
-    const float ds = red[0][C + tid] + red[1][C + tid];
-    sv = s[tid];
-    dz2[tid] = ds * sv * (1.f - sv);
-  }
-  __syncthreads();
-  {
-    float a = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a += wa[i] * dz2[pj * 8 + i];
-    a += __shfl_xor(a, 1, 64);
-    a += __shfl_xor(a, 2, 64);
-    a += __shfl_xor(a, 4, 64);
-    if (j < CR && pj == 0) dz1[j] = (zj > 0.f) ? a : 0.f;
-  }
-  __syncthreads();
-  {
-    float a = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      if (i < per) a += wb[i] * dz1[p4 * per + i];
-    a += __shfl_xor(a, 1, 64);
-    a += __shfl_xor(a, 2, 64);
-    if (p4 == 0) dm[c4] = a;
-  }
-  __syncthreads();
-  if (tid < C) {
-    float* br = brec + (size_t)n * (2 * C + CR);
-    br[tid] = dz2[tid];
-    brec[(size_t)N * (2 * C + CR) + (size_t)n * C + tid] = dm[tid];
-    br[C + CR + tid] = sv * G + dm[tid];  // conv2 bias grad: sum_p du
-  }
-  if (tid < CR) brec[(size_t)n * (2 * C + CR) + C + tid] = dz1[tid];
-  const float invHW = 1.f / (float)HW;
-  if (tid < 64) {
-    // T[ci][ky][kx] from conv1's per-strip statistics ([S | first col | last col |
-    // edge-row sum | its first | its last pixel] x 64): rows 0..H-2 for ky = 0, all for
-    // ky = 1, 1..H-1 for ky = 2; columns likewise
-    const int nsx = f.W / 48, nsy = f.H / 4;
-    const float* st = f.stats + (size_t)n * nstrips * 384;
-    float S = 0.f, C0 = 0.f, CL = 0.f, Ft = 0.f, F0t = 0.f, FLt = 0.f, Fb = 0.f, F0b = 0.f, FLb = 0.f;
-    for (int k = 0; k < nstrips; ++k) {
-      const float* q = st + (size_t)k * 384;
-      S += q[tid];
-      C0 += q[64 + tid];
-      CL += q[128 + tid];
-      const int ky = k / nsx;
-      if (ky == 0) {
-        Ft += q[192 + tid];
-        F0t += q[256 + tid];
-        FLt += q[320 + tid];
-      } else if (ky == nsy - 1) {
-        Fb += q[192 + tid];
-        F0b += q[256 + tid];
-        FLb += q[320 + tid];
-      }
-    }
-    const float A[3] = {S - Fb, S, S - Ft}, B0[3] = {C0 - F0b, C0, C0 - F0t}, BL[3] = {CL - FLb, CL, CL - FLt};
-    float* T = f.T + (size_t)n * 576 + tid * 9;
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) T[ky * 3 + kx] = A[ky] - (kx == 0 ? BL[ky] : 0.f) - (kx == 2 ? B0[ky] : 0.f);
-  }
-  // corr: the conv2 dgrad of the constant dm / HW, per tap, then per border class
-  const bf16_t* wd = static_cast<const bf16_t*>(f.dpack);
-  for (int q = tid; q < 576; q += 256) {
-    const int tap = q >> 6, ci = q & 63;
-    const uint4* row = reinterpret_cast<const uint4*>(wd + ((size_t)tap * 64 + ci) * 64);
-    float a = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint4 w = row[k];
-      const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        a += bf2f(ww[e] & 0xFFFFu) * dm[k * 8 + 2 * e] + bf2f(ww[e] >> 16) * dm[k * 8 + 2 * e + 1];
-    }
-    P[tap][ci] = a * invHW;
-  }
-  __syncthreads();
-  for (int q = tid; q < 576; q += 256) {
-    const int cls = q >> 6, ci = q & 63, ry = cls / 3, rx = cls % 3;
-    float a = 0.f;
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const bool ok = !(ry == 0 && ky == 0) && !(ry == 2 && ky == 2) && !(rx == 0 && kx == 0) && !(rx == 2 && kx == 2);
-        if (ok) a += P[ky * 3 + kx][ci];
-      }
-    f.corr[(size_t)n * 576 + q] = a;
-  }
-}
-
-int ca_bwd_fold_launch(const float* part, int nstrips, const float* rec, const float* w1, const float* w2, int N,
-                       int HW, int C, int R, float* brec, const CaFold& f, hipStream_t st, const ReduceSet* red0,
-                       const ReduceSet* red1) {
-  if (C != 64 || C % R || (C / R) > 32 || (C / R) % 4) return SRMI_ERR_SHAPE;
-  if (f.W % 48 || f.H % 4 || f.H < 8 || f.W < 2 || !f.stats || !f.T || !f.dpack || !f.corr) return SRMI_ERR_ARG;
-  if ((red0 == nullptr) != (red1 == nullptr)) return SRMI_ERR_ARG;
-  if (red0 && (red0->Cout != red1->Cout)) return SRMI_ERR_SHAPE;
-  const int nred = red0 ? wgrad_reduce_blocks(red0->Cout) : 0;
-  const ReduceSet none{};
-  hipLaunchKernelGGL(ca_bwd_fold_kernel, dim3(N + 2 * nred), dim3(256), 0, st, part, nstrips, rec, w1, w2, N, HW, C,
-                     C / R, brec, f, red0 ? *red0 : none, red1 ? *red1 : none, nred);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

@@ -44,14 +44,6 @@ struct ConvParams {
   int cu_budget;               // CUs a launch should fill (0 = all 256)
   int f32;                     // exact-fp32 mode: x, w, yb, aux point at fp32 data
                                // (the bf16_t* fields are plain addresses then)
-  // CA-backward fold (bf16 RCAN engine, TW = 48 bodies):
-  //   RELU with part: per-strip statistics of the output t (S, first / last column,
-  //     edge-row sum, first, last pixel: 6 x 64, part_stride 384)
-  //   DG_ACC_CA / DG_ACC with du_out: also du' = bf16(g * s) (s from s_rec: [n][160], at 96)
-  //   DG_RELUMASK with corr: dx += corr[n][border class][ci] before the mask
-  bf16_t* du_out;
-  const float* s_rec;
-  const float* corr;
 };
 
 void conv3x3_set_debug_stamps(unsigned long long* buf);
@@ -89,12 +81,6 @@ struct ReduceSet {  // one slab reduction: slabs -> torch-layout dW (and db)
   float alpha;
   float* gw;
   float* gb;
-  // CA-backward fold: dW[co][ci][tap] += sum_n cdm[n][co] * cT[n][ci * 9 + tap] / HW
-  // (the constant dm / HW the filter gradient's dy = du' left out), images in order
-  const float* cdm = nullptr;
-  const float* cT = nullptr;
-  int cN = 0;
-  float cinvHW = 0.f;
 };
 int wgrad_reduce2_launch(const ReduceSet& r0, const ReduceSet& r1, hipStream_t st);
 // fused RCAB backward launch: dgrad conv (epi RELUMASK / DG_ACC_CA / DG_ACC, its runs
@@ -146,21 +132,6 @@ int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1
 int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
                      const float* w2, int N, int HW, int C, int R, void* du, float* brec, int f32, hipStream_t st,
                      const ReduceSet* red0 = nullptr, const ReduceSet* red1 = nullptr);
-// CA-backward fold (no du pass): one block per image computes the MLP backward (brec
-// as ca_bwd_du) and, from conv1's per-strip statistics of t (stats: [N][nstrips][384]),
-// T[n][ci][tap] = sum of t over tap's valid window (T: [N][576]), and from the conv2
-// dgrad pack (bf16 [9][64][64]) the dgrad of the constant dm / HW per border class
-// (corr: [N][9][64]); the slab reductions ride in the same launch
-struct CaFold {
-  const float* stats;
-  float* T;
-  const void* dpack;
-  float* corr;
-  int H, W;
-};
-int ca_bwd_fold_launch(const float* part, int nstrips, const float* rec, const float* w1, const float* w2, int N,
-                       int HW, int C, int R, float* brec, const CaFold& f, hipStream_t st, const ReduceSet* red0,
-                       const ReduceSet* red1);
 // records of consecutive RCABs Ncap images apart (the engine capacity), N summed
 int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int Ncap, int C, int R,
                                   const long long* offs, float* grads, hipStream_t st);

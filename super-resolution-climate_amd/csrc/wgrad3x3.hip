@@ -712,16 +712,14 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
 }
 
 __global__ void __launch_bounds__(kRedQ * kRedPh) wgrad_reduce_kernel(ReduceSet r) {
-  wgrad_reduce_body<kRedPh>(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb, blockIdx.x,
-                            r.cdm, r.cT, r.cN, r.cinvHW);
+  wgrad_reduce_body<kRedPh>(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb, blockIdx.x);
 }
 
 // two independent reductions in one launch (blockIdx.y selects the set): the two
 // filter gradients of an RCAB on the side stream share one launch and one boundary
 __global__ void __launch_bounds__(kRedQ * kRedPh) wgrad_reduce2_kernel(ReduceSet r0, ReduceSet r1) {
   const ReduceSet& r = blockIdx.y ? r1 : r0;
-  wgrad_reduce_body<kRedPh>(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb, blockIdx.x,
-                            r.cdm, r.cT, r.cN, r.cinvHW);
+  wgrad_reduce_body<kRedPh>(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb, blockIdx.x);
 }
 
 int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, int layout, float alpha,

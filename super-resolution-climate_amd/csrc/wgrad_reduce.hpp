@@ -19,29 +19,10 @@ inline int wgrad_reduce_blocks(int Cout) { return Cout * 576 / (4 * kRedQ) + (Co
 
 // PH = slab phases per block (blockDim = kRedQ * PH: 32 -> 512 threads, 16 -> 256);
 // bid = this block's index within the reduction's wgrad_reduce_blocks(Cout)
-// (cop, ci, tap) of weight output o of a slab layout
-__device__ __forceinline__ void wgrad_out_index(int o, int Cout, int layout, int& cop, int& ci, int& tap) {
-  if (layout == 1) {  // wgrad48 native order [cb][wave][t][ct][lane][4]
-    const int cb = o / (64 * 576), l = o - cb * (64 * 576);
-    const int r = l & 3, lane = (l >> 2) & 63, ct = (l >> 8) & 3, wt = l >> 10;
-    const int wave = wt / 9, j = wt;  // j = 9 * wave + t
-    tap = j >> 2;
-    ci = (j & 3) * 16 + (lane & 15);
-    cop = cb * 64 + ((ct + wave) & 3) * 16 + 4 * (lane >> 4) + r;
-  } else {  // [tap][ci][Cout]
-    cop = o % Cout;
-    ci = (o / Cout) & 63;
-    tap = o / (Cout * 64);
-  }
-}
-
 template <int PH>
 __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab, const float* __restrict__ bslab,
                                                   int nslab, int Cout, int ps, int layout, float alpha,
-                                                  float* __restrict__ gw, float* __restrict__ gb, int bid,
-                                                  const float* __restrict__ cdm = nullptr,
-                                                  const float* __restrict__ cT = nullptr, int cN = 0,
-                                                  float cinvHW = 0.f) {
+                                                  float* __restrict__ gw, float* __restrict__ gb, int bid) {
   __shared__ float4 red[PH][kRedQ], red2[4][kRedQ];
   const int per = Cout * 576;
   const int nwb = per / (4 * kRedQ);  // weight blocks (per % 64 == 0 since Cout % 64 == 0)
@@ -83,21 +64,6 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab
       }
     }
   }
-  if (is_w && cT && valid) {
-    // CA-backward fold: + sum_n dm[n][co] / HW * T[n][ci][tap] -- phase ph takes
-    // images ph, ph + PH, ... (into the same fixed-order combine as the slabs)
-    float cv[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      int cop, ci, tap;
-      wgrad_out_index(o4 + e, Cout, layout, cop, ci, tap);
-      for (int nn = ph; nn < cN; nn += PH) cv[e] += cdm[nn * 64 + cop] * cT[nn * 576 + ci * 9 + tap];
-    }
-    a[0].x += cv[0] * cinvHW;
-    a[0].y += cv[1] * cinvHW;
-    a[0].z += cv[2] * cinvHW;
-    a[0].w += cv[3] * cinvHW;
-  }
   red[ph][qd] = make_float4((a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y),
                             (a[0].z + a[1].z) + (a[2].z + a[3].z), (a[0].w + a[1].w) + (a[2].w + a[3].w));
   __syncthreads();
@@ -126,7 +92,18 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab
     const int o = o4 + e;
     if (is_w) {
       int cop, ci, tap;
-      wgrad_out_index(o, Cout, layout, cop, ci, tap);
+      if (layout == 1) {  // wgrad48 native order [cb][wave][t][ct][lane][4]
+        const int cb = o / (64 * 576), l = o - cb * (64 * 576);
+        const int r = l & 3, lane = (l >> 2) & 63, ct = (l >> 8) & 3, wt = l >> 10;
+        const int wave = wt / 9, j = wt;  // j = 9 * wave + t
+        tap = j >> 2;
+        ci = (j & 3) * 16 + (lane & 15);
+        cop = cb * 64 + ((ct + wave) & 3) * 16 + 4 * (lane >> 4) + r;
+      } else {  // [tap][ci][Cout]
+        cop = o % Cout;
+        ci = (o / Cout) & 63;
+        tap = o / (Cout * 64);
+      }
       const int cot = ps ? (4 * (cop & 63) + (cop >> 6)) : cop;
       gw[((size_t)cot * 64 + ci) * 9 + tap] = alpha * s4[e];
     } else if (o < Cout) {
