@@ -149,6 +149,12 @@ int srmi_loss_finalize(float* loss4, int kind, void* stream);
  * loss (at most 1024 batches); work: ntiles floats */
 int srmi_batch_losses(const float* pred, const float* target, int ntiles, long long tile_elems, int batch_size,
                       int kind, float eps, float* work, float* out, void* stream);
+/* the second half of srmi_batch_losses on per-tile sums already formed (its `work`
+ * output, e.g. gathered from the ranks of a multi-rank tiled inference, srmi.inference):
+ * out[0] = mean of the batch losses, out[1 + b] = batch b's loss, the same arithmetic
+ * (process_image's np.array(batch_losses).mean(), dual_trainer.py:443-446) */
+int srmi_batch_loss_means(const float* sums, int ntiles, long long tile_elems, int batch_size, int kind, float* out,
+                          void* stream);
 /* loss4 = the sum over nparts micro-batch records parts4[k][4] (S summed in a fixed
  * order, the count of part 0), then finalised as `kind` (-1: not finalised, e.g.
  * before a data-parallel all-reduce of loss4[0]) */

@@ -368,25 +368,43 @@ def process_region(model, region: np.ndarray, ty: int, tx: int, scale: int, batc
 
 
 def evaluate(model, regions: Sequence[np.ndarray], ty: int, tx: int, scale: int, batch_size: int,
-             loss_fn: str = "l2"):
+             loss_fn: str = "l2", time_index: int = -1, tile_index: int = -1, batch_domain: str = "tiles"):
     """ModelTrainer.evaluate (dual_trainer.py:482-543) over the time slices of a
-    tset (no flips): losses = mean over all batches of all regions (:532, :541);
-    results = the normalised tiles of the LAST region only: clear_results at the
-    start of every time slice (:505, :545-549), then that slice's batches
-    concatenated along the tile axis (merge_results_tiles, :38-42, :551-555)."""
+    tset (no flips): losses = mean over all scored batches of all scored regions
+    (:532, :541); results = the normalised tiles of the LAST scored region only:
+    clear_results at the start of every time slice (:505, :545-549), then that
+    slice's scored batches concatenated along the tile axis (merge_results_tiles,
+    :38-42, :551-555).  time_index >= 0: only slice itime == time_index, then stop
+    (:508-509, :527); tile_index >= 0: only the batch tile_in_batch accepts
+    (:366-372: 'tiles' -- its range [start, end) holds tile_index; 'time' -- its
+    ordinal equals it), then the next slice (:525)."""
     bm, bi, results = [], [], {}
-    for region in regions:
+    for itime, region in enumerate(regions):
+        if not (time_index < 0 or itime == time_index):
+            continue
+        results = {}  # clear_results
         tiles, _, _, _, _ = region_to_tiles(region, ty, tx)
         dt = torch.float64 if tiles.dtype == np.float64 else torch.float32
         target = torch.tensor(tiles, dtype=dt)
-        lr = downsample(target, scale)
-        with torch.no_grad():
-            sr = model(lr)
-        interp = upsample(lr, scale)
-        bm += batch_losses(sr, target, batch_size, loss_fn)
-        bi += batch_losses(interp, target, batch_size, loss_fn)
-        results = {k: v.numpy() for k, v in (("input", lr), ("target", target), ("model", sr),
-                                               ("interpolated", interp))}
+        for ib, a in enumerate(range(0, target.shape[0], batch_size)):
+            end = min(a + batch_size, target.shape[0])
+            if tile_index >= 0:
+                ok = (a <= tile_index < end) if batch_domain == "tiles" else (ib == tile_index)
+                if not ok:
+                    continue
+            tb = target[a:end]
+            lr = downsample(tb, scale)
+            with torch.no_grad():
+                sr = model(lr)
+            interp = upsample(lr, scale)
+            bm.append(float(single_product_loss(sr, tb, loss_fn)))
+            bi.append(float(single_product_loss(interp, tb, loss_fn)))
+            for k, v in (("input", lr), ("target", tb), ("model", sr), ("interpolated", interp)):
+                results[k] = v.numpy() if k not in results else np.concatenate([results[k], v.numpy()])
+            if tile_index >= 0:
+                break
+        if time_index >= 0:
+            break
     return results, {"model": float(np.array(bm).mean()), "interpolated": float(np.array(bi).mean())}
 
 

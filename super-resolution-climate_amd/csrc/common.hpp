@@ -103,6 +103,16 @@ __device__ __forceinline__ void st_wt8(__amdgpu_buffer_rsrc_t r, void* base, uin
 #endif
 }
 
+__device__ __forceinline__ void st_wt4(__amdgpu_buffer_rsrc_t r, void* base, uint32_t byte_off, uint32_t v) {
+#if SRMI_WT
+  (void)base;
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, byte_off, 0, 16);
+#else
+  (void)r;
+  *reinterpret_cast<uint32_t*>(static_cast<char*>(base) + byte_off) = v;
+#endif
+}
+
 // 16-byte chunk swizzle for an LDS image of 128-byte rows (64 bf16 channels per
 // pixel/row).  Chunk c of row q lives at slot c ^ (q & 7).  The MFMA operand read is
 // a ds_read_b128 of rows q0 + (lane & 15) at chunk c0 + (lane >> 4), served in the

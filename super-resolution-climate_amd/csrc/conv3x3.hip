@@ -396,9 +396,14 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
   if (epi == EPI_PS_BF16 && p.Cout != 256) return SRMI_ERR_SHAPE;
   if (p.in_mode == IN_UNSHUF && p.Cin != 256) return SRMI_ERR_SHAPE;
   // outputs are stored through buffer resources whose byte range is 32-bit: an
-  // output map of 2^32 bytes or more would wrap num_records and drop its stores
-  // (the fp32 form of the map bounds every output this launch writes)
-  if ((size_t)p.N * p.H * p.W * p.Cout * 4 >= (1ull << 32)) return SRMI_ERR_SHAPE;
+  // output map of 2^32 bytes or more would wrap num_records and drop its stores.
+  // Sized from the bytes each output actually holds: yb 2 B (bf16) or 4 B (f32
+  // engine) per element, yf always 4 B -- the same quantity init_engine checks.
+  {
+    const size_t elems = (size_t)p.N * p.H * p.W * p.Cout;
+    if (p.yb && elems * (p.f32 ? 4 : 2) >= (1ull << 32)) return SRMI_ERR_SHAPE;
+    if (p.yf && elems * 4 >= (1ull << 32)) return SRMI_ERR_SHAPE;
+  }
   if (p.f32) return conv3x3_f32_launch(p, epi, st);
   switch (epi) {
     case EPI_RELU_BF16: return launch_epi<EPI_RELU_BF16>(p, st);

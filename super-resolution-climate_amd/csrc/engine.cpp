@@ -556,8 +556,9 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
                            n, HW, 64, R, b == 1 ? rin : e->Hf, e->Hf, e->hb(g, b), e->recp(g, b), 1, st));
         } else {
           // the residual stream inside the group as the pair hb (bf16, the next conv's
-          // input) + lo (bf16 remainder, in Hf's memory); the group input rin is fp32
-          bf16_t* lo = reinterpret_cast<bf16_t*>(e->Hf);
+          // input) + lo (the 8-bit lo8 remainder, 1 B per element, in Hf's memory):
+          // 16 significant bits per element (common.hpp); the group input rin is fp32
+          uint8_t* lo = reinterpret_cast<uint8_t*>(e->Hf);
           RC(ca_fwd_launch(e->Um(g, b), e->ppool, nstrips, prm + r.ca_w1, prm + r.ca_b1, prm + r.ca_w2, prm + r.ca_b2,
                            n, HW, 64, R, b == 1 ? rin : nullptr, nullptr, e->hb(g, b), e->recp(g, b), 0, st,
                            b == 1 ? nullptr : e->hb(g, b - 1), b == 1 ? nullptr : lo, lo));
@@ -837,6 +838,12 @@ int srmi_batch_losses(const float* pred, const float* target, int ntiles, long l
                       int kind, float eps, float* work, float* out, void* stream) {
   if (!pred || !target || !work || !out || (kind != SRMI_LOSS_RMSE && kind != SRMI_LOSS_MEAN)) return SRMI_ERR_ARG;
   return batch_losses_launch(pred, target, ntiles, tile_elems, batch_size, kind, eps, work, out, S_(stream));
+}
+
+int srmi_batch_loss_means(const float* sums, int ntiles, long long tile_elems, int batch_size, int kind, float* out,
+                          void* stream) {
+  if (!sums || !out || (kind != SRMI_LOSS_RMSE && kind != SRMI_LOSS_MEAN)) return SRMI_ERR_ARG;
+  return batch_loss_means_launch(sums, ntiles, tile_elems, batch_size, kind, out, S_(stream));
 }
 
 int srmi_loss_combine(float* loss4, const float* parts4, int nparts, int kind, void* stream) {

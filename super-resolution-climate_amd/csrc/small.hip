@@ -948,6 +948,14 @@ int batch_losses_launch(const float* y, const float* t, int ntiles, long long ti
   return 0;
 }
 
+int batch_loss_means_launch(const float* sums, int ntiles, long long tile_elems, int bs, int kind, float* out,
+                            hipStream_t st) {
+  if (ntiles < 1 || tile_elems < 1 || bs < 1 || (ntiles + bs - 1) / bs > 1024) return SRMI_ERR_SHAPE;
+  hipLaunchKernelGGL(batch_loss_mean_kernel, dim3(1), dim3(256), 0, st, sums, ntiles, tile_elems, bs, kind, out);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
 // =============================================================== channel attention
 // Channel attention (CALayer, reference sres/model/rcan/network.py:31-47):
 //   m = avgpool(u); z1 = W1 m + b1; s = sigmoid(W2 relu(z1) + b2); h += s * u
@@ -1123,7 +1131,7 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
       uint2 hi;
       const uint32_t lo = pair_encode4(o[0], o[1], o[2], o[3], hi);
       st_wt8(rhb, hb_out, (uint32_t)(e * 2), hi);
-      __builtin_amdgcn_raw_buffer_store_b32(lo, rlo, (uint32_t)e, 0, 16);
+      st_wt4(rlo, lo_out, (uint32_t)e, lo);
     }
   }
 }

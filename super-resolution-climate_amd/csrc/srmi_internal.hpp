@@ -117,6 +117,8 @@ int loss_finalize_launch(float* loss, int kind, hipStream_t st);
 int loss_combine_launch(float* loss, const float* parts, int nparts, int kind, hipStream_t st);
 int batch_losses_launch(const float* y, const float* t, int ntiles, long long tile_elems, int bs, int kind, float eps,
                         float* work, float* out, hipStream_t st);
+int batch_loss_means_launch(const float* sums, int ntiles, long long tile_elems, int bs, int kind, float* out,
+                            hipStream_t st);
 int charb_partial_launch(const float* y, const float* t, size_t n, float eps, double count, float* dy,
                          float* partial, int nblk, hipStream_t st);
 

@@ -633,8 +633,14 @@ int rcab_bwd_fusable(const ConvParams& cp, const WgradParams& wp) {
 #endif
 constexpr int kFuseNW = SRMI_FUSE_NW;
 
+// the partial slabs are stored through a buffer resource with a 32-bit byte range
+static bool slab_range_ok(const WgradParams& p, int nslabs) {
+  return (size_t)nslabs * p.Cout * 576 * 4 < ((size_t)1 << 32);
+}
+
 int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradParams& wp, hipStream_t st) {
   if (!rcab_bwd_fusable(cp, wp)) return SRMI_ERR_SHAPE;
+  if (!slab_range_ok(wp, wp.N * wp.row_splits)) return SRMI_ERR_SHAPE;
   const int run_len = conv64_run_len(cp, 48, conv_cus);
   const int nconv = conv64_blocks(cp, 48, run_len);
   const int nwg = wp.N * wp.row_splits * (wp.Cout / 64);
@@ -695,6 +701,7 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
   if (p.f32) return wgrad_f32_launch(p, st);
   if (p.Cout % 64 || p.H % p.row_splits || (p.H / p.row_splits) % 4) return SRMI_ERR_SHAPE;
   if (p.dy_mode == IN_UNSHUF && p.Cout != 256) return SRMI_ERR_SHAPE;
+  if (!slab_range_ok(p, wgrad3x3_nslabs(p))) return SRMI_ERR_SHAPE;
   dim3 grid(wgrad3x3_nslabs(p), p.Cout / 64);
   WgradParams q = p;
   q.stamps = g_wg_stamps;

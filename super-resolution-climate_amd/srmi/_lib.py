@@ -55,6 +55,7 @@ _SIGS = {
     "srmi_loss_finalize": ([P, C.c_int, P], C.c_int),
     "srmi_loss_combine": ([P, P, C.c_int, C.c_int, P], C.c_int),
     "srmi_batch_losses": ([P, P, C.c_int, C.c_longlong, C.c_int, C.c_int, C.c_float, P, P, P], C.c_int),
+    "srmi_batch_loss_means": ([P, C.c_int, C.c_longlong, C.c_int, C.c_int, P, P], C.c_int),
     "srmi_downsample": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),
     "srmi_upsample": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),
     "srmi_adam_step": ([P, P, P, P, C.c_size_t, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, P],

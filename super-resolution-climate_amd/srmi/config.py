@@ -116,10 +116,16 @@ class ConfigContext:
         self.dataset = self.configuration.get("dataset")
         self.pipeline = self.configuration.get("pipeline")
         self.platform = self.configuration.get("platform")
-        # config.py:51 joins the four names (the reference raises on a missing one;
-        # here the id is formed from the names present, as a partial context still
-        # has to name its checkpoints)
-        self.cid = "-".join(str(v) for v in (cname, self.model, self.dataset, self.task) if v is not None)
+        # config.py:51 joins the four names; the reference raises there when one is
+        # missing.  A partial context (no dataset, say) is allowed here for the
+        # hot-path plumbing, but it gets NO id: task.training_version stays unset, so
+        # naming a checkpoint from it raises (CheckpointStore.from_config) instead of
+        # silently using a name no reference run would write.
+        names = (cname, self.model, self.dataset, self.task)
+        self.cid = "-".join(str(v) for v in names) if all(v is not None for v in names) else None
+        # the round-1..2 stem '{cname}-{model}': a resume that finds no checkpoint
+        # under the reference name but one under this stem warns (harness.py)
+        self.legacy_version = f"{cname}-{self.model}" if self.model is not None else None
         self._prev = None
 
     def load(self) -> _Cfg:
@@ -144,8 +150,10 @@ class ConfigContext:
             c["task"]["name"] = self.task
         if self.dataset is not None:
             c["task"]["dataset"] = self.dataset
-        if self.model is not None:
+        if self.cid is not None:
             c["task"]["training_version"] = self.cid
+        if self.legacy_version is not None:
+            c["task"]["legacy_training_version"] = self.legacy_version
         return c
 
     def __enter__(self):
@@ -185,22 +193,41 @@ def init_parms(model: str, custom: Dict[str, Any], model_cfg: Optional[Any] = No
     return parms
 
 
-def check_fused_task(task, nchannels_in: int, nchannels_out: int) -> None:
-    """Refuse what the fused trainer does not implement from apply_network
-    (dual_trainer.py:557-571): an extra ``task.data_downsample`` > 1 before the
-    model's own bicubic 1/s, and a target that is a channel subset of the input
-    (``index_select`` of task.target_variables).  Every in-scope task yaml has
-    input == target variables and data_downsample 1."""
+def check_fused_task(task, nchannels_in: int, nchannels_out: int) -> Optional[List[int]]:
+    """What the fused trainer takes from apply_network (dual_trainer.py:557-571).
+
+    * ``task.data_downsample``: the reference downsamples the HR batch first only when
+      it is > 1.0 (:561-563); that changes the engine's tile geometry, so > 1 raises
+      NotImplementedError; any value <= 1 is a no-op there and here.
+    * The target channels: when the batch has MORE channels than
+      ``task.target_variables`` the reference index_selects them (:564-568) with
+      ``np.in1d(channels, target_variables).nonzero()`` -- the input's own order.
+      Returned as that index list (the trainer selects the same channels of the HR
+      batch on the device); None when nothing is selected (equal counts, whatever
+      the order, are a no-op in the reference).  Without variable names the counts
+      alone decide: fewer output channels than inputs cannot be resolved, and raise.
+    """
     ds = float(task.get("data_downsample", 1.0) or 1.0) if task is not None else 1.0
-    if ds != 1.0:
-        raise NotImplementedError(f"task.data_downsample={ds}: the fused trainer implements data_downsample == 1 only")
-    if nchannels_in != nchannels_out:
-        raise NotImplementedError(f"target channel subset ({nchannels_out} of {nchannels_in} input variables): "
-                                  "the fused trainer needs input_variables == target_variables")
-    if task is not None and "input_variables" in task and "target_variables" in task:
-        if list(task["input_variables"]) != list(task["target_variables"]):
-            raise NotImplementedError(f"target_variables {list(task['target_variables'])} != input_variables "
-                                      f"{list(task['input_variables'])}: not implemented by the fused trainer")
+    if ds > 1.0:
+        raise NotImplementedError(f"task.data_downsample={ds}: the fused trainer implements data_downsample <= 1 only")
+    names_in = list(task["input_variables"]) if task is not None and "input_variables" in task else None
+    names_out = list(task["target_variables"]) if task is not None and "target_variables" in task else None
+    if names_in is None or names_out is None:
+        if nchannels_in != nchannels_out:
+            raise NotImplementedError(f"target channel subset ({nchannels_out} of {nchannels_in} input variables) "
+                                      "needs task.input_variables and task.target_variables")
+        return None
+    if len(names_in) != nchannels_in:
+        raise ValueError(f"model has {nchannels_in} input channels, task.input_variables {names_in}")
+    if len(names_in) <= len(names_out):
+        if nchannels_out != nchannels_in:
+            raise ValueError(f"model has {nchannels_out} output channels for target_variables {names_out}")
+        return None
+    idx = [i for i, v in enumerate(names_in) if v in set(names_out)]
+    if len(idx) != nchannels_out:
+        raise ValueError(f"target_variables {names_out} select {len(idx)} of the input channels {names_in}; "
+                         f"the model has {nchannels_out} output channels")
+    return idx
 
 
 def tile_sizes(task) -> tuple:

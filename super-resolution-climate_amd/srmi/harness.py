@@ -23,6 +23,7 @@ import math
 import os
 import random
 import shutil
+import warnings
 from typing import Callable, Dict, List, Optional, Sequence
 
 import torch
@@ -41,18 +42,25 @@ def _tset(tset: str) -> str:
 class CheckpointStore:
     """CheckpointManager's files (checkpoints.py:18-67) for a FusedTrainer."""
 
-    def __init__(self, results_dir: str, training_version: str):
+    def __init__(self, results_dir: str, training_version: str, legacy_version: Optional[str] = None):
         self.results_dir = results_dir
         self.training_version = training_version
+        self.legacy_version = legacy_version
 
     @classmethod
     def from_config(cls, c=None) -> "CheckpointStore":
         """checkpoint_path's inputs (checkpoints.py:60-66): ``cfg().platform.results``
-        and ``cfg().task.training_version`` (set by ConfigContext, config.py:84)."""
+        and ``cfg().task.training_version`` (set by ConfigContext, config.py:84; a
+        context missing the model, dataset or task name has none, and the reference's
+        ConfigContext raises for it too)."""
         if c is None:
             from .config import cfg
             c = cfg()
-        return cls(str(c["platform"]["results"]), str(c["task"]["training_version"]))
+        tv = c["task"].get("training_version")
+        if tv is None:
+            raise ValueError("no task.training_version: the ConfigContext needs model, dataset and task names "
+                             "(sres/base/util/config.py:51 joins all four)")
+        return cls(str(c["platform"]["results"]), str(tv), c["task"].get("legacy_training_version"))
 
     def path(self, tset: str, backup: bool = False) -> str:
         v = _tset(tset)
@@ -75,6 +83,12 @@ class CheckpointStore:
         loaded, else the train state (model/optimizer dicts popped once applied)."""
         cpath = self.path(tset)
         if not os.path.exists(cpath):
+            if self.legacy_version and self.legacy_version != self.training_version:
+                v = "valid" if _tset(tset) == "test" else _tset(tset)
+                old = os.path.join(self.results_dir, "checkpoints", f"{self.legacy_version}.{v}.pt")
+                if os.path.exists(old):
+                    warnings.warn(f"no checkpoint {cpath}, but {old} exists under the pre-round-3 name "
+                                  f"'{self.legacy_version}': starting from scratch; rename it to resume", stacklevel=2)
             return {}
         try:
             state = torch.load(cpath, map_location="cpu", weights_only=True)

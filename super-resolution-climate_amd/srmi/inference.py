@@ -31,18 +31,50 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ._lib import SRMI_LOSS_MEAN, SRMI_LOSS_RMSE, call, ptr, stream_handle
+from .dist import DistInfo
 from .engine import Engine, NetSpec, downsample, upsample
 
 LOSS_KINDS = {"l2": SRMI_LOSS_RMSE, "charbonnier": SRMI_LOSS_MEAN}
 CHARBONNIER_EPS = 1e-6  # dual_trainer.py:122
 
 
+def gather_round_robin(x: torch.Tensor, n: int, world: int) -> torch.Tensor:
+    """All-gather of this rank's rows of a round-robin split into grid order: rank r
+    holds rows for grid tiles r, r + W, r + 2W, ... (x [n_r, ...]); every rank gets
+    the [n, ...] tensor with tile i at row i.  Ranks pad to a common slot of
+    ceil(n / W) rows; RCCL gathers device tensors directly, gloo (the CPU and
+    one-GPU tests) through host memory."""
+    import torch.distributed as dist
+    npd = (n + world - 1) // world
+    slot = torch.zeros((npd,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    slot[:x.shape[0]] = x
+    if dist.get_backend() == "nccl":
+        out = torch.empty((world * npd,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, slot)
+    else:
+        parts = [torch.empty_like(slot, device="cpu") for _ in range(world)]
+        dist.all_gather(parts, slot.cpu())
+        out = torch.cat(parts).to(x.device)
+    order = torch.arange(n, device=x.device)  # tile i = rank i % W, row i // W
+    return out.index_select(0, (order % world) * npd + order // world)
+
+
 class TiledInference:
     def __init__(self, spec: NetSpec, params: torch.Tensor, region_chw: Tuple[int, int, int],
                  tile_hr: Tuple[int, int] = (192, 192), device: Optional[torch.device] = None, graph: bool = True,
-                 micro: Optional[int] = None, batch_size: int = 36, loss_fn: str = "l2"):
+                 micro: Optional[int] = None, batch_size: int = 36, loss_fn: str = "l2",
+                 info: Optional[DistInfo] = None):
         """batch_size: task.batch_size (the tiles scored per batch; 36 in every
-        reference task yaml); loss_fn: model.loss_fn."""
+        reference task yaml); loss_fn: model.loss_fn.
+
+        info (world > 1): multi-rank inference: the region's tile
+        grid is dealt round-robin over the ranks (rank r runs grid tiles r, r + W,
+        ...), each rank forms its tiles' per-tile loss sums, and the tiles and sums
+        are all-gathered, so every rank -- rank 0 being the one that writes results --
+        holds the full mosaics and the per-batch losses, bit-identical to one rank:
+        the forward is batch-invariant (every tile is computed alone, whatever engine
+        batch it rides in) and the batch losses are formed from the gathered per-tile
+        sums in the one-rank order (srmi_batch_loss_means).  No graph in this mode."""
         if loss_fn not in LOSS_KINDS:
             raise ValueError(f"Unknown single-product loss function {loss_fn}")
         self.loss_kind = LOSS_KINDS[loss_fn]
@@ -62,6 +94,12 @@ class TiledInference:
         if n < 1:
             raise ValueError("region smaller than one tile")
         self.n = n
+        self.info = info or DistInfo()
+        # this rank's grid tiles (all of them at one rank)
+        W_, r_ = (self.info.world, self.info.rank) if self.info.enabled else (1, 0)
+        self.rr_world = W_
+        self.n_local = len(range(r_, n, W_))
+        self.n_pad = (n + W_ - 1) // W_  # per-rank gather slot
         self.params = params
         d = self.device
         f32 = dict(dtype=torch.float32, device=d)
@@ -88,11 +126,22 @@ class TiledInference:
         # the tile batch is split over `micro` engines on their own streams, each
         # sized for 1/micro of the chip (as srmi.trainer.FusedTrainer does): each
         # engine's launch ramps and tails overlap the other's work
+        nl = self.n_local
         if micro is None:
-            micro = 2 if n >= 32 else 1
-        self.micro = max(1, min(int(micro), n))
-        per = (n + self.micro - 1) // self.micro
-        self.split = [min(per, n - k * per) for k in range(self.micro)]
+            micro = 2 if nl >= 32 else 1
+        self.micro = max(1, min(int(micro), max(nl, 1)))
+        per = (max(nl, 1) + self.micro - 1) // self.micro
+        self.split = [max(1, min(per, nl - k * per)) for k in range(self.micro)]
+        if self.info.enabled:
+            graph = False
+            self.idx_local = torch.arange(r_, n, W_, device=d)
+            sub = (max(nl, 1), C)
+            self.sub_tiles = torch.empty(sub + (ty, tx), **f32)
+            self.sub_lr = torch.empty(sub + (ty // s, tx // s), **f32)
+            self.sub_sr = torch.empty(sub + (ty, tx), **f32)
+            self.sub_interp = torch.empty(sub + (ty, tx), **f32)
+            self.sub_out = torch.zeros(1 + max(nl, 1), **f32)
+            self.sums = {"model": torch.zeros(n, **f32), "interpolated": torch.zeros(n, **f32)}
         budget = 256 // self.micro if self.micro > 1 else 0
         self.engs = [Engine(spec, m, (ty // s, tx // s), train=False, device=d, cu_budget=budget)
                      for m in self.split]
@@ -159,6 +208,9 @@ class TiledInference:
         self.region.copy_(region)
         self._tile()
         self.n_kept = self.n
+        if self.info.enabled:
+            self._process_region_ranks()
+            return self.images, {"model": self.loss_m[0:1], "interpolated": self.loss_i[0:1]}
         # every path below scores self.tiles except the compacted one, which resets
         # this to its compacted copy (a graph replay after a compacted region must
         # not leave the previous region's tiles here)
@@ -187,30 +239,78 @@ class TiledInference:
         for e in self.engs:
             e.pack(self.params)
 
-    def evaluate(self, regions: Sequence[torch.Tensor]) -> Tuple[Dict[str, torch.Tensor], Dict[str, float]]:
+    def process_image(self, region: torch.Tensor, varnames: Sequence[str], var: Optional[str] = None
+                      ) -> Tuple[Dict[str, Dict[str, torch.Tensor]], Dict[str, Dict[str, float]]]:
+        """process_image (dual_trainer.py:396-447) with the reference's per-variable
+        return: ({vname: {image type: [y, x]}}, {vname: {'model', 'interpolated'}}).
+        ``var`` selects the output variables as ``kwargs.get('var')`` does
+        (:413-414): output_vars = [var] if given, else varnames.  The image of the
+        i-th OUTPUT variable is channel i of the batch (assemble_images(batches,
+        ivar, ...) with ivar from enumerate(output_vars), :437-438) -- so with var
+        given, channel 0 is returned under that name whatever its position, exactly
+        as the reference does.  The losses are over all channels, the same for every
+        variable (:443-446).  The images are views of the mosaic buffers, valid until
+        the next region is processed (as process_region's)."""
+        images, losses = self.process_region(region)
+        lm, li = float(losses["model"]), float(losses["interpolated"])
+        output_vars = [var] if var is not None else list(varnames)
+        out_im: Dict[str, Dict[str, torch.Tensor]] = {}
+        out_l: Dict[str, Dict[str, float]] = {}
+        for ivar, v in enumerate(output_vars):
+            out_im[v] = {k: img[ivar] for k, img in images.items()}
+            out_l[v] = {"model": lm, "interpolated": li}
+        return out_im, out_l
+
+    def evaluate(self, regions: Sequence[torch.Tensor], time_index: int = -1, tile_index: int = -1,
+                 batch_domain: str = "tiles") -> Tuple[Dict[str, torch.Tensor], Dict[str, float]]:
         """ModelTrainer.evaluate (dual_trainer.py:482-543) over the time slices of a
         tset: every region is tiled, normalised and scored batch by batch; the loss
-        is the mean over ALL batches of all regions (:532, :541), while the results
-        are those of the LAST evaluated region only -- the reference clears them at
-        the start of every time slice (clear_results, :505, :545-549) and then
-        concatenates that slice's batches (merge_results / merge_results_tiles,
+        is the mean over ALL scored batches of all scored regions (:532, :541), while
+        the results are those of the LAST evaluated region only -- the reference
+        clears them at the start of every time slice (clear_results, :505, :545-549)
+        and then concatenates that slice's batches (merge_results / merge_results_tiles,
         :551-555, :38-42): input [n, C, ty/s, tx/s], target / model / interpolated
-        [n, C, ty, tx] (device tensors, normalised tiles).  The
-        validation-checkpoint policy applied to the returned loss is
+        [n, C, ty, tx] (device tensors, normalised tiles).
+
+        Selection (:487-488, :504, :508-527):
+        * ``time_index`` >= 0 scores only ``regions[time_index]`` (itime == time_index);
+        * ``tile_index`` >= 0 scores only the batch that tile_in_batch accepts (:366-372)
+          and stops there: batch_domain 'tiles' (the SWOT datasets) -- the batch whose
+          tile range [start, end) holds tile_index; 'time' -- the batch whose ordinal
+          is tile_index.  No matching batch: nothing is scored in that region (its
+          results stay cleared).
+        The validation-checkpoint policy applied to the returned loss is
         ValidationCheckpoint.update (srmi.harness)."""
+        if batch_domain not in ("tiles", "time"):
+            raise ValueError(f"unknown batch domain {batch_domain!r}")
         bm: List[torch.Tensor] = []
         bi: List[torch.Tensor] = []
-        results: Dict[str, torch.Tensor] = {k: torch.empty(0, device=self.device)
-                                            for k in ("input", "target", "model", "interpolated")}
-        for region in regions:
+        empty = {k: torch.empty(0, device=self.device) for k in ("input", "target", "model", "interpolated")}
+        results: Dict[str, torch.Tensor] = dict(empty)
+        for itime, region in enumerate(regions):
+            if time_index >= 0 and itime != time_index:
+                continue
             self.process_region(region)
             nt = self.n_kept
             b = self.batch_losses()
-            bm.append(b["model"].clone())
-            bi.append(b["interpolated"].clone())
-            # clear_results(tset) per time slice, then this slice's tiles
-            results = {"input": self.lr[:nt].clone(), "target": self._kept_tiles[:nt].clone(),
-                       "model": self.sr[:nt].clone(), "interpolated": self.interp[:nt].clone()}
+            results = dict(empty)  # clear_results(tset) at the start of the time slice
+            if tile_index < 0:
+                a0, a1, sel = 0, nt, slice(None)
+            else:
+                bs = self.batch_size
+                ib = tile_index // bs if batch_domain == "tiles" else tile_index
+                a0, a1 = ib * bs, min(nt, (ib + 1) * bs)
+                sel = slice(ib, ib + 1)
+                if a0 >= nt:  # no batch of this slice holds the tile
+                    if time_index >= 0:
+                        break
+                    continue
+            bm.append(b["model"][sel].clone())
+            bi.append(b["interpolated"][sel].clone())
+            results = {"input": self.lr[a0:a1].clone(), "target": self._kept_tiles[a0:a1].clone(),
+                       "model": self.sr[a0:a1].clone(), "interpolated": self.interp[a0:a1].clone()}
+            if time_index >= 0:
+                break
         m = torch.cat(bm).double().cpu() if bm else torch.empty(0, dtype=torch.float64)
         i = torch.cat(bi).double().cpu() if bi else torch.empty(0, dtype=torch.float64)
         losses = {"model": float(m.mean()) if m.numel() else float("nan"),
@@ -235,6 +335,66 @@ class TiledInference:
                 self._all_tiles()
         torch.cuda.current_stream(self.device).wait_stream(s)
         self._graph = g
+
+    # ------------------------------------------------------------ multi-rank
+    def _gather(self, x: torch.Tensor) -> torch.Tensor:
+        return gather_round_robin(x[:self.n_local], self.n, self.rr_world)
+
+    def _process_region_ranks(self):
+        nl = self.n_local
+        if nl > 0:
+            torch.index_select(self.tiles, 0, self.idx_local, out=self.sub_tiles[:nl])
+            downsample(self.sub_tiles[:nl], self.s, out=self.sub_lr[:nl])
+            a = 0
+            for e, m in zip(self.engs, self.split):
+                b = min(nl, a + m)
+                if b > a:
+                    e.forward(self.params, self.sub_lr[a:b], out=self.sub_sr[a:b])
+                a = b
+            upsample(self.sub_lr[:nl], self.s, out=self.sub_interp[:nl])
+        st = stream_handle()
+        te = self.C * self.ty * self.tx
+        sums = {}
+        for name, pred in (("model", self.sub_sr), ("interpolated", self.sub_interp)):
+            work = torch.zeros(max(nl, 1), dtype=torch.float32, device=self.device)
+            if nl > 0:  # per-tile sums (srmi_batch_losses' first pass, batches of one tile)
+                call("srmi_batch_losses", ptr(pred), ptr(self.sub_tiles), nl, te, 1, self.loss_kind, CHARBONNIER_EPS,
+                     ptr(work), ptr(self.sub_out), st)
+            sums[name] = self._gather(work[:, None])[:, 0]
+        lr = self._gather(self.sub_lr)
+        sr = self._gather(self.sub_sr)
+        interp = self._gather(self.sub_interp)
+        keep = torch.nonzero(self.bad == 0).flatten()
+        nt = int(keep.numel())
+        self.n_kept = nt
+        if nt == 0:
+            for img in self.images.values():
+                img.fill_(float("nan"))
+            self.loss_m.fill_(float("nan"))
+            self.loss_i.fill_(float("nan"))
+            self._kept_tiles = self.tiles[:0]
+            return
+        inv = None
+        mean, std, tiles = self.mean, self.std, self.tiles
+        if nt < self.n:
+            inv = torch.full((self.n,), -1, dtype=torch.int32, device=self.device)
+            inv[keep] = torch.arange(nt, dtype=torch.int32, device=self.device)
+            tiles = tiles.index_select(0, keep).contiguous()
+            mean = mean.index_select(0, keep).contiguous()
+            std = std.index_select(0, keep).contiguous()
+            lr, sr, interp = (x.index_select(0, keep).contiguous() for x in (lr, sr, interp))
+            sums = {k: v.index_select(0, keep).contiguous() for k, v in sums.items()}
+        self._kept_tiles = tiles
+        self.lr[:nt].copy_(lr)
+        self.sr[:nt].copy_(sr)
+        self.interp[:nt].copy_(interp)
+        for name, lo in (("model", self.loss_m), ("interpolated", self.loss_i)):
+            call("srmi_batch_loss_means", ptr(sums[name]), nt, te, self.batch_size, self.loss_kind, ptr(lo), st)
+        C, gy, gx, s = self.C, self.gy, self.gx, self.s
+        for name, src, ty, tx in (("input", self.lr, self.ty // s, self.tx // s), ("target", tiles, self.ty, self.tx),
+                                  ("interpolated", self.interp, self.ty, self.tx), ("model", self.sr, self.ty, self.tx)):
+            call("srmi_tiles_to_region", ptr(src), ptr(mean), ptr(std), ptr(inv), C, ty, tx, gy, gx,
+                 ptr(self.images[name]), st)
 
     def _run_compacted(self):
         keep = torch.nonzero(self.bad == 0).flatten()

@@ -72,18 +72,26 @@ class FusedTrainer:
                  params: Optional[torch.Tensor] = None, micro: Optional[int] = None, loss_fn: str = "l2",
                  cu_budget: Optional[int] = None, task=None):
         """task: the task config section (default: the active srmi ConfigContext's,
-        if any); apply_network features the fused step does not implement
-        (data_downsample > 1, target channel subsets) raise NotImplementedError."""
+        if any).  apply_network's target selection is followed: when
+        task.target_variables names fewer channels than the input, the loss target is
+        those HR channels (index_select in the input's order, dual_trainer.py:564-568)
+        and the model has that many output channels; task.data_downsample > 1 raises
+        NotImplementedError (config.check_fused_task)."""
         if loss_fn not in LOSS_KINDS:  # single_product_loss, dual_trainer.py:210-211
             raise ValueError(f"Unknown single-product loss function {loss_fn}")
         if task is None:
             from . import config as _config
             task = _config._CURRENT.get("task") if _config._CURRENT is not None else None
-        check_fused_task(task, spec.nchannels_in, spec.nchannels_out)
+        tindx = check_fused_task(task, spec.nchannels_in, spec.nchannels_out)
+        if tindx is not None and interp_loss and spec.nchannels_out != 1:
+            # loss(btarget, upsample(binput)) (:315-317) needs equal or broadcastable channels
+            raise ValueError(f"interp loss of a {spec.nchannels_out}-channel target against the "
+                             f"{spec.nchannels_in}-channel interpolated input does not broadcast (as in the reference)")
         self.loss_fn = loss_fn
         self.loss_kind = LOSS_KINDS[loss_fn]
         self.info = info or DistInfo()
         self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.tindx = None if tindx is None else torch.tensor(tindx, dtype=torch.long, device=self.device)
         self.spec = spec
         self.batch = batch
         if micro is None:
@@ -116,9 +124,15 @@ class FusedTrainer:
         C, h, w, s = spec.nchannels_in, lr_hw[0], lr_hw[1], spec.scale
         self.lrbuf = torch.empty((batch, C, h, w), dtype=torch.float32, device=self.device)
         self.sr = torch.empty((batch, spec.nchannels_out, h * s, w * s), dtype=torch.float32, device=self.device)
-        self.up = torch.empty_like(self.sr) if interp_loss else None
+        self.up = (torch.empty((batch, C, h * s, w * s), dtype=torch.float32, device=self.device)
+                   if interp_loss else None)
         # Charbonnier: the elementwise loss gradient is the backward's upstream gradient
         self.dy = torch.empty_like(self.sr) if self.loss_kind == SRMI_LOSS_MEAN else None
+        # the selected target channels (index_select) and, for the interp metric, that
+        # target broadcast over the input's channels (1-channel target, :316-317)
+        self.tgt = torch.empty_like(self.sr) if self.tindx is not None else None
+        self.tgt_b = (torch.empty((batch, C, h * s, w * s), dtype=torch.float32, device=self.device)
+                      if self.tindx is not None and interp_loss else None)
         self.loss4 = torch.zeros(4, dtype=torch.float32, device=self.device)
         self.iloss4 = torch.zeros(4, dtype=torch.float32, device=self.device)
         self.mloss4 = torch.zeros((micro, 4), dtype=torch.float32, device=self.device)   # per micro-batch
@@ -161,7 +175,14 @@ class FusedTrainer:
         mb = (b + self.micro - 1) // self.micro
         sls = [slice(min(b, k * mb), min(b, (k + 1) * mb)) for k in range(self.micro)]
         main = torch.cuda.current_stream(self.device)
-        count = float(hr.numel()) * self.info.world
+        if self.tindx is not None:  # apply_network's index_select of the target channels
+            tgt = torch.index_select(hr, 1, self.tindx, out=self.tgt[:b])
+            if self.tgt_b is not None:
+                self.tgt_b[:b].copy_(tgt.expand(-1, hr.shape[1], -1, -1))
+        else:
+            tgt = hr
+        count = float(tgt.numel()) * self.info.world
+        icount = float(hr.numel()) * self.info.world
         for st in self.streams[1:]:
             st.wait_stream(main)
         # forward + loss partials per micro-batch (an empty micro-batch adds nothing)
@@ -174,11 +195,12 @@ class FusedTrainer:
             with self._ctx(k):
                 downsample(hr[sl], s, out=self.lrbuf[sl])
                 eng.forward(self.params, self.lrbuf[sl], out=self.sr[sl])
-                self._loss_partial(eng, self.sr[sl], hr[sl], self.mloss4[k], count,
+                self._loss_partial(eng, self.sr[sl], tgt[sl], self.mloss4[k], count,
                                    None if self.dy is None else self.dy[sl])
                 if self.interp_loss:  # self.loss(btarget, binterp), dual_trainer.py:316-317
                     up = upsample(self.lrbuf[sl], s, out=self.up[sl])
-                    self._loss_partial(eng, hr[sl], up, self.miloss4[k], count)
+                    itgt = hr[sl] if self.tgt_b is None else self.tgt_b[sl]
+                    self._loss_partial(eng, itgt, up, self.miloss4[k], icount)
         for st in self.streams[1:]:
             main.wait_stream(st)
         self._reduce_loss(self.loss4, self.mloss4)
@@ -204,7 +226,7 @@ class FusedTrainer:
                 if self.dy is not None:
                     eng.backward(self.params, self.lrbuf[sl], self.mgrads[k], dy=self.dy[sl], events=evs[k])
                 else:
-                    eng.backward(self.params, self.lrbuf[sl], self.mgrads[k], sr=self.sr[sl], hr=hr[sl],
+                    eng.backward(self.params, self.lrbuf[sl], self.mgrads[k], sr=self.sr[sl], hr=tgt[sl],
                                  loss4=self.loss4, events=evs[k])
         for st in self.streams[1:]:
             main.wait_stream(st)

@@ -153,3 +153,78 @@ def test_force_dp_rccl_bucketed_allreduce_waits_for_backward():
     for l_dp, l_ref, g_equal, gmax in out:
         assert l_dp == l_ref and g_equal, (l_dp, l_ref, gmax)
     assert params_equal
+
+
+def _infer_worker(rank, port, q, regions, flat_np):
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "super-resolution-climate_amd"), ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                      LOCAL_RANK="0")
+    import torch.distributed as dist
+    from srmi.dist import init_from_env
+    from srmi.engine import NetSpec
+    from srmi.inference import TiledInference
+    info = init_from_env("gloo")
+    d = torch.device("cuda", 0)
+    torch.cuda.set_device(d)
+    spec = NetSpec(arch="rcan", nchannels_in=1, nchannels_out=1, nfeatures=64, nlayers=1, nblocks=2, cbottleneck=2,
+                   scale=4)
+    ti = TiledInference(spec, torch.tensor(flat_np, device=d), regions[0].shape, (192, 192), device=d,
+                        batch_size=4, info=info)
+    out = []
+    for r in regions:
+        images, losses = ti.process_region(torch.tensor(r, device=d))
+        b = ti.batch_losses()
+        torch.cuda.synchronize()
+        out.append(({k: v.cpu().numpy() for k, v in images.items()}, float(losses["model"]),
+                    float(losses["interpolated"]), b["model"].cpu().numpy(), b["interpolated"].cpu().numpy()))
+    res, el = ti.evaluate([torch.tensor(r, device=d) for r in regions])
+    q.put((rank, out, {k: v.cpu().numpy() for k, v in res.items()}, el))
+    dist.destroy_process_group()
+
+
+def test_multirank_tiled_inference_world2_bit_identical_to_one_rank():
+    """SURVEY.md §8(e) for C5: the region's tiles dealt round-robin over 2 ranks
+    (gloo, both on cuda:0), mosaics and per-batch losses all-gathered -- bit-identical
+    to the one-rank TiledInference (graph replay, two micro-batch engines), also for
+    a region with a dropped (non-finite) tile, and through evaluate()."""
+    import multiprocessing as mp
+    from srmi.engine import NetSpec, param_table
+    from srmi.inference import TiledInference
+    from srmi.trainer import default_init_
+    spec = NetSpec(arch="rcan", nchannels_in=1, nchannels_out=1, nfeatures=64, nlayers=1, nblocks=2, cbottleneck=2,
+                   scale=4)
+    table = param_table(spec)
+    flat = torch.empty(sum(t[2] for t in table))
+    default_init_(flat, table, seed=8)
+    rng = np.random.RandomState(29)
+    regions = [rng.randn(1, 5 * 192, 7 * 192 + 50).astype(np.float32) for _ in range(2)]  # 35 tiles, ragged edge
+    regions[1][0, 2 * 192 + 7, 3 * 192 + 9] = np.inf
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 37000 + random.randint(0, 2000)
+    ps = [ctx.Process(target=_infer_worker, args=(r, port, q, regions, flat.numpy())) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=200) for _ in ps], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    d = torch.device("cuda", 0)
+    ti = TiledInference(spec, flat.to(d), regions[0].shape, (192, 192), device=d, batch_size=4)
+    for i, r in enumerate(regions):
+        images, losses = ti.process_region(torch.tensor(r, device=d))
+        b = ti.batch_losses()
+        torch.cuda.synchronize()
+        for rank, out, _, _ in res:
+            im_r, lm, li, bm, bi = out[i]
+            for k, v in images.items():
+                np.testing.assert_array_equal(im_r[k], v.cpu().numpy(), err_msg=f"rank {rank} region {i} {k}")
+            assert lm == float(losses["model"]) and li == float(losses["interpolated"])
+            np.testing.assert_array_equal(bm, b["model"].cpu().numpy())
+            np.testing.assert_array_equal(bi, b["interpolated"].cpu().numpy())
+    ref_res, ref_l = ti.evaluate([torch.tensor(r, device=d) for r in regions])
+    for rank, _, er, el in res:
+        assert el == ref_l
+        for k, v in ref_res.items():
+            np.testing.assert_array_equal(er[k], v.cpu().numpy())

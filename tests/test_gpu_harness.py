@@ -163,6 +163,52 @@ def test_evaluate_vs_oracle_and_validation_policy(tmp_path):
     ti.set_params(tr.params)
 
 
+def test_evaluate_time_and_tile_index_selection_vs_oracle():
+    """evaluate(time_index=, tile_index=) (dual_trainer.py:487-488, :504-527,
+    tile_in_batch :366-372) against the oracle's restatement: one time slice, one
+    batch per slice (tile domain and time domain), no matching batch."""
+    from srmi.inference import TiledInference
+    d = dev()
+    spec, model, flat = _flat1()
+    rng = np.random.RandomState(19)
+    regions = [rng.randn(1, 2 * 192, 3 * 192).astype(np.float32) for _ in range(3)]
+    ti = TiledInference(spec, flat.to(d), regions[0].shape, (192, 192), device=d, graph=True, batch_size=4)
+    dr = [torch.tensor(r, device=d) for r in regions]
+    r64 = [r.astype(np.float64) for r in regions]
+    for kw in (dict(time_index=1), dict(tile_index=5), dict(time_index=2, tile_index=2),
+               dict(tile_index=1, batch_domain="time"), dict(time_index=0, tile_index=0, batch_domain="time")):
+        res, losses = ti.evaluate(dr, **kw)
+        ref_res, ref = ro.evaluate(model, r64, 192, 192, 4, batch_size=4, **kw)
+        for k in ("input", "target", "model", "interpolated"):
+            assert tuple(res[k].shape) == ref_res[k].shape, (kw, k)
+        assert rel_l2(res["target"], ref_res["target"]) < 1e-5
+        assert abs(losses["interpolated"] - ref["interpolated"]) < 1e-5 * ref["interpolated"], kw
+        assert abs(losses["model"] - ref["model"]) < 2e-3 * ref["model"], kw
+    res, losses = ti.evaluate(dr, tile_index=6)  # 6 tiles per slice: no batch holds tile 6
+    assert res["model"].numel() == 0 and np.isnan(losses["model"])
+
+
+def test_process_image_var_selection():
+    """process_image's per-variable return and kwargs 'var' (dual_trainer.py:413-414,
+    :437-446): with var given, the images under that name are channel 0 (ivar from
+    enumerate(output_vars)), the losses are those of all channels."""
+    from srmi.inference import TiledInference
+    d = dev()
+    spec, _, table, flat = _small(C=2, nl=1, nb=1)
+    rng = np.random.RandomState(23)
+    region = torch.tensor(rng.randn(2, 192, 2 * 192).astype(np.float32), device=d)
+    ti = TiledInference(spec, flat.to(d), tuple(region.shape), (192, 192), device=d, graph=False, batch_size=4)
+    imgs, losses = ti.process_image(region, ["SSS", "SST"])
+    imgs = {v: {k: t.clone() for k, t in d_.items()} for v, d_ in imgs.items()}  # (views of the engine's buffers)
+    assert sorted(imgs) == ["SSS", "SST"] and imgs["SST"]["model"].shape == (192, 384)
+    full, fl = ti.process_region(region)
+    assert torch.equal(imgs["SST"]["model"], full["model"][1]) and torch.equal(imgs["SSS"]["target"], full["target"][0])
+    assert losses["SST"] == losses["SSS"] == {"model": float(fl["model"]), "interpolated": float(fl["interpolated"])}
+    one, l1 = ti.process_image(region, ["SSS", "SST"], var="SST")
+    assert list(one) == ["SST"] and torch.equal(one["SST"]["model"], full["model"][0])
+    assert l1["SST"] == losses["SST"]
+
+
 def test_evaluate_graph_replay_after_compacted_region():
     """[clean, one NaN tile, clean] with the graph path: the middle region takes the
     compacted (tile-dropping) path, the last one replays the graph; the results
@@ -223,3 +269,37 @@ def test_train_timeslices_checkpoints_csv_and_resume(tmp_path):
     assert state["epoch"] == 1 and state["itime"] == 2 and c.t == b.t
     torch.cuda.synchronize()
     assert torch.equal(c.params, b.params)
+
+
+def test_target_channel_subset_step_vs_oracle():
+    """apply_network's index_select (dual_trainer.py:564-568): a 2-variable input
+    with target_variables = [SST] trains a 2-in / 1-out model against HR channel 1;
+    the interp metric is loss(btarget, upsample(binput)) with the 1-channel target
+    broadcast over the 2 interpolated channels, as torch evaluates it (:316-317)."""
+    d = dev()
+    spec = NetSpec(arch="rcan", nchannels_in=2, nchannels_out=1, nfeatures=64, nlayers=1, nblocks=2,
+                   cbottleneck=2, scale=4)
+    model = ro.RCANOracle(nchannels_in=2, nchannels_out=1, nlayers=1, nblocks=2)
+    ro.init_params_numpy(model, 5)
+    table = param_table(spec)
+    sd = dict(model.named_parameters())
+    flat = torch.cat([sd[n].detach().reshape(-1).float() for n, _, _, _ in table])
+    task = {"input_variables": {"SSS": "a", "SST": "b"}, "target_variables": ["SST"]}
+    hr = ro.synthetic_hr(4, 2, 192, 77)
+    tr = FusedTrainer(spec, 4, (48, 48), device=d, params=flat.to(d), task=task)
+    res = tr.step(torch.tensor(hr, device=d))
+    torch.cuda.synchronize()
+    model = model.double()
+    h = torch.tensor(hr, dtype=torch.float64)
+    lr_in = ro.downsample(h, 4)
+    tgt = h[:, 1:2]
+    out = model(lr_in)
+    loss = ro.l2loss(out, tgt)
+    loss.backward()
+    iloss = float(ro.l2loss(tgt, ro.upsample(lr_in, 4)))  # broadcast [4,1] against [4,2]
+    assert abs(float(res["loss"]) - float(loss)) < 2e-3 * float(loss)
+    assert abs(float(res["interp_loss"]) - iloss) < 1e-5 * iloss
+    g = dict(model.named_parameters())
+    grads = tr.grads.cpu()
+    for name, off, n, shape in table:
+        assert rel_l2(grads[off:off + n].view(shape), g[name].grad) < 8e-2, name

@@ -127,6 +127,28 @@ def test_conv_pixelshuffle_forward(N, H, W, dt):
     assert rel_l2(y.float(), nhwc(ref)) < TOL[dt]
 
 
+def test_conv_pixelshuffle_bf16_at_32bit_boundary():
+    """The output-range guard sizes the map from the bytes actually stored: a bf16
+    pixel-shuffle output of 456 x 192^2 x 64 elements is 2.15 GB (< 2^32 bytes) and
+    must run, although the same map in fp32 would be refused.  The last image -- the
+    far end of the buffer resource -- equals that image convolved alone."""
+    d = dev()
+    N, H, W = 456, 96, 96
+    assert N * H * W * 256 * 4 >= 2 ** 32 > N * H * W * 256 * 2
+    g = torch.Generator(device="cpu").manual_seed(9)
+    w = (torch.randn(256, 64, 3, 3, generator=g) * 0.06).to(d)
+    b = (torch.randn(256, generator=g) * 0.1).to(d)
+    fp, dp, pb = pack(w, b, ps=1)
+    x = torch.randn(N, H, W, 64, device=d, dtype=torch.bfloat16)
+    y = torch.empty(N, 2 * H, 2 * W, 64, dtype=torch.bfloat16, device=d)
+    conv(x, fp, pb, N, H, W, 64, 256, 3, yb=y)
+    y1 = torch.empty(1, 2 * H, 2 * W, 64, dtype=torch.bfloat16, device=d)
+    conv(x[N - 1:].contiguous(), fp, pb, 1, H, W, 64, 256, 3, yb=y1)
+    torch.cuda.synchronize()
+    assert torch.equal(y[N - 1:], y1)
+    assert float(y1.float().abs().sum()) > 0
+
+
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("N,H,W", SHAPES)
 def test_conv_dgrad_epilogues(N, H, W, dt):

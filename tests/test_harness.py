@@ -110,6 +110,24 @@ def test_oracle_batch_loss_mean_and_evaluate():
     np.testing.assert_array_equal(res["model"], ro.evaluate(model, [region], 32, 32, 4, batch_size=4)[0]["model"])
     res, le = ro.evaluate(model, [region, region], 32, 32, 4, batch_size=4)
     assert abs(le["model"] - l["model"]) < 1e-12  # same batches twice: same mean
+    # time_index / tile_index selection (dual_trainer.py:487-488, :504-527, tile_in_batch :366-372)
+    r1, l1 = ro.evaluate(model, [region2, region], 32, 32, 4, batch_size=4, time_index=1)
+    np.testing.assert_array_equal(r1["model"], res["model"])
+    assert abs(l1["model"] - l["model"]) < 1e-12
+    rt, lt = ro.evaluate(model, [region2, region], 32, 32, 4, batch_size=4, time_index=1, tile_index=5)
+    assert rt["model"].shape == (2, 1, 32, 32)  # batch [4, 6) of the 6 tiles
+    assert abs(lt["model"] - l["batch_model"][1]) < 1e-12
+    np.testing.assert_array_equal(rt["model"], res["model"][4:6])
+    rb, lb = ro.evaluate(model, [region2, region], 32, 32, 4, batch_size=4, time_index=1, tile_index=0,
+                         batch_domain="time")
+    assert rb["model"].shape == (4, 1, 32, 32) and abs(lb["model"] - l["batch_model"][0]) < 1e-12
+    # every slice scores its matching batch; results are the last slice's
+    ra, la = ro.evaluate(model, [region2, region], 32, 32, 4, batch_size=4, tile_index=5)
+    _, l2 = ro.process_region(model, region2, 32, 32, 4, batch_size=4)
+    assert abs(la["model"] - 0.5 * (l2["batch_model"][1] + l["batch_model"][1])) < 1e-12
+    np.testing.assert_array_equal(ra["model"], res["model"][4:6])
+    rn, _ = ro.evaluate(model, [region2, region], 32, 32, 4, batch_size=4, tile_index=6)  # no such tile
+    assert rn == {}
     # charbonnier (dual_trainer.py:196-198)
     p, t = torch.zeros(2, 3), torch.ones(2, 3)
     assert abs(float(ro.single_product_loss(p, t, "charbonnier")) - np.sqrt(1 + 1e-6)) < 1e-7

@@ -271,3 +271,40 @@ def test_force_dp_single_rank_gloo():
     p.join(timeout=60)
     assert p.exitcode == 0
     assert enabled and world == 1 and pg_world == 1 and v == 3.0
+
+
+def _rr_rank(rank, world, port, q):
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "super-resolution-climate_amd"), ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    from srmi.dist import init_from_env
+    from srmi.inference import gather_round_robin
+    init_from_env("gloo")
+    n = 11
+    mine = torch.arange(rank, n, world, dtype=torch.float32)[:, None] * torch.tensor([[1.0, -1.0]])
+    out = gather_round_robin(mine, n, world)
+    q.put((rank, out.numpy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_round_robin_tile_gather_world_gloo(world):
+    """Multi-rank tiled inference deals the grid tiles round-robin (rank r: tiles
+    r, r + W, ...) and all-gathers them back into grid order (srmi.inference,
+    SURVEY.md §8(e)); 11 tiles leave the ranks with unequal counts."""
+    import multiprocessing as mp
+    import random
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 35000 + random.randint(0, 2000)
+    ps = [ctx.Process(target=_rr_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    exp = np.arange(11, dtype=np.float32)[:, None] * np.array([[1.0, -1.0]], dtype=np.float32)
+    for _, out in res:
+        np.testing.assert_array_equal(out, exp)

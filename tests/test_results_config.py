@@ -116,22 +116,65 @@ def test_config_identity_keys_and_derived_paths(tmp_path, monkeypatch):
                                           "swot_SSS_SST-tiles-48_rcan-10-20-64_losses.csv")
 
 
-def test_fused_trainer_refuses_unimplemented_apply_network_features():
+def test_fused_trainer_apply_network_target_selection_and_refusals():
+    """apply_network (dual_trainer.py:557-571): data_downsample only acts when > 1
+    (refused: it changes the tile geometry); the target is index_selected only when
+    the batch has more channels than target_variables, in the INPUT's order
+    (np.in1d(channels, targets)); equal counts in another order are a no-op."""
     from srmi.engine import NetSpec
     from srmi.trainer import FusedTrainer
-    check_fused_task({"data_downsample": 1, "input_variables": {"SST": "x"}, "target_variables": ["SST"]}, 1, 1)
+    assert check_fused_task({"data_downsample": 1, "input_variables": {"SST": "x"}, "target_variables": ["SST"]},
+                            1, 1) is None
+    assert check_fused_task({"data_downsample": 0.5}, 1, 1) is None  # <= 1: a no-op in the reference
     with pytest.raises(NotImplementedError, match="data_downsample"):
         check_fused_task({"data_downsample": 2.0}, 1, 1)
     with pytest.raises(NotImplementedError, match="subset"):
         check_fused_task({}, 2, 1)
-    with pytest.raises(NotImplementedError, match="target_variables"):
-        check_fused_task({"input_variables": {"SSS": "a", "SST": "b"}, "target_variables": ["SST"]}, 2, 2)
+    two = {"input_variables": {"SSS": "a", "SST": "b"}}
+    assert check_fused_task(dict(two, target_variables=["SST"]), 2, 1) == [1]
+    assert check_fused_task(dict(two, target_variables=["SSS"]), 2, 1) == [0]
+    assert check_fused_task(dict(two, target_variables=["SST", "SSS"]), 2, 2) is None  # same set, other order
+    with pytest.raises(ValueError):
+        check_fused_task(dict(two, target_variables=["SST"]), 2, 2)  # model outputs do not match the target
+    with pytest.raises(ValueError):
+        check_fused_task(dict(two, target_variables=["U"]), 2, 1)  # selects nothing
     # the trainer checks before it touches a device
     with pytest.raises(NotImplementedError):
         FusedTrainer(NetSpec(nchannels_in=2, nchannels_out=1), 2, device=torch.device("cpu"))
+    with pytest.raises(ValueError, match="broadcast"):  # a 2-of-3 target cannot meet the 3-channel interp input
+        FusedTrainer(NetSpec(nchannels_in=3, nchannels_out=2), 2, device=torch.device("cpu"),
+                     task={"input_variables": ["A", "B", "C"], "target_variables": ["A", "C"]})
     with pytest.raises(NotImplementedError):
         FusedTrainer(NetSpec(), 2, device=torch.device("cpu"), task={"data_downsample": 4})
     with ConfigContext("sres", dict(model="rcan-10-20-64", task="SST-tiles-48"), **{"task.data_downsample": 2}):
         assert cfg().task.data_downsample == 2
         with pytest.raises(NotImplementedError):
             FusedTrainer(NetSpec(), 2, device=torch.device("cpu"))
+
+
+def test_partial_context_has_no_training_version_and_legacy_stem_warns(tmp_path, monkeypatch):
+    """A context without a dataset gets no training_version (the reference's join
+    raises there), so no checkpoint is named from it; a resume that finds only a
+    checkpoint under the pre-round-3 '{cname}-{model}' stem warns instead of
+    silently starting over."""
+    import warnings as W
+    plat = tmp_path / "cfg" / "platform"
+    plat.mkdir(parents=True)
+    (plat / "box.yaml").write_text(f'root: "{tmp_path}"\nresults: "${{.root}}/results"\n')
+    monkeypatch.setenv("SRMI_CONFIG_PATH", str(tmp_path / "cfg"))
+    with ConfigContext("sres", dict(model="rcan-10-20-64", task="SST-tiles-48", platform="box")) as c:
+        assert "training_version" not in c.task
+        with pytest.raises(ValueError, match="training_version"):
+            CheckpointStore.from_config()
+    conf = dict(model="rcan-10-20-64", task="SST-tiles-48", dataset="swot", platform="box")
+    with ConfigContext("sres", conf):
+        store = CheckpointStore.from_config()
+        old = tmp_path / "results" / "checkpoints" / "sres-rcan-10-20-64.train.pt"
+        old.parent.mkdir(parents=True, exist_ok=True)
+        old.write_bytes(b"x")
+        with pytest.warns(UserWarning, match="pre-round-3"):
+            assert store.load(None, "train") == {}
+        old.unlink()
+        with W.catch_warnings():
+            W.simplefilter("error")
+            assert store.load(None, "train") == {}
