@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--no-dp-probe", action="store_true", help="skip the dp_overhead_1rank measurement")
     ap.add_argument("--force-dp", action="store_true",
                     help="diagnostic: the DP path (RCCL group, reducer stream, bucketed all-reduce) at one rank")
+    ap.add_argument("--no-ca-fold", action="store_true",
+                    help="A/B: materialise du in a CA-backward pass per RCAB (SRMI_FLAG_NO_CA_FOLD)")
     return ap.parse_args()
 
 
@@ -116,7 +118,11 @@ WGRAD_OUT_BYTES = 64 * 577 * 4           # dW (64x64x9) + db, fp32, once per lau
 #  F2 = rcab_bwd_kernel<DG_RELUMASK>: conv2's dgrad (reads du bf16, reads the ReLU
 #       output t bf16 as the mask, writes dz bf16) and conv2's filter gradient (t, du
 #       already counted)
+#  with the CA-backward fold (the default) F1 also writes du' = bf16(g s) of the next
+#  RCAB (one more bf16 map; the CA-backward pass that read g and wrote du is gone) and
+#  F2 reads du' instead of du (same bytes)
 F1_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE + 2 * ACT_F32_PER_TILE
+F1_FOLD_BYTES_PER_TILE = F1_BYTES_PER_TILE + ACT_BF16_PER_TILE
 F2_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE
 FUSED_FLOP_PER_TILE = 2 * CONV64_FLOP_PER_TILE   # one dgrad conv + one filter-gradient conv
 
@@ -141,7 +147,8 @@ def fused_rooflines(tr, step_ms, reps=20):
     out = {}
     nl, nb = tr.spec.nlayers, tr.spec.nblocks
     per_step = {1: nl * (nb - 1), 2: nl * nb}
-    for which, name, bpt in ((1, "rcab_bwd_kernel<EPI_DG_ACC_CA>", F1_BYTES_PER_TILE),
+    fold = not (tr.spec.flags & 1)
+    for which, name, bpt in ((1, "rcab_bwd_kernel<EPI_DG_ACC_CA>", F1_FOLD_BYTES_PER_TILE if fold else F1_BYTES_PER_TILE),
                              (2, "rcab_bwd_kernel<EPI_DG_RELUMASK>", F2_BYTES_PER_TILE)):
         streams = [tr.streams[k] or main_st for k in range(n_eng)]
 
@@ -171,7 +178,7 @@ def fused_rooflines(tr, step_ms, reps=20):
             "traffic": (tr_["bytes"] * n_eng if tr_ and tr_["bytes"] is not None else None),
             "traffic_per_launch": tr_["bytes"] if tr_ else None,
             "traffic_source": tr_["source"] if tr_ else None,
-            "kernel": "srmi::" + name, "in_step": True,
+            "kernel": "srmi::" + name, "in_step": True, "ca_fold": fold,
             "config": f"{n_eng} concurrent launch(es) (one per micro-batch engine), {tiles_per_engine} tiles each, "
                       "in-step grid and CU split",
             "avg_launch_ms": round(ms, 4), "per_stream_ms": [round(x, 4) for x in per_stream],
@@ -296,6 +303,8 @@ def dp_overhead_probe(args, reps=2):
             "--no-dp-probe", "--steps", str(args.steps), "--warmup", str(args.warmup), "--batch", str(args.batch)]
     if args.micro is not None:
         base += ["--micro", str(args.micro)]
+    if args.no_ca_fold:
+        base += ["--no-ca-fold"]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
     best = {"plain": 0.0, "dp": 0.0}
     micro = None
@@ -399,8 +408,9 @@ def main():
                "inference": None if args.no_inference else inference_bench(dev, args.infer_region, args.infer_iters)}
         print(json.dumps(rec), flush=True)
         return
+    from srmi._lib import SRMI_FLAG_NO_CA_FOLD
     spec = NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=10, nblocks=20,
-                   cbottleneck=2, scale=4)
+                   cbottleneck=2, scale=4, flags=SRMI_FLAG_NO_CA_FOLD if args.no_ca_fold else 0)
     tr = FusedTrainer(spec, B, (48, 48), lr=1e-4, interp_loss=not args.no_interp_loss, info=info, device=dev, seed=0,
                       micro=args.micro, cu_budget=args.cu_budget)
     hr = torch.tensor(synthetic_hr(B, C, 192, 1234 + info.rank)).to(dev)
@@ -414,9 +424,15 @@ def main():
     if info.enabled:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    # per-step GPU times: an event on the main stream behind every step (the step ends
+    # with the main stream joined to every engine stream); consecutive differences
+    main_st = torch.cuda.current_stream()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record(main_st)
+    for k in range(args.steps):
         out = tr.step(hr)
+        evs[k + 1].record(main_st)
     t_host = time.perf_counter() - t0  # host enqueue time of the K steps (GPU may still run)
     torch.cuda.synchronize()
     if info.enabled:
@@ -428,6 +444,12 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t)
     loss = float(out["loss"])
+    step_ev = sorted(evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps))
+    nq = len(step_ev)
+    step_stats = {"median_ms": round(step_ev[nq // 2] if nq % 2 else 0.5 * (step_ev[nq // 2 - 1] + step_ev[nq // 2]), 3),
+                  "min_ms": round(step_ev[0], 3), "max_ms": round(step_ev[-1], 3),
+                  "p10_ms": round(step_ev[int(0.1 * (nq - 1))], 3), "p90_ms": round(step_ev[int(0.9 * (nq - 1))], 3),
+                  "n": nq, "source": "HIP events on the main stream behind every timed step"}
     tiles = B * world * args.steps
     value = tiles / dt
     step_ms = 1000 * dt / args.steps
@@ -472,7 +494,8 @@ def main():
             cpu = cpu_baseline(args.cpu_steps)
         rec = {
             "metric": METRIC, "value": round(value, 2), "unit": "tiles/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3),
+            "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "step_times": step_stats,
+            "ca_fold": not args.no_ca_fold,
             "host_enqueue_ms_per_step": round(1000 * t_host / args.steps, 3),
             "host_enqueue_idle_ms_per_step": round(host_idle_ms, 3), "micro": micro, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",

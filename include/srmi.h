@@ -66,7 +66,7 @@ extern "C" {
 typedef struct srmi_model_config {
   int arch;          /* SRMI_ARCH_RCAN | SRMI_ARCH_EDSR                     */
   int nchannels_in;  /* len(task.input_variables)   (1..4)                  */
-  int nchannels_out; /* len(task.target_variables)  (== nchannels_in)       */
+  int nchannels_out; /* len(task.target_variables)  (1..4)                  */
   int nfeatures;     /* model.nfeatures (64)                                */
   int nlayers;       /* RCAN residual groups / EDSR resblocks               */
   int nblocks;       /* RCAN RCABs per group (ignored for EDSR)             */
@@ -78,7 +78,11 @@ typedef struct srmi_model_config {
   int cu_budget;     /* CUs one launch should fill (0 = the whole GPU); two
                         engines on two streams each take half the chip     */
   int dtype;         /* SRMI_DTYPE_BF16 | SRMI_DTYPE_F32                    */
+  int flags;         /* SRMI_FLAG_* (0 = defaults)                           */
 } srmi_model_config;
+/* flags: SRMI_FLAG_NO_CA_FOLD runs every RCAB's channel-attention backward as its own
+ * pass (materialised du) instead of the fold into the conv launches (A/B, tests) */
+#define SRMI_FLAG_NO_CA_FOLD 1
 
 typedef struct srmi_param_info {
   long long offset; /* element offset in the flat fp32 parameter buffer     */

@@ -4,6 +4,7 @@
 #pragma once
 #include <type_traits>
 
+#include "ca_fold.hpp"
 #include "common.hpp"
 #include "srmi_internal.hpp"
 
@@ -127,7 +128,8 @@ template <int NPT, int EPI, int NCT = 4>
 __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)[NPT][NCT],
                                                const EpiPre<NPT, EPI, NCT>& e, const float4 (&bias)[NCT], int n,
                                                int cb, int y, int x0, int strip, int nstrips, float* red, int fr,
-                                               int fk, int row, int ct0, int tid, char* stage) {
+                                               int fk, int row, int ct0, int tid, char* stage,
+                                               const float4& fs = float4{0.f, 0.f, 0.f, 0.f}) {
   constexpr bool kShared = NCT < 4;
   const int half_id = ct0 >> 1;  // shared form: which of the two waves of the row
   auto stage_sync = [&]() __attribute__((always_inline)) {
@@ -225,6 +227,9 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       constexpr int RUNS = HALF / 4;  // 1 KiB runs per half
       const auto rf = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
       [[maybe_unused]] const auto rbb = wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
+      // CA-backward fold producer (EPI_DG_ACC_CA): du' = bf16(g * s) of the next RCAB
+      [[maybe_unused]] const bool fold_out = EPI == EPI_DG_ACC_CA && p.fold.du_out != nullptr;
+      [[maybe_unused]] const auto rdu = wt_rsrc(p.fold.du_out, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
       const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -267,6 +272,11 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             ps1[0][3] += val.w * bf2f(uu.y >> 16);
           }
           st_wt16(rf, p.yf, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 4), val);
+          if constexpr (EPI == EPI_DG_ACC_CA) {
+            if (fold_out)  // the lane's channels 4c..4c+3 are the same in every run: s in fs
+              st_wt8(rdu, p.fold.du_out, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 2),
+                     make_uint2(pack2(val.x * fs.x, val.y * fs.y), pack2(val.z * fs.z, val.w * fs.w)));
+          }
           if constexpr (EPI == EPI_DG_ACC) {
             if (p.yb)  // its bf16 copy: 512 contiguous bytes per instruction
               st_wt8(rbb, p.yb, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 2),
@@ -389,7 +399,7 @@ constexpr bool conv64_defers() {
   return ((SRMI_DEFER & 1) && EPI == EPI_RELU_BF16) || ((SRMI_DEFER & 2) && EPI == EPI_POOL_BF16) ||
          ((SRMI_DEFER & 4) && EPI == EPI_DG_RELUMASK) || ((SRMI_DEFER & 8) && EPI == EPI_DG_ACC_CA);
 }
-template <int TW, int EPI>
+template <int TW, int EPI, bool FOLD = false>
 __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_len, int bid, char* smem, int tail,
                                                   bool tail_part);
 
@@ -403,12 +413,17 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
 // NW = waves per workgroup: 4 (one per output row of the strip, all 64 output
 // channels) or 8 (a wave per row and channel half: two waves per SIMD, so one wave's
 // LDS / memory waits overlap the other's MFMAs; same LDS footprint)
-template <int TW, int EPI, int NW = 4>
+// FOLD (EPI_DG_RELUMASK, deferred form only): the consumer side of the CA-backward
+// fold (srmi_internal.hpp CaFold, ca_fold.hpp); the producer side (EPI_DG_ACC_CA) is
+// the runtime p.fold.du_out.
+template <int TW, int EPI, int NW = 4, bool FOLD = false>
 __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, int bid, char* smem, int tail = 0,
                                             bool tail_part = false) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(!FOLD || (EPI == EPI_DG_RELUMASK && NW == 8 && conv64_defers<EPI>()),
+                "the fold consumer is the deferred 8-wave ReLU-mask dgrad");
   if constexpr (NW == 8 && conv64_defers<EPI>()) {
-    conv64_body_defer<TW, EPI>(p, run_len, bid, smem, tail, tail_part);
+    conv64_body_defer<TW, EPI, FOLD>(p, run_len, bid, smem, tail, tail_part);
     return;
   }
   constexpr int NCT = NW == 8 ? 2 : 4;  // 16-wide output-channel tiles per wave
@@ -509,6 +524,13 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
     for (int c = 0; c < NCT; ++c) aoff[kk][c] = swz128((ct0 + c) * 16 + fr, kk * 4 + fk);
+  // fold producer: s of the next RCAB for the lane's 4 run-layout channels (conv_epilogue2)
+  float4 fs = float4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI == EPI_DG_ACC_CA) {
+    if (p.fold.du_out)
+      fs = *reinterpret_cast<const float4*>(p.fold.s_rec + (size_t)n * (128 + p.fold.CR) + 64 + p.fold.CR +
+                                            4 * (lane & 15));
+  }
   __syncthreads();
 
 #pragma unroll 1
@@ -597,7 +619,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     conv_epilogue2<NPT, EPI, NCT>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx, nsy * nsx, red, fr, fk, row, ct0,
-                                  tid, ring + (k % 3) * S::GROUPB + row * TW * 128);
+                                  tid, ring + (k % 3) * S::GROUPB + row * TW * 128, fs);
     STAMP(sj + 3);
     // LDS-only barrier: this strip's global stores stay in flight into the next strip
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -667,7 +689,7 @@ struct DeferOps {
   uint2 u[NPT][2];   // DG_ACC_CA: the CA input u
 };
 
-template <int TW, int EPI>
+template <int TW, int EPI, bool FOLD>
 __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_len, int bid, char* smem, int tail,
                                                   bool tail_part) {
   constexpr int NW = 8, NCT = 2;
@@ -759,6 +781,14 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     group_dma(k0 + 1);
     wait_vm<0>();
   }
+  // fold consumer: the image's CA MLP backward (c = dm / HW) and the border-class
+  // dgrad of c, from the filter image just landed (the first barrier inside makes
+  // every wave's DMA visible); the first run of the image writes its brec
+  float* const fsm = reinterpret_cast<float*>(smem + S::TOTAL);
+  if constexpr (FOLD) {
+    ca_fold_mlp(p.fold, n, p.N, (int)HW, fsm, ry == 0 && sx == 0 && cb == 0 && !tail_part);
+    ca_fold_corr(wl, fsm);
+  }
   STAMP(1);
   // A-fragment rows: lane fr of tile c reads the filter row of the channel its
   // accumulator row fr will hold (permuted for bf16 outputs)
@@ -813,6 +843,19 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     const size_t pix = (size_t)n * HW + (size_t)yy * p.W + x0 + pt * 16 + fr;
     if constexpr (kPerm) {
       float o[8];
+      // fold: + the dgrad of the constant c for this pixel's border class (8 contiguous
+      // channels ct0*16 + 8fk ..), before the ReLU mask
+      [[maybe_unused]] float cv[8];
+      if constexpr (FOLD) {
+        const int cy = yy == 0 ? 0 : (yy == p.H - 1 ? 2 : 1);
+        const int xx = x0 + pt * 16 + fr;
+        const int cx = xx == 0 ? 0 : (xx == p.W - 1 ? 2 : 1);
+        const float* cp = fsm + kFoldCorr + (cy * 3 + cx) * 64 + ct0 * 16 + 8 * fk;
+        const float4 c0 = *reinterpret_cast<const float4*>(cp);
+        const float4 c1 = *reinterpret_cast<const float4*>(cp + 4);
+        cv[0] = c0.x; cv[1] = c0.y; cv[2] = c0.z; cv[3] = c0.w;
+        cv[4] = c1.x; cv[5] = c1.y; cv[6] = c1.z; cv[7] = c1.w;
+      }
 #pragma unroll
       for (int c = 0; c < NCT; ++c) {
         const f32x4 v = accp[pt][c];
@@ -827,6 +870,7 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
           }
           if constexpr (EPI == EPI_DG_RELUMASK) {
             const uint32_t w = (c ? (rr < 2 ? ops.t[pt].z : ops.t[pt].w) : (rr < 2 ? ops.t[pt].x : ops.t[pt].y));
+            if constexpr (FOLD) x += cv[4 * c + rr];
             x = p.alpha * relu_mask((rr & 1) ? (w >> 16) : (w & 0xFFFFu), x);
           }
           o[4 * c + rr] = x;

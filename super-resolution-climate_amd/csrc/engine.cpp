@@ -213,6 +213,7 @@ struct srmi_engine {
   int max_cob = 0, max_cib = 0;  // largest Cout / 64, Cin / 64 of the packed convs
   bool tables_uploaded = false;
   int last_n = 0;
+  const float* probe_prm = nullptr;  // the parameters of the last backward (srmi_engine_probe)
 
   bf16_t* at(bf16_t* base, size_t elems) const {
     return reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(base) + elems * esz);
@@ -508,6 +509,34 @@ static int dgrad_with_wgrad(srmi_engine* e, const ConvParams& cp, int epi, const
   return conv3x3_launch(cp, epi, st);
 }
 
+// the CA-backward fold runs where both halves of the RCAB backward are fused launches
+// (bf16, 48-wide tiles) and the producer's epilogue is the specialised DG_ACC_CA
+#ifndef SRMI_CA_FOLD
+#define SRMI_CA_FOLD 1
+#endif
+static bool use_ca_fold(const srmi_engine* e, int n) {
+  if (!SRMI_CA_FOLD || (e->P.cfg.flags & SRMI_FLAG_NO_CA_FOLD) || e->f32 || e->P.cfg.arch != SRMI_ARCH_RCAN ||
+      e->w != 48 || e->h % 4)
+    return false;
+  const int R = e->P.cfg.reduction, CR = 64 / R;
+  if (CR < 4 || CR > 32 || CR % 4) return false;
+  const int rs2 = rcab_row_splits(e, n, 2);
+  return (e->h / rs2) % 4 == 0;
+}
+
+static CaFold fold_consumer(const srmi_engine* e, const float* prm, const RCABRef& r, int g, int b, int nstrips) {
+  CaFold f{};
+  f.part = e->pacc;
+  f.nstrips = nstrips;
+  f.CR = 64 / e->P.cfg.reduction;
+  f.rec = e->recp(g, b);
+  f.w1 = prm + r.ca_w1;
+  f.w2 = prm + r.ca_w2;
+  f.brec = e->brecp(g, b);
+  f.on = 1;
+  return f;
+}
+
 #define RC(x)              \
   do {                     \
     int _rc = (x);         \
@@ -598,6 +627,7 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
   const int n = e->last_n, h = e->h, w = e->w, HW = h * w;
   const int nstrips = conv3x3_nstrips(h, w);
   int H = h << P.nups, W = w << P.nups;
+  e->probe_prm = prm;
   // tail conv 64 -> C
   const bf16_t* xlast = e->PS[P.nups - 1];
   const float* yv = dy ? dy : sr;
@@ -636,6 +666,11 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
     // The filter gradients write the slab set of their RCAB's parity; the last
     // RCAB of a group reduces its own slabs before the group's event.
     const int rs2 = rcab_row_splits(e, n, 2), rs1 = rcab_row_splits(e, n, 1);
+    // The CA-backward fold (srmi_internal.hpp CaFold): every RCAB but the first one of
+    // a group in backward order gets du' = bf16(g * s) from the conv1 dgrad of the RCAB
+    // above (F1) instead of a CA-backward pass; its conv2 backward (F2) adds the
+    // constant dm / HW itself.  bf16 engine, fused-launch shapes only.
+    const bool fold = use_ca_fold(e, n);
     int it = 0;  // RCAB counter (slab-set parity)
     for (int g = nl - 1; g >= 0; --g) {
       const ConvRef& gt = P.group_tail[g];
@@ -649,8 +684,13 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         const int q = it++ & 1;
         bf16_t* du = e->DU;
         bf16_t* dz = e->DZ;
-        RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
-                            e->brecp(g, b), e->f32, st, have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
+        const bool folded = fold && b < nb;  // du' came from the previous F1
+        if (!folded) {
+          RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
+                              e->brecp(g, b), e->f32, st, have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
+        } else {
+          RC(wgrad_reduce2_launch(prev2, prev1, st));
+        }
         ReduceSet red2, red1;
         WgradParams wp;
         int epi = EPI_DG_RELUMASK;
@@ -658,12 +698,21 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
                                      nullptr, 1.f);
         RC(wgrad_params(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, rs2, e->slab_r[q][0], e->bslab_r[q][0],
                         e->slab_r_floats, e->bslab_r_floats, &wp, &red2));
+        if (folded) {
+          cp.fold = fold_consumer(e, prm, r, g, b, nstrips);
+          wp.fold = cp.fold;
+        }
         RC(dgrad_with_wgrad(e, cp, epi, wp, 2, st));
         const bool last = (b == 1);
         epi = EPI_DG_ACC;
         cp = dgrad_params(e, r.c1, dz, n, h, w, &epi, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
                           (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
                           last ? nullptr : e->pacc, 1.f);
+        if (fold && !last) {  // du' of RCAB b - 1
+          cp.fold.du_out = e->DU;
+          cp.fold.s_rec = e->recp(g, b - 1);
+          cp.fold.CR = 64 / R;
+        }
         RC(wgrad_params(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, rs1, e->slab_r[q][1],
                         e->bslab_r[q][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red1));
         RC(dgrad_with_wgrad(e, cp, epi, wp, 1, st));
@@ -792,12 +841,17 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
   ReduceSet red;
   ConvParams cp;
   int epi;
+  const bool fold = use_ca_fold(e, n) && b < e->P.cfg.nblocks && e->probe_prm;  // (as backward_impl has it)
   if (which == 2) {
     epi = EPI_DG_RELUMASK;
     cp = dgrad_params(e, r.c2, e->DU, n, h, w, &epi, e->DZ, nullptr, nullptr, nullptr, nullptr, e->Tm(0, b), nullptr,
                       1.f);
     RC(wgrad_params(e, r.c2, e->Tm(0, b), e->DU, n, h, w, grads, false, 1.f, rcab_row_splits(e, n, 2),
                     e->slab_r[0][0], e->bslab_r[0][0], e->slab_r_floats, e->bslab_r_floats, &wp, &red));
+    if (fold) {
+      cp.fold = fold_consumer(e, e->probe_prm, r, 0, b, conv3x3_nstrips(h, w));
+      wp.fold = cp.fold;
+    }
   } else {
     const bool last = (b == 1);
     epi = EPI_DG_ACC;
@@ -805,6 +859,11 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
                       nullptr, last ? nullptr : e->Um(0, b - 1), last ? nullptr : e->pacc, 1.f);
     RC(wgrad_params(e, r.c1, e->hb(0, b - 1), e->DZ, n, h, w, grads, true, 1.f, rcab_row_splits(e, n, 1),
                     e->slab_r[0][1], e->bslab_r[0][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red));
+    if (use_ca_fold(e, n) && !last) {
+      cp.fold.du_out = e->DU;
+      cp.fold.s_rec = e->recp(0, b - 1);
+      cp.fold.CR = 64 / e->P.cfg.reduction;
+    }
   }
   for (int i = 0; i < reps; ++i) RC(dgrad_with_wgrad(e, cp, epi, wp, which, S_(stream)));
   return 0;

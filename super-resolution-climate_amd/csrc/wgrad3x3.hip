@@ -235,6 +235,15 @@ constexpr int NGP = 2 * GD + 2 * GX;                             // groups per p
 }  // namespace v4
 
 
+#ifndef SRMI_FOLD_PARTS
+#define SRMI_FOLD_PARTS 3  // diagnostic: 1 = only the dgrad side of the fold consumer, 2 = only the filter gradient's
+#endif
+// the fold's LDS scratch in the fused launch: after the conv body's own LDS (which
+// is larger than the filter gradient's rings)
+constexpr int kFoldOff = Conv2Smem<48>::TOTAL;
+static_assert(Conv2Smem<48>::TOTAL >= v4::LDS, "fold scratch must not overlap the rings");
+static_assert(kFoldOff + kFoldBytes <= 160 * 1024, "LDS");
+
 #ifndef SRMI_SLAB_WT
 #define SRMI_SLAB_WT 1  // partial slabs stored write-through (in-step A/B +1.1 %)
 #endif
@@ -247,7 +256,105 @@ constexpr int NGP = 2 * GD + 2 * GX;                             // groups per p
 // 0-3 also issue the DMA (the 4-wave schedule) and the bias gradient; every wave
 // keeps all four output-channel tiles and writes its partial slab in the 4-wave
 // layout, so wgrad_reduce is unchanged.
-template <int WV, int NW = 4>
+// The fold's filter-gradient term for one chunk (rows ybase .. ybase + Hr - 1 of image
+// n, W == 48): T[tap][ci] = sum over the chunk's pixels p of x[p + off(tap)][ci]
+// (zero outside the image), then acc += c[co] T[tap][ci] (c = dm / HW, ca_fold_mlp).
+// Runs after the K-loop (every wave): the rings are free, the input rows are L2-hot.
+//   T[ky][kx] = sum over input rows r of the ky window (ky 0: rows -1 .. Hr-2, 1: 0 ..
+//   Hr-1, 2: 1 .. Hr) of the row sum over the kx window (kx 0: columns 0 .. 46, 1:
+//   all, 2: 1 .. 47).  Thread (pixel pg, 8-channel chunk cc) sums its pixel over the
+//   rows into the three ky windows; the pixel partials are combined in LDS in a fixed
+//   order (deterministic), the kx windows by subtracting the pixel-0 / pixel-47 parts.
+template <int NT, int J0>
+__device__ __forceinline__ void wgrad48_fold_correction(const WgradParams& p, char* smem, f32x4 (&acc)[4][NT], int n,
+                                                        int ybase, int Hr, int wave, int lane) {
+  constexpr int Wd = 48;
+  float* const fsm = reinterpret_cast<float*>(smem + kFoldOff);
+  float* const tpart = reinterpret_cast<float*>(smem);              // [48 pg][3 ky][64 ci] (ring: free now)
+  float* const tsum = reinterpret_cast<float*>(smem + 48 * 3 * 64 * 4);  // [9 taps][64 ci]
+  const int tid = threadIdx.x;
+  fold_barrier();  // every wave is past its last ring read
+  ca_fold_mlp(p.fold, n, p.N, p.H * Wd, fsm, false);
+  {
+    const int cc = tid & 7, pg = tid >> 3;
+    float a[3][8];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[k][e] = 0.f;
+    if (pg < Wd) {
+      const bf16_t* xr = p.x + ((size_t)n * p.H * Wd + pg) * 64 + cc * 8;
+      // rows -1 .. Hr, 8 loads in flight per batch (the rows were just streamed: L2 hits)
+      for (int r0 = -1; r0 <= Hr; r0 += 8) {
+        uint4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int y = ybase + r0 + i;
+          const bool ok = r0 + i <= Hr && y >= 0 && y < p.H;
+          v[i] = ok ? *reinterpret_cast<const uint4*>(xr + (size_t)y * Wd * 64) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int r = r0 + i;
+          const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+          float x[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            x[2 * e] = __uint_as_float(w[e] << 16);
+            x[2 * e + 1] = __uint_as_float(w[e] & 0xFFFF0000u);
+          }
+          const bool k0 = r <= Hr - 2, k1 = r >= 0 && r <= Hr - 1, k2 = r >= 1;  // (r > Hr: zeros)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            a[0][e] += k0 ? x[e] : 0.f;
+            a[1][e] += k1 ? x[e] : 0.f;
+            a[2][e] += k2 ? x[e] : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        float4* d = reinterpret_cast<float4*>(tpart + (pg * 3 + k) * 64 + cc * 8);
+        d[0] = make_float4(a[k][0], a[k][1], a[k][2], a[k][3]);
+        d[1] = make_float4(a[k][4], a[k][5], a[k][6], a[k][7]);
+      }
+    }
+  }
+  fold_barrier();
+  if (tid < 192) {  // (ky, ci): the pixel partials in order, then the three kx windows
+    const int ky = tid >> 6, ci = tid & 63;
+    float sum = 0.f;
+    for (int pg = 0; pg < Wd; ++pg) sum += tpart[(pg * 3 + ky) * 64 + ci];
+    tsum[(ky * 3 + 0) * 64 + ci] = sum - tpart[((Wd - 1) * 3 + ky) * 64 + ci];
+    tsum[(ky * 3 + 1) * 64 + ci] = sum;
+    tsum[(ky * 3 + 2) * 64 + ci] = sum - tpart[ky * 64 + ci];
+  }
+  fold_barrier();
+  // acc[ct][t]: rows 4 (lane >> 4) + r of co tile (ct + wave) & 3, column ci of N tile
+  // J0 + t (tap = J >> 2, ci = 16 (J & 3) + (lane & 15))
+  float tv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int J = J0 + t;
+    tv[t] = tsum[(J >> 2) * 64 + (J & 3) * 16 + (lane & 15)];
+  }
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    const float4 cv = *reinterpret_cast<const float4*>(fsm + kFoldC + ((ct + wave) & 3) * 16 + 4 * (lane >> 4));
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      acc[ct][t][0] += cv.x * tv[t];
+      acc[ct][t][1] += cv.y * tv[t];
+      acc[ct][t][2] += cv.z * tv[t];
+      acc[ct][t][3] += cv.w * tv[t];
+    }
+  }
+}
+
+// FOLD (the conv2 filter gradient of a folded RCAB, fused launch only, W == 48):
+// before the slab store the partial gains c[co] T[tap][ci] (wgrad48_fold_correction):
+// the filter gradient of du = du' + c, exactly.
+template <int WV, int NW = 4, bool FOLD = false>
 __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, int chunk, int cb) {
   using namespace v4;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
@@ -515,6 +622,7 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   // other way round in round 2: the launch 0.9 us shorter, the reduce 1.9 us longer)
   // (N tile J, slot ct of rotation `wave`) -> the 4-wave position (wave J / 9, tile
   // J % 9, the slot of the same output-channel tile under that wave's rotation)
+  if constexpr (FOLD) wgrad48_fold_correction<NT, J0>(p, smem, acc, n, ybase, Hr, wave, lane);
   const size_t soff = (size_t)chunk * Cout * 576 + (size_t)cb * (64 * 576);
   // (write-through: the slab leaves the XCD's L2 while the other waves still
   //  compute, instead of in the dirty-line flush at the end of the launch)
@@ -540,20 +648,20 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   WSTAMP(63);
 }
 
-template <int NW = 4>
+template <int NW = 4, bool FOLD = false>
 __device__ __forceinline__ void wgrad48_dispatch(const WgradParams& p, char* smem, int chunk, int cb) {
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: wgrad48_body<0, NW>(p, smem, chunk, cb); break;
-    case 1: wgrad48_body<1, NW>(p, smem, chunk, cb); break;
-    case 2: wgrad48_body<2, NW>(p, smem, chunk, cb); break;
-    case 3: wgrad48_body<3, NW>(p, smem, chunk, cb); break;
+    case 0: wgrad48_body<0, NW, FOLD>(p, smem, chunk, cb); break;
+    case 1: wgrad48_body<1, NW, FOLD>(p, smem, chunk, cb); break;
+    case 2: wgrad48_body<2, NW, FOLD>(p, smem, chunk, cb); break;
+    case 3: wgrad48_body<3, NW, FOLD>(p, smem, chunk, cb); break;
     default:
       if constexpr (NW == 8) {
         switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-          case 4: wgrad48_body<4, NW>(p, smem, chunk, cb); break;
-          case 5: wgrad48_body<5, NW>(p, smem, chunk, cb); break;
-          case 6: wgrad48_body<6, NW>(p, smem, chunk, cb); break;
-          default: wgrad48_body<7, NW>(p, smem, chunk, cb); break;
+          case 4: wgrad48_body<4, NW, FOLD>(p, smem, chunk, cb); break;
+          case 5: wgrad48_body<5, NW, FOLD>(p, smem, chunk, cb); break;
+          case 6: wgrad48_body<6, NW, FOLD>(p, smem, chunk, cb); break;
+          default: wgrad48_body<7, NW, FOLD>(p, smem, chunk, cb); break;
         }
       }
       break;
@@ -591,7 +699,7 @@ __global__ void __launch_bounds__(kWgradNW * 64, 1) wgrad48_kernel(WgradParams p
 // dgrad half (F1: 24.7 vs 36.9 us at C2), so the last `tail` strips of dgrad run k
 // move to the workgroup of chunk k, which runs them after its chunk (same rows, same
 // XCD), with its own filter prologue.
-template <int EPI, int NW>
+template <int EPI, int NW, bool FOLD = false>
 __global__ void __launch_bounds__(NW * 64, 1) rcab_bwd_kernel(ConvParams cp, int run_len, int nconv, WgradParams wp,
                                                               int nwg, int paired, int tail) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -610,14 +718,14 @@ __global__ void __launch_bounds__(NW * 64, 1) rcab_bwd_kernel(ConvParams cp, int
     else w = b - c0;
   }
   if (conv >= 0) {
-    if (!(SRMI_FUSE_DIAG & 2)) conv64_body<48, EPI, NW>(cp, run_len, conv, smem, tail, false);
+    if (!(SRMI_FUSE_DIAG & 2)) conv64_body<48, EPI, NW, FOLD && (SRMI_FOLD_PARTS & 1)>(cp, run_len, conv, smem, tail, false);
     return;
   }
   const int nch = wp.N * wp.row_splits;
-  if (!(SRMI_FUSE_DIAG & 1)) wgrad48_dispatch<NW>(wp, smem, w % nch, w / nch);
+  if (!(SRMI_FUSE_DIAG & 1)) wgrad48_dispatch<NW, FOLD && (SRMI_FOLD_PARTS & 2)>(wp, smem, w % nch, w / nch);
   if (tail > 0 && !(SRMI_FUSE_DIAG & 2)) {
     __syncthreads();  // every wave is past its last LDS read of the chunk
-    conv64_body<48, EPI, NW>(cp, run_len, w, smem, tail, true);
+    conv64_body<48, EPI, NW, FOLD>(cp, run_len, w, smem, tail, true);
   }
 }
 
@@ -644,7 +752,14 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
   const int run_len = conv64_run_len(cp, 48, conv_cus);
   const int nconv = conv64_blocks(cp, 48, run_len);
   const int nwg = wp.N * wp.row_splits * (wp.Cout / 64);
-  const int lds = Conv2Smem<48>::TOTAL > v4::LDS ? Conv2Smem<48>::TOTAL : v4::LDS;
+  const bool fold = cp.fold.on != 0;
+  if (fold && (epi != EPI_DG_RELUMASK || !wp.fold.on || !cp.fold.part || !cp.fold.rec || !cp.fold.w1 ||
+               !cp.fold.w2 || !cp.fold.brec || cp.fold.CR < 4 || cp.fold.CR > 32 || cp.fold.CR % 4 ||
+               cp.alpha != 1.f))
+    return SRMI_ERR_ARG;
+  if (epi == EPI_DG_ACC_CA && cp.fold.du_out && (!cp.fold.s_rec || cp.fold.CR < 4 || cp.fold.CR > 32))
+    return SRMI_ERR_ARG;
+  const int lds = (Conv2Smem<48>::TOTAL > v4::LDS ? Conv2Smem<48>::TOTAL : v4::LDS) + (fold ? kFoldBytes : 0);
   ConvParams c = cp;
   c.stamps = nullptr;
   WgradParams w = wp;
@@ -668,8 +783,12 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
   switch (epi) {
     case EPI_DG_RELUMASK:
       if (!c.aux) return SRMI_ERR_ARG;
-      hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_RELUMASK, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len, nconv, w, nwg,
-                         paired, tail);
+      if (fold)
+        hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_RELUMASK, kFuseNW, true>), grid, dim3(kFuseNW * 64), lds, st, c,
+                           run_len, nconv, w, nwg, paired, tail);
+      else
+        hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_RELUMASK, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len,
+                           nconv, w, nwg, paired, tail);
       break;
     case EPI_DG_ACC_CA:
       if (!c.r1 || !c.aux || !c.part || c.yb || c.r2 || c.r3 || !c.yf) return SRMI_ERR_ARG;

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("SRMI_LIB") or LIB_PATH_DEFAULT  # SRMI_LIB: diagnosti
 SRMI_ARCH_RCAN = 0
 SRMI_ARCH_EDSR = 1
 SRMI_DTYPE_BF16 = 0
+SRMI_FLAG_NO_CA_FOLD = 1
 SRMI_DTYPE_F32 = 1
 SRMI_LOSS_RMSE = 0
 SRMI_LOSS_MEAN = 1
@@ -29,7 +30,7 @@ class ModelConfig(C.Structure):
     _fields_ = [("arch", C.c_int), ("nchannels_in", C.c_int), ("nchannels_out", C.c_int),
                 ("nfeatures", C.c_int), ("nlayers", C.c_int), ("nblocks", C.c_int), ("reduction", C.c_int),
                 ("scale", C.c_int), ("res_scale", C.c_float), ("batch", C.c_int), ("lr_h", C.c_int),
-                ("lr_w", C.c_int), ("cu_budget", C.c_int), ("dtype", C.c_int)]
+                ("lr_w", C.c_int), ("cu_budget", C.c_int), ("dtype", C.c_int), ("flags", C.c_int)]
 
 
 class ParamInfo(C.Structure):

@@ -36,6 +36,7 @@ class NetSpec:
     scale: int = 4
     res_scale: float = 1.0
     dtype: str = "bf16"   # engine operand type: "bf16" (bf16 MFMA operands) or "fp32" (exact fp32)
+    flags: int = 0        # srmi_model_config.flags (SRMI_FLAG_NO_CA_FOLD: A/B and tests)
 
     @staticmethod
     def from_parms(arch: str, parms: Dict, dtype: str = "bf16") -> "NetSpec":
@@ -55,7 +56,8 @@ class NetSpec:
             raise _lib.SrmiError(f"unknown engine dtype {self.dtype!r} (bf16 | fp32)")
         return ModelConfig(ARCHS[self.arch], self.nchannels_in, self.nchannels_out, self.nfeatures, self.nlayers,
                            self.nblocks if self.arch == "rcan" else 0, self.cbottleneck if self.arch == "rcan" else 1,
-                           self.scale, self.res_scale, batch, lr_h, lr_w, int(cu_budget), DTYPES[self.dtype])
+                           self.scale, self.res_scale, batch, lr_h, lr_w, int(cu_budget), DTYPES[self.dtype],
+                           int(self.flags))
 
 
 def param_names(spec: NetSpec) -> List[str]:

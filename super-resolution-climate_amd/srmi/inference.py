@@ -301,7 +301,7 @@ class TiledInference:
                 ib = tile_index // bs if batch_domain == "tiles" else tile_index
                 a0, a1 = ib * bs, min(nt, (ib + 1) * bs)
                 sel = slice(ib, ib + 1)
-                if a0 >= nt:  # no batch of this slice holds the tile
+                if a0 >= nt or (batch_domain == "tiles" and tile_index >= nt):  # no batch of this slice holds it
                     if time_index >= 0:
                         break
                     continue

@@ -6,12 +6,21 @@ tests run the same oracle module (oracle/rcan_oracle.py, PyTorch) on the GPU in
 fp32 as the checker, with MIOpen disabled (no kernel JIT on a fresh box: convs
 run as unfold + rocBLAS GEMM) and no reduced-precision math.
 
-`bf16_operand_emulation` turns an oracle model into the reference arithmetic
-with bf16-rounded conv OPERANDS (the engine's precision model, SURVEY.md §8(c):
-bf16 operands, fp32 accumulation, fp32 residual stream): every 3x3 conv with 64
-input channels computes y = conv(bf16(x), bf16(w)) + b, and its backward
-dx = conv^T(bf16(dy), bf16(w)), dw = corr(bf16(x), bf16(dy)); everything else
-stays fp32.  Its drift from the fp32 oracle is the reference's own bf16 drift,
+`bf16_operand_emulation` turns an oracle model into the engine's precision model
+(what the bf16 engine actually computes):
+* every 3x3 conv with 64 input channels computes y = conv(bf16(x), bf16(w)) + b,
+  its backward dx = conv^T(bf16(dy), bf16(w)), dw = corr(bf16(x), bf16(dy)) (the
+  engine's MFMA operands and its bf16 activation / gradient maps t, u, hb, dz, du);
+* in every RCAB the channel-attention product uses the stored bf16 u while the
+  pooled mean is taken from the fp32 conv output (the conv2 POOL epilogue sums
+  before rounding): out = bf16(u) * s(mean(u));
+* the residual stream INSIDE a residual group is the pair hi + lo (bf16 hi plus an
+  8-bit remainder in units of ulp(hi) / 256, common.hpp lo8 codec): 16 significant
+  bits, rounded after every CA add (h = pair16(h + out)); the group input, the
+  group-tail / body-tail outputs and the whole gradient stream stay fp32.
+Rounding is straight-through in backward, as in the engine (the stored values are
+what backward reads; the gradient of an add is the identity).  The model's drift
+from the fp32 oracle is the reference's own drift under the engine's arithmetic,
 from which the tests derive their gradient bounds.
 """
 from __future__ import annotations
@@ -57,6 +66,51 @@ class _Bf16OperandConv(torch.autograd.Function):
         return dx, dw, dy.sum(dim=(0, 2, 3)), None
 
 
+class _StraightBf16(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return _bf(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+def pair16(h: torch.Tensor) -> torch.Tensor:
+    """The lo8 pair codec (csrc/common.hpp lo8_encode / lo8_decode): hi = bf16(h)
+    (round to nearest even), q = rint((h - hi) * 2^(15 - E)) clamped to +-127 for
+    hi = m 2^E (1 <= |m| < 2), value = hi + q 2^(E - 15); hi zero, subnormal, tiny
+    (biased exponent <= 15), inf or nan carries no remainder."""
+    hf = h.float()
+    hi = hf.to(torch.bfloat16).float()
+    bits = hi.view(torch.int32)
+    e = (bits >> 23) & 0xFF
+    ok = (e > 15) & (e < 255)
+    scale = torch.ldexp(torch.ones_like(hi), (142 - e).clamp(-126, 127))  # 2^(15 - E), E = e - 127
+    q = torch.round((hf - hi) * scale).clamp(-127.0, 127.0)
+    unit = torch.ldexp(torch.ones_like(hi), (e - 142).clamp(-149, 127))    # 2^(E - 15)
+    val = torch.where(ok, hi + q * unit, hi)
+    return val.to(h.dtype)
+
+
+class _StraightPair16(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return pair16(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+def _emul_rcab_forward(self, x):
+    """RCAB (sres/model/rcan/network.py:54-64) as the bf16 engine computes it."""
+    b = self.body
+    u = b[2](b[1](b[0](x)))
+    s = b[3].conv_du(u.mean(dim=(2, 3), keepdim=True))
+    return _StraightPair16.apply(_StraightBf16.apply(u) * s + x)
+
+
 class _EmulConv(nn.Module):
     def __init__(self, conv: nn.Conv2d):
         super().__init__()
@@ -67,12 +121,20 @@ class _EmulConv(nn.Module):
         return _Bf16OperandConv.apply(x, c.weight, c.bias, c.padding)
 
 
-def bf16_operand_emulation(model: nn.Module) -> nn.Module:
-    """In place: wrap every 3x3 conv with 64 input channels (not the C-channel head)."""
+def bf16_operand_emulation(model: nn.Module, pair_stream: bool = True) -> nn.Module:
+    """In place: wrap every 3x3 conv with 64 input channels (not the C-channel head)
+    and, with pair_stream, give every RCAB the engine's CA product and in-group pair
+    residual stream (module docstring)."""
+    import types
+    from oracle.rcan_oracle import _RCAB
     for name, mod in list(model.named_modules()):
         for cname, child in list(mod.named_children()):
             if isinstance(child, nn.Conv2d) and child.kernel_size == (3, 3) and child.in_channels == 64:
                 setattr(mod, cname, _EmulConv(child))
+    if pair_stream:
+        for mod in model.modules():
+            if isinstance(mod, _RCAB):
+                mod.forward = types.MethodType(_emul_rcab_forward, mod)
     return model
 
 

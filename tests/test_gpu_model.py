@@ -2,7 +2,8 @@
 generated from the reference (tests/golden/make_golden.py).
 
 Tolerances: the engine computes conv operands in bf16 with
-fp32 accumulation and an fp32 residual stream, so element-wise outputs are
+fp32 accumulation and a 16-bit pair residual stream inside each residual group
+(emulated by tests/gpu_oracle.py), so element-wise outputs are
 compared by relative L2 (<= 2e-2), the loss within 2e-3 relative (the
 north-star "results within 1e-3 rel" is met for the loss at full size, see
 test_full_rcan_loss_parity), gradients by relative L2 per tensor family.
@@ -293,3 +294,46 @@ def test_checkpoint_resume_matches_uninterrupted():
     torch.cuda.synchronize()
     assert torch.equal(a.params, c.params)
     assert torch.equal(a.m, c.m) and torch.equal(a.v, c.v)
+
+
+@pytest.mark.parametrize("lr_hw", [(48, 48), (32, 48), (8, 48)])
+def test_ca_fold_matches_materialised_du(lr_hw):
+    """The CA-backward fold (du never materialised; srmi_internal.hpp CaFold, DESIGN.md
+    §3) against the materialised path (SRMI_FLAG_NO_CA_FOLD) on the same step: the
+    forward is untouched (bit-identical output and loss) and every gradient -- the
+    conv2 filter gradients with their c (x) T term, the conv1 chain through the dgrad's
+    border-class correction, the CA MLP parameter gradients from the fold's backward
+    record -- agrees to the bf16 rounding of du (the materialised path rounds
+    g s + dm/HW once, the fold rounds g s and adds dm/HW in fp32).  Both paths sit
+    within the drift bounds of the fp64 oracle.  Three tile heights move the border
+    rows between strips and runs."""
+    from srmi.trainer import default_init_
+    d = dev()
+    h, w = lr_hw
+    C, nl, nb, B = 2, 2, 4, 6
+    specs = [NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=nl, nblocks=nb,
+                     cbottleneck=2, scale=4, flags=f) for f in (0, 1)]
+    table = _table(specs[0])
+    flat = torch.empty(sum(t[2] for t in table))
+    default_init_(flat, table, seed=21)
+    g = torch.Generator().manual_seed(5)
+    hr = torch.randn(B, C, 4 * h, 4 * w, generator=g, dtype=torch.float64)
+    trs = [FusedTrainer(sp, B, (h, w), device=d, params=flat.to(d), micro=1) for sp in specs]
+    outs = [t.step(hr.float().to(d)) for t in trs]
+    torch.cuda.synchronize()
+    assert torch.equal(trs[0].sr, trs[1].sr)
+    assert float(outs[0]["loss"]) == float(outs[1]["loss"])
+    ga, gb = trs[0].grads.cpu(), trs[1].grads.cpu()
+    assert rel_l2(ga, gb) < 5e-3
+    model = ro.RCANOracle(nchannels_in=C, nchannels_out=C, nlayers=nl, nblocks=nb, nfeatures=64, cbottleneck=2).double()
+    sd = dict(model.named_parameters())
+    with torch.no_grad():
+        for name, off, n, shape in table:
+            sd[name].copy_(flat[off:off + n].view(shape).double())
+    _, _, g_ref = oracle_grads(model, hr.numpy(), 4)
+    bound = drift_bounds(model, hr.numpy(), 4, g_ref)
+    for name, off, n, shape in table:
+        ra = rel_l2(ga[off:off + n].view(shape), g_ref[name])
+        rb = rel_l2(gb[off:off + n].view(shape), g_ref[name])
+        assert ra <= bound[name] and rb <= bound[name], (name, ra, rb, bound[name])
+        assert rel_l2(ga[off:off + n], gb[off:off + n]) < 3e-2, name
