@@ -514,6 +514,11 @@ static int dgrad_with_wgrad(srmi_engine* e, const ConvParams& cp, int epi, const
 #ifndef SRMI_CA_FOLD
 #define SRMI_CA_FOLD 1
 #endif
+// folded RCABs: the previous RCAB's two slab reductions run in the conv2 backward
+// launch's filter-gradient workgroups after their chunk (0: a reduction launch)
+#ifndef SRMI_RED_IN_F2
+#define SRMI_RED_IN_F2 1
+#endif
 static bool use_ca_fold(const srmi_engine* e, int n) {
   if (!SRMI_CA_FOLD || (e->P.cfg.flags & SRMI_FLAG_NO_CA_FOLD) || e->f32 || e->P.cfg.arch != SRMI_ARCH_RCAN ||
       e->w != 48 || e->h % 4)
@@ -688,7 +693,7 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         if (!folded) {
           RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
                               e->brecp(g, b), e->f32, st, have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
-        } else {
+        } else if (!SRMI_RED_IN_F2) {
           RC(wgrad_reduce2_launch(prev2, prev1, st));
         }
         ReduceSet red2, red1;
@@ -701,6 +706,11 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         if (folded) {
           cp.fold = fold_consumer(e, prm, r, g, b, nstrips);
           wp.fold = cp.fold;
+          if (SRMI_RED_IN_F2) {  // the previous RCAB's slab reductions ride in this launch
+            wp.red[0] = prev2;
+            wp.red[1] = prev1;
+            wp.nred = 2;
+          }
         }
         RC(dgrad_with_wgrad(e, cp, epi, wp, 2, st));
         const bool last = (b == 1);
@@ -851,6 +861,21 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
     if (fold) {
       cp.fold = fold_consumer(e, e->probe_prm, r, 0, b, conv3x3_nstrips(h, w));
       wp.fold = cp.fold;
+      // and, as in the step, the previous RCAB's two slab reductions (the other slab
+      // parity; results into GAf -- scratch after the timed region -- when they fit)
+      const RCABRef& rp = e->P.groups[0][b];
+      float* gs = e->GAf - rp.c1.w;
+      ReduceSet r2, r1;
+      WgradParams tmp;
+      if (SRMI_RED_IN_F2 && rp.c1.b + 64 <= (long long)e->mapn && rp.c2.w + 64 * 576 <= (long long)e->mapn &&
+          wgrad_params(e, rp.c2, e->Tm(0, b + 1), e->DU, n, h, w, gs, false, 1.f, rcab_row_splits(e, n, 2),
+                       e->slab_r[1][0], e->bslab_r[1][0], e->slab_r_floats, e->bslab_r_floats, &tmp, &r2) == 0 &&
+          wgrad_params(e, rp.c1, e->hb(0, b), e->DZ, n, h, w, gs, true, 1.f, rcab_row_splits(e, n, 1),
+                       e->slab_r[1][1], e->bslab_r[1][1], e->slab_r_floats, e->bslab_r_floats, &tmp, &r1) == 0) {
+        wp.red[0] = r2;
+        wp.red[1] = r1;
+        wp.nred = 2;
+      }
     }
   } else {
     const bool last = (b == 1);

@@ -73,6 +73,15 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st);  // dispatches
 int conv3x3_f32_launch(const ConvParams& p, int epi, hipStream_t st);
 int conv3x3_nstrips(int H, int W);
 
+struct ReduceSet {  // one slab reduction: slabs -> torch-layout dW (and db)
+  const float* slab;
+  const float* bslab;
+  int nslab, Cout, ps, layout;
+  float alpha;
+  float* gw;
+  float* gb;
+};
+
 // weight gradient of a 3x3 conv: slab[s][Cout][9][64] + bias slab[s][Cout]
 struct WgradParams {
   const bf16_t* x;     // forward input NHWC [N][H][W][64]
@@ -87,6 +96,11 @@ struct WgradParams {
   unsigned long long* stamps;  // diagnostic (null in production)
   int f32;             // exact-fp32 mode: x, dy point at fp32 data
   CaFold fold;         // consumer side (the conv2 filter gradient of a folded RCAB)
+  // fused launch only: two slab reductions of an earlier launch (the previous RCAB's
+  // filter gradients) shared out over this launch's filter-gradient workgroups,
+  // after their own chunk (nred = 0: none)
+  ReduceSet red[2];
+  int nred;
 };
 void wgrad3x3_set_debug_stamps(unsigned long long* buf);
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st);  // dispatches p.f32
@@ -97,14 +111,7 @@ int wgrad3x3_nslabs(const WgradParams& p);
 int wgrad3x3_slab_layout(const WgradParams& p);
 // slab reduction into the torch-layout grad [Cout][64][3][3] (+ bias [Cout]);
 // ps != 0 un-permutes the packed PixelShuffle channel order (c'' = 64q + c -> 4c + q)
-struct ReduceSet {  // one slab reduction: slabs -> torch-layout dW (and db)
-  const float* slab;
-  const float* bslab;
-  int nslab, Cout, ps, layout;
-  float alpha;
-  float* gw;
-  float* gb;
-};
+
 int wgrad_reduce2_launch(const ReduceSet& r0, const ReduceSet& r1, hipStream_t st);
 // fused RCAB backward launch: dgrad conv (epi RELUMASK / DG_ACC_CA / DG_ACC, its runs
 // sized for conv_cus CUs) beside the filter gradient wp of the same conv (wgrad48)

@@ -723,6 +723,10 @@ __global__ void __launch_bounds__(NW * 64, 1) rcab_bwd_kernel(ConvParams cp, int
   }
   const int nch = wp.N * wp.row_splits;
   if (!(SRMI_FUSE_DIAG & 1)) wgrad48_dispatch<NW, FOLD && (SRMI_FOLD_PARTS & 2)>(wp, smem, w % nch, w / nch);
+  if (wp.nred > 0) {  // the previous RCAB's slab reductions, shared over this launch's filter-gradient workgroups
+    static_assert(NW * 64 == 512, "slab_reduce_share runs on 512 threads");
+    slab_reduce_share(wp.red[0], wp.red[1], wp.nred, w, nwg, reinterpret_cast<float4*>(smem));
+  }
   if (tail > 0 && !(SRMI_FUSE_DIAG & 2)) {
     __syncthreads();  // every wave is past its last LDS read of the chunk
     conv64_body<48, EPI, NW, FOLD>(cp, run_len, w, smem, tail, true);
@@ -759,6 +763,11 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
     return SRMI_ERR_ARG;
   if (epi == EPI_DG_ACC_CA && cp.fold.du_out && (!cp.fold.s_rec || cp.fold.CR < 4 || cp.fold.CR > 32))
     return SRMI_ERR_ARG;
+  if (wp.nred < 0 || wp.nred > 2) return SRMI_ERR_ARG;
+  for (int k = 0; k < wp.nred; ++k)
+    if (!wp.red[k].slab || !wp.red[k].gw || wp.red[k].Cout != 64 || wp.red[k].layout != 1 || wp.red[k].ps ||
+        wp.red[k].nslab < 1 || (wp.red[k].gb && !wp.red[k].bslab))
+      return SRMI_ERR_ARG;
   const int lds = (Conv2Smem<48>::TOTAL > v4::LDS ? Conv2Smem<48>::TOTAL : v4::LDS) + (fold ? kFoldBytes : 0);
   ConvParams c = cp;
   c.stamps = nullptr;
@@ -780,6 +789,7 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
 #define SRMI_TAIL_F2 0
 #endif
   const int tail = !paired ? 0 : std::min(run_len - 1, epi == EPI_DG_RELUMASK ? SRMI_TAIL_F2 : SRMI_TAIL_F1);
+  if (wp.nred > 0 && tail > 0) return SRMI_ERR_ARG;  // (the reduction share uses the ring LDS the tail needs)
   switch (epi) {
     case EPI_DG_RELUMASK:
       if (!c.aux) return SRMI_ERR_ARG;
