@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 measurement of the in-tree library: every -m gpu test, smoke(), the default
+# Measurement of the in-tree library: every -m gpu test, smoke(), the default
 # bench line, a kernel trace of a short bench (stats + per-step timeline + roofline
 # agreement), then the PMC passes (tools/pmc_step.sh).  Each GPU step has its own limit.
 R=${GRAFT_REPO_ROOT:-/root/repo}
