@@ -67,6 +67,8 @@ def parse():
                     help="diagnostic: the DP path (RCCL group, reducer stream, bucketed all-reduce) at one rank")
     ap.add_argument("--no-ca-fold", action="store_true",
                     help="A/B: materialise du in a CA-backward pass per RCAB (SRMI_FLAG_NO_CA_FOLD)")
+    ap.add_argument("--no-rcab-infer", action="store_true",
+                    help="A/B: inference RCABs as three launches (SRMI_FLAG_NO_RCAB_INFER)")
     return ap.parse_args()
 
 
@@ -219,7 +221,7 @@ def conv_fwd_roofline(dev, batch):
             "bytes_per_launch": 2 * N * ACT_BF16_PER_TILE + 64 * 576 * 2}
 
 
-def inference_bench(dev, side, iters):
+def inference_bench(dev, side, iters, flags=0):
     """BASELINE config 5: RCAN inference over a full region, 1 variable, HR side x side
     cut floor-wise into 192x192 tiles (4096 -> 21 x 21 = 441 tiles, 4032^2 HR produced),
     per region: tiling + lnorm, bicubic 1/4, rcan-10-20-64 forward (bf16 MFMA), bicubic
@@ -230,7 +232,7 @@ def inference_bench(dev, side, iters):
     from srmi.inference import TiledInference
     from srmi.trainer import default_init_
     spec = NetSpec(arch="rcan", nchannels_in=1, nchannels_out=1, nfeatures=64, nlayers=10, nblocks=20,
-                   cbottleneck=2, scale=4)
+                   cbottleneck=2, scale=4, flags=flags)
     from srmi.engine import param_table
     table = param_table(spec)
     params = torch.empty(sum(t[2] for t in table), dtype=torch.float32, device=dev)
@@ -253,6 +255,7 @@ def inference_bench(dev, side, iters):
             "model_tflops": round(ti.n * 73.26e9 / (ms * 1e-3) / 1e12, 1),
             "mfma_frac": round(ti.n * 73.26e9 / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
             "dtype": "bf16", "data": "synthetic",
+            "rcab_one_launch": not (flags & 2),
             "config": {"workload": f"rcan-10-20-64 tiled inference, 1 var, {side}x{side} HR region, 192^2 tiles "
                                    "(floor), graph-replayed", "graph": True}}
 
@@ -405,7 +408,8 @@ def main():
     C, B = args.channels, args.batch
     if args.no_train:  # diagnostic: the C4 / C5 lines alone
         rec = {"edsr_x8": None if args.no_edsr else edsr_bench(dev, args.edsr_batch, 10, 3),
-               "inference": None if args.no_inference else inference_bench(dev, args.infer_region, args.infer_iters)}
+               "inference": None if args.no_inference else inference_bench(dev, args.infer_region, args.infer_iters,
+                                                                           2 if args.no_rcab_infer else 0)}
         print(json.dumps(rec), flush=True)
         return
     from srmi._lib import SRMI_FLAG_NO_CA_FOLD
@@ -487,7 +491,7 @@ def main():
             _log("edsr done")
         infer = None
         if not args.no_inference and world == 1:
-            infer = inference_bench(dev, args.infer_region, args.infer_iters)
+            infer = inference_bench(dev, args.infer_region, args.infer_iters, 2 if args.no_rcab_infer else 0)
             _log("inference done")
         cpu = None
         if not args.no_cpu_baseline and world == 1:

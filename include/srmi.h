@@ -83,6 +83,9 @@ typedef struct srmi_model_config {
 /* flags: SRMI_FLAG_NO_CA_FOLD runs every RCAB's channel-attention backward as its own
  * pass (materialised du) instead of the fold into the conv launches (A/B, tests) */
 #define SRMI_FLAG_NO_CA_FOLD 1
+/* SRMI_FLAG_NO_RCAB_INFER: inference engines run each RCAB as three launches (conv1,
+ * conv2 + pool, CA) instead of one launch with a workgroup per image (A/B, tests) */
+#define SRMI_FLAG_NO_RCAB_INFER 2
 
 typedef struct srmi_param_info {
   long long offset; /* element offset in the flat fp32 parameter buffer     */

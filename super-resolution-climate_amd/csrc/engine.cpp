@@ -395,8 +395,8 @@ static void build_tables(srmi_engine* e) {
 static inline hipStream_t S_(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // --------------------------------------------------------------- conv helpers
-static int conv_fwd(srmi_engine* e, const ConvRef& c, const bf16_t* x, int n, int H, int W, int epi, bf16_t* yb,
-                    float* yf, const float* r1, float* part, float alpha, hipStream_t st) {
+static ConvParams fwd_params(srmi_engine* e, const ConvRef& c, const bf16_t* x, int n, int H, int W, bf16_t* yb,
+                             float* yf, const float* r1, float* part, float alpha) {
   ConvParams p{};
   p.x = x;
   p.w = e->at(e->packs, c.f_off);
@@ -416,7 +416,12 @@ static int conv_fwd(srmi_engine* e, const ConvRef& c, const bf16_t* x, int n, in
   p.alpha = alpha;
   p.zeros = e->zeros;
   p.cu_budget = e->cu_budget;
-  return conv3x3_launch(p, epi, st);
+  return p;
+}
+
+static int conv_fwd(srmi_engine* e, const ConvRef& c, const bf16_t* x, int n, int H, int W, int epi, bf16_t* yb,
+                    float* yf, const float* r1, float* part, float alpha, hipStream_t st) {
+  return conv3x3_launch(fwd_params(e, c, x, n, H, W, yb, yf, r1, part, alpha), epi, st);
 }
 
 // dgrad of conv c: input dy (Cout channels, PS layout if c.ps), output Cin channels
@@ -571,6 +576,17 @@ static int upload_tables(srmi_engine* e, hipStream_t st) {
   return 0;
 }
 
+// inference (no saved activations): each RCAB as one launch with a workgroup per image
+// (rcab_infer.hip) -- bf16, 48-wide tiles, a CA bottleneck the MLP code handles
+#ifndef SRMI_RCAB_INFER
+#define SRMI_RCAB_INFER 1
+#endif
+static bool use_rcab_infer(const srmi_engine* e) {
+  const int CR = 64 / e->P.cfg.reduction;
+  return SRMI_RCAB_INFER && !(e->P.cfg.flags & SRMI_FLAG_NO_RCAB_INFER) && !e->train && !e->f32 &&
+         e->P.cfg.arch == SRMI_ARCH_RCAN && e->w == 48 && e->h % 4 == 0 && CR >= 4 && CR <= 32 && CR % 4 == 0;
+}
+
 // ------------------------------------------------------------------ forward
 static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float* sr, int n, hipStream_t st) {
   const Plan& P = e->P;
@@ -583,6 +599,15 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
       const float* rin = g == 0 ? e->X0f : e->Rf;
       for (int b = 1; b <= nb; ++b) {
         const RCABRef& r = P.groups[g][b - 1];
+        if (use_rcab_infer(e)) {  // inference: the RCAB as one launch, a workgroup per image
+          bf16_t* lo = reinterpret_cast<bf16_t*>(e->Hf);
+          const ConvParams c1 = fwd_params(e, r.c1, e->hb(g, b - 1), n, h, w, e->Tm(g, b), nullptr, nullptr, nullptr, 1.f);
+          const ConvParams c2 = fwd_params(e, r.c2, e->Tm(g, b), n, h, w, e->Um(g, b), nullptr, nullptr, e->ppool, 1.f);
+          RC(rcab_infer_launch(c1, c2, e->ppool, nstrips, prm + r.ca_w1, prm + r.ca_b1, prm + r.ca_w2, prm + r.ca_b2,
+                               64 / R, b == 1 ? rin : nullptr, b == 1 ? nullptr : e->hb(g, b - 1),
+                               b == 1 ? nullptr : lo, e->hb(g, b), lo, e->recp(g, b), st));
+          continue;
+        }
         RC(conv_fwd(e, r.c1, e->hb(g, b - 1), n, h, w, EPI_RELU_BF16, e->Tm(g, b), nullptr, nullptr, nullptr, 1.f, st));
         RC(conv_fwd(e, r.c2, e->Tm(g, b), n, h, w, EPI_POOL_BF16, e->Um(g, b), nullptr, nullptr, e->ppool, 1.f, st));
         if (e->f32) {

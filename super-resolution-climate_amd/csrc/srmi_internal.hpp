@@ -164,6 +164,11 @@ int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1
 int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
                      const float* w2, int N, int HW, int C, int R, void* du, float* brec, int f32, hipStream_t st,
                      const ReduceSet* red0 = nullptr, const ReduceSet* red1 = nullptr);
+// inference RCAB, one launch (rcab_infer.hip): c1 = conv1 (RELU, yb = t), c2 = conv2
+// (POOL, yb = u, part), then the CA MLP and the residual pair update per image
+int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* part, int nstrips, const float* w1,
+                      const float* b1, const float* w2, const float* b2, int CR, const float* h_in, const void* hi_in,
+                      const void* lo_in, void* hi_out, void* lo_out, float* rec, hipStream_t st);
 // records of consecutive RCABs Ncap images apart (the engine capacity), N summed
 int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int Ncap, int C, int R,
                                   const long long* offs, float* grads, hipStream_t st);

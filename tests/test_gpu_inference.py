@@ -135,3 +135,30 @@ def test_tiled_inference_micro_engines_bit_identical(graph):
             for k in imgs:
                 assert torch.equal(torch.nan_to_num(imgs[k], 7.0), torch.nan_to_num(ref_imgs[k], 7.0)), (micro, k)
             assert loss == ref_loss
+
+
+@pytest.mark.parametrize("C,nl,nb,hw,N", [(1, 2, 3, (48, 48), 5), (2, 1, 2, (32, 48), 3), (1, 1, 1, (8, 48), 2)])
+def test_fused_inference_rcab_bit_identical_to_three_launches(C, nl, nb, hw, N):
+    """The inference RCAB as one launch with a workgroup per image (rcab_infer.hip:
+    conv1 -> conv2 + pool -> CA MLP + residual pair, all in the workgroup) computes
+    exactly what the three launches compute (SRMI_FLAG_NO_RCAB_INFER): same MFMA
+    order, the pool summed in ca_fwd's order, the same pair codec -- bit for bit."""
+    from srmi._lib import SRMI_FLAG_NO_RCAB_INFER
+    from srmi.engine import Engine
+    from srmi.trainer import default_init_
+    d = dev()
+    out = []
+    for flags in (0, SRMI_FLAG_NO_RCAB_INFER):
+        spec = NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=nl, nblocks=nb,
+                       cbottleneck=2, scale=4, flags=flags)
+        table = param_table(spec)
+        flat = torch.empty(sum(t[2] for t in table), device=d)
+        default_init_(flat, table, seed=3)
+        e = Engine(spec, N, hw, train=False, device=d)
+        e.pack(flat)
+        g = torch.Generator().manual_seed(11)
+        lr = torch.randn(N, C, hw[0], hw[1], generator=g).to(d)
+        out.append(e.forward(flat, lr).clone())
+    torch.cuda.synchronize()
+    assert torch.equal(out[0], out[1])
+    assert float(out[0].abs().sum()) > 0
