@@ -228,7 +228,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       const auto rf = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
       [[maybe_unused]] const auto rbb = wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
       // CA-backward fold producer (EPI_DG_ACC_CA): du' = bf16(g * s) of the next RCAB
-      [[maybe_unused]] const bool fold_out = EPI == EPI_DG_ACC_CA && p.fold.du_out != nullptr;
+      [[maybe_unused]] const bool fold_out = (EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC) && p.fold.du_out != nullptr;
       [[maybe_unused]] const auto rdu = wt_rsrc(p.fold.du_out, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
       const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
 #pragma unroll
@@ -272,7 +272,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             ps1[0][3] += val.w * bf2f(uu.y >> 16);
           }
           st_wt16(rf, p.yf, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 4), val);
-          if constexpr (EPI == EPI_DG_ACC_CA) {
+          if constexpr (EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC) {
             if (fold_out)  // the lane's channels 4c..4c+3 are the same in every run: s in fs
               st_wt8(rdu, p.fold.du_out, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 2),
                      make_uint2(pack2(val.x * fs.x, val.y * fs.y), pack2(val.z * fs.z, val.w * fs.w)));
@@ -526,7 +526,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     for (int c = 0; c < NCT; ++c) aoff[kk][c] = swz128((ct0 + c) * 16 + fr, kk * 4 + fk);
   // fold producer: s of the next RCAB for the lane's 4 run-layout channels (conv_epilogue2)
   float4 fs = float4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (EPI == EPI_DG_ACC_CA) {
+  if constexpr (EPI == EPI_DG_ACC_CA || (EPI == EPI_DG_ACC && epi_run<EPI>())) {
     if (p.fold.du_out)
       fs = *reinterpret_cast<const float4*>(p.fold.s_rec + (size_t)n * (128 + p.fold.CR) + 64 + p.fold.CR +
                                             4 * (lane & 15));

@@ -457,8 +457,9 @@ static ConvParams dgrad_params(srmi_engine* e, const ConvRef& c, const bf16_t* d
 
 static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n, int H, int W, int epi, bf16_t* yb,
                       float* yf, const float* r1, const float* r2, const float* r3, const bf16_t* aux, float* part,
-                      float alpha, hipStream_t st) {
-  const ConvParams p = dgrad_params(e, c, dy, n, H, W, &epi, yb, yf, r1, r2, r3, aux, part, alpha);
+                      float alpha, hipStream_t st, const CaFold* fold = nullptr) {
+  ConvParams p = dgrad_params(e, c, dy, n, H, W, &epi, yb, yf, r1, r2, r3, aux, part, alpha);
+  if (fold) p.fold = *fold;
   return conv3x3_launch(p, epi, st);
 }
 
@@ -705,8 +706,15 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
     for (int g = nl - 1; g >= 0; --g) {
       const ConvRef& gt = P.group_tail[g];
       RC(conv_wgrad(e, gt, e->hb(g, nb), gRb, n, h, w, grads, true, 1.f, st));
+      // the group tail's dgrad is the fold producer of the group's last RCAB (du' of RCAB nb)
+      CaFold tail_fold{};
+      if (fold) {
+        tail_fold.du_out = e->DU;
+        tail_fold.s_rec = e->recp(g, nb);
+        tail_fold.CR = 64 / R;
+      }
       RC(conv_dgrad(e, gt, gRb, n, h, w, EPI_DG_ACC, nullptr, ghf, nullptr, nullptr, nullptr, e->Um(g, nb), e->pacc,
-                    1.f, st));
+                    1.f, st, fold ? &tail_fold : nullptr));
       ReduceSet prev2{}, prev1{};
       bool have_prev = false;
       for (int b = nb; b >= 1; --b) {
@@ -714,11 +722,11 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         const int q = it++ & 1;
         bf16_t* du = e->DU;
         bf16_t* dz = e->DZ;
-        const bool folded = fold && b < nb;  // du' came from the previous F1
+        const bool folded = fold;  // du' came from the previous F1 (the group tail's dgrad for b == nb)
         if (!folded) {
           RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
                               e->brecp(g, b), e->f32, st, have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
-        } else if (!SRMI_RED_IN_F2) {
+        } else if (!SRMI_RED_IN_F2 && have_prev) {
           RC(wgrad_reduce2_launch(prev2, prev1, st));
         }
         ReduceSet red2, red1;
@@ -731,7 +739,7 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         if (folded) {
           cp.fold = fold_consumer(e, prm, r, g, b, nstrips);
           wp.fold = cp.fold;
-          if (SRMI_RED_IN_F2) {  // the previous RCAB's slab reductions ride in this launch
+          if (SRMI_RED_IN_F2 && have_prev) {  // the previous RCAB's slab reductions ride in this launch
             wp.red[0] = prev2;
             wp.red[1] = prev1;
             wp.nred = 2;
@@ -877,6 +885,7 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
   ConvParams cp;
   int epi;
   const bool fold = use_ca_fold(e, n) && b < e->P.cfg.nblocks && e->probe_prm;  // (as backward_impl has it)
+  // (b < nblocks: the probe's in-launch reductions read the slabs of RCAB b + 1)
   if (which == 2) {
     epi = EPI_DG_RELUMASK;
     cp = dgrad_params(e, r.c2, e->DU, n, h, w, &epi, e->DZ, nullptr, nullptr, nullptr, nullptr, e->Tm(0, b), nullptr,
