@@ -221,7 +221,7 @@ def conv_fwd_roofline(dev, batch):
             "bytes_per_launch": 2 * N * ACT_BF16_PER_TILE + 64 * 576 * 2}
 
 
-def inference_bench(dev, side, iters, flags=0):
+def inference_bench(dev, side, iters, flags=0, info=None):
     """BASELINE config 5: RCAN inference over a full region, 1 variable, HR side x side
     cut floor-wise into 192x192 tiles (4096 -> 21 x 21 = 441 tiles, 4032^2 HR produced),
     per region: tiling + lnorm, bicubic 1/4, rcan-10-20-64 forward (bf16 MFMA), bicubic
@@ -238,26 +238,40 @@ def inference_bench(dev, side, iters, flags=0):
     params = torch.empty(sum(t[2] for t in table), dtype=torch.float32, device=dev)
     default_init_(params, table, 0)
     region = torch.tensor(synthetic_hr(1, 1, side, 99)[0]).to(dev)
-    ti = TiledInference(spec, params, tuple(region.shape), (192, 192), device=dev, graph=True)
+    multi = info is not None and info.enabled
+    ti = TiledInference(spec, params, tuple(region.shape), (192, 192), device=dev, graph=not multi,
+                        info=info if multi else None)
     ti.process_region(region)  # builds + captures the graph
     torch.cuda.synchronize()
-    st = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for _ in range(iters):
-        ti.replay()
-    e1.record(st)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / iters
+    if multi:
+        # multi-rank: the region's tiles round-robin over the ranks,
+        # mosaics and per-tile loss sums all-gathered; wall time of whole regions
+        torch.distributed.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            ti.process_region(region)
+        torch.cuda.synchronize()
+        torch.distributed.barrier()
+        ms = 1000 * (time.perf_counter() - t0) / iters
+    else:
+        st = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(iters):
+            ti.replay()
+        e1.record(st)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / iters
     mpix = ti.n * 192 * 192 / 1e6
     return {"metric": "inference MPix/sec (HR pixels produced)", "value": round(mpix / (ms * 1e-3), 2),
             "unit": "MPix/s", "ms_per_region": round(ms, 3), "tiles": ti.n, "hr_mpix_per_region": round(mpix, 3),
             "model_tflops": round(ti.n * 73.26e9 / (ms * 1e-3) / 1e12, 1),
             "mfma_frac": round(ti.n * 73.26e9 / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
             "dtype": "bf16", "data": "synthetic",
-            "rcab_one_launch": not (flags & 2),
+            "rcab_one_launch": not (flags & 2), "n_gpus": info.world if multi else 1,
             "config": {"workload": f"rcan-10-20-64 tiled inference, 1 var, {side}x{side} HR region, 192^2 tiles "
-                                   "(floor), graph-replayed", "graph": True}}
+                                   "(floor)" + (f", tiles round-robin over {info.world} ranks + all-gather"
+                                                if multi else ", graph-replayed"), "graph": not multi}}
 
 
 def edsr_bench(dev, batch, steps, warmup):
@@ -480,6 +494,10 @@ def main():
         dp_probe = dp_overhead_probe(args)
         _log(f"dp probe: {dp_probe}")
     _log(f"timed: {value:.1f} tiles/s")
+    infer_dp = None
+    if world > 1 and not args.no_inference:  # every rank takes part (collectives)
+        infer_dp = inference_bench(dev, args.infer_region, args.infer_iters, 2 if args.no_rcab_infer else 0, info)
+        _log("multi-rank inference done")
     if info.rank == 0:
         roof_conv = conv_fwd_roofline(dev, B)
         _log("rooflines done")
@@ -493,6 +511,8 @@ def main():
         if not args.no_inference and world == 1:
             infer = inference_bench(dev, args.infer_region, args.infer_iters, 2 if args.no_rcab_infer else 0)
             _log("inference done")
+        if world > 1:
+            infer = infer_dp
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.cpu_steps)
