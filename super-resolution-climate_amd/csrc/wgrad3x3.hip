@@ -274,44 +274,46 @@ __device__ __forceinline__ void wgrad48_fold_correction(const WgradParams& p, ch
   float* const tsum = reinterpret_cast<float*>(smem + 48 * 3 * 64 * 4);  // [9 taps][64 ci]
   const int tid = threadIdx.x;
   fold_barrier();  // every wave is past its last ring read
-  ca_fold_mlp(p.fold, n, p.N, p.H * Wd, fsm, false);
   {
+    // the chunk's input rows -1 .. Hr: the first (up to) 16 rows' loads are issued
+    // before the MLP's, so the two latencies overlap; then the rest
     const int cc = tid & 7, pg = tid >> 3;
+    const bool act = pg < Wd;
+    const bf16_t* xr = p.x + ((size_t)n * p.H * Wd + (act ? pg : 0)) * 64 + cc * 8;
     float a[3][8];
 #pragma unroll
     for (int k = 0; k < 3; ++k)
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[k][e] = 0.f;
-    if (pg < Wd) {
-      const bf16_t* xr = p.x + ((size_t)n * p.H * Wd + pg) * 64 + cc * 8;
-      // rows -1 .. Hr, 8 loads in flight per batch (the rows were just streamed: L2 hits)
-      for (int r0 = -1; r0 <= Hr; r0 += 8) {
-        uint4 v[8];
+    auto row_batch = [&](int r0, auto issue_mlp) __attribute__((always_inline)) {
+      uint4 v[16];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int y = ybase + r0 + i;
-          const bool ok = r0 + i <= Hr && y >= 0 && y < p.H;
-          v[i] = ok ? *reinterpret_cast<const uint4*>(xr + (size_t)y * Wd * 64) : make_uint4(0, 0, 0, 0);
-        }
+      for (int i = 0; i < 16; ++i) {  // clamped unconditional loads, zeroed outside the rows / image
+        const int y = min(max(ybase + r0 + i, 0), p.H - 1);
+        v[i] = *reinterpret_cast<const uint4*>(xr + (size_t)y * Wd * 64);
+      }
+      if constexpr (decltype(issue_mlp)::value) ca_fold_mlp(p.fold, n, p.N, p.H * Wd, fsm, false);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int r = r0 + i;
-          const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-          float x[8];
+      for (int i = 0; i < 16; ++i) {
+        const int r = r0 + i, y = ybase + r;
+        const bool in = act && r <= Hr && y >= 0 && y < p.H;
+        const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+        const bool k0 = in && r <= Hr - 2, k1 = in && r >= 0 && r <= Hr - 1, k2 = in && r >= 1;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            x[2 * e] = __uint_as_float(w[e] << 16);
-            x[2 * e + 1] = __uint_as_float(w[e] & 0xFFFF0000u);
-          }
-          const bool k0 = r <= Hr - 2, k1 = r >= 0 && r <= Hr - 1, k2 = r >= 1;  // (r > Hr: zeros)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            a[0][e] += k0 ? x[e] : 0.f;
-            a[1][e] += k1 ? x[e] : 0.f;
-            a[2][e] += k2 ? x[e] : 0.f;
-          }
+        for (int e = 0; e < 4; ++e) {
+          const float x0 = __uint_as_float(w[e] << 16), x1 = __uint_as_float(w[e] & 0xFFFF0000u);
+          a[0][2 * e] += k0 ? x0 : 0.f;
+          a[0][2 * e + 1] += k0 ? x1 : 0.f;
+          a[1][2 * e] += k1 ? x0 : 0.f;
+          a[1][2 * e + 1] += k1 ? x1 : 0.f;
+          a[2][2 * e] += k2 ? x0 : 0.f;
+          a[2][2 * e + 1] += k2 ? x1 : 0.f;
         }
       }
+    };
+    row_batch(-1, std::true_type{});
+    for (int r0 = 15; r0 <= Hr; r0 += 16) row_batch(r0, std::false_type{});
+    if (act) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         float4* d = reinterpret_cast<float4*>(tpart + (pg * 3 + k) * 64 + cc * 8);

@@ -118,17 +118,18 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab
 // inside another launch: the fused RCAB backward's filter-gradient workgroups reduce
 // the previous RCAB's slabs after their own chunk (no reduction launch of its own).
 // Output quads of the concatenated sets are split evenly over the parts; per round a
-// thread sums one quad over a quarter of the slabs (up to 16 loads in flight, clamped
-// and zeroed past the end), the four quarters are combined in LDS in a fixed order:
+// thread sums one quad over half of the slabs (up to 32 loads in flight, clamped and
+// zeroed past the end), the two halves are combined in LDS in a fixed order:
 // deterministic, independent of placement.  The conv1 bias (r.gb) is reduced by the
 // last part.  lds: >= 512 float4 scratch.  Every thread of the workgroup calls this.
 __device__ __forceinline__ void slab_reduce_share(const ReduceSet& ra, const ReduceSet& rb, int nred, int part,
                                                   int nparts, float4* lds) {
   constexpr int PERQ = 64 * 576 / 4;  // output quads per set
-  const int tid = threadIdx.x, qi = tid & 127, ph = tid >> 7;
+  // 256 quads per round x 2 slab halves, up to 32 loads in flight per thread
+  const int tid = threadIdx.x, qi = tid & 255, ph = tid >> 8;
   const int total = nred * PERQ;
   const int q0 = (int)((long long)total * part / nparts), q1 = (int)((long long)total * (part + 1) / nparts);
-  for (int qb = q0; qb < q1; qb += 128) {
+  for (int qb = q0; qb < q1; qb += 256) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // the previous round's (or the caller's) LDS reads are done
     const int q = min(qb + qi, q1 - 1);
@@ -136,31 +137,28 @@ __device__ __forceinline__ void slab_reduce_share(const ReduceSet& ra, const Red
     const float* slab = set ? rb.slab : ra.slab;
     const int nslab = set ? rb.nslab : ra.nslab;
     const int o4 = (q - set * PERQ) * 4;
-    const int S = (nslab + 3) >> 2, s0 = ph * S, s1 = min(nslab, s0 + S);
+    const int S = (nslab + 1) >> 1, s0 = ph * S, s1 = min(nslab, s0 + S);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int sb = s0; sb < s1; sb += 16) {
-      float4 v[16];
+    for (int sb = s0; sb < s1; sb += 32) {
+      float4 v[32];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
+      for (int i = 0; i < 32; ++i) {
         const int sl = sb + i;
         v[i] = *reinterpret_cast<const float4*>(slab + (size_t)min(sl, nslab - 1) * (64 * 576) + o4);
         if (sl >= s1) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
+      for (int i = 0; i < 32; ++i) {
         acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w;
       }
     }
-    lds[ph * 128 + qi] = acc;
+    lds[ph * 256 + qi] = acc;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (ph == 0 && qb + qi < q1) {
+      const float4 t = lds[256 + qi];
       float4 r = lds[qi];
-#pragma unroll
-      for (int k = 1; k < 4; ++k) {
-        const float4 t = lds[k * 128 + qi];
-        r.x += t.x; r.y += t.y; r.z += t.z; r.w += t.w;
-      }
+      r.x += t.x; r.y += t.y; r.z += t.z; r.w += t.w;
       const float alpha = set ? rb.alpha : ra.alpha;
       float* gw = set ? rb.gw : ra.gw;
       const float s4[4] = {r.x, r.y, r.z, r.w};
