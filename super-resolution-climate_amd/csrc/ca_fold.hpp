@@ -29,25 +29,41 @@ __device__ __forceinline__ void fold_barrier() {
 // bias gradient sum_p du = s G + dm, then dm) as ca_bwd_du writes it.  Every thread of
 // the workgroup calls this (it holds barriers); threads 0..255 compute.  Same
 // arithmetic and order as ca_bwd_du_kernel (small.hip).
-__device__ __forceinline__ void ca_fold_mlp(const CaFold& f, int n, int N, int HW, float* sm, bool write_brec) {
+struct CaFoldRegs {  // the MLP's global operands of one thread (threads 0..255)
+  float pa, zj, svl;
+  float wa[8], wb[8];
+};
+
+// the global loads of ca_fold_mlp, issued on their own so that a caller can put them
+// in flight ahead of its LDS-DMA prologue (their latency then hides under it)
+__device__ __forceinline__ void ca_fold_mlp_load(const CaFold& f, int n, CaFoldRegs& r) {
+  constexpr int C = 64;
+  const int tid = threadIdx.x, CR = f.CR, per = CR / 4;
+  const int j = tid >> 3, pj = tid & 7, c4 = (tid >> 2) & 63, p4 = tid & 3;
+  const int jc = min(j & 31, CR - 1);
+  r.pa = 0.f;
+  r.zj = r.svl = 0.f;
+  if (tid < 256) {  // (wave-uniform)
+    for (int k = tid >> 7; k < f.nstrips; k += 2) r.pa += f.part[((size_t)n * f.nstrips + k) * (2 * C) + (tid & 127)];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.wa[i] = f.w2[(pj * 8 + i) * CR + jc];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.wb[i] = f.w1[(p4 * per + min(i, per - 1)) * C + c4];
+    const float* rr = f.rec + (size_t)n * (2 * C + CR);
+    r.zj = rr[C + jc];
+    r.svl = rr[C + CR + (tid & 63)];
+  }
+}
+
+__device__ __forceinline__ void ca_fold_mlp_compute(const CaFold& f, int n, int N, int HW, float* sm, bool write_brec,
+                                                    const CaFoldRegs& r) {
   constexpr int C = 64;
   const int tid = threadIdx.x, CR = f.CR, per = CR / 4;
   const bool act = tid < 256;  // (wave-uniform)
   const int j = tid >> 3, pj = tid & 7, c4 = (tid >> 2) & 63, p4 = tid & 3;
-  const int jc = min(j & 31, CR - 1);
-  float wa[8], wb[8], zj = 0.f;
   if (act) {
-    float pa = 0.f;
-    for (int k = tid >> 7; k < f.nstrips; k += 2) pa += f.part[((size_t)n * f.nstrips + k) * (2 * C) + (tid & 127)];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) wa[i] = f.w2[(pj * 8 + i) * CR + jc];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) wb[i] = f.w1[(p4 * per + min(i, per - 1)) * C + c4];
-    const float* r = f.rec + (size_t)n * (2 * C + CR);
-    zj = r[C + jc];
-    const float svl = r[C + CR + (tid & 63)];
-    sm[kFoldRed + (tid >> 7) * 128 + (tid & 127)] = pa;
-    if (tid < C) sm[kFoldS + tid] = svl;
+    sm[kFoldRed + (tid >> 7) * 128 + (tid & 127)] = r.pa;
+    if (tid < C) sm[kFoldS + tid] = r.svl;
   }
   fold_barrier();
   if (tid < C) {
@@ -61,18 +77,18 @@ __device__ __forceinline__ void ca_fold_mlp(const CaFold& f, int n, int N, int H
   if (act) {  // dz1[j] = relu'(z1[j]) sum_c W2[c][j] dz2[c]
     float a = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) a += wa[i] * sm[kFoldDz2 + pj * 8 + i];
+    for (int i = 0; i < 8; ++i) a += r.wa[i] * sm[kFoldDz2 + pj * 8 + i];
     a += __shfl_xor(a, 1, 64);
     a += __shfl_xor(a, 2, 64);
     a += __shfl_xor(a, 4, 64);
-    if (j < CR && pj == 0) sm[kFoldDz1 + j] = (zj > 0.f) ? a : 0.f;
+    if (j < CR && pj == 0) sm[kFoldDz1 + j] = (r.zj > 0.f) ? a : 0.f;
   }
   fold_barrier();
   if (act) {  // dm[c] = sum_j W1[j][c] dz1[j]
     float a = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      if (i < per) a += wb[i] * sm[kFoldDz1 + p4 * per + i];
+      if (i < per) a += r.wb[i] * sm[kFoldDz1 + p4 * per + i];
     a += __shfl_xor(a, 1, 64);
     a += __shfl_xor(a, 2, 64);
     if (p4 == 0) {
@@ -89,6 +105,12 @@ __device__ __forceinline__ void ca_fold_mlp(const CaFold& f, int n, int N, int H
     br[C + CR + tid] = sm[kFoldS + tid] * sm[kFoldG + tid] + dm;
     if (tid < CR) br[C + tid] = sm[kFoldDz1 + tid];
   }
+}
+
+__device__ __forceinline__ void ca_fold_mlp(const CaFold& f, int n, int N, int HW, float* sm, bool write_brec) {
+  CaFoldRegs r;
+  ca_fold_mlp_load(f, n, r);
+  ca_fold_mlp_compute(f, n, N, HW, sm, write_brec, r);
 }
 
 // The dgrad of the constant field c (zero outside the image) through the dgrad

@@ -766,6 +766,8 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
 #pragma unroll
     for (int c = 0; c < NCT; ++c) bias[c] = *reinterpret_cast<const float4*>(bp + cb * 64 + chan(c, 0));
   }
+  [[maybe_unused]] CaFoldRegs fregs;
+  if constexpr (FOLD) ca_fold_mlp_load(p.fold, n, fregs);  // in flight under the DMA prologue
   {
     const uint32_t wbase = lds_u32(wl);
     // the filter image uses the swz128t chunk swizzle (c ^ (bit1, bit3 of the row)):
@@ -786,7 +788,7 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
   // every wave's DMA visible); the first run of the image writes its brec
   float* const fsm = reinterpret_cast<float*>(smem + S::TOTAL);
   if constexpr (FOLD) {
-    ca_fold_mlp(p.fold, n, p.N, (int)HW, fsm, ry == 0 && sx == 0 && cb == 0 && !tail_part);
+    ca_fold_mlp_compute(p.fold, n, p.N, (int)HW, fsm, ry == 0 && sx == 0 && cb == 0 && !tail_part, fregs);
     ca_fold_corr(wl, fsm);
   }
   STAMP(1);

@@ -356,8 +356,15 @@ __device__ __forceinline__ void wgrad48_fold_correction(const WgradParams& p, ch
 // FOLD (the conv2 filter gradient of a folded RCAB, fused launch only, W == 48):
 // before the slab store the partial gains c[co] T[tap][ci] (wgrad48_fold_correction):
 // the filter gradient of du = du' + c, exactly.
+// SRMI_FOLD_WG: 2 = c added to the dY fragments in the K-loop (the filter gradient of
+// bf16(du' + c), as the materialised path rounds du); 1 = c (x) T added to the partial
+// after the K-loop (exact; its row-sum pass after the chunk measured +7-11 us in F2)
+#ifndef SRMI_FOLD_WG
+#define SRMI_FOLD_WG 2
+#endif
 template <int WV, int NW = 4, bool FOLD = false>
 __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, int chunk, int cb) {
+  constexpr bool FOLD_A = FOLD && SRMI_FOLD_WG == 2;
   using namespace v4;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
 #ifndef SRMI_WG_OLD5
@@ -530,6 +537,9 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
     else wait_vm<0>();
   };
 
+  // fold (A-operand form): the MLP's operands in flight under the DMA prologue
+  [[maybe_unused]] CaFoldRegs fregs;
+  if constexpr (FOLD_A) ca_fold_mlp_load(p.fold, n, fregs);
   // prologue: input rows -1, 0 and pairs 0 .. PF-1; wait for the rows and pair 0
   if constexpr (kMain) {
 #pragma unroll
@@ -539,6 +549,15 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   }
   wait_groups(min(PF, np) - 1, 0);
   __syncthreads();
+  // fold, A-operand form: c = dm / HW of the image for the lane's A rows (co =
+  // tile (ct + wave) & 3, row lane & 15), added to every dY fragment before its MFMAs
+  [[maybe_unused]] float fc[4];
+  if constexpr (FOLD_A) {
+    float* const fsm = reinterpret_cast<float*>(smem + kFoldOff);
+    ca_fold_mlp_compute(p.fold, n, p.N, H * Wd, fsm, false, fregs);
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) fc[ct] = fsm[kFoldC + ((ct + wave) & 3) * 16 + (lane & 15)];
+  }
   WSTAMP(1);
 #ifdef SRMI_WG_PRIO
   if constexpr (NW == 8 && WV >= 4) __builtin_amdgcn_s_setprio(1);
@@ -570,6 +589,18 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
         if (kMain && pf)
           dma_pair_part(j + PF, kc == 0 ? 0 : (kc == 1 ? 3 : 5), kc == 0 ? 3 : (kc == 1 ? 5 : 7));
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (FOLD_A) {
+          // du = du' + c: this K-step's dY fragments (8 pixels of one co row per lane)
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) {
+            u32x4 q = __builtin_bit_cast(u32x4, A[cur][ct]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              q[e] = pack2(__uint_as_float(q[e] << 16) + fc[ct], __uint_as_float(q[e] & 0xFFFF0000u) + fc[ct]);
+            A[cur][ct] = __builtin_bit_cast(bf16x8, q);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
         const bool ld = kc < 2 || more;
         if constexpr (NB == 2) {
           if (kc < 2) load_step(ra, rb, kc + 1, A[nxt], B[nxt]);
@@ -624,7 +655,7 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   // other way round in round 2: the launch 0.9 us shorter, the reduce 1.9 us longer)
   // (N tile J, slot ct of rotation `wave`) -> the 4-wave position (wave J / 9, tile
   // J % 9, the slot of the same output-channel tile under that wave's rotation)
-  if constexpr (FOLD) wgrad48_fold_correction<NT, J0>(p, smem, acc, n, ybase, Hr, wave, lane);
+  if constexpr (FOLD && !FOLD_A) wgrad48_fold_correction<NT, J0>(p, smem, acc, n, ybase, Hr, wave, lane);
   const size_t soff = (size_t)chunk * Cout * 576 + (size_t)cb * (64 * 576);
   // (write-through: the slab leaves the XCD's L2 while the other waves still
   //  compute, instead of in the dirty-line flush at the end of the launch)

@@ -125,11 +125,15 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab
 __device__ __forceinline__ void slab_reduce_share(const ReduceSet& ra, const ReduceSet& rb, int nred, int part,
                                                   int nparts, float4* lds) {
   constexpr int PERQ = 64 * 576 / 4;  // output quads per set
-  // 256 quads per round x 2 slab halves, up to 32 loads in flight per thread
-  const int tid = threadIdx.x, qi = tid & 255, ph = tid >> 8;
+#ifndef SRMI_RED_LOADS
+#define SRMI_RED_LOADS 16
+#endif
+  // QR quads per round x NPH slab phases, up to NL loads in flight per thread
+  constexpr int NL = SRMI_RED_LOADS, NPH = NL == 32 ? 2 : 4, QR = 512 / NPH;
+  const int tid = threadIdx.x, qi = tid % QR, ph = tid / QR;
   const int total = nred * PERQ;
   const int q0 = (int)((long long)total * part / nparts), q1 = (int)((long long)total * (part + 1) / nparts);
-  for (int qb = q0; qb < q1; qb += 256) {
+  for (int qb = q0; qb < q1; qb += QR) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // the previous round's (or the caller's) LDS reads are done
     const int q = min(qb + qi, q1 - 1);
@@ -137,28 +141,31 @@ __device__ __forceinline__ void slab_reduce_share(const ReduceSet& ra, const Red
     const float* slab = set ? rb.slab : ra.slab;
     const int nslab = set ? rb.nslab : ra.nslab;
     const int o4 = (q - set * PERQ) * 4;
-    const int S = (nslab + 1) >> 1, s0 = ph * S, s1 = min(nslab, s0 + S);
+    const int S = (nslab + NPH - 1) / NPH, s0 = ph * S, s1 = min(nslab, s0 + S);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int sb = s0; sb < s1; sb += 32) {
-      float4 v[32];
+    for (int sb = s0; sb < s1; sb += NL) {
+      float4 v[NL];
 #pragma unroll
-      for (int i = 0; i < 32; ++i) {
+      for (int i = 0; i < NL; ++i) {
         const int sl = sb + i;
         v[i] = *reinterpret_cast<const float4*>(slab + (size_t)min(sl, nslab - 1) * (64 * 576) + o4);
         if (sl >= s1) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
-      for (int i = 0; i < 32; ++i) {
+      for (int i = 0; i < NL; ++i) {
         acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w;
       }
     }
-    lds[ph * 256 + qi] = acc;
+    lds[ph * QR + qi] = acc;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (ph == 0 && qb + qi < q1) {
-      const float4 t = lds[256 + qi];
       float4 r = lds[qi];
-      r.x += t.x; r.y += t.y; r.z += t.z; r.w += t.w;
+#pragma unroll
+      for (int k = 1; k < NPH; ++k) {
+        const float4 t = lds[k * QR + qi];
+        r.x += t.x; r.y += t.y; r.z += t.z; r.w += t.w;
+      }
       const float alpha = set ? rb.alpha : ra.alpha;
       float* gw = set ? rb.gw : ra.gw;
       const float s4[4] = {r.x, r.y, r.z, r.w};
