@@ -825,6 +825,22 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
       ops.u[pt][c] = *reinterpret_cast<const uint2*>(p.aux + o);
     }
   };
+  // fold: the border-class corrections of strip kp's row for this lane (LDS, issued
+  // early in a strip so the epilogue K-steps find them in registers)
+  [[maybe_unused]] float fb[8], fd[8];
+  [[maybe_unused]] const int fpt = (fr == 0 && x0 == 0) ? 0 : ((fr == 15 && x0 + TW == p.W) ? NPT - 1 : -1);
+  auto fold_corr_load = [&](int kp) __attribute__((always_inline)) {
+    if constexpr (FOLD) {
+      const int yy = 4 * kp + row, cy = yy == 0 ? 0 : (yy == p.H - 1 ? 2 : 1);
+      const float* cb1 = fsm + kFoldCorr + (cy * 3 + 1) * 64 + ct0 * 16 + 8 * fk;
+      const float* cbx = fsm + kFoldCorr + (cy * 3 + (fpt == 0 ? 0 : (fpt > 0 ? 2 : 1))) * 64 + ct0 * 16 + 8 * fk;
+      const float4 b0 = *reinterpret_cast<const float4*>(cb1), b1 = *reinterpret_cast<const float4*>(cb1 + 4);
+      const float4 x0v = *reinterpret_cast<const float4*>(cbx), x1v = *reinterpret_cast<const float4*>(cbx + 4);
+      fb[0] = b0.x; fb[1] = b0.y; fb[2] = b0.z; fb[3] = b0.w; fb[4] = b1.x; fb[5] = b1.y; fb[6] = b1.z; fb[7] = b1.w;
+      fd[0] = x0v.x - b0.x; fd[1] = x0v.y - b0.y; fd[2] = x0v.z - b0.z; fd[3] = x0v.w - b0.w;
+      fd[4] = x1v.x - b1.x; fd[5] = x1v.y - b1.y; fd[6] = x1v.z - b1.z; fd[7] = x1v.w - b1.w;
+    }
+  };
   // epilogue of pixel tile pt of strip kp from accp
   float ps0[NCT][4], ps1[NCT][4];
   auto epi_tile = [&](int kp, int pt) __attribute__((always_inline)) {
@@ -846,17 +862,12 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     if constexpr (kPerm) {
       float o[8];
       // fold: + the dgrad of the constant c for this pixel's border class (8 contiguous
-      // channels ct0*16 + 8fk ..), before the ReLU mask
+      // channels ct0*16 + 8fk ..), before the ReLU mask: the row class's x-inner value
+      // fb, plus fd on the lane's x-border pixel (fold_corr_load)
       [[maybe_unused]] float cv[8];
       if constexpr (FOLD) {
-        const int cy = yy == 0 ? 0 : (yy == p.H - 1 ? 2 : 1);
-        const int xx = x0 + pt * 16 + fr;
-        const int cx = xx == 0 ? 0 : (xx == p.W - 1 ? 2 : 1);
-        const float* cp = fsm + kFoldCorr + (cy * 3 + cx) * 64 + ct0 * 16 + 8 * fk;
-        const float4 c0 = *reinterpret_cast<const float4*>(cp);
-        const float4 c1 = *reinterpret_cast<const float4*>(cp + 4);
-        cv[0] = c0.x; cv[1] = c0.y; cv[2] = c0.z; cv[3] = c0.w;
-        cv[4] = c1.x; cv[5] = c1.y; cv[6] = c1.z; cv[7] = c1.w;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cv[i] = fb[i] + (pt == fpt ? fd[i] : 0.f);
       }
 #pragma unroll
       for (int c = 0; c < NCT; ++c) {
@@ -980,6 +991,8 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
           if (st < 3 && st * PER + i < NLD) op_load(k - 1, st * PER + i);
       }
       if (st < NGW && pf && wv_s + NW * st < NGRP) group_dma_one(k + 2, st);
+      if constexpr (FOLD && PREV)
+        if (st == 0) fold_corr_load(k - 1);
       __builtin_amdgcn_sched_barrier(0);
       const bool ld = st + LA < 18;
       if (ld) load_step(st + LA, A[(st + LA) % kFragBuf], B[(st + LA) % kFragBuf]);
@@ -1059,6 +1072,7 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
   // the last strip's epilogue, exposed
   if constexpr (kPart)
     if (k1 - 2 >= k0) part_store(k1 - 2);
+  fold_corr_load(k1 - 1);
   zero_ps();
 #pragma unroll
   for (int pt = 0; pt < NPT; ++pt) epi_tile(k1 - 1, pt);

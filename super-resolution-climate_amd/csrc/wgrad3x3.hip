@@ -356,6 +356,19 @@ __device__ __forceinline__ void wgrad48_fold_correction(const WgradParams& p, ch
 // FOLD (the conv2 filter gradient of a folded RCAB, fused launch only, W == 48):
 // before the slab store the partial gains c[co] T[tap][ci] (wgrad48_fold_correction):
 // the filter gradient of du = du' + c, exactly.
+// du' + c on one K-step's dY fragments: lane l of co tile ct holds 8 pixels of row co
+// = tile (ct + wave) & 3, l & 15 -- one c per fragment, rounded back to bf16
+__device__ __forceinline__ void add_fold_c(bf16x8 (&a)[4], const float (&fc)[4]) {
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    u32x4 q = __builtin_bit_cast(u32x4, a[ct]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      q[e] = pack2(__uint_as_float(q[e] << 16) + fc[ct], __uint_as_float(q[e] & 0xFFFF0000u) + fc[ct]);
+    a[ct] = __builtin_bit_cast(bf16x8, q);
+  }
+}
+
 // SRMI_FOLD_WG: 2 = c added to the dY fragments in the K-loop (the filter gradient of
 // bf16(du' + c), as the materialised path rounds du); 1 = c (x) T added to the partial
 // after the K-loop (exact; its row-sum pass after the chunk measured +7-11 us in F2)
@@ -572,6 +585,7 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   uint32_t ra, rb[NT];
   slots(0, ra, rb);
   load_step(ra, rb, 0, A[0], B[0]);
+  if constexpr (FOLD_A) add_fold_c(A[0], fc);
 
 #pragma unroll 1
   for (int j0 = 0; j0 < np; j0 += 2) {
@@ -589,18 +603,6 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
         if (kMain && pf)
           dma_pair_part(j + PF, kc == 0 ? 0 : (kc == 1 ? 3 : 5), kc == 0 ? 3 : (kc == 1 ? 5 : 7));
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (FOLD_A) {
-          // du = du' + c: this K-step's dY fragments (8 pixels of one co row per lane)
-#pragma unroll
-          for (int ct = 0; ct < 4; ++ct) {
-            u32x4 q = __builtin_bit_cast(u32x4, A[cur][ct]);
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              q[e] = pack2(__uint_as_float(q[e] << 16) + fc[ct], __uint_as_float(q[e] & 0xFFFF0000u) + fc[ct]);
-            A[cur][ct] = __builtin_bit_cast(bf16x8, q);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
         const bool ld = kc < 2 || more;
         if constexpr (NB == 2) {
           if (kc < 2) load_step(ra, rb, kc + 1, A[nxt], B[nxt]);
@@ -631,6 +633,12 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
           if constexpr (NRD > NPAIR) __builtin_amdgcn_sched_group_barrier(0x100, NRD - NPAIR, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (FOLD_A) {
+          // du = du' + c on the NEXT K-step's dY fragments (loaded during these MFMAs):
+          // the VALU runs while the MFMA pipe drains instead of ahead of it
+          if (kc < 2 || more) add_fold_c(A[nxt], fc);
+          __builtin_amdgcn_sched_barrier(0);
+        }
         if (kc == 1) {
           // pair j+1 must have landed before K-step 2 reads its first fragments.  In
           // flight may stay: pair j+2 (whole) and the 5 groups of pair j+PF issued above.

@@ -31,7 +31,7 @@ def main(path, nsteps=2):
     # trace (roofline leg, tiled inference, the EDSR line) end in an Adam too
     def is_train(seg):
         names = [e[2] for e in seg]
-        return (any("ca_bwd_du_kernel" in n for n in names) and not any("region_to_tiles" in n for n in names)
+        return (any("ca_fwd_kernel" in n for n in names) and not any("region_to_tiles" in n for n in names)
                 and not any("<32," in n for n in names))
     ks = [k for k in range(1, len(adam)) if is_train(ev[adam[k - 1] + 1:adam[k] + 1])]
     for k in ks[-nsteps:]:
