@@ -65,8 +65,8 @@ def parse():
     ap.add_argument("--no-dp-probe", action="store_true", help="skip the dp_overhead_1rank measurement")
     ap.add_argument("--force-dp", action="store_true",
                     help="diagnostic: the DP path (RCCL group, reducer stream, bucketed all-reduce) at one rank")
-    ap.add_argument("--no-ca-fold", action="store_true",
-                    help="A/B: materialise du in a CA-backward pass per RCAB (SRMI_FLAG_NO_CA_FOLD)")
+    ap.add_argument("--ca-fold", action="store_true",
+                    help="A/B: fold each RCAB's CA backward into the conv launches (SRMI_FLAG_CA_FOLD)")
     ap.add_argument("--no-rcab-infer", action="store_true",
                     help="A/B: inference RCABs as three launches (SRMI_FLAG_NO_RCAB_INFER)")
     return ap.parse_args()
@@ -120,7 +120,7 @@ WGRAD_OUT_BYTES = 64 * 577 * 4           # dW (64x64x9) + db, fp32, once per lau
 #  F2 = rcab_bwd_kernel<DG_RELUMASK>: conv2's dgrad (reads du bf16, reads the ReLU
 #       output t bf16 as the mask, writes dz bf16) and conv2's filter gradient (t, du
 #       already counted)
-#  with the CA-backward fold (the default) F1 also writes du' = bf16(g s) of the next
+#  with the CA-backward fold (opt-in, --ca-fold) F1 also writes du' = bf16(g s) of the next
 #  RCAB (one more bf16 map; the CA-backward pass that read g and wrote du is gone) and
 #  F2 reads du' instead of du (same bytes)
 F1_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE + 2 * ACT_F32_PER_TILE
@@ -149,7 +149,7 @@ def fused_rooflines(tr, step_ms, reps=20):
     out = {}
     nl, nb = tr.spec.nlayers, tr.spec.nblocks
     per_step = {1: nl * (nb - 1), 2: nl * nb}
-    fold = not (tr.spec.flags & 1)
+    fold = bool(tr.spec.flags & 1)
     for which, name, bpt in ((1, "rcab_bwd_kernel<EPI_DG_ACC_CA>", F1_FOLD_BYTES_PER_TILE if fold else F1_BYTES_PER_TILE),
                              (2, "rcab_bwd_kernel<EPI_DG_RELUMASK>", F2_BYTES_PER_TILE)):
         streams = [tr.streams[k] or main_st for k in range(n_eng)]
@@ -320,8 +320,8 @@ def dp_overhead_probe(args, reps=2):
             "--no-dp-probe", "--steps", str(args.steps), "--warmup", str(args.warmup), "--batch", str(args.batch)]
     if args.micro is not None:
         base += ["--micro", str(args.micro)]
-    if args.no_ca_fold:
-        base += ["--no-ca-fold"]
+    if args.ca_fold:
+        base += ["--ca-fold"]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
     best = {"plain": 0.0, "dp": 0.0}
     micro = None
@@ -426,9 +426,9 @@ def main():
                                                                            2 if args.no_rcab_infer else 0)}
         print(json.dumps(rec), flush=True)
         return
-    from srmi._lib import SRMI_FLAG_NO_CA_FOLD
+    from srmi._lib import SRMI_FLAG_CA_FOLD
     spec = NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=10, nblocks=20,
-                   cbottleneck=2, scale=4, flags=SRMI_FLAG_NO_CA_FOLD if args.no_ca_fold else 0)
+                   cbottleneck=2, scale=4, flags=SRMI_FLAG_CA_FOLD if args.ca_fold else 0)
     tr = FusedTrainer(spec, B, (48, 48), lr=1e-4, interp_loss=not args.no_interp_loss, info=info, device=dev, seed=0,
                       micro=args.micro, cu_budget=args.cu_budget)
     hr = torch.tensor(synthetic_hr(B, C, 192, 1234 + info.rank)).to(dev)
@@ -519,7 +519,7 @@ def main():
         rec = {
             "metric": METRIC, "value": round(value, 2), "unit": "tiles/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "step_times": step_stats,
-            "ca_fold": not args.no_ca_fold,
+            "ca_fold": bool(args.ca_fold),
             "host_enqueue_ms_per_step": round(1000 * t_host / args.steps, 3),
             "host_enqueue_idle_ms_per_step": round(host_idle_ms, 3), "micro": micro, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",

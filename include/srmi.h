@@ -80,9 +80,10 @@ typedef struct srmi_model_config {
   int dtype;         /* SRMI_DTYPE_BF16 | SRMI_DTYPE_F32                    */
   int flags;         /* SRMI_FLAG_* (0 = defaults)                           */
 } srmi_model_config;
-/* flags: SRMI_FLAG_NO_CA_FOLD runs every RCAB's channel-attention backward as its own
- * pass (materialised du) instead of the fold into the conv launches (A/B, tests) */
-#define SRMI_FLAG_NO_CA_FOLD 1
+/* flags: SRMI_FLAG_CA_FOLD folds every RCAB's channel-attention backward into the
+ * conv launches (du never materialised) instead of its own pass.  Opt-in:
+ * parity-green but measured slower than the materialised path on MI355X (A/B, tests) */
+#define SRMI_FLAG_CA_FOLD 1
 /* SRMI_FLAG_NO_RCAB_INFER: inference engines run each RCAB as three launches (conv1,
  * conv2 + pool, CA) instead of one launch with a workgroup per image (A/B, tests) */
 #define SRMI_FLAG_NO_RCAB_INFER 2

@@ -517,6 +517,7 @@ static int dgrad_with_wgrad(srmi_engine* e, const ConvParams& cp, int epi, const
 
 // the CA-backward fold runs where both halves of the RCAB backward are fused launches
 // (bf16, 48-wide tiles) and the producer's epilogue is the specialised DG_ACC_CA
+// (opt-in per engine: SRMI_FLAG_CA_FOLD; SRMI_CA_FOLD=0 compiles it out)
 #ifndef SRMI_CA_FOLD
 #define SRMI_CA_FOLD 1
 #endif
@@ -526,7 +527,7 @@ static int dgrad_with_wgrad(srmi_engine* e, const ConvParams& cp, int epi, const
 #define SRMI_RED_IN_F2 1
 #endif
 static bool use_ca_fold(const srmi_engine* e, int n) {
-  if (!SRMI_CA_FOLD || (e->P.cfg.flags & SRMI_FLAG_NO_CA_FOLD) || e->f32 || e->P.cfg.arch != SRMI_ARCH_RCAN ||
+  if (!SRMI_CA_FOLD || !(e->P.cfg.flags & SRMI_FLAG_CA_FOLD) || e->f32 || e->P.cfg.arch != SRMI_ARCH_RCAN ||
       e->w != 48 || e->h % 4)
     return false;
   const int R = e->P.cfg.reduction, CR = 64 / R;

@@ -299,7 +299,7 @@ def test_checkpoint_resume_matches_uninterrupted():
 @pytest.mark.parametrize("lr_hw", [(48, 48), (32, 48), (8, 48)])
 def test_ca_fold_matches_materialised_du(lr_hw):
     """The CA-backward fold (du never materialised; srmi_internal.hpp CaFold, DESIGN.md
-    §3) against the materialised path (SRMI_FLAG_NO_CA_FOLD) on the same step: the
+    §3) against the materialised path (the default; the fold is SRMI_FLAG_CA_FOLD) on the same step: the
     forward is untouched (bit-identical output and loss) and every gradient -- the
     conv2 filter gradients with their c (x) T term, the conv1 chain through the dgrad's
     border-class correction, the CA MLP parameter gradients from the fold's backward
@@ -312,7 +312,7 @@ def test_ca_fold_matches_materialised_du(lr_hw):
     h, w = lr_hw
     C, nl, nb, B = 2, 2, 4, 6
     specs = [NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=nl, nblocks=nb,
-                     cbottleneck=2, scale=4, flags=f) for f in (0, 1)]
+                     cbottleneck=2, scale=4, flags=f) for f in (1, 0)]
     table = _table(specs[0])
     flat = torch.empty(sum(t[2] for t in table))
     default_init_(flat, table, seed=21)
