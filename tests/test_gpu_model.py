@@ -296,23 +296,17 @@ def test_checkpoint_resume_matches_uninterrupted():
     assert torch.equal(a.m, c.m) and torch.equal(a.v, c.v)
 
 
-@pytest.mark.parametrize("lr_hw", [(48, 48), (32, 48), (8, 48)])
-def test_ca_fold_matches_materialised_du(lr_hw):
-    """The CA-backward fold (du never materialised; srmi_internal.hpp CaFold, DESIGN.md
-    §3) against the materialised path (the default; the fold is SRMI_FLAG_CA_FOLD) on the same step: the
-    forward is untouched (bit-identical output and loss) and every gradient -- the
-    conv2 filter gradients with their c (x) T term, the conv1 chain through the dgrad's
-    border-class correction, the CA MLP parameter gradients from the fold's backward
-    record -- agrees to the bf16 rounding of du (the materialised path rounds
-    g s + dm/HW once, the fold rounds g s and adds dm/HW in fp32).  Both paths sit
-    within the drift bounds of the fp64 oracle.  Three tile heights move the border
-    rows between strips and runs."""
+def _engine_variants_agree(lr_hw, flags, grad_tol):
+    """One training step of the same weights and tiles through two engine variants
+    (srmi_model_config.flags): the forward is untouched (bit-identical output and
+    loss), the gradients agree to grad_tol (rel. L2 of the whole vector, 3e-2 per
+    tensor) and both sit within the drift bounds of the fp64 oracle."""
     from srmi.trainer import default_init_
     d = dev()
     h, w = lr_hw
     C, nl, nb, B = 2, 2, 4, 6
     specs = [NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=nl, nblocks=nb,
-                     cbottleneck=2, scale=4, flags=f) for f in (1, 0)]
+                     cbottleneck=2, scale=4, flags=f) for f in flags]
     table = _table(specs[0])
     flat = torch.empty(sum(t[2] for t in table))
     default_init_(flat, table, seed=21)
@@ -324,7 +318,7 @@ def test_ca_fold_matches_materialised_du(lr_hw):
     assert torch.equal(trs[0].sr, trs[1].sr)
     assert float(outs[0]["loss"]) == float(outs[1]["loss"])
     ga, gb = trs[0].grads.cpu(), trs[1].grads.cpu()
-    assert rel_l2(ga, gb) < 5e-3
+    assert rel_l2(ga, gb) < grad_tol
     model = ro.RCANOracle(nchannels_in=C, nchannels_out=C, nlayers=nl, nblocks=nb, nfeatures=64, cbottleneck=2).double()
     sd = dict(model.named_parameters())
     with torch.no_grad():
@@ -337,3 +331,27 @@ def test_ca_fold_matches_materialised_du(lr_hw):
         rb = rel_l2(gb[off:off + n].view(shape), g_ref[name])
         assert ra <= bound[name] and rb <= bound[name], (name, ra, rb, bound[name])
         assert rel_l2(ga[off:off + n], gb[off:off + n]) < 3e-2, name
+
+
+@pytest.mark.parametrize("lr_hw", [(48, 48), (32, 48), (8, 48)])
+def test_ca_fold_matches_materialised_du(lr_hw):
+    """The CA-backward fold (du never materialised; srmi_internal.hpp CaFold, DESIGN.md
+    §3) against the materialised path (the default; the fold is SRMI_FLAG_CA_FOLD):
+    every gradient -- the conv2 filter gradients with their c term, the conv1 chain
+    through the dgrad's border-class correction, the CA MLP parameter gradients from
+    the fold's backward record -- agrees to the bf16 rounding of du (the materialised
+    path rounds g s + dm/HW once, the fold rounds g s and adds dm/HW in fp32).  Three
+    tile heights move the border rows between strips and runs."""
+    from srmi._lib import SRMI_FLAG_CA_FOLD
+    _engine_variants_agree(lr_hw, (SRMI_FLAG_CA_FOLD, 0), 5e-3)
+
+
+@pytest.mark.parametrize("lr_hw", [(48, 48), (16, 32)])
+def test_pair_gradient_stream_matches_fp32(lr_hw):
+    """The in-group gradient stream stored as a pair (bf16 + 8-bit remainder, the
+    default of the bf16 engine; engine.cpp use_g_pair) against fp32
+    (SRMI_FLAG_FP32_GSTREAM): 16 significant bits per accumulation step, so the
+    gradients agree far inside the bf16 rounding of the operands.  (16, 32) runs
+    the 32-wide tile kernels (no fused launch)."""
+    from srmi._lib import SRMI_FLAG_FP32_GSTREAM
+    _engine_variants_agree(lr_hw, (0, SRMI_FLAG_FP32_GSTREAM), 2e-3)

@@ -1,13 +1,13 @@
 #!/bin/bash
 # Interleaved bench A/B of library builds and engine flags on ONE box (training leg only):
 #   bash tools/ab_var.sh "main::" "redl:alt/libsrmi_redl.so:" "fold::--ca-fold"
-# each variant = name:library (empty = in-tree):extra bench flags
+# each variant = name:library (empty = in-tree):extra bench flags[:VAR=x,VAR2=y env]
 R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R; O=$R/gpurun_out; mkdir -p $O
 REPS=${REPS:-2}
 for rep in $(seq $REPS); do
   for v in "$@"; do
-    IFS=: read -r name lib flags <<< "$v"
-    SRMI_LIB=${lib:+$R/$lib} timeout -k 10 200 python bench.py --no-cpu-baseline --no-inference --no-edsr --no-dp-probe \
+    IFS=: read -r name lib flags envs <<< "$v"
+    env ${envs//,/ } SRMI_LIB=${lib:+$R/$lib} timeout -k 10 200 python bench.py --no-cpu-baseline --no-inference --no-edsr --no-dp-probe \
       --steps 20 --warmup 3 $flags > $O/abv.json 2>> $O/abv.err || { echo "variant $name failed"; exit 2; }
     python -c "
 import json; d=json.loads(open('$O/abv.json').read().strip().splitlines()[-1])
