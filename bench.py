@@ -67,8 +67,6 @@ def parse():
                     help="diagnostic: the DP path (RCCL group, reducer stream, bucketed all-reduce) at one rank")
     ap.add_argument("--ca-fold", action="store_true",
                     help="A/B: fold each RCAB's CA backward into the conv launches (SRMI_FLAG_CA_FOLD)")
-    ap.add_argument("--fp32-gstream", action="store_true",
-                    help="A/B: the in-group gradient stream in fp32 instead of the pair (SRMI_FLAG_FP32_GSTREAM)")
     ap.add_argument("--no-rcab-infer", action="store_true",
                     help="A/B: inference RCABs as three launches (SRMI_FLAG_NO_RCAB_INFER)")
     return ap.parse_args()
@@ -113,22 +111,20 @@ def _time_launches(launch, stream, n=50, warm=5):
 
 ACT_BF16_PER_TILE = 48 * 48 * 64 * 2    # one bf16 48x48x64 activation
 ACT_F32_PER_TILE = 48 * 48 * 64 * 4
-ACT_PAIR_PER_TILE = 48 * 48 * 64 * 3    # the pair: bf16 hi + 8-bit remainder
 WGRAD_OUT_BYTES = 64 * 577 * 4           # dW (64x64x9) + db, fp32, once per launch
 # Algorithmic bytes per tile of the two fused RCAB-backward launches (SURVEY.md §8(d),
 # DESIGN.md "Kernels"): what each must move at least, every operand once.
 #  F1 = rcab_bwd_kernel<DG_ACC_CA>: conv1's dgrad (reads dz bf16, reads + writes the
-#       in-group gradient stream g -- a 3-byte pair, fp32 with --fp32-gstream --, reads
-#       the CA input u bf16 for the CA sums) and conv1's filter gradient (reads its
-#       input hb bf16; dz already counted)
+#       fp32 residual-stream gradient g, reads the CA input u bf16 for the CA sums) and
+#       conv1's filter gradient (reads its input hb bf16; dz already counted)
 #  F2 = rcab_bwd_kernel<DG_RELUMASK>: conv2's dgrad (reads du bf16, reads the ReLU
 #       output t bf16 as the mask, writes dz bf16) and conv2's filter gradient (t, du
 #       already counted)
 #  with the CA-backward fold (opt-in, --ca-fold) F1 also writes du' = bf16(g s) of the next
 #  RCAB (one more bf16 map; the CA-backward pass that read g and wrote du is gone) and
 #  F2 reads du' instead of du (same bytes)
-F1_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE + 2 * ACT_PAIR_PER_TILE
-F1_F32G_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE + 2 * ACT_F32_PER_TILE
+F1_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE + 2 * ACT_F32_PER_TILE
+F1_FOLD_BYTES_PER_TILE = F1_BYTES_PER_TILE + ACT_BF16_PER_TILE
 F2_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE
 FUSED_FLOP_PER_TILE = 2 * CONV64_FLOP_PER_TILE   # one dgrad conv + one filter-gradient conv
 
@@ -154,8 +150,7 @@ def fused_rooflines(tr, step_ms, reps=20):
     nl, nb = tr.spec.nlayers, tr.spec.nblocks
     per_step = {1: nl * (nb - 1), 2: nl * nb}
     fold = bool(tr.spec.flags & 1)
-    f1_bytes = (F1_F32G_BYTES_PER_TILE if tr.spec.flags & 4 else F1_BYTES_PER_TILE) + (ACT_BF16_PER_TILE if fold else 0)
-    for which, name, bpt in ((1, "rcab_bwd_kernel<EPI_DG_ACC_CA>", f1_bytes),
+    for which, name, bpt in ((1, "rcab_bwd_kernel<EPI_DG_ACC_CA>", F1_FOLD_BYTES_PER_TILE if fold else F1_BYTES_PER_TILE),
                              (2, "rcab_bwd_kernel<EPI_DG_RELUMASK>", F2_BYTES_PER_TILE)):
         streams = [tr.streams[k] or main_st for k in range(n_eng)]
 
@@ -327,8 +322,6 @@ def dp_overhead_probe(args, reps=2):
         base += ["--micro", str(args.micro)]
     if args.ca_fold:
         base += ["--ca-fold"]
-    if args.fp32_gstream:
-        base += ["--fp32-gstream"]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
     best = {"plain": 0.0, "dp": 0.0}
     micro = None
@@ -433,9 +426,9 @@ def main():
                                                                            2 if args.no_rcab_infer else 0)}
         print(json.dumps(rec), flush=True)
         return
-    from srmi._lib import SRMI_FLAG_CA_FOLD, SRMI_FLAG_FP32_GSTREAM
+    from srmi._lib import SRMI_FLAG_CA_FOLD
     spec = NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=10, nblocks=20,
-                   cbottleneck=2, scale=4, flags=(SRMI_FLAG_CA_FOLD if args.ca_fold else 0) | (SRMI_FLAG_FP32_GSTREAM if args.fp32_gstream else 0))
+                   cbottleneck=2, scale=4, flags=SRMI_FLAG_CA_FOLD if args.ca_fold else 0)
     tr = FusedTrainer(spec, B, (48, 48), lr=1e-4, interp_loss=not args.no_interp_loss, info=info, device=dev, seed=0,
                       micro=args.micro, cu_budget=args.cu_budget)
     hr = torch.tensor(synthetic_hr(B, C, 192, 1234 + info.rank)).to(dev)
@@ -526,7 +519,7 @@ def main():
         rec = {
             "metric": METRIC, "value": round(value, 2), "unit": "tiles/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "step_times": step_stats,
-            "ca_fold": bool(args.ca_fold), "g_stream": "fp32" if args.fp32_gstream else "pair",
+            "ca_fold": bool(args.ca_fold),
             "host_enqueue_ms_per_step": round(1000 * t_host / args.steps, 3),
             "host_enqueue_idle_ms_per_step": round(host_idle_ms, 3), "micro": micro, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",

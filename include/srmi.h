@@ -87,9 +87,6 @@ typedef struct srmi_model_config {
 /* SRMI_FLAG_NO_RCAB_INFER: inference engines run each RCAB as three launches (conv1,
  * conv2 + pool, CA) instead of one launch with a workgroup per image (A/B, tests) */
 #define SRMI_FLAG_NO_RCAB_INFER 2
-/* SRMI_FLAG_FP32_GSTREAM: the gradient stream inside a residual group stays fp32 instead
- * of the 3-byte pair (bf16 + 8-bit remainder) the bf16 engine stores it as (A/B, tests) */
-#define SRMI_FLAG_FP32_GSTREAM 4
 
 typedef struct srmi_param_info {
   long long offset; /* element offset in the flat fp32 parameter buffer     */

@@ -356,16 +356,6 @@ static int launch_tw(const ConvParams& p, hipStream_t st) {
   return 0;
 }
 
-// the pair form of the gradient stream (ConvParams r1h / yph) exists in the run-layout
-// epilogue of the 64-channel kernel only: both halves of a pair or neither, never
-// beside its fp32 form
-bool conv_pair_ok(const ConvParams& p, int epi) {
-  if (!p.r1h && !p.r1l && !p.yph && !p.ypl) return true;
-  if ((!p.r1h) != (!p.r1l) || (!p.yph) != (!p.ypl) || (p.r1h && p.r1) || (p.yph && p.yf)) return false;
-  const bool run = epi == EPI_DG_ACC_CA || (SRMI_DGACC_RUN && epi == EPI_DG_ACC);
-  return run && !p.f32 && p.Cin == 64 && p.in_mode == IN_PLAIN && !((SRMI_DEFER & 8) && epi == EPI_DG_ACC_CA);
-}
-
 template <int EPI>
 static int launch_epi(const ConvParams& p, hipStream_t st) {
   if (p.W % 48 == 0 && p.H % kTH == 0) return launch_tw<48, EPI>(p, st);
@@ -383,9 +373,7 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
   if (p.Cin % 64 || p.Cout % 64 || p.N <= 0 || p.H % kTH) return SRMI_ERR_SHAPE;
   // operands each epilogue dereferences unconditionally: refuse, never fault
   if (!p.x || !p.w) return SRMI_ERR_ARG;
-  if (epi == EPI_DG_ACC_CA && ((!p.r1 && !p.r1h) || !p.aux || !p.part || p.yb || p.r2 || p.r3 || (!p.yf && !p.yph)))
-    return SRMI_ERR_ARG;
-  if (!conv_pair_ok(p, epi)) return SRMI_ERR_ARG;
+  if (epi == EPI_DG_ACC_CA && (!p.r1 || !p.aux || !p.part || p.yb || p.r2 || p.r3 || !p.yf)) return SRMI_ERR_ARG;
   switch (epi) {
     case EPI_PS_BF16:
       if (!p.yb) return SRMI_ERR_ARG;
@@ -400,7 +388,7 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
       if (!p.aux) return SRMI_ERR_ARG;
       break;
     case EPI_DG_ACC:
-      if ((!p.yf && !p.yph) || (p.part && !p.aux)) return SRMI_ERR_ARG;
+      if (!p.yf || (p.part && !p.aux)) return SRMI_ERR_ARG;
       break;
     default:
       break;
@@ -414,7 +402,7 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
   {
     const size_t elems = (size_t)p.N * p.H * p.W * p.Cout;
     if (p.yb && elems * (p.f32 ? 4 : 2) >= (1ull << 32)) return SRMI_ERR_SHAPE;
-    if ((p.yf || p.yph || p.r1h) && elems * 4 >= (1ull << 32)) return SRMI_ERR_SHAPE;
+    if (p.yf && elems * 4 >= (1ull << 32)) return SRMI_ERR_SHAPE;
   }
   if (p.f32) return conv3x3_f32_launch(p, epi, st);
   switch (epi) {

@@ -96,17 +96,12 @@ __device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT
       const int i = kSh ? 2 * j + (ct0 >> 1) : j;
       const int lin = i * 1024 + lane * 16, lpx = lin >> 8, ch = (lin >> 4) & 15;
       const size_t oc = ((size_t)n * HW + (size_t)y * p.W + x0 + h * HALF + lpx) * p.Cout + cb * 64 + ch * 4;
-      if (p.r1h) {  // g as a pair: raw hi / lo bits, decoded in the store loop (uniform)
-        const uint2 hh = *reinterpret_cast<const uint2*>(p.r1h + oc);
-        const uint32_t ll = *reinterpret_cast<const uint32_t*>(p.r1l + oc);
-        e.r1[pt][c] = make_float4(__uint_as_float(hh.x), __uint_as_float(hh.y), __uint_as_float(ll), 0.f);
-      }
       if constexpr (EPI == EPI_DG_ACC_CA) {
-        if (!p.r1h) e.r1[pt][c] = *reinterpret_cast<const float4*>(p.r1 + oc);  // (load q = idx at [q / NCT][q % NCT])
+        e.r1[pt][c] = *reinterpret_cast<const float4*>(p.r1 + oc);  // (load q = idx at [q / NCT][q % NCT])
         e.aux[pt][c] = *reinterpret_cast<const uint2*>(p.aux + oc);
       } else {  // DG_ACC: every operand optional (uniform branches)
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (!p.r1h) e.r1[pt][c] = p.r1 ? *reinterpret_cast<const float4*>(p.r1 + oc) : z;
+        e.r1[pt][c] = p.r1 ? *reinterpret_cast<const float4*>(p.r1 + oc) : z;
         e.r2[pt][c] = p.r2 ? *reinterpret_cast<const float4*>(p.r2 + oc) : z;
         e.aux[pt][c] = p.part ? *reinterpret_cast<const uint2*>(p.aux + oc) : make_uint2(0, 0);
       }
@@ -235,8 +230,6 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       // CA-backward fold producer (EPI_DG_ACC_CA): du' = bf16(g * s) of the next RCAB
       [[maybe_unused]] const bool fold_out = (EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC) && p.fold.du_out != nullptr;
       [[maybe_unused]] const auto rdu = wt_rsrc(p.fold.du_out, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
-      [[maybe_unused]] const auto rph = wt_rsrc(p.yph, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
-      [[maybe_unused]] const auto rpl = wt_rsrc(p.ypl, (uint32_t)((size_t)p.N * HW * p.Cout));
       const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -260,9 +253,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             // g += dx in the run layout; the lane's channels 4c..4c+3 (c = lane & 15)
             // are the same in every run, so its sums accumulate in registers
             const int q = h * (kShared ? RUNS / 2 : RUNS) + j;
-            float4 gg = e.r1[q / NCT][q % NCT];
-            if (p.r1h)
-              gg = pair_decode4(make_uint2(__float_as_uint(gg.x), __float_as_uint(gg.y)), __float_as_uint(gg.z));
+            const float4 gg = e.r1[q / NCT][q % NCT];
             const uint2 uu = e.aux[q / NCT][q % NCT];
             val.x += gg.x; val.y += gg.y; val.z += gg.z; val.w += gg.w;
             if constexpr (EPI == EPI_DG_ACC) {
@@ -280,15 +271,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             ps1[0][2] += val.z * bf2f(uu.y & 0xFFFFu);
             ps1[0][3] += val.w * bf2f(uu.y >> 16);
           }
-          const uint32_t oe = (uint32_t)((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4);  // element
-          if (kRun && p.yph) {  // g out as a pair: 512 + 256 contiguous bytes per instruction
-            uint2 hi;
-            const uint32_t lo = pair_encode4(val.x, val.y, val.z, val.w, hi);
-            st_wt8(rph, p.yph, oe * 2, hi);
-            st_wt4(rpl, p.ypl, oe, lo);
-          } else {
-            st_wt16(rf, p.yf, oe * 4, val);
-          }
+          st_wt16(rf, p.yf, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 4), val);
           if constexpr (EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC) {
             if (fold_out)  // the lane's channels 4c..4c+3 are the same in every run: s in fs
               st_wt8(rdu, p.fold.du_out, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 2),

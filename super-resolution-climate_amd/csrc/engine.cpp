@@ -194,8 +194,6 @@ struct srmi_engine {
   float *ppool, *pacc;
   // backward
   float *GAf, *GBf, *dRESf;
-  bf16_t* GPh;  // the in-group gradient stream as a pair (hi; lo in GPl), see use_g_pair
-  uint8_t* GPl;
   bf16_t *GAb, *GBb, *DU, *DZ, *dRESb;
   bf16_t* dPS[3];
   float *slab, *bslab;
@@ -291,8 +289,6 @@ static size_t carve(srmi_engine* e, char* base) {
   if (e->train) {
     e->GAf = cv.take<float>(m);
     e->GBf = cv.take<float>(m);
-    e->GPh = reinterpret_cast<bf16_t*>(cv.take<char>(m * 2));
-    e->GPl = reinterpret_cast<uint8_t*>(cv.take<char>(m));
     e->dRESf = cv.take<float>(m);
     e->GAb = act(m);
     e->GBb = act(m);
@@ -542,30 +538,6 @@ static bool use_ca_fold(const srmi_engine* e, int n) {
   return (e->h / rs2) % 4 == 0;
 }
 
-// The gradient stream inside a residual group (g: written by the group tail's dgrad,
-// accumulated by every RCAB's conv1 dgrad, read by the CA backward) is stored as a
-// pair -- bf16 hi + 8-bit remainder, 16 significant bits in 3 bytes, the codec of
-// the forward residual stream -- instead of fp32: the hottest launch (F1) reads and
-// writes it, so 25 % of its bytes go.  The group-level streams stay fp32.
-#ifndef SRMI_G_PAIR
-#define SRMI_G_PAIR 1
-#endif
-static bool use_g_pair(const srmi_engine* e) {
-  return SRMI_G_PAIR && !(e->P.cfg.flags & SRMI_FLAG_FP32_GSTREAM) && !e->f32 && e->P.cfg.arch == SRMI_ARCH_RCAN;
-}
-static void to_pair(const srmi_engine* e, ConvParams& p, bool in, bool out) {
-  if (in) {
-    p.r1 = nullptr;
-    p.r1h = e->GPh;
-    p.r1l = e->GPl;
-  }
-  if (out) {
-    p.yf = nullptr;
-    p.yph = e->GPh;
-    p.ypl = e->GPl;
-  }
-}
-
 static CaFold fold_consumer(const srmi_engine* e, const float* prm, const RCABRef& r, int g, int b, int nstrips) {
   CaFold f{};
   f.part = e->pacc;
@@ -739,7 +711,6 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
     // above (F1) instead of a CA-backward pass; its conv2 backward (F2) adds the
     // constant dm / HW itself.  bf16 engine, fused-launch shapes only.
     const bool fold = use_ca_fold(e, n);
-    const bool gp = use_g_pair(e);  // g inside the group as a pair (GPh / GPl)
     int it = 0;  // RCAB counter (slab-set parity)
     for (int g = nl - 1; g >= 0; --g) {
       const ConvRef& gt = P.group_tail[g];
@@ -751,14 +722,8 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         tail_fold.s_rec = e->recp(g, nb);
         tail_fold.CR = 64 / R;
       }
-      {
-        int tepi = EPI_DG_ACC;
-        ConvParams tp = dgrad_params(e, gt, gRb, n, h, w, &tepi, nullptr, ghf, nullptr, nullptr, nullptr, e->Um(g, nb),
-                                     e->pacc, 1.f);
-        if (fold) tp.fold = tail_fold;
-        if (gp) to_pair(e, tp, false, true);
-        RC(conv3x3_launch(tp, tepi, st));
-      }
+      RC(conv_dgrad(e, gt, gRb, n, h, w, EPI_DG_ACC, nullptr, ghf, nullptr, nullptr, nullptr, e->Um(g, nb), e->pacc,
+                    1.f, st, fold ? &tail_fold : nullptr));
       ReduceSet prev2{}, prev1{};
       bool have_prev = false;
       for (int b = nb; b >= 1; --b) {
@@ -768,9 +733,8 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         bf16_t* dz = e->DZ;
         const bool folded = fold;  // du' came from the previous F1 (the group tail's dgrad for b == nb)
         if (!folded) {
-          RC(ca_bwd_du_launch(gp ? nullptr : ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW,
-                              64, R, du, e->brecp(g, b), e->f32, st, have_prev ? &prev2 : nullptr,
-                              have_prev ? &prev1 : nullptr, gp ? e->GPh : nullptr, gp ? e->GPl : nullptr));
+          RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
+                              e->brecp(g, b), e->f32, st, have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
         } else if (!SRMI_RED_IN_F2 && have_prev) {
           RC(wgrad_reduce2_launch(prev2, prev1, st));
         }
@@ -796,7 +760,6 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         cp = dgrad_params(e, r.c1, dz, n, h, w, &epi, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
                           (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
                           last ? nullptr : e->pacc, 1.f);
-        if (gp) to_pair(e, cp, true, !last);  // the last one writes the group's fp32 stream
         if (fold && !last) {  // du' of RCAB b - 1
           cp.fold.du_out = e->DU;
           cp.fold.s_rec = e->recp(g, b - 1);
@@ -964,7 +927,6 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
                       nullptr, last ? nullptr : e->Um(0, b - 1), last ? nullptr : e->pacc, 1.f);
     RC(wgrad_params(e, r.c1, e->hb(0, b - 1), e->DZ, n, h, w, grads, true, 1.f, rcab_row_splits(e, n, 1),
                     e->slab_r[0][1], e->bslab_r[0][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red));
-    if (use_g_pair(e)) to_pair(e, cp, true, !last);
     if (use_ca_fold(e, n) && !last) {
       cp.fold.du_out = e->DU;
       cp.fold.s_rec = e->recp(0, b - 1);

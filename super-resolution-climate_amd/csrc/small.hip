@@ -1185,9 +1185,8 @@ int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1
 // reductions of the previous RCAB's two filter gradients (r0, r1: nred blocks
 // each, 256-thread wgrad_reduce_body): both are memory-bound passes of many small
 // blocks, so the reduction rides in this launch instead of a launch of its own.
-template <typename T, bool PAIR>
-__global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict__ g, const bf16_t* __restrict__ ghi,
-                                                        const uint8_t* __restrict__ glo, const float* __restrict__ part,
+template <typename T>
+__global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict__ g, const float* __restrict__ part,
                                                         int nstrips, const float* __restrict__ rec,
                                                         const float* __restrict__ w1, const float* __restrict__ w2,
                                                         int N, int HW, int C, int CR, T* __restrict__ du,
@@ -1221,19 +1220,12 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
   const size_t base = (size_t)n * HW * C;
   const size_t nv = (size_t)HW * C / 8;
   const size_t v0 = ((size_t)blockIdx.x * kCaVec) * blockDim.x + tid;
-  float4 g0[kCaVec], g1[kCaVec];  // PAIR: the raw hi (g0) and lo (g1.x, g1.y) bits, decoded below
+  float4 g0[kCaVec], g1[kCaVec];
 #pragma unroll
   for (int k = 0; k < kCaVec; ++k) {  // clamped, unconditional (tail lanes store nothing)
     const size_t e = base + min(v0 + (size_t)k * blockDim.x, nv - 1) * 8;
-    if constexpr (PAIR) {
-      const uint4 hh = *reinterpret_cast<const uint4*>(ghi + e);
-      const uint2 ll = *reinterpret_cast<const uint2*>(glo + e);
-      g0[k] = make_float4(__uint_as_float(hh.x), __uint_as_float(hh.y), __uint_as_float(hh.z), __uint_as_float(hh.w));
-      g1[k] = make_float4(__uint_as_float(ll.x), __uint_as_float(ll.y), 0.f, 0.f);
-    } else {
-      g0[k] = *reinterpret_cast<const float4*>(g + e);
-      g1[k] = *reinterpret_cast<const float4*>(g + e + 4);
-    }
+    g0[k] = *reinterpret_cast<const float4*>(g + e);
+    g1[k] = *reinterpret_cast<const float4*>(g + e + 4);
   }
   __builtin_amdgcn_sched_barrier(0);
   red[tid >> 7][tid & 127] = pa;
@@ -1281,12 +1273,6 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
   for (int k = 0; k < kCaVec; ++k) {
     const size_t v = v0 + (size_t)k * blockDim.x;
     if (v >= nv) continue;
-    if constexpr (PAIR) {
-      const float4 a = pair_decode4(make_uint2(__float_as_uint(g0[k].x), __float_as_uint(g0[k].y)), __float_as_uint(g1[k].x));
-      const float4 b = pair_decode4(make_uint2(__float_as_uint(g0[k].z), __float_as_uint(g0[k].w)), __float_as_uint(g1[k].y));
-      g0[k] = a;
-      g1[k] = b;
-    }
     const int c0 = (int)((v * 8) % C);
     float dmh[8];
 #pragma unroll
@@ -1306,9 +1292,8 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
 
 int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
                      const float* w2, int N, int HW, int C, int R, void* du, float* brec, int f32, hipStream_t st,
-                     const ReduceSet* red0, const ReduceSet* red1, const bf16_t* ghi, const uint8_t* glo) {
+                     const ReduceSet* red0, const ReduceSet* red1) {
   if (C != 64 || C % R || (C / R) > 32 || (C / R) % 4 || (HW * C) % 8) return SRMI_ERR_SHAPE;
-  if ((ghi == nullptr) != (glo == nullptr) || (ghi == nullptr) == (g == nullptr) || (ghi && f32)) return SRMI_ERR_ARG;
   if ((red0 == nullptr) != (red1 == nullptr)) return SRMI_ERR_ARG;
   if (red0 && (red0->Cout != red1->Cout)) return SRMI_ERR_SHAPE;
   const int gx = ca_grid_x(HW, C);
@@ -1318,14 +1303,11 @@ int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float
   const ReduceSet& a = red0 ? *red0 : none;
   const ReduceSet& b = red1 ? *red1 : none;
   if (f32)
-    hipLaunchKernelGGL((ca_bwd_du_kernel<float, false>), grid, dim3(256), 0, st, g, nullptr, nullptr, part, nstrips,
-                       rec, w1, w2, N, HW, C, C / R, static_cast<float*>(du), brec, a, b, nred);
-  else if (ghi)
-    hipLaunchKernelGGL((ca_bwd_du_kernel<bf16_t, true>), grid, dim3(256), 0, st, nullptr, ghi, glo, part, nstrips,
-                       rec, w1, w2, N, HW, C, C / R, static_cast<bf16_t*>(du), brec, a, b, nred);
+    hipLaunchKernelGGL(ca_bwd_du_kernel<float>, grid, dim3(256), 0, st, g, part, nstrips, rec, w1, w2, N, HW, C,
+                       C / R, static_cast<float*>(du), brec, a, b, nred);
   else
-    hipLaunchKernelGGL((ca_bwd_du_kernel<bf16_t, false>), grid, dim3(256), 0, st, g, nullptr, nullptr, part, nstrips,
-                       rec, w1, w2, N, HW, C, C / R, static_cast<bf16_t*>(du), brec, a, b, nred);
+    hipLaunchKernelGGL(ca_bwd_du_kernel<bf16_t>, grid, dim3(256), 0, st, g, part, nstrips, rec, w1, w2, N, HW, C,
+                       C / R, static_cast<bf16_t*>(du), brec, a, b, nred);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

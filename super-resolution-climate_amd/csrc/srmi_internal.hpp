@@ -66,17 +66,10 @@ struct ConvParams {
   int f32;                     // exact-fp32 mode: x, w, yb, aux point at fp32 data
                                // (the bf16_t* fields are plain addresses then)
   CaFold fold;                 // zero-initialised: no fold
-  // the in-group gradient stream as a pair (hi bf16 + lo8, common.hpp) instead of fp32:
-  // r1h / r1l replace r1, yph / ypl replace yf (run-layout DG_ACC / DG_ACC_CA only)
-  const bf16_t* r1h;
-  const uint8_t* r1l;
-  bf16_t* yph;
-  uint8_t* ypl;
 };
 
 void conv3x3_set_debug_stamps(unsigned long long* buf);
 int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st);  // dispatches p.f32
-bool conv_pair_ok(const ConvParams& p, int epi);  // the pair-stream fields are valid for epi
 int conv3x3_f32_launch(const ConvParams& p, int epi, hipStream_t st);
 int conv3x3_nstrips(int H, int W);
 
@@ -170,8 +163,7 @@ int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1
 // red0/red1 (both or neither): two slab reductions carried in the same launch
 int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
                      const float* w2, int N, int HW, int C, int R, void* du, float* brec, int f32, hipStream_t st,
-                     const ReduceSet* red0 = nullptr, const ReduceSet* red1 = nullptr,
-                     const bf16_t* ghi = nullptr, const uint8_t* glo = nullptr);  // g as a pair (g null)
+                     const ReduceSet* red0 = nullptr, const ReduceSet* red1 = nullptr);
 // inference RCAB, one launch (rcab_infer.hip): c1 = conv1 (RELU, yb = t), c2 = conv2
 // (POOL, yb = u, part), then the CA MLP and the residual pair update per image
 int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* part, int nstrips, const float* w1,

@@ -805,7 +805,6 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
   if (epi == EPI_DG_ACC_CA && cp.fold.du_out && (!cp.fold.s_rec || cp.fold.CR < 4 || cp.fold.CR > 32))
     return SRMI_ERR_ARG;
   if (wp.nred < 0 || wp.nred > 2) return SRMI_ERR_ARG;
-  if (!conv_pair_ok(cp, epi)) return SRMI_ERR_ARG;
   for (int k = 0; k < wp.nred; ++k)
     if (!wp.red[k].slab || !wp.red[k].gw || wp.red[k].Cout != 64 || wp.red[k].layout != 1 || wp.red[k].ps ||
         wp.red[k].nslab < 1 || (wp.red[k].gb && !wp.red[k].bslab))
@@ -843,11 +842,11 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
                            nconv, w, nwg, paired, tail);
       break;
     case EPI_DG_ACC_CA:
-      if ((!c.r1 && !c.r1h) || !c.aux || !c.part || c.yb || c.r2 || c.r3 || (!c.yf && !c.yph)) return SRMI_ERR_ARG;
+      if (!c.r1 || !c.aux || !c.part || c.yb || c.r2 || c.r3 || !c.yf) return SRMI_ERR_ARG;
       hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len, nconv, w, nwg, paired, tail);
       break;
     case EPI_DG_ACC:
-      if ((!c.yf && !c.yph) || (c.part && !c.aux)) return SRMI_ERR_ARG;
+      if (!c.yf || (c.part && !c.aux)) return SRMI_ERR_ARG;
       hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len, nconv, w, nwg, paired, tail);
       break;
     default:

@@ -19,7 +19,6 @@ SRMI_ARCH_EDSR = 1
 SRMI_DTYPE_BF16 = 0
 SRMI_FLAG_CA_FOLD = 1
 SRMI_FLAG_NO_RCAB_INFER = 2
-SRMI_FLAG_FP32_GSTREAM = 4
 SRMI_DTYPE_F32 = 1
 SRMI_LOSS_RMSE = 0
 SRMI_LOSS_MEAN = 1

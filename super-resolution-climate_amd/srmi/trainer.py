@@ -18,7 +18,6 @@ gradients are all-reduced as described in srmi/dist.py.
 """
 from __future__ import annotations
 
-import os
 import math
 from typing import Dict, Optional
 
@@ -139,7 +138,6 @@ class FusedTrainer:
         self.mloss4 = torch.zeros((micro, 4), dtype=torch.float32, device=self.device)   # per micro-batch
         self.miloss4 = torch.zeros((micro, 4), dtype=torch.float32, device=self.device)
         self.streams = [None] + [torch.cuda.Stream(device=self.device) for _ in range(micro - 1)]
-        self._stagger = int(os.environ.get("SRMI_STAGGER_CYCLES", "0"))  # A/B: engine k starts k x later
         self.reducer = GradReducer(self.eng.table, spec.arch, spec.nlayers, self.info, self.device)
         # group events of engines 1.. (engine 0 records into reducer.events)
         self.xevents = [self.reducer.new_events() for _ in range(micro - 1)]
@@ -195,8 +193,6 @@ class FusedTrainer:
                 self.miloss4[k].zero_()
                 continue
             with self._ctx(k):
-                if k and self._stagger:
-                    torch.cuda._sleep(self._stagger * k)
                 downsample(hr[sl], s, out=self.lrbuf[sl])
                 eng.forward(self.params, self.lrbuf[sl], out=self.sr[sl])
                 self._loss_partial(eng, self.sr[sl], tgt[sl], self.mloss4[k], count,
@@ -221,8 +217,6 @@ class FusedTrainer:
         for k, eng in enumerate(self.engines):
             sl = sls[k]
             with self._ctx(k):
-                if k and self._stagger:
-                    torch.cuda._sleep(self._stagger * k)
                 if sl.stop == sl.start:  # no tiles: zero gradient (and its group events)
                     self.mgrads[k].zero_()
                     if evs[k] is not None:

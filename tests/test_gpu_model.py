@@ -344,14 +344,3 @@ def test_ca_fold_matches_materialised_du(lr_hw):
     tile heights move the border rows between strips and runs."""
     from srmi._lib import SRMI_FLAG_CA_FOLD
     _engine_variants_agree(lr_hw, (SRMI_FLAG_CA_FOLD, 0), 5e-3)
-
-
-@pytest.mark.parametrize("lr_hw", [(48, 48), (16, 32)])
-def test_pair_gradient_stream_matches_fp32(lr_hw):
-    """The in-group gradient stream stored as a pair (bf16 + 8-bit remainder, the
-    default of the bf16 engine; engine.cpp use_g_pair) against fp32
-    (SRMI_FLAG_FP32_GSTREAM): 16 significant bits per accumulation step, so the
-    gradients agree far inside the bf16 rounding of the operands.  (16, 32) runs
-    the 32-wide tile kernels (no fused launch)."""
-    from srmi._lib import SRMI_FLAG_FP32_GSTREAM
-    _engine_variants_agree(lr_hw, (0, SRMI_FLAG_FP32_GSTREAM), 2e-3)
