@@ -97,6 +97,27 @@ def _pmc_traffic(kernel_prefix):
     return None
 
 
+def _pmc_region_bytes():
+    """Fabric bytes of one C5 region from the committed rocprofv3 --pmc summary of the
+    inference leg (tools/pmc_infer.sh): per-launch FETCH_SIZE x2 + WRITE_SIZE times the
+    launches of that run, over its regions (region_to_tiles_kernel runs once per region)."""
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_infer*.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        kern = {k: v for k, v in d.items() if isinstance(v, dict) and "hbm_bytes_per_launch" in v}
+        regions = [v["dispatches"][0] for k, v in kern.items() if "region_to_tiles" in k]
+        if not regions or not regions[0]:
+            continue
+        total = sum(v["hbm_bytes_per_launch"] * v["dispatches"][0] for k, v in kern.items()
+                    if "pack_tile" not in k)  # (the filter packs: once per model, not per region)
+        rcab = {k: v["hbm_bytes_per_launch"] for k, v in kern.items() if "rcab_infer_kernel<false>" in k}
+        return {"bytes": total / regions[0], "source": os.path.relpath(f, ROOT),
+                "rcab_launch_bytes": next(iter(rcab.values()), None)}
+    return None
+
+
 def _time_launches(launch, stream, n=50, warm=5):
     for _ in range(warm):
         launch()
@@ -263,7 +284,16 @@ def inference_bench(dev, side, iters, flags=0, info=None):
         e1.synchronize()
         ms = e0.elapsed_time(e1) / iters
     mpix = ti.n * 192 * 192 / 1e6
+    tr_ = _pmc_region_bytes()
+    roof = None
+    if tr_ and not multi:  # the region's fabric bytes (PMC) over its time: the bound of C5
+        gbs = tr_["bytes"] / (ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": round(tr_["bytes"]),
+                "traffic_rcab_launch": tr_["rcab_launch_bytes"], "traffic_source": tr_["source"],
+                "note": "PMC fabric bytes per region (all kernels) / ms_per_region"}
     return {"metric": "inference MPix/sec (HR pixels produced)", "value": round(mpix / (ms * 1e-3), 2),
+            "roofline": roof,
             "unit": "MPix/s", "ms_per_region": round(ms, 3), "tiles": ti.n, "hr_mpix_per_region": round(mpix, 3),
             "model_tflops": round(ti.n * 73.26e9 / (ms * 1e-3) / 1e12, 1),
             "mfma_frac": round(ti.n * 73.26e9 / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),

@@ -416,12 +416,16 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
 // FOLD (EPI_DG_RELUMASK, deferred form only): the consumer side of the CA-backward
 // fold (srmi_internal.hpp CaFold, ca_fold.hpp); the producer side (EPI_DG_ACC_CA) is
 // the runtime p.fold.du_out.
-template <int TW, int EPI, int NW = 4, bool FOLD = false>
+// REV: the run's strips last to first (the one-launch inference RCAB runs conv2 that
+// way, so that its first strips read the ReLU output rows conv1 wrote last, still in
+// L2); same arithmetic per strip, so the same results.
+template <int TW, int EPI, int NW = 4, bool FOLD = false, bool REV = false>
 __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, int bid, char* smem, int tail = 0,
                                             bool tail_part = false) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(!FOLD || (EPI == EPI_DG_RELUMASK && NW == 8 && conv64_defers<EPI>()),
                 "the fold consumer is the deferred 8-wave ReLU-mask dgrad");
+  static_assert(!REV || !(NW == 8 && conv64_defers<EPI>()), "reversed runs: the non-deferred body only");
   if constexpr (NW == 8 && conv64_defers<EPI>()) {
     conv64_body_defer<TW, EPI, FOLD>(p, run_len, bid, smem, tail, tail_part);
     return;
@@ -513,8 +517,8 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
       const int tap = i >> 3, row = 8 * (i & 7) + (lane >> 3), c = (lane & 7) ^ (row & 7);
       glds16(p.w + ((size_t)(tap * p.Cout + cb * 64 + row)) * 64 + c * 8, wbase + (uint32_t)i * 1024u);
     }
-    group_dma(k0);
-    group_dma(k0 + 1);
+    group_dma(REV ? k1 - 1 : k0);  // strip k reads input groups k and k + 1
+    group_dma(REV ? k1 : k0 + 1);
     wait_vm<0>();
   }
   STAMP(1);
@@ -534,13 +538,16 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   __syncthreads();
 
 #pragma unroll 1
-  for (int k = k0; k < k1; ++k) {
+  for (int i = 0; i < k1 - k0; ++i) {
+    const int k = REV ? k1 - 1 - i : k0 + i;
     const int y = 4 * k + row;
-    const bool pf = (k + 1 < k1);
+    const bool pf = (i + 1 < k1 - k0);
     // group k+2 -> ring slot (k+2)%3, which held group k-1 (last read by strip k-1,
-    // released by the barrier that ended it)
+    // released by the barrier that ended it); REV: group k-1 -> slot (k-1)%3, which
+    // held group k+2 (strip k+1's)
+    const int gpf = REV ? k - 1 : k + 2;
     EpiPre<NPT, EPI, NCT> ep;
-    [[maybe_unused]] const int sj = 2 + 5 * min(k - k0, 11);
+    [[maybe_unused]] const int sj = 2 + 5 * min(i, 11);
     STAMP(sj);
 
     // B-fragment byte offsets per (ky, kx, kk); +2048 per 16-pixel tile
@@ -578,7 +585,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     for (int s = 0; s < 18; ++s) {
       // group k+2's DMA pieces and the epilogue operands are issued one or two per
       // K-step, so a full memory queue stalls the wave between MFMA groups only
-      if (s < NGW && pf && wv_s + NW * s < NGRP) group_dma_one(k + 2, s);
+      if (s < NGW && pf && wv_s + NW * s < NGRP) group_dma_one(gpf, s);
       // the epilogue operands, two per K-step from the first one: a whole strip of
       // MFMAs to land (spread over K-steps 2..13, the heavy fp32 epilogue of
       // DG_ACC_CA waited on its last ones at the end of the K-loop: +1.3 % step)
@@ -614,12 +621,13 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     STAMP(sj + 2);
     // every wave is past its last read of input group k: its ring slot stages the
     // strip's bf16 output rows (slot k%3 is next written by group k+3's DMA,
-    // issued after the barrier that ends this strip)
+    // issued after the barrier that ends this strip; REV: group k+1's slot, next
+    // written by group k-2's DMA)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     conv_epilogue2<NPT, EPI, NCT>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx, nsy * nsx, red, fr, fk, row, ct0,
-                                  tid, ring + (k % 3) * S::GROUPB + row * TW * 128, fs);
+                                  tid, ring + ((REV ? k + 1 : k) % 3) * S::GROUPB + row * TW * 128, fs);
     STAMP(sj + 3);
     // LDS-only barrier: this strip's global stores stay in flight into the next strip
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

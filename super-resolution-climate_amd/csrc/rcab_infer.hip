@@ -9,10 +9,39 @@
 // other workgroup: no launch boundaries between them, the MLP once per image instead
 // of once per elementwise block, and t / u re-read by the workgroup that just wrote
 // them (L2 / Infinity-Cache hits instead of HBM).
+// t and u are re-read by this workgroup within the launch: plain stores keep their
+// lines in the XCD's L2 (write-through ones drop them); conv2 runs its strips last to
+// first so that it starts on the t rows conv1 wrote last, and the CA pass starts on the
+// u rows conv2 wrote last.  The residual pair stays write-through (stw_* below).
+#ifndef SRMI_INFER_WT
+#define SRMI_INFER_WT 0
+#endif
+#ifndef SRMI_INFER_REV
+#define SRMI_INFER_REV 1
+#endif
+// deferred conv epilogues (conv64_body.hpp SRMI_DEFER) for this launch's convs: an
+// image is one run of 12 strips here, not 3 as in training
+#ifndef SRMI_INFER_DEFER
+#define SRMI_INFER_DEFER 7
+#endif
+// diagnostic builds only (wrong results): 1 skips the CA pass, 2 conv2, 4 conv1
+#ifndef SRMI_INFER_DIAG
+#define SRMI_INFER_DIAG 0
+#endif
+#define SRMI_WT SRMI_INFER_WT
+#define SRMI_DEFER SRMI_INFER_DEFER
 #include "conv64_body.hpp"
 #include "srmi_internal.hpp"
 
 namespace srmi {
+
+__device__ __forceinline__ void stw8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint2 v) {  // write-through (sc1)
+  typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 16);
+}
+__device__ __forceinline__ void stw4(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 16);
+}
 
 struct CaInfer {
   const bf16_t* u;      // conv2 output [N][HW][64] bf16
@@ -108,8 +137,8 @@ __device__ __forceinline__ void ca_image_body(const CaInfer& c, int n, int HW, f
       const float o3 = bf2f(uu[k].y >> 16) * s[c0 + 3] + hh[k].w;
       uint2 hi;
       const uint32_t lo = pair_encode4(o0, o1, o2, o3, hi);
-      st_wt8(rhb, c.hi_out, (uint32_t)(e * 2), hi);
-      st_wt4(rlo, c.lo_out, (uint32_t)e, lo);
+      stw8(rhb, (uint32_t)(e * 2), hi);
+      stw4(rlo, (uint32_t)e, lo);
     }
   }
 }
@@ -127,11 +156,12 @@ __global__ void __launch_bounds__(512, 1) rcab_infer_kernel(ConvParams c1, ConvP
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = blockIdx.x;
   const int nsy = c1.H / kTH;
-  conv64_body<48, EPI_RELU_BF16, 8>(c1, nsy, n, smem);  // the whole image: one run
+  if (!(SRMI_INFER_DIAG & 4)) conv64_body<48, EPI_RELU_BF16, 8>(c1, nsy, n, smem);  // the whole image: one run
   own_stores_visible();
-  conv64_body<48, EPI_POOL_BF16, 8>(c2, nsy, n, smem);
+  constexpr bool kRev = SRMI_INFER_REV && !(SRMI_INFER_DEFER & 2);  // (reversal: the non-deferred body)
+  if (!(SRMI_INFER_DIAG & 2)) conv64_body<48, EPI_POOL_BF16, 8, false, kRev>(c2, nsy, n, smem);
   own_stores_visible();
-  ca_image_body<F32IN>(ca, n, c1.H * c1.W, reinterpret_cast<float*>(smem));
+  if (!(SRMI_INFER_DIAG & 1)) ca_image_body<F32IN>(ca, n, c1.H * c1.W, reinterpret_cast<float*>(smem));
 }
 
 int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* part, int nstrips, const float* w1,
