@@ -68,14 +68,15 @@ struct EpiPre {
 #endif
 template <int EPI>
 constexpr bool epi_run() {
-  return EPI == EPI_DG_ACC_CA || (SRMI_DGACC_RUN && EPI == EPI_DG_ACC);
+  return EPI == EPI_DG_ACC_CA || (SRMI_DGACC_RUN && EPI == EPI_DG_ACC) || EPI == EPI_CA_RESID;
 }
 
 // one (pt, c) element (idx = pt * NCT + c), issued one or two per K-step
 template <int NPT, int EPI, int NCT>
 __device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT, EPI, NCT>& e, int n, int cb, int y,
                                                  int x0, int fr, int fk, int ct0, int idx) {
-  if constexpr (EPI == EPI_RESID || EPI == EPI_DG_ACC || EPI == EPI_DG_RELUMASK || EPI == EPI_DG_ACC_CA) {
+  if constexpr (EPI == EPI_RESID || EPI == EPI_DG_ACC || EPI == EPI_DG_RELUMASK || EPI == EPI_DG_ACC_CA ||
+                EPI == EPI_CA_RESID) {
     const int pt = idx / NCT, c = idx % NCT;
     const size_t HW = (size_t)p.H * p.W;
     const size_t pix = (size_t)n * HW + (size_t)y * p.W + x0 + pt * 16 + fr;
@@ -96,7 +97,15 @@ __device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT
       const int i = kSh ? 2 * j + (ct0 >> 1) : j;
       const int lin = i * 1024 + lane * 16, lpx = lin >> 8, ch = (lin >> 4) & 15;
       const size_t oc = ((size_t)n * HW + (size_t)y * p.W + x0 + h * HALF + lpx) * p.Cout + cb * 64 + ch * 4;
-      if constexpr (EPI == EPI_DG_ACC_CA) {
+      if constexpr (EPI == EPI_CA_RESID) {  // h: the pair's raw bits (decoded in the store loop) or fp32
+        if (p.r1h) {
+          const uint2 hh = *reinterpret_cast<const uint2*>(p.r1h + oc);
+          const uint32_t ll = *reinterpret_cast<const uint32_t*>(p.r1l + oc);
+          e.r1[pt][c] = make_float4(__uint_as_float(hh.x), __uint_as_float(hh.y), __uint_as_float(ll), 0.f);
+        } else {
+          e.r1[pt][c] = *reinterpret_cast<const float4*>(p.r1 + oc);
+        }
+      } else if constexpr (EPI == EPI_DG_ACC_CA) {
         e.r1[pt][c] = *reinterpret_cast<const float4*>(p.r1 + oc);  // (load q = idx at [q / NCT][q % NCT])
         e.aux[pt][c] = *reinterpret_cast<const uint2*>(p.aux + oc);
       } else {  // DG_ACC: every operand optional (uniform branches)
@@ -143,7 +152,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
   };
   const size_t HW = (size_t)p.H * p.W;
   [[maybe_unused]] const auto rfa = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
-  constexpr bool kPart1 = (EPI == EPI_POOL_BF16);
+  constexpr bool kPart1 = (EPI == EPI_POOL_BF16 || EPI == EPI_RELU_POOL);
   constexpr bool kPart2 = (EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_CA);
   float ps0[NCT][4], ps1[NCT][4];
   // fp32 output staged through LDS (DG_ACC, whose epilogue also reads r2/r3 from
@@ -167,10 +176,10 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       const size_t o = pix * p.Cout + co;
       f32x4 v = acc[pt][c];
       if constexpr (EPI == EPI_RELU_BF16 || EPI == EPI_POOL_BF16 || EPI == EPI_RESID || EPI == EPI_PS_BF16 ||
-                    EPI == EPI_PLAIN_BF16) {
+                    EPI == EPI_PLAIN_BF16 || EPI == EPI_RELU_POOL || EPI == EPI_CA_RESID) {
         v[0] += bias[c].x; v[1] += bias[c].y; v[2] += bias[c].z; v[3] += bias[c].w;
       }
-      if constexpr (EPI == EPI_RELU_BF16) {
+      if constexpr (EPI == EPI_RELU_BF16 || EPI == EPI_RELU_POOL) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
       }
@@ -230,6 +239,8 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       // CA-backward fold producer (EPI_DG_ACC_CA): du' = bf16(g * s) of the next RCAB
       [[maybe_unused]] const bool fold_out = (EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC) && p.fold.du_out != nullptr;
       [[maybe_unused]] const auto rdu = wt_rsrc(p.fold.du_out, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
+      [[maybe_unused]] const auto rph = wt_rsrc(p.yph, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
+      [[maybe_unused]] const auto rpl = wt_rsrc(p.ypl, (uint32_t)((size_t)p.N * HW * p.Cout));
       const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -249,6 +260,21 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
           const int i = kShared ? 2 * j + half_id : j;
           const int lin = i * 1024 + lane * 16, lpx = lin >> 8, c = (lin >> 4) & 15;
           float4 val = *reinterpret_cast<const float4*>(stage + lpx * 256 + ((c ^ (lpx & 15)) << 4));
+          if constexpr (EPI == EPI_CA_RESID) {
+            // h' = h + s u in the run layout (the lane's channels 4c..4c+3: s in fs), out as the pair
+            const int q = h * (kShared ? RUNS / 2 : RUNS) + j;
+            float4 hh = e.r1[q / NCT][q % NCT];
+            if (p.r1h)
+              hh = pair_decode4(make_uint2(__float_as_uint(hh.x), __float_as_uint(hh.y)), __float_as_uint(hh.z));
+            const float o0 = fmaf(val.x, fs.x, hh.x), o1 = fmaf(val.y, fs.y, hh.y);
+            const float o2 = fmaf(val.z, fs.z, hh.z), o3 = fmaf(val.w, fs.w, hh.w);
+            const uint32_t oe = (uint32_t)((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4);  // element
+            uint2 hi;
+            const uint32_t lo = pair_encode4(o0, o1, o2, o3, hi);
+            st_wt8(rph, p.yph, oe * 2, hi);
+            st_wt4(rpl, p.ypl, oe, lo);
+            continue;
+          }
           if constexpr (kRun) {
             // g += dx in the run layout; the lane's channels 4c..4c+3 (c = lane & 15)
             // are the same in every run, so its sums accumulate in registers
@@ -397,7 +423,8 @@ constexpr int kFragBuf = SRMI_CONV_FRAGBUF;
 template <int EPI>
 constexpr bool conv64_defers() {
   return ((SRMI_DEFER & 1) && EPI == EPI_RELU_BF16) || ((SRMI_DEFER & 2) && EPI == EPI_POOL_BF16) ||
-         ((SRMI_DEFER & 4) && EPI == EPI_DG_RELUMASK) || ((SRMI_DEFER & 8) && EPI == EPI_DG_ACC_CA);
+         ((SRMI_DEFER & 4) && EPI == EPI_DG_RELUMASK) || ((SRMI_DEFER & 8) && EPI == EPI_DG_ACC_CA) ||
+         ((SRMI_DEFER & 16) && EPI == EPI_RELU_POOL) || ((SRMI_DEFER & 32) && EPI == EPI_CA_RESID);
 }
 template <int TW, int EPI, bool FOLD = false>
 __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_len, int bid, char* smem, int tail,
@@ -530,6 +557,8 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     for (int c = 0; c < NCT; ++c) aoff[kk][c] = swz128((ct0 + c) * 16 + fr, kk * 4 + fk);
   // fold producer: s of the next RCAB for the lane's 4 run-layout channels (conv_epilogue2)
   float4 fs = float4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI == EPI_CA_RESID)
+    fs = *reinterpret_cast<const float4*>(p.escale + (size_t)n * p.escale_stride + 4 * (lane & 15));
   if constexpr (EPI == EPI_DG_ACC_CA || (EPI == EPI_DG_ACC && epi_run<EPI>())) {
     if (p.fold.du_out)
       fs = *reinterpret_cast<const float4*>(p.fold.s_rec + (size_t)n * (128 + p.fold.CR) + 64 + p.fold.CR +
@@ -704,8 +733,9 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
   using S = Conv2Smem<TW>;
   constexpr int NPT = TW / 16;
   constexpr bool kPerm = EPI != EPI_DG_ACC_CA;  // bf16 output: permuted filter rows
-  constexpr bool kPart = EPI == EPI_POOL_BF16 || EPI == EPI_DG_ACC_CA;
+  constexpr bool kPart = EPI == EPI_POOL_BF16 || EPI == EPI_DG_ACC_CA || EPI == EPI_RELU_POOL;
   constexpr bool kCA = EPI == EPI_DG_ACC_CA;
+  constexpr bool kCR = EPI == EPI_CA_RESID;  // h' = h + s u: 8 contiguous channels per lane (permuted rows)
   constexpr int ES = 10;  // K-step of the first deferred epilogue tile
   char* wl = smem;
   char* ring = smem + S::WB;
@@ -814,12 +844,20 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
 
   const auto rout = kPerm ? wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2))
                           : wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
+  [[maybe_unused]] const auto rph = wt_rsrc(p.yph, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
+  [[maybe_unused]] const auto rpl = wt_rsrc(p.ypl, (uint32_t)((size_t)p.N * HW * p.Cout));
+  [[maybe_unused]] float sv[8];  // CA_RESID: s of the lane's 8 channels
+  if constexpr (kCR) {
+    const float* sp = p.escale + (size_t)n * p.escale_stride + ct0 * 16 + 8 * fk;
+    const float4 a = *reinterpret_cast<const float4*>(sp), b = *reinterpret_cast<const float4*>(sp + 4);
+    sv[0] = a.x; sv[1] = a.y; sv[2] = a.z; sv[3] = a.w; sv[4] = b.x; sv[5] = b.y; sv[6] = b.z; sv[7] = b.w;
+  }
   const int nstrips_all = nsy * nsx;
   f32x4 accp[NPT][NCT];  // the previous strip's accumulators
   DeferOps<NPT> ops;     // operands of the pending epilogue
 
   // operand loads of the epilogue of strip kp (pixel row 4 kp + row), load slot i
-  constexpr int NLD = EPI == EPI_DG_RELUMASK ? NPT : (kCA ? NPT * NCT : 0);
+  constexpr int NLD = (EPI == EPI_DG_RELUMASK || kCR) ? NPT : (kCA ? NPT * NCT : 0);
   auto op_load = [&](int kp, int i) __attribute__((always_inline)) {
     const int yy = 4 * kp + row;
     if constexpr (EPI == EPI_DG_RELUMASK) {
@@ -831,6 +869,16 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
       const size_t o = pix * p.Cout + cb * 64 + chan(c, 0);
       ops.g[pt][c] = *reinterpret_cast<const float4*>(p.r1 + o);
       ops.u[pt][c] = *reinterpret_cast<const uint2*>(p.aux + o);
+    } else if constexpr (kCR) {  // h: the pair (hi 16 B + lo 8 B) or fp32 (32 B), 8 channels
+      const size_t pix = (size_t)n * HW + (size_t)yy * p.W + x0 + i * 16 + fr;
+      const size_t o = pix * p.Cout + cb * 64 + chan(0, 0);
+      if (p.r1h) {
+        ops.t[i] = *reinterpret_cast<const uint4*>(p.r1h + o);
+        ops.u[i][0] = *reinterpret_cast<const uint2*>(p.r1l + o);
+      } else {
+        ops.g[i][0] = *reinterpret_cast<const float4*>(p.r1 + o);
+        ops.g[i][1] = *reinterpret_cast<const float4*>(p.r1 + o + 4);
+      }
     }
   };
   // fold: the border-class corrections of strip kp's row for this lane (LDS, issued
@@ -857,6 +905,16 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
 #pragma unroll
     for (int c = 0; c < NCT; ++c) pin4(accp[pt][c]);
     if constexpr (EPI == EPI_DG_RELUMASK) pin4u(ops.t[pt]);
+    if constexpr (kCR) {
+      if (p.r1h) {
+        pin4u(ops.t[pt]);
+        pin(ops.u[pt][0].x);
+        pin(ops.u[pt][0].y);
+      } else {
+        pin4f(ops.g[pt][0]);
+        pin4f(ops.g[pt][1]);
+      }
+    }
     if constexpr (kCA) {
 #pragma unroll
       for (int c = 0; c < NCT; ++c) {
@@ -867,7 +925,32 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     }
     const int yy = 4 * kp + row;
     const size_t pix = (size_t)n * HW + (size_t)yy * p.W + x0 + pt * 16 + fr;
-    if constexpr (kPerm) {
+    if constexpr (kCR) {
+      float hv[8];
+      if (p.r1h) {
+        const uint4 th = ops.t[pt];
+        const uint2 tl = ops.u[pt][0];
+        const float4 a = pair_decode4(make_uint2(th.x, th.y), tl.x), b = pair_decode4(make_uint2(th.z, th.w), tl.y);
+        hv[0] = a.x; hv[1] = a.y; hv[2] = a.z; hv[3] = a.w; hv[4] = b.x; hv[5] = b.y; hv[6] = b.z; hv[7] = b.w;
+      } else {
+        const float4 a = ops.g[pt][0], b = ops.g[pt][1];
+        hv[0] = a.x; hv[1] = a.y; hv[2] = a.z; hv[3] = a.w; hv[4] = b.x; hv[5] = b.y; hv[6] = b.z; hv[7] = b.w;
+      }
+      float o[8];
+#pragma unroll
+      for (int c = 0; c < NCT; ++c) {
+        const f32x4 v = accp[pt][c];
+        const float b[4] = {bias[c].x, bias[c].y, bias[c].z, bias[c].w};
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) o[4 * c + rr] = fmaf(v[rr] + b[rr], sv[4 * c + rr], hv[4 * c + rr]);
+      }
+      uint2 h0, h1;
+      const uint32_t l0 = pair_encode4(o[0], o[1], o[2], o[3], h0);
+      const uint32_t l1 = pair_encode4(o[4], o[5], o[6], o[7], h1);
+      const uint32_t oe = (uint32_t)(pix * p.Cout + cb * 64 + chan(0, 0));
+      st_wt16(rph, p.yph, oe * 2, make_uint4(h0.x, h0.y, h1.x, h1.y));
+      st_wt8(rpl, p.ypl, oe, make_uint2(l0, l1));
+    } else if constexpr (kPerm) {
       float o[8];
       // fold: + the dgrad of the constant c for this pixel's border class (8 contiguous
       // channels ct0*16 + 8fk ..), before the ReLU mask: the row class's x-inner value
@@ -885,6 +968,10 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
         for (int rr = 0; rr < 4; ++rr) {
           float x = v[rr];
           if constexpr (EPI == EPI_RELU_BF16) x = fmaxf(x + b[rr], 0.f);
+          if constexpr (EPI == EPI_RELU_POOL) {
+            x = fmaxf(x + b[rr], 0.f);
+            ps0[c][rr] += x;
+          }
           if constexpr (EPI == EPI_POOL_BF16) {
             x += b[rr];
             ps0[c][rr] += x;
@@ -1036,7 +1123,7 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     STAMP(sj + 1);
     // group k+2 has landed once only this strip's deferred stores (and the partial
     // record) may still be in flight behind it
-    constexpr int NST = PREV ? (kPerm ? NPT : NPT * NCT) : 0;
+    constexpr int NST = PREV ? (kCR ? 2 * NPT : (kPerm ? NPT : NPT * NCT)) : 0;
     if (!pf) {
       // no DMA in this strip: nothing to wait for (the loads of the exposed
       // epilogue are waited for where they are used)

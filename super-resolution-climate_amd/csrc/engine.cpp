@@ -610,12 +610,12 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
       for (int b = 1; b <= nb; ++b) {
         const RCABRef& r = P.groups[g][b - 1];
         if (use_rcab_infer(e)) {  // inference: the RCAB as one launch, a workgroup per image
-          bf16_t* lo = reinterpret_cast<bf16_t*>(e->Hf);
+          uint8_t* lo = reinterpret_cast<uint8_t*>(e->Hf);  // the pair's lo8 remainder, 1 B / element
           const ConvParams c1 = fwd_params(e, r.c1, e->hb(g, b - 1), n, h, w, e->Tm(g, b), nullptr, nullptr, nullptr, 1.f);
           const ConvParams c2 = fwd_params(e, r.c2, e->Tm(g, b), n, h, w, e->Um(g, b), nullptr, nullptr, e->ppool, 1.f);
           RC(rcab_infer_launch(c1, c2, e->ppool, nstrips, prm + r.ca_w1, prm + r.ca_b1, prm + r.ca_w2, prm + r.ca_b2,
                                64 / R, b == 1 ? rin : nullptr, b == 1 ? nullptr : e->hb(g, b - 1),
-                               b == 1 ? nullptr : lo, e->hb(g, b), lo, e->recp(g, b), st));
+                               b == 1 ? nullptr : lo, e->hb(g, b), lo, e->recp(g, b), st, prm + r.c2.w, prm + r.c2.b));
           continue;
         }
         RC(conv_fwd(e, r.c1, e->hb(g, b - 1), n, h, w, EPI_RELU_BF16, e->Tm(g, b), nullptr, nullptr, nullptr, 1.f, st));

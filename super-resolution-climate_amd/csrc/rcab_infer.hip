@@ -1,20 +1,27 @@
 // Inference RCAB as ONE launch, one workgroup per image (RCAB, sres/model/rcan/
-// network.py:50-64; CALayer :31-47):
-//   phase A  t = relu(conv1(h) + b1)        conv64_body<RELU>, the whole image as one run
-//   phase B  u = conv2(t) + b2, pool sums   conv64_body<POOL>, likewise
-//   phase C  s = sigmoid(W2 relu(W1 mean(u) + c1) + c2); h' = h + s u   (residual pair)
-// Training keeps the three launches (t, u and the CA record are saved for backward and
-// an image there is split over several workgroups); in inference an image is one run
-// anyway (run_len = all strips at the C5 batch), so the image's three passes need no
-// other workgroup: no launch boundaries between them, the MLP once per image instead
-// of once per elementwise block, and t / u re-read by the workgroup that just wrote
-// them (L2 / Infinity-Cache hits instead of HBM).
-// t and u are re-read by this workgroup within the launch: plain stores keep their
-// lines in the XCD's L2 (write-through ones drop them); conv2 runs its strips last to
-// first so that it starts on the t rows conv1 wrote last, and the CA pass starts on the
-// u rows conv2 wrote last.  The residual pair stays write-through (stw_* below).
+// network.py:50-64; CALayer :31-47).  In inference an image is one run of the conv
+// body anyway (run_len = all strips at the C5 batch), so an RCAB needs no other
+// workgroup and no launch boundary inside it.
+//
+// v2 (default): u = conv2(t) + b2 is never stored.  The CA pool needs only mean(u),
+// and by linearity
+//   mean_p u[p][c] = b2[c] + (1/HW) sum_{tap, ci} W2[c][ci][tap] S_tap[ci],
+//   S_tap[ci] = sum over the input pixels tap (dy, dx) reaches of t[.][ci]
+//             = T[ci] - (row excluded by dy) - (column excluded by dx) + (their corner),
+// so s = sigmoid(W2' relu(W1' mean(u) + c1) + c2) is known before conv2 runs:
+//   phase A  t = relu(conv1(h) + b1), + per-strip channel sums T   conv64_body<RELU_POOL>
+//   phase S  border rows / columns / corners of t, S_tap, mean(u), the CA MLP -> s
+//   phase B  h' = h + s (conv2(t) + b2) in conv2's epilogue          conv64_body<CA_RESID>
+// against v1's three passes (conv1; conv2 + pool writing u; the CA pass reading u, h
+// and writing h'): per image 0.6 MB less traffic and no elementwise pass, and u enters
+// h' in fp32 instead of rounded to bf16.  The sums differ from the pooled fp32 u only
+// in summation order and in conv2's bf16 weights (the mean uses the fp32 weights).
+// v1 (SRMI_INFER_V=1): bit-identical to the three training-path launches.
+#ifndef SRMI_INFER_V
+#define SRMI_INFER_V 1
+#endif
 #ifndef SRMI_INFER_WT
-#define SRMI_INFER_WT 0
+#define SRMI_INFER_WT 1
 #endif
 #ifndef SRMI_INFER_REV
 #define SRMI_INFER_REV 1
@@ -54,28 +61,16 @@ struct CaInfer {
   const uint8_t* lo_in;
   bf16_t* hi_out;       // the pair out (hi = the next conv1's operand)
   uint8_t* lo_out;
-  float* rec;           // optional: m | z1 | s per image
+  float* rec;           // m | z1 | s per image (v1: optional; v2: s is conv2's scale)
+  const float* wc2;     // v2: conv2's fp32 weight [64][64][3][3] and bias [64] (the mean)
+  const float* bc2;
+  const bf16_t* t;      // v2: conv1's output
 };
 
-// phase C for image n, 512 threads: the MLP in LDS scratch (sm >= 64 + 64 + 32 + 64 floats),
-// then the elementwise pair update, 8 units of 4 channels in flight per thread
-template <bool F32IN>
-__device__ __forceinline__ void ca_image_body(const CaInfer& c, int n, int HW, float* sm) {
+// the CA MLP of image n from m (LDS) -> z1, s (LDS) and the record (512 threads)
+__device__ __forceinline__ void ca_mlp(const CaInfer& c, int n, float* m, float* z1, float* s) {
   constexpr int C = 64;
   const int tid = threadIdx.x, CR = c.CR, per = CR / 4;
-  float* red = sm;            // [4][64]
-  float* m = sm + 512;        // [64]
-  float* z1 = m + 64;         // [32]
-  float* s = z1 + 32;         // [64]
-  if (tid < 256) {  // pool: 4 strip phases x 64 channels, the order of ca_fwd_kernel (bit-identical)
-    const int ch = tid & 63, ph = tid >> 6;
-    float a = 0.f;
-    for (int k = ph; k < c.nstrips; k += 4) a += c.part[((size_t)n * c.nstrips + k) * C + ch];
-    red[ph * 64 + ch] = a;
-  }
-  __syncthreads();
-  if (tid < C) m[tid] = (red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid]) / (float)HW;
-  __syncthreads();
   if (tid < 256) {  // z1[j] = b1[j] + W1[j] . m  (8 lanes per j)
     const int j = tid >> 3, pj = tid & 7, jc = min(j, CR - 1);
     float a = 0.f;
@@ -106,6 +101,110 @@ __device__ __forceinline__ void ca_image_body(const CaInfer& c, int n, int HW, f
     }
     if (tid < CR) r[C + tid] = z1[tid];
   }
+}
+
+// v2 phase S for image n (512 threads, sm >= 1600 floats): mean(u) from t's statistics
+// (the header), then the MLP; s lands in the record, where conv2's epilogue reads it
+__device__ __forceinline__ void ca_scale_from_t(const CaInfer& c, int n, int H, int W, float* sm) {
+  constexpr int C = 64;
+  const int tid = threadIdx.x, HW = H * W;
+  float* red = sm;          // [4][64] strip-phase partials of T
+  float* T = sm + 256;      // [64]
+  float* bs = sm + 320;     // [4][64] sums of row 0, row H-1, column 0, column W-1
+  float* cn = sm + 576;     // [4][64] corners (0,0) (0,W-1) (H-1,0) (H-1,W-1)
+  float* St = sm + 832;     // [9][64]
+  float* m = sm + 1408;     // [64]
+  float* z1 = m + 64;       // [32]
+  float* s = z1 + 32;       // [64]
+  const bf16_t* tn = c.t + (size_t)n * HW * C;
+  if (tid < 256) {  // T: conv1's per-strip sums, 4 strip phases, fixed order
+    const int ch = tid & 63, ph = tid >> 6;
+    float a = 0.f;
+    for (int k = ph; k < c.nstrips; k += 4) a += c.part[((size_t)n * c.nstrips + k) * C + ch];
+    red[ph * 64 + ch] = a;
+    // corners
+    const int y = (ph & 2) ? H - 1 : 0, x = (ph & 1) ? W - 1 : 0;
+    cn[ph * 64 + ch] = bf2f(tn[((size_t)y * W + x) * C + ch]);
+  }
+  {  // border lines: line l = tid >> 7, channel group g (8 channels), positions j, j + 16, ...
+    const int l = tid >> 7, g = (tid >> 4) & 7, j = tid & 15;
+    const int len = l < 2 ? W : H;
+    float a[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = 0.f;
+    for (int q = j; q < len; q += 16) {
+      const int y = l == 0 ? 0 : l == 1 ? H - 1 : q;
+      const int x = l < 2 ? q : l == 2 ? 0 : W - 1;
+      const uint4 v = *reinterpret_cast<const uint4*>(tn + ((size_t)y * W + x) * C + g * 8);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[2 * e] += bf2f(w[e] & 0xFFFFu);
+        a[2 * e + 1] += bf2f(w[e] >> 16);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a[e] += __shfl_xor(a[e], 1, 64);
+      a[e] += __shfl_xor(a[e], 2, 64);
+      a[e] += __shfl_xor(a[e], 4, 64);
+      a[e] += __shfl_xor(a[e], 8, 64);
+    }
+    if (j == 0)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bs[l * 64 + g * 8 + e] = a[e];
+  }
+  __syncthreads();
+  if (tid < C) T[tid] = (red[tid] + red[64 + tid]) + (red[128 + tid] + red[192 + tid]);
+  __syncthreads();
+  for (int i = tid; i < 9 * C; i += 512) {  // S_tap: tap (dy, dx) reads t[y + dy][x + dx]
+    const int tap = i >> 6, ci = i & 63, dy = tap / 3 - 1, dx = tap % 3 - 1;
+    float v = T[ci];
+    if (dy == -1) v -= bs[64 + ci];   // row H-1 is never read
+    if (dy == 1) v -= bs[ci];         // row 0
+    if (dx == -1) v -= bs[192 + ci];  // column W-1
+    if (dx == 1) v -= bs[128 + ci];   // column 0
+    if (dy != 0 && dx != 0) v += cn[((dy == -1) ? 2 : 0) * 64 + ((dx == -1) ? 1 : 0) * 64 + ci];
+    St[i] = v;
+  }
+  __syncthreads();
+  {  // m[c] = b2[c] + (1/HW) sum_{ci, tap} W2[c][ci][tap] S_tap[ci]: 8 lanes per c, 8 ci each
+    const int co = tid >> 3, pc = tid & 7;
+    const float* wr = c.wc2 + ((size_t)co * C + pc * 8) * 9;  // 72 contiguous floats
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) a += wr[k * 9 + tap] * St[tap * 64 + pc * 8 + k];
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    a += __shfl_xor(a, 4, 64);
+    if (pc == 0) m[co] = c.bc2[co] + a / (float)HW;
+  }
+  __syncthreads();
+  ca_mlp(c, n, m, z1, s);
+}
+
+// phase C for image n, 512 threads: the MLP in LDS scratch (sm >= 64 + 64 + 32 + 64 floats),
+// then the elementwise pair update, 8 units of 4 channels in flight per thread
+template <bool F32IN>
+__device__ __forceinline__ void ca_image_body(const CaInfer& c, int n, int HW, float* sm) {
+  constexpr int C = 64;
+  const int tid = threadIdx.x;
+  float* red = sm;            // [4][64]
+  float* m = sm + 512;        // [64]
+  float* z1 = m + 64;         // [32]
+  float* s = z1 + 32;         // [64]
+  if (tid < 256) {  // pool: 4 strip phases x 64 channels, the order of ca_fwd_kernel (bit-identical)
+    const int ch = tid & 63, ph = tid >> 6;
+    float a = 0.f;
+    for (int k = ph; k < c.nstrips; k += 4) a += c.part[((size_t)n * c.nstrips + k) * C + ch];
+    red[ph * 64 + ch] = a;
+  }
+  __syncthreads();
+  if (tid < C) m[tid] = (red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid]) / (float)HW;
+  __syncthreads();
+  ca_mlp(c, n, m, z1, s);
   // elementwise: units of 4 channels, consecutive lanes on consecutive units
   const size_t base = (size_t)n * HW * C;
   const int nq = HW * C / 4;
@@ -164,15 +263,29 @@ __global__ void __launch_bounds__(512, 1) rcab_infer_kernel(ConvParams c1, ConvP
   if (!(SRMI_INFER_DIAG & 1)) ca_image_body<F32IN>(ca, n, c1.H * c1.W, reinterpret_cast<float*>(smem));
 }
 
+__global__ void __launch_bounds__(512, 1) rcab_infer2_kernel(ConvParams c1, ConvParams c2, CaInfer ca) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int n = blockIdx.x;
+  const int nsy = c1.H / kTH;
+  conv64_body<48, EPI_RELU_POOL, 8>(c1, nsy, n, smem);  // t and its per-strip channel sums
+  own_stores_visible();
+  ca_scale_from_t(ca, n, c1.H, c1.W, reinterpret_cast<float*>(smem));  // s into the record
+  own_stores_visible();
+  conv64_body<48, EPI_CA_RESID, 8>(c2, nsy, n, smem);  // h' = h + s (conv2(t) + b2)
+}
+
 int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* part, int nstrips, const float* w1,
                       const float* b1, const float* w2, const float* b2, int CR, const float* h_in, const void* hi_in,
-                      const void* lo_in, void* hi_out, void* lo_out, float* rec, hipStream_t st) {
+                      const void* lo_in, void* hi_out, void* lo_out, float* rec, hipStream_t st, const float* wc2,
+                      const float* bc2) {
   if (c1.f32 || c2.f32 || c1.W != 48 || c1.H % kTH || c1.Cin != 64 || c1.Cout != 64 || c2.Cin != 64 ||
       c2.Cout != 64 || c1.N != c2.N || c1.H != c2.H || c1.W != c2.W || c1.in_mode != IN_PLAIN)
     return SRMI_ERR_SHAPE;
-  if (!c1.yb || !c2.yb || !c2.part || !part || !hi_out || !lo_out || (!h_in && (!hi_in || !lo_in)) || CR < 4 ||
-      CR > 32 || CR % 4 || nstrips != (c1.H / kTH))
+  if (!c1.yb || !part || !hi_out || !lo_out || (!h_in && (!hi_in || !lo_in)) || CR < 4 || CR > 32 || CR % 4 ||
+      nstrips != (c1.H / kTH))
     return SRMI_ERR_ARG;
+  const bool v2 = SRMI_INFER_V == 2 && wc2 && bc2 && rec;
+  if (!v2 && (!c2.yb || !c2.part)) return SRMI_ERR_ARG;
   if ((size_t)c1.N * c1.H * c1.W * 64 * 2 >= ((size_t)1 << 32)) return SRMI_ERR_SHAPE;
   CaInfer ca{};
   ca.u = c2.yb;
@@ -192,6 +305,26 @@ int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* p
   ConvParams a = c1, b = c2;
   a.stamps = b.stamps = nullptr;
   const dim3 grid(c1.N);
+  if (v2) {
+    ca.wc2 = wc2;
+    ca.bc2 = bc2;
+    ca.t = c1.yb;
+    a.part = const_cast<float*>(part);  // conv1's per-strip sums of t
+    a.part_stride = 64;
+    b.yb = nullptr;  // u is never stored
+    b.part = nullptr;
+    b.yf = nullptr;
+    b.r1 = h_in;
+    b.r1h = h_in ? nullptr : static_cast<const bf16_t*>(hi_in);
+    b.r1l = h_in ? nullptr : static_cast<const uint8_t*>(lo_in);
+    b.yph = static_cast<bf16_t*>(hi_out);
+    b.ypl = static_cast<uint8_t*>(lo_out);
+    b.escale = rec + 64 + CR;  // s of the record m | z1 | s
+    b.escale_stride = 128 + CR;
+    hipLaunchKernelGGL(rcab_infer2_kernel, grid, dim3(512), Conv2Smem<48>::TOTAL, st, a, b, ca);
+    SRMI_CHECK_LAUNCH();
+    return 0;
+  }
   if (h_in)
     hipLaunchKernelGGL((rcab_infer_kernel<true>), grid, dim3(512), Conv2Smem<48>::TOTAL, st, a, b, ca);
   else

@@ -22,6 +22,10 @@ enum Epi {
   EPI_PLAIN_BF16 = 6,  // y = acc (+ b)                              -> bf16
   EPI_DG_ACC_CA = 7,   // g = acc + r1, sums of g and g*aux; r1/aux/part non-null, no yb/r2/r3
                        // (the hot RCAB case of EPI_DG_ACC, specialised: no runtime operand checks)
+  // the inference RCAB (rcab_infer.hip), 64-channel non-deferred body only:
+  EPI_RELU_POOL = 8,   // t = relu(acc + b) -> bf16, + per-strip channel sums of t
+  EPI_CA_RESID = 9,    // h' = h + s[c] (acc + b): h in as fp32 r1 or the pair r1h / r1l,
+                       // h' out as the pair yph / ypl, s = escale[n * escale_stride + c]
 };
 
 // The CA-backward fold of the bf16 RCAB backward (engine.cpp backward_impl).  du =
@@ -66,6 +70,13 @@ struct ConvParams {
   int f32;                     // exact-fp32 mode: x, w, yb, aux point at fp32 data
                                // (the bf16_t* fields are plain addresses then)
   CaFold fold;                 // zero-initialised: no fold
+  // EPI_CA_RESID: the residual stream as the pair (bf16 hi + lo8 remainder, common.hpp)
+  const bf16_t* r1h;
+  const uint8_t* r1l;
+  bf16_t* yph;
+  uint8_t* ypl;
+  const float* escale;         // per-image channel scale s [N][escale_stride]
+  int escale_stride;
 };
 
 void conv3x3_set_debug_stamps(unsigned long long* buf);
@@ -168,7 +179,8 @@ int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float
 // (POOL, yb = u, part), then the CA MLP and the residual pair update per image
 int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* part, int nstrips, const float* w1,
                       const float* b1, const float* w2, const float* b2, int CR, const float* h_in, const void* hi_in,
-                      const void* lo_in, void* hi_out, void* lo_out, float* rec, hipStream_t st);
+                      const void* lo_in, void* hi_out, void* lo_out, float* rec, hipStream_t st,
+                      const float* wc2 = nullptr, const float* bc2 = nullptr);  // v2: conv2's fp32 weight, bias
 // records of consecutive RCABs Ncap images apart (the engine capacity), N summed
 int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int Ncap, int C, int R,
                                   const long long* offs, float* grads, hipStream_t st);
