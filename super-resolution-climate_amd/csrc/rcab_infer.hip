@@ -18,7 +18,7 @@
 // in summation order and in conv2's bf16 weights (the mean uses the fp32 weights).
 // v1 (SRMI_INFER_V=1): bit-identical to the three training-path launches.
 #ifndef SRMI_INFER_V
-#define SRMI_INFER_V 1
+#define SRMI_INFER_V 2
 #endif
 #ifndef SRMI_INFER_WT
 #define SRMI_INFER_WT 1
