@@ -133,7 +133,9 @@ __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 // channel halves) share the row's LDS staging, so their writes and the full-line
 // stores that read them are separated by workgroup barriers and each wave stores
 // every other 1 KiB run.
-template <int NPT, int EPI, int NCT = 4>
+// FP: the CA-fold producer's du' store may be on (DG_ACC_CA: a template switch of the
+// fused launch, so the default kernel carries none of it; DG_ACC: a runtime check)
+template <int NPT, int EPI, int NCT = 4, bool FP = true>
 __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)[NPT][NCT],
                                                const EpiPre<NPT, EPI, NCT>& e, const float4 (&bias)[NCT], int n,
                                                int cb, int y, int x0, int strip, int nstrips, float* red, int fr,
@@ -237,7 +239,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       const auto rf = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
       [[maybe_unused]] const auto rbb = wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
       // CA-backward fold producer (EPI_DG_ACC_CA): du' = bf16(g * s) of the next RCAB
-      [[maybe_unused]] const bool fold_out = (EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC) && p.fold.du_out != nullptr;
+      [[maybe_unused]] const bool fold_out = FP && (EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC) && p.fold.du_out != nullptr;
       [[maybe_unused]] const auto rdu = wt_rsrc(p.fold.du_out, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
       [[maybe_unused]] const auto rph = wt_rsrc(p.yph, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
       [[maybe_unused]] const auto rpl = wt_rsrc(p.ypl, (uint32_t)((size_t)p.N * HW * p.Cout));
@@ -298,7 +300,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             ps1[0][3] += val.w * bf2f(uu.y >> 16);
           }
           st_wt16(rf, p.yf, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 4), val);
-          if constexpr (EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC) {
+          if constexpr (FP && (EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC)) {
             if (fold_out)  // the lane's channels 4c..4c+3 are the same in every run: s in fs
               st_wt8(rdu, p.fold.du_out, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 2),
                      make_uint2(pack2(val.x * fs.x, val.y * fs.y), pack2(val.z * fs.z, val.w * fs.w)));
@@ -450,8 +452,11 @@ template <int TW, int EPI, int NW = 4, bool FOLD = false, bool REV = false>
 __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, int bid, char* smem, int tail = 0,
                                             bool tail_part = false) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  static_assert(!FOLD || (EPI == EPI_DG_RELUMASK && NW == 8 && conv64_defers<EPI>()),
-                "the fold consumer is the deferred 8-wave ReLU-mask dgrad");
+  // FOLD: the CA-fold consumer (the deferred 8-wave ReLU-mask dgrad) or producer
+  // (the non-deferred DG_ACC_CA epilogue's du' store)
+  static_assert(!FOLD || (EPI == EPI_DG_RELUMASK && NW == 8 && conv64_defers<EPI>()) ||
+                    (EPI == EPI_DG_ACC_CA && !(NW == 8 && conv64_defers<EPI>())),
+                "fold: the deferred ReLU-mask dgrad (consumer) or the non-deferred DG_ACC_CA (producer)");
   static_assert(!REV || !(NW == 8 && conv64_defers<EPI>()), "reversed runs: the non-deferred body only");
   if constexpr (NW == 8 && conv64_defers<EPI>()) {
     conv64_body_defer<TW, EPI, FOLD>(p, run_len, bid, smem, tail, tail_part);
@@ -559,7 +564,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   float4 fs = float4{0.f, 0.f, 0.f, 0.f};
   if constexpr (EPI == EPI_CA_RESID)
     fs = *reinterpret_cast<const float4*>(p.escale + (size_t)n * p.escale_stride + 4 * (lane & 15));
-  if constexpr (EPI == EPI_DG_ACC_CA || (EPI == EPI_DG_ACC && epi_run<EPI>())) {
+  if constexpr ((EPI == EPI_DG_ACC_CA && FOLD) || (EPI == EPI_DG_ACC && epi_run<EPI>())) {
     if (p.fold.du_out)
       fs = *reinterpret_cast<const float4*>(p.fold.s_rec + (size_t)n * (128 + p.fold.CR) + 64 + p.fold.CR +
                                             4 * (lane & 15));
@@ -655,7 +660,8 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    conv_epilogue2<NPT, EPI, NCT>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx, nsy * nsx, red, fr, fk, row, ct0,
+    conv_epilogue2<NPT, EPI, NCT, (EPI != EPI_DG_ACC_CA || FOLD)>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx,
+                                                               nsy * nsx, red, fr, fk, row, ct0,
                                   tid, ring + ((REV ? k + 1 : k) % 3) * S::GROUPB + row * TW * 128, fs);
     STAMP(sj + 3);
     // LDS-only barrier: this strip's global stores stay in flight into the next strip

@@ -758,19 +758,26 @@ __global__ void __launch_bounds__(NW * 64, 1) rcab_bwd_kernel(ConvParams cp, int
     if (c1 > c0) conv = c0;
     else w = b - c0;
   }
+  // FOLD: in F2 (DG_RELUMASK) the fold consumer -- its dgrad, its filter gradient and the
+  // previous RCAB's slab reductions; in F1 (DG_ACC_CA) the producer's du' store only
+  constexpr bool kF2 = EPI == EPI_DG_RELUMASK;
+  constexpr bool kFoldConv = kF2 ? (FOLD && (SRMI_FOLD_PARTS & 1)) : FOLD;
+  constexpr bool kFoldWg = kF2 && FOLD && (SRMI_FOLD_PARTS & 2);
   if (conv >= 0) {
-    if (!(SRMI_FUSE_DIAG & 2)) conv64_body<48, EPI, NW, FOLD && (SRMI_FOLD_PARTS & 1)>(cp, run_len, conv, smem, tail, false);
+    if (!(SRMI_FUSE_DIAG & 2)) conv64_body<48, EPI, NW, kFoldConv>(cp, run_len, conv, smem, tail, false);
     return;
   }
   const int nch = wp.N * wp.row_splits;
-  if (!(SRMI_FUSE_DIAG & 1)) wgrad48_dispatch<NW, FOLD && (SRMI_FOLD_PARTS & 2)>(wp, smem, w % nch, w / nch);
-  if (wp.nred > 0) {  // the previous RCAB's slab reductions, shared over this launch's filter-gradient workgroups
-    static_assert(NW * 64 == 512, "slab_reduce_share runs on 512 threads");
-    slab_reduce_share(wp.red[0], wp.red[1], wp.nred, w, nwg, reinterpret_cast<float4*>(smem));
+  if (!(SRMI_FUSE_DIAG & 1)) wgrad48_dispatch<NW, kFoldWg>(wp, smem, w % nch, w / nch);
+  if constexpr (kF2 && FOLD) {
+    if (wp.nred > 0) {  // the previous RCAB's slab reductions, shared over this launch's filter-gradient workgroups
+      static_assert(NW * 64 == 512, "slab_reduce_share runs on 512 threads");
+      slab_reduce_share(wp.red[0], wp.red[1], wp.nred, w, nwg, reinterpret_cast<float4*>(smem));
+    }
   }
   if (tail > 0 && !(SRMI_FUSE_DIAG & 2)) {
     __syncthreads();  // every wave is past its last LDS read of the chunk
-    conv64_body<48, EPI, NW, FOLD>(cp, run_len, w, smem, tail, true);
+    conv64_body<48, EPI, NW, kFoldConv>(cp, run_len, w, smem, tail, true);
   }
 }
 
@@ -804,7 +811,7 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
     return SRMI_ERR_ARG;
   if (epi == EPI_DG_ACC_CA && cp.fold.du_out && (!cp.fold.s_rec || cp.fold.CR < 4 || cp.fold.CR > 32))
     return SRMI_ERR_ARG;
-  if (wp.nred < 0 || wp.nred > 2) return SRMI_ERR_ARG;
+  if (wp.nred < 0 || wp.nred > 2 || (wp.nred > 0 && (!fold || epi != EPI_DG_RELUMASK))) return SRMI_ERR_ARG;
   for (int k = 0; k < wp.nred; ++k)
     if (!wp.red[k].slab || !wp.red[k].gw || wp.red[k].Cout != 64 || wp.red[k].layout != 1 || wp.red[k].ps ||
         wp.red[k].nslab < 1 || (wp.red[k].gb && !wp.red[k].bslab))
@@ -843,7 +850,12 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
       break;
     case EPI_DG_ACC_CA:
       if (!c.r1 || !c.aux || !c.part || c.yb || c.r2 || c.r3 || !c.yf) return SRMI_ERR_ARG;
-      hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len, nconv, w, nwg, paired, tail);
+      if (c.fold.du_out)  // the fold producer (du' beside g)
+        hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA, kFuseNW, true>), grid, dim3(kFuseNW * 64), lds, st, c,
+                           run_len, nconv, w, nwg, paired, tail);
+      else
+        hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len,
+                           nconv, w, nwg, paired, tail);
       break;
     case EPI_DG_ACC:
       if (!c.yf || (c.part && !c.aux)) return SRMI_ERR_ARG;
