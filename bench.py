@@ -112,7 +112,8 @@ def _pmc_region_bytes():
             continue
         total = sum(v["hbm_bytes_per_launch"] * v["dispatches"][0] for k, v in kern.items()
                     if "pack_tile" not in k)  # (the filter packs: once per model, not per region)
-        rcab = {k: v["hbm_bytes_per_launch"] for k, v in kern.items() if "rcab_infer_kernel<false>" in k}
+        rcab = {k: v["hbm_bytes_per_launch"] for k, v in kern.items()
+                if "rcab_infer2_kernel" in k or "rcab_infer_kernel<false>" in k}
         return {"bytes": total / regions[0], "source": os.path.relpath(f, ROOT),
                 "rcab_launch_bytes": next(iter(rcab.values()), None)}
     return None
