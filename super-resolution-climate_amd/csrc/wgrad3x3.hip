@@ -850,10 +850,13 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
       break;
     case EPI_DG_ACC_CA:
       if (!c.r1 || !c.aux || !c.part || c.yb || c.r2 || c.r3 || !c.yf) return SRMI_ERR_ARG;
-      if (c.fold.du_out)  // the fold producer (du' beside g)
-        hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA, kFuseNW, true>), grid, dim3(kFuseNW * 64), lds, st, c,
-                           run_len, nconv, w, nwg, paired, tail);
-      else
+      if (c.fold.du_out) {  // the fold producer (du' beside g): the non-deferred epilogue only
+        if constexpr (!(kFuseNW == 8 && conv64_defers<EPI_DG_ACC_CA>()))
+          hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA, kFuseNW, true>), grid, dim3(kFuseNW * 64), lds, st, c,
+                             run_len, nconv, w, nwg, paired, tail);
+        else
+          return SRMI_ERR_ARG;
+      } else
         hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len,
                            nconv, w, nwg, paired, tail);
       break;
