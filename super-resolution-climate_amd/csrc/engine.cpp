@@ -397,6 +397,10 @@ static void build_tables(srmi_engine* e) {
 static inline hipStream_t S_(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // --------------------------------------------------------------- conv helpers
+// forward convs sized for this share of the engine's CU budget (A/B: fewer, longer runs)
+#ifndef SRMI_FWD_CUS_PCT
+#define SRMI_FWD_CUS_PCT 100
+#endif
 static ConvParams fwd_params(srmi_engine* e, const ConvRef& c, const bf16_t* x, int n, int H, int W, bf16_t* yb,
                              float* yf, const float* r1, float* part, float alpha) {
   ConvParams p{};
@@ -417,7 +421,7 @@ static ConvParams fwd_params(srmi_engine* e, const ConvRef& c, const bf16_t* x, 
   p.part_stride = 64;
   p.alpha = alpha;
   p.zeros = e->zeros;
-  p.cu_budget = e->cu_budget;
+  p.cu_budget = e->cu_budget > 0 ? e->cu_budget * SRMI_FWD_CUS_PCT / 100 : e->cu_budget;
   return p;
 }
 
