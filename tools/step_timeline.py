@@ -25,13 +25,11 @@ def main(path, nsteps=2):
     if len(adam) < 2:
         print("fewer than 2 adam launches")
         return
-    # training steps of the headline config only (RCAN: the step holds ca_fwd
-    # launches; later benches in the same trace -- EDSR -- do not)
     # training steps of the headline RCAN config only: other phases of a bench
     # trace (roofline leg, tiled inference, the EDSR line) end in an Adam too
     def is_train(seg):
         names = [e[2] for e in seg]
-        return (any("ca_fwd_kernel" in n for n in names) and not any("region_to_tiles" in n for n in names)
+        return (sum("rcab_bwd_kernel" in n for n in names) >= 100 and not any("region_to_tiles" in n for n in names)
                 and not any("<32," in n for n in names))
     ks = [k for k in range(1, len(adam)) if is_train(ev[adam[k - 1] + 1:adam[k] + 1])]
     for k in ks[-nsteps:]:
