@@ -1068,8 +1068,11 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
   for (int k = 0; k < NU; ++k) {  // clamped, unconditional (tail lanes store nothing)
     const size_t e = base + min(q0 + (size_t)k * blockDim.x, nq - 1) * 4;
     uu[k] = Unit4<T>::ld(u + e);
-    if constexpr (MODE == CA_LO) {
-      hh[k] = pair_decode4(*reinterpret_cast<const uint2*>(hi_in + e), *reinterpret_cast<const uint32_t*>(lo_in + e));
+    if constexpr (MODE == CA_LO) {  // the pair's raw bits: decoded after the MLP, so that these loads stay
+                                    // in flight under it (a decode here waits for them first)
+      const uint2 hb = *reinterpret_cast<const uint2*>(hi_in + e);
+      const uint32_t lb = *reinterpret_cast<const uint32_t*>(lo_in + e);
+      hh[k] = make_float4(__uint_as_float(hb.x), __uint_as_float(hb.y), __uint_as_float(lb), 0.f);
     } else {
       hh[k] = *reinterpret_cast<const float4*>(h_in + e);
     }
@@ -1119,6 +1122,8 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
     if (q >= nq) continue;
     const size_t e = base + q * 4;
     const int c0 = (int)((q * 4) % C);
+    if constexpr (MODE == CA_LO)
+      hh[k] = pair_decode4(make_uint2(__float_as_uint(hh[k].x), __float_as_uint(hh[k].y)), __float_as_uint(hh[k].z));
     float o[4];
     o[0] = Unit4<T>::get(uu[k], 0) * s[c0 + 0] + hh[k].x;
     o[1] = Unit4<T>::get(uu[k], 1) * s[c0 + 1] + hh[k].y;
