@@ -50,8 +50,12 @@ __device__ __forceinline__ void ca_mlp(const CA& c, int n, float* m, float* z1, 
 
 // v2 phase S for image n (512 threads, sm >= 1600 floats): mean(u) from t's statistics
 // (the header), then the MLP; s lands in the record, where conv2's epilogue reads it
+// wl: conv2's forward filter image in LDS ([9 taps][64 out rows][64 in] bf16, swz128
+// chunks, as conv64_body loads it) for the matvec -- the weights conv2 itself uses --
+// or null for the fp32 weights c.wc2 from global memory
 template <class CA>
-__device__ __forceinline__ void ca_scale_from_t(const CA& c, const bf16_t* t, int n, int H, int W, float* sm) {
+__device__ __forceinline__ void ca_scale_from_t(const CA& c, const bf16_t* t, int n, int H, int W, float* sm,
+                                                const char* wl = nullptr) {
   constexpr int C = 64;
   const int tid = threadIdx.x, HW = H * W;
   float* red = sm;          // [4][64] strip-phase partials of T
@@ -113,15 +117,30 @@ __device__ __forceinline__ void ca_scale_from_t(const CA& c, const bf16_t* t, in
     if (dy != 0 && dx != 0) v += cn[((dy == -1) ? 2 : 0) * 64 + ((dx == -1) ? 1 : 0) * 64 + ci];
     St[i] = v;
   }
+  if (wl) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the caller's filter-image DMA (not compiler-tracked)
   __syncthreads();
   {  // m[c] = b2[c] + (1/HW) sum_{ci, tap} W2[c][ci][tap] S_tap[ci]: 8 lanes per c, 8 ci each
     const int co = tid >> 3, pc = tid & 7;
-    const float* wr = c.wc2 + ((size_t)co * C + pc * 8) * 9;  // 72 contiguous floats
     float a = 0.f;
+    if (wl) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
+      for (int tap = 0; tap < 9; ++tap) {
+        const uint4 q = *reinterpret_cast<const uint4*>(wl + tap * 8192 + swz128(co, pc));
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+        const float* sv = St + tap * 64 + pc * 8;
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) a += wr[k * 9 + tap] * St[tap * 64 + pc * 8 + k];
+        for (int e = 0; e < 4; ++e) {
+          a += bf2f(w[e] & 0xFFFFu) * sv[2 * e];
+          a += bf2f(w[e] >> 16) * sv[2 * e + 1];
+        }
+      }
+    } else {
+      const float* wr = c.wc2 + ((size_t)co * C + pc * 8) * 9;  // 72 contiguous floats
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) a += wr[k * 9 + tap] * St[tap * 64 + pc * 8 + k];
+    }
     a += __shfl_xor(a, 1, 64);
     a += __shfl_xor(a, 2, 64);
     a += __shfl_xor(a, 4, 64);

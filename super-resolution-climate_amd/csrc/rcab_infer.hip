@@ -20,6 +20,10 @@
 #ifndef SRMI_INFER_V
 #define SRMI_INFER_V 2
 #endif
+// v2: the mean's matvec from conv2's bf16 filter image in LDS (1) or the fp32 weights (0)
+#ifndef SRMI_INFER_WLDS
+#define SRMI_INFER_WLDS 1
+#endif
 #ifndef SRMI_INFER_WT
 #define SRMI_INFER_WT 1
 #endif
@@ -31,7 +35,7 @@
 #ifndef SRMI_INFER_DEFER
 #define SRMI_INFER_DEFER 7
 #endif
-// diagnostic builds only (wrong results): 1 skips the CA pass, 2 conv2, 4 conv1
+// diagnostic builds only (wrong results): 1 skips the CA pass (v2: the scale), 2 conv2, 4 conv1
 #ifndef SRMI_INFER_DIAG
 #define SRMI_INFER_DIAG 0
 #endif
@@ -150,11 +154,27 @@ __global__ void __launch_bounds__(512, 1) rcab_infer2_kernel(ConvParams c1, Conv
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = blockIdx.x;
   const int nsy = c1.H / kTH;
-  conv64_body<48, EPI_RELU_POOL, 8>(c1, nsy, n, smem);  // t and its per-strip channel sums
+  if (!(SRMI_INFER_DIAG & 4)) conv64_body<48, EPI_RELU_POOL, 8>(c1, nsy, n, smem);  // t and its per-strip sums
   own_stores_visible();
-  ca_scale_from_t(ca, c1.yb, n, c1.H, c1.W, reinterpret_cast<float*>(smem));  // s into the record
+  if (!(SRMI_INFER_DIAG & 1)) {
+#if SRMI_INFER_WLDS
+    // conv2's filter image into the filter slot (conv1 is done with it): the mean's
+    // matvec reads it there, with the weights conv2 computes with; scratch in the ring
+    {
+      const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      const uint32_t wbase = lds_u32(smem);
+      for (int i = wv; i < 72; i += 8) {
+        const int tap = i >> 3, row = 8 * (i & 7) + (lane >> 3), ch = (lane & 7) ^ (row & 7);
+        glds16(c2.w + ((size_t)(tap * 64 + row)) * 64 + ch * 8, wbase + (uint32_t)i * 1024u);
+      }
+    }
+    ca_scale_from_t(ca, c1.yb, n, c1.H, c1.W, reinterpret_cast<float*>(smem + Conv2Smem<48>::WB), smem);
+#else
+    ca_scale_from_t(ca, c1.yb, n, c1.H, c1.W, reinterpret_cast<float*>(smem));  // s
+#endif
+  }
   own_stores_visible();
-  conv64_body<48, EPI_CA_RESID, 8>(c2, nsy, n, smem);  // h' = h + s (conv2(t) + b2)
+  if (!(SRMI_INFER_DIAG & 2)) conv64_body<48, EPI_CA_RESID, 8>(c2, nsy, n, smem);  // h' = h + s (conv2(t) + b2)
 }
 
 int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* part, int nstrips, const float* w1,
