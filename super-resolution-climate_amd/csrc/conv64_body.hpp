@@ -448,7 +448,8 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
 // REV: the run's strips last to first (the one-launch inference RCAB runs conv2 that
 // way, so that its first strips read the ReLU output rows conv1 wrote last, still in
 // L2); same arithmetic per strip, so the same results.
-template <int TW, int EPI, int NW = 4, bool FOLD = false, bool REV = false>
+// WRES: the filter image is already resident in LDS (the caller loaded it): no filter DMA
+template <int TW, int EPI, int NW = 4, bool FOLD = false, bool REV = false, bool WRES = false>
 __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, int bid, char* smem, int tail = 0,
                                             bool tail_part = false) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
@@ -545,9 +546,11 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   // while the first strip's MFMA phase grew by 500.)
   {
     const uint32_t wbase = lds_u32(wl);
-    for (int i = wv_s; i < 72; i += NW) {
-      const int tap = i >> 3, row = 8 * (i & 7) + (lane >> 3), c = (lane & 7) ^ (row & 7);
-      glds16(p.w + ((size_t)(tap * p.Cout + cb * 64 + row)) * 64 + c * 8, wbase + (uint32_t)i * 1024u);
+    if constexpr (!WRES) {
+      for (int i = wv_s; i < 72; i += NW) {
+        const int tap = i >> 3, row = 8 * (i & 7) + (lane >> 3), c = (lane & 7) ^ (row & 7);
+        glds16(p.w + ((size_t)(tap * p.Cout + cb * 64 + row)) * 64 + c * 8, wbase + (uint32_t)i * 1024u);
+      }
     }
     group_dma(REV ? k1 - 1 : k0);  // strip k reads input groups k and k + 1
     group_dma(REV ? k1 : k0 + 1);

@@ -174,7 +174,9 @@ __global__ void __launch_bounds__(512, 1) rcab_infer2_kernel(ConvParams c1, Conv
 #endif
   }
   own_stores_visible();
-  if (!(SRMI_INFER_DIAG & 2)) conv64_body<48, EPI_CA_RESID, 8>(c2, nsy, n, smem);  // h' = h + s (conv2(t) + b2)
+  // h' = h + s (conv2(t) + b2); with WLDS its filter image is resident from the scale phase
+  if (!(SRMI_INFER_DIAG & 2))
+    conv64_body<48, EPI_CA_RESID, 8, false, false, SRMI_INFER_WLDS && !(SRMI_INFER_DIAG & 1)>(c2, nsy, n, smem);
 }
 
 int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* part, int nstrips, const float* w1,
