@@ -445,11 +445,8 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
 // FOLD (EPI_DG_RELUMASK, deferred form only): the consumer side of the CA-backward
 // fold (srmi_internal.hpp CaFold, ca_fold.hpp); the producer side (EPI_DG_ACC_CA) is
 // the runtime p.fold.du_out.
-// REV: the run's strips last to first (the one-launch inference RCAB runs conv2 that
-// way, so that its first strips read the ReLU output rows conv1 wrote last, still in
-// L2); same arithmetic per strip, so the same results.
 // WRES: the filter image is already resident in LDS (the caller loaded it): no filter DMA
-template <int TW, int EPI, int NW = 4, bool FOLD = false, bool REV = false, bool WRES = false>
+template <int TW, int EPI, int NW = 4, bool FOLD = false, bool WRES = false>
 __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, int bid, char* smem, int tail = 0,
                                             bool tail_part = false) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
@@ -458,7 +455,6 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   static_assert(!FOLD || (EPI == EPI_DG_RELUMASK && NW == 8 && conv64_defers<EPI>()) ||
                     (EPI == EPI_DG_ACC_CA && !(NW == 8 && conv64_defers<EPI>())),
                 "fold: the deferred ReLU-mask dgrad (consumer) or the non-deferred DG_ACC_CA (producer)");
-  static_assert(!REV || !(NW == 8 && conv64_defers<EPI>()), "reversed runs: the non-deferred body only");
   if constexpr (NW == 8 && conv64_defers<EPI>()) {
     conv64_body_defer<TW, EPI, FOLD>(p, run_len, bid, smem, tail, tail_part);
     return;
@@ -552,8 +548,8 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
         glds16(p.w + ((size_t)(tap * p.Cout + cb * 64 + row)) * 64 + c * 8, wbase + (uint32_t)i * 1024u);
       }
     }
-    group_dma(REV ? k1 - 1 : k0);  // strip k reads input groups k and k + 1
-    group_dma(REV ? k1 : k0 + 1);
+    group_dma(k0);  // strip k reads input groups k and k + 1
+    group_dma(k0 + 1);
     wait_vm<0>();
   }
   STAMP(1);
@@ -575,16 +571,13 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   __syncthreads();
 
 #pragma unroll 1
-  for (int i = 0; i < k1 - k0; ++i) {
-    const int k = REV ? k1 - 1 - i : k0 + i;
+  for (int k = k0; k < k1; ++k) {
     const int y = 4 * k + row;
-    const bool pf = (i + 1 < k1 - k0);
+    const bool pf = (k + 1 < k1);
     // group k+2 -> ring slot (k+2)%3, which held group k-1 (last read by strip k-1,
-    // released by the barrier that ended it); REV: group k-1 -> slot (k-1)%3, which
-    // held group k+2 (strip k+1's)
-    const int gpf = REV ? k - 1 : k + 2;
+    // released by the barrier that ended it)
     EpiPre<NPT, EPI, NCT> ep;
-    [[maybe_unused]] const int sj = 2 + 5 * min(i, 11);
+    [[maybe_unused]] const int sj = 2 + 5 * min(k - k0, 11);
     STAMP(sj);
 
     // B-fragment byte offsets per (ky, kx, kk); +2048 per 16-pixel tile
@@ -622,7 +615,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     for (int s = 0; s < 18; ++s) {
       // group k+2's DMA pieces and the epilogue operands are issued one or two per
       // K-step, so a full memory queue stalls the wave between MFMA groups only
-      if (s < NGW && pf && wv_s + NW * s < NGRP) group_dma_one(gpf, s);
+      if (s < NGW && pf && wv_s + NW * s < NGRP) group_dma_one(k + 2, s);
       // the epilogue operands, two per K-step from the first one: a whole strip of
       // MFMAs to land (spread over K-steps 2..13, the heavy fp32 epilogue of
       // DG_ACC_CA waited on its last ones at the end of the K-loop: +1.3 % step)
@@ -658,14 +651,13 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     STAMP(sj + 2);
     // every wave is past its last read of input group k: its ring slot stages the
     // strip's bf16 output rows (slot k%3 is next written by group k+3's DMA,
-    // issued after the barrier that ends this strip; REV: group k+1's slot, next
-    // written by group k-2's DMA)
+    // issued after the barrier that ends this strip)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     conv_epilogue2<NPT, EPI, NCT, (EPI != EPI_DG_ACC_CA || FOLD)>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx,
                                                                nsy * nsx, red, fr, fk, row, ct0,
-                                  tid, ring + ((REV ? k + 1 : k) % 3) * S::GROUPB + row * TW * 128, fs);
+                                  tid, ring + (k % 3) * S::GROUPB + row * TW * 128, fs);
     STAMP(sj + 3);
     // LDS-only barrier: this strip's global stores stay in flight into the next strip
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

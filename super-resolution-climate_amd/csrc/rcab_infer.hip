@@ -27,9 +27,6 @@
 #ifndef SRMI_INFER_WT
 #define SRMI_INFER_WT 1
 #endif
-#ifndef SRMI_INFER_REV
-#define SRMI_INFER_REV 1
-#endif
 // deferred conv epilogues (conv64_body.hpp SRMI_DEFER) for this launch's convs: an
 // image is one run of 12 strips here, not 3 as in training
 #ifndef SRMI_INFER_DEFER
@@ -144,8 +141,7 @@ __global__ void __launch_bounds__(512, 1) rcab_infer_kernel(ConvParams c1, ConvP
   const int nsy = c1.H / kTH;
   if (!(SRMI_INFER_DIAG & 4)) conv64_body<48, EPI_RELU_BF16, 8>(c1, nsy, n, smem);  // the whole image: one run
   own_stores_visible();
-  constexpr bool kRev = SRMI_INFER_REV && !(SRMI_INFER_DEFER & 2);  // (reversal: the non-deferred body)
-  if (!(SRMI_INFER_DIAG & 2)) conv64_body<48, EPI_POOL_BF16, 8, false, kRev>(c2, nsy, n, smem);
+  if (!(SRMI_INFER_DIAG & 2)) conv64_body<48, EPI_POOL_BF16, 8>(c2, nsy, n, smem);
   own_stores_visible();
   if (!(SRMI_INFER_DIAG & 1)) ca_image_body<F32IN>(ca, n, c1.H * c1.W, reinterpret_cast<float*>(smem));
 }
@@ -176,7 +172,7 @@ __global__ void __launch_bounds__(512, 1) rcab_infer2_kernel(ConvParams c1, Conv
   own_stores_visible();
   // h' = h + s (conv2(t) + b2); with WLDS its filter image is resident from the scale phase
   if (!(SRMI_INFER_DIAG & 2))
-    conv64_body<48, EPI_CA_RESID, 8, false, false, SRMI_INFER_WLDS && !(SRMI_INFER_DIAG & 1)>(c2, nsy, n, smem);
+    conv64_body<48, EPI_CA_RESID, 8, false, SRMI_INFER_WLDS && !(SRMI_INFER_DIAG & 1)>(c2, nsy, n, smem);
 }
 
 int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* part, int nstrips, const float* w1,
