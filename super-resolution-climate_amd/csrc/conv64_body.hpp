@@ -5,6 +5,19 @@
 #include <type_traits>
 
 #include "ca_fold.hpp"
+
+// the pair codec of the inference RCAB's CA_RESID epilogue (common.hpp: the fast form
+// by default; SRMI_PAIR_FAST=0 for the reference form, bit-identical to ca_fwd's)
+#ifndef SRMI_PAIR_FAST
+#define SRMI_PAIR_FAST 1
+#endif
+#if SRMI_PAIR_FAST
+#define PAIR_DEC4 pair_decode4_fast
+#define PAIR_ENC4 pair_encode4_fast
+#else
+#define PAIR_DEC4 pair_decode4
+#define PAIR_ENC4 pair_encode4
+#endif
 #include "common.hpp"
 #include "srmi_internal.hpp"
 
@@ -267,12 +280,12 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             const int q = h * (kShared ? RUNS / 2 : RUNS) + j;
             float4 hh = e.r1[q / NCT][q % NCT];
             if (p.r1h)
-              hh = pair_decode4(make_uint2(__float_as_uint(hh.x), __float_as_uint(hh.y)), __float_as_uint(hh.z));
+              hh = PAIR_DEC4(make_uint2(__float_as_uint(hh.x), __float_as_uint(hh.y)), __float_as_uint(hh.z));
             const float o0 = fmaf(val.x, fs.x, hh.x), o1 = fmaf(val.y, fs.y, hh.y);
             const float o2 = fmaf(val.z, fs.z, hh.z), o3 = fmaf(val.w, fs.w, hh.w);
             const uint32_t oe = (uint32_t)((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4);  // element
             uint2 hi;
-            const uint32_t lo = pair_encode4(o0, o1, o2, o3, hi);
+            const uint32_t lo = PAIR_ENC4(o0, o1, o2, o3, hi);
             st_wt8(rph, p.yph, oe * 2, hi);
             st_wt4(rpl, p.ypl, oe, lo);
             continue;
@@ -931,7 +944,7 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
       if (p.r1h) {
         const uint4 th = ops.t[pt];
         const uint2 tl = ops.u[pt][0];
-        const float4 a = pair_decode4(make_uint2(th.x, th.y), tl.x), b = pair_decode4(make_uint2(th.z, th.w), tl.y);
+        const float4 a = PAIR_DEC4(make_uint2(th.x, th.y), tl.x), b = PAIR_DEC4(make_uint2(th.z, th.w), tl.y);
         hv[0] = a.x; hv[1] = a.y; hv[2] = a.z; hv[3] = a.w; hv[4] = b.x; hv[5] = b.y; hv[6] = b.z; hv[7] = b.w;
       } else {
         const float4 a = ops.g[pt][0], b = ops.g[pt][1];
@@ -946,8 +959,8 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
         for (int rr = 0; rr < 4; ++rr) o[4 * c + rr] = fmaf(v[rr] + b[rr], sv[4 * c + rr], hv[4 * c + rr]);
       }
       uint2 h0, h1;
-      const uint32_t l0 = pair_encode4(o[0], o[1], o[2], o[3], h0);
-      const uint32_t l1 = pair_encode4(o[4], o[5], o[6], o[7], h1);
+      const uint32_t l0 = PAIR_ENC4(o[0], o[1], o[2], o[3], h0);
+      const uint32_t l1 = PAIR_ENC4(o[4], o[5], o[6], o[7], h1);
       const uint32_t oe = (uint32_t)(pix * p.Cout + cb * 64 + chan(0, 0));
       st_wt16(rph, p.yph, oe * 2, make_uint4(h0.x, h0.y, h1.x, h1.y));
       st_wt8(rpl, p.ypl, oe, make_uint2(l0, l1));
