@@ -28,9 +28,11 @@
 #define SRMI_INFER_WT 1
 #endif
 // deferred conv epilogues (conv64_body.hpp SRMI_DEFER) for this launch's convs: an
-// image is one run of 12 strips here, not 3 as in training
+// image is one run of 12 strips here, not 3 as in training.  23 = v1's RELU / POOL
+// (1, 2) and v2's RELU_POOL (16); v2's CA_RESID epilogue (32) measured 5 % slower
+// deferred (its pair codec then competes with the next strip's MFMA issue)
 #ifndef SRMI_INFER_DEFER
-#define SRMI_INFER_DEFER 7
+#define SRMI_INFER_DEFER 23
 #endif
 // diagnostic builds only (wrong results): 1 skips the CA pass (v2: the scale), 2 conv2, 4 conv1
 #ifndef SRMI_INFER_DIAG
