@@ -1023,6 +1023,17 @@ constexpr int kCaVec = SRMI_CA_VEC;
 // while the pass moves 8 B per element (u 2 + hi 2 + lo 1 in, hi 2 + lo 1 out)
 // instead of 12 with an fp32 stream (10 with a bf16 lo).
 enum CaMode { CA_F32 = 0, CA_F32LO = 1, CA_LO = 2 };
+// the training pass's codec: the reference form (1: the fast form of common.hpp)
+#ifndef SRMI_CA_PAIR_FAST
+#define SRMI_CA_PAIR_FAST 0
+#endif
+#if SRMI_CA_PAIR_FAST
+#define CA_DEC4 pair_decode4_fast
+#define CA_ENC4 pair_encode4_fast
+#else
+#define CA_DEC4 pair_decode4
+#define CA_ENC4 pair_encode4
+#endif
 
 // (lo8_encode / lo8_decode, the pair codec: common.hpp)
 template <typename T, int MODE>
@@ -1123,7 +1134,7 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
     const size_t e = base + q * 4;
     const int c0 = (int)((q * 4) % C);
     if constexpr (MODE == CA_LO)
-      hh[k] = pair_decode4(make_uint2(__float_as_uint(hh[k].x), __float_as_uint(hh[k].y)), __float_as_uint(hh[k].z));
+      hh[k] = CA_DEC4(make_uint2(__float_as_uint(hh[k].x), __float_as_uint(hh[k].y)), __float_as_uint(hh[k].z));
     float o[4];
     o[0] = Unit4<T>::get(uu[k], 0) * s[c0 + 0] + hh[k].x;
     o[1] = Unit4<T>::get(uu[k], 1) * s[c0 + 1] + hh[k].y;
@@ -1134,7 +1145,7 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
       Unit4<T>::st(rhb, hb_out, e, o);
     } else {
       uint2 hi;
-      const uint32_t lo = pair_encode4(o[0], o[1], o[2], o[3], hi);
+      const uint32_t lo = CA_ENC4(o[0], o[1], o[2], o[3], hi);
       st_wt8(rhb, hb_out, (uint32_t)(e * 2), hi);
       st_wt4(rlo, lo_out, (uint32_t)e, lo);
     }
