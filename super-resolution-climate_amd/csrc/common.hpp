@@ -74,8 +74,10 @@ __device__ __forceinline__ uint32_t pair_encode4(float a, float b, float c, floa
 // In a conv epilogue the codec, not the memory traffic, bounds the pass.
 __device__ __forceinline__ uint32_t lo8_encode_fast(float h, float hi) {
   const int e = (int)((__float_as_uint(hi) >> 23) & 0xFFu);
-  const float q = fminf(fmaxf(rintf(__builtin_ldexpf(h - hi, 142 - e)), -127.f), 127.f);
-  return (uint32_t)(int)q & 0xFFu;
+  const float x = fminf(fmaxf(__builtin_ldexpf(h - hi, 142 - e), -127.f), 127.f);
+  // + 1.5 * 2^23 rounds x to the nearest integer (ties to even, as rintf) into the low
+  // mantissa bits: their low byte is that integer's two's-complement byte
+  return __float_as_uint(x + 12582912.0f) & 0xFFu;
 }
 __device__ __forceinline__ float lo8_decode_fast(float hi, uint32_t byte) {
   const int e = (int)((__float_as_uint(hi) >> 23) & 0xFFu);
