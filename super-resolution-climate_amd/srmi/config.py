@@ -193,12 +193,25 @@ def init_parms(model: str, custom: Dict[str, Any], model_cfg: Optional[Any] = No
     return parms
 
 
+def data_downsample_factor(task) -> int:
+    """apply_network's pre-downsampling of the HR batch (dual_trainer.py:561-563):
+    ``downsample(input, scale_factor=ds)`` -- F.interpolate(1/ds, bicubic), array.py:72-76
+    -- only when ds > 1.0; any value <= 1 is a no-op there and here (returns 1).  The
+    engine's bicubic kernel is the half-way 4-tap form, exact for EVEN integer factors;
+    other factors raise NotImplementedError."""
+    ds = float(task.get("data_downsample", 1.0) or 1.0) if task is not None else 1.0
+    if ds <= 1.0:
+        return 1
+    if ds != int(ds) or int(ds) % 2:
+        raise NotImplementedError(f"task.data_downsample={ds}: even integer factors only")
+    return int(ds)
+
+
 def check_fused_task(task, nchannels_in: int, nchannels_out: int) -> Optional[List[int]]:
     """What the fused trainer takes from apply_network (dual_trainer.py:557-571).
 
-    * ``task.data_downsample``: the reference downsamples the HR batch first only when
-      it is > 1.0 (:561-563); that changes the engine's tile geometry, so > 1 raises
-      NotImplementedError; any value <= 1 is a no-op there and here.
+    * ``task.data_downsample`` (:561-563): ``data_downsample_factor`` (validated here
+      too; the trainer downsamples the HR batch by it first).
     * The target channels: when the batch has MORE channels than
       ``task.target_variables`` the reference index_selects them (:564-568) with
       ``np.in1d(channels, target_variables).nonzero()`` -- the input's own order.
@@ -207,9 +220,7 @@ def check_fused_task(task, nchannels_in: int, nchannels_out: int) -> Optional[Li
       the order, are a no-op in the reference).  Without variable names the counts
       alone decide: fewer output channels than inputs cannot be resolved, and raise.
     """
-    ds = float(task.get("data_downsample", 1.0) or 1.0) if task is not None else 1.0
-    if ds > 1.0:
-        raise NotImplementedError(f"task.data_downsample={ds}: the fused trainer implements data_downsample <= 1 only")
+    data_downsample_factor(task)
     names_in = list(task["input_variables"]) if task is not None and "input_variables" in task else None
     names_out = list(task["target_variables"]) if task is not None and "target_variables" in task else None
     if names_in is None or names_out is None:

@@ -63,7 +63,7 @@ class TiledInference:
     def __init__(self, spec: NetSpec, params: torch.Tensor, region_chw: Tuple[int, int, int],
                  tile_hr: Tuple[int, int] = (192, 192), device: Optional[torch.device] = None, graph: bool = True,
                  micro: Optional[int] = None, batch_size: int = 36, loss_fn: str = "l2",
-                 info: Optional[DistInfo] = None):
+                 info: Optional[DistInfo] = None, task=None):
         """batch_size: task.batch_size (the tiles scored per batch; 36 in every
         reference task yaml); loss_fn: model.loss_fn.
 
@@ -77,6 +77,13 @@ class TiledInference:
         sums in the one-rank order (srmi_batch_loss_means).  No graph in this mode."""
         if loss_fn not in LOSS_KINDS:
             raise ValueError(f"Unknown single-product loss function {loss_fn}")
+        if task is None:  # the active srmi ConfigContext's task section, if any
+            from . import config as _config
+            task = _config._CURRENT.get("task") if _config._CURRENT is not None else None
+        from .config import data_downsample_factor
+        if data_downsample_factor(task) > 1:  # apply_network's pre-downsampling (:561-563)
+            raise NotImplementedError("task.data_downsample > 1 in tiled inference: the tiles would be scored at "
+                                      "1/ds resolution; only the fused trainer implements it")
         self.loss_kind = LOSS_KINDS[loss_fn]
         self.batch_size = int(batch_size)
         self.spec = spec

@@ -25,7 +25,7 @@ import torch
 
 from . import checkpoint as ckpt
 from ._lib import SRMI_LOSS_MEAN, SRMI_LOSS_RMSE
-from .config import check_fused_task
+from .config import check_fused_task, data_downsample_factor
 from .dist import DistInfo, GradReducer, allreduce_sum_
 from .engine import Engine, NetSpec, adam_step, axpy, downsample, upsample
 
@@ -75,14 +75,16 @@ class FusedTrainer:
         if any).  apply_network's target selection is followed: when
         task.target_variables names fewer channels than the input, the loss target is
         those HR channels (index_select in the input's order, dual_trainer.py:564-568)
-        and the model has that many output channels; task.data_downsample > 1 raises
-        NotImplementedError (config.check_fused_task)."""
+        and the model has that many output channels.  task.data_downsample = ds > 1
+        (even integers) downsamples every HR batch by ds first, as apply_network does
+        (:561-563): step() then takes tiles of lr_hw * scale * ds."""
         if loss_fn not in LOSS_KINDS:  # single_product_loss, dual_trainer.py:210-211
             raise ValueError(f"Unknown single-product loss function {loss_fn}")
         if task is None:
             from . import config as _config
             task = _config._CURRENT.get("task") if _config._CURRENT is not None else None
         tindx = check_fused_task(task, spec.nchannels_in, spec.nchannels_out)
+        self.ds = data_downsample_factor(task)
         if tindx is not None and interp_loss and spec.nchannels_out != 1:
             # loss(btarget, upsample(binput)) (:315-317) needs equal or broadcastable channels
             raise ValueError(f"interp loss of a {spec.nchannels_out}-channel target against the "
@@ -133,6 +135,9 @@ class FusedTrainer:
         self.tgt = torch.empty_like(self.sr) if self.tindx is not None else None
         self.tgt_b = (torch.empty((batch, C, h * s, w * s), dtype=torch.float32, device=self.device)
                       if self.tindx is not None and interp_loss else None)
+        # apply_network's data_downsample: the HR batch downsampled by ds first
+        self.hrds = (torch.empty((batch, C, h * s, w * s), dtype=torch.float32, device=self.device)
+                     if self.ds > 1 else None)
         self.loss4 = torch.zeros(4, dtype=torch.float32, device=self.device)
         self.iloss4 = torch.zeros(4, dtype=torch.float32, device=self.device)
         self.mloss4 = torch.zeros((micro, 4), dtype=torch.float32, device=self.device)   # per micro-batch
@@ -172,6 +177,11 @@ class FusedTrainer:
         if b < 1 or b > self.batch:
             raise ValueError(f"batch {b} outside 1..{self.batch}")
         s = self.spec.scale
+        if self.ds > 1:  # apply_network: downsample(input, scale_factor=ds) first (:561-563)
+            want = (self.hrds.shape[2] * self.ds, self.hrds.shape[3] * self.ds)
+            if tuple(hr.shape[2:]) != want:
+                raise ValueError(f"data_downsample={self.ds}: HR tiles {tuple(hr.shape[2:])}, expected {want}")
+            hr = downsample(hr, self.ds, out=self.hrds[:b])
         mb = (b + self.micro - 1) // self.micro
         sls = [slice(min(b, k * mb), min(b, (k + 1) * mb)) for k in range(self.micro)]
         main = torch.cuda.current_stream(self.device)

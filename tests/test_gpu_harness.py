@@ -303,3 +303,37 @@ def test_target_channel_subset_step_vs_oracle():
     grads = tr.grads.cpu()
     for name, off, n, shape in table:
         assert rel_l2(grads[off:off + n].view(shape), g[name].grad) < 8e-2, name
+
+
+def test_data_downsample_step_vs_oracle():
+    """apply_network's data_downsample (dual_trainer.py:561-563): with
+    task.data_downsample = 2 the HR batch is downsampled by 2 first (bicubic,
+    array.py:72-76) and becomes both the loss target and the source of the model
+    input; the interp metric compares it with the upsampled input (:316-317)."""
+    d = dev()
+    spec = NetSpec(arch="rcan", nchannels_in=2, nchannels_out=2, nfeatures=64, nlayers=1, nblocks=2,
+                   cbottleneck=2, scale=4)
+    model = ro.RCANOracle(nchannels_in=2, nchannels_out=2, nlayers=1, nblocks=2)
+    ro.init_params_numpy(model, 6)
+    table = param_table(spec)
+    sd = dict(model.named_parameters())
+    flat = torch.cat([sd[n].detach().reshape(-1).float() for n, _, _, _ in table])
+    hr = ro.synthetic_hr(4, 2, 384, 78)
+    tr = FusedTrainer(spec, 4, (48, 48), device=d, params=flat.to(d), task={"data_downsample": 2})
+    res = tr.step(torch.tensor(hr, device=d))
+    torch.cuda.synchronize()
+    with pytest.raises(ValueError, match="data_downsample"):  # tiles of the wrong size
+        tr.step(torch.zeros(4, 2, 192, 192, device=d))
+    model = model.double()
+    h = ro.downsample(torch.tensor(hr, dtype=torch.float64), 2)
+    lr_in = ro.downsample(h, 4)
+    out = model(lr_in)
+    loss = ro.l2loss(out, h)
+    loss.backward()
+    iloss = float(ro.l2loss(h, ro.upsample(lr_in, 4)))
+    assert abs(float(res["loss"]) - float(loss)) < 2e-3 * float(loss)
+    assert abs(float(res["interp_loss"]) - iloss) < 1e-5 * iloss
+    g = dict(model.named_parameters())
+    grads = tr.grads.cpu()
+    for name, off, n, shape in table:
+        assert rel_l2(grads[off:off + n].view(shape), g[name].grad) < 8e-2, name

@@ -13,7 +13,7 @@ import pytest
 import torch
 
 from srmi import results as R
-from srmi.config import ConfigContext, cfg, check_fused_task
+from srmi.config import ConfigContext, cfg, check_fused_task, data_downsample_factor
 from srmi.harness import CheckpointStore, LossRecords
 
 
@@ -118,7 +118,7 @@ def test_config_identity_keys_and_derived_paths(tmp_path, monkeypatch):
 
 def test_fused_trainer_apply_network_target_selection_and_refusals():
     """apply_network (dual_trainer.py:557-571): data_downsample only acts when > 1
-    (refused: it changes the tile geometry); the target is index_selected only when
+    (even integer factors; others refused); the target is index_selected only when
     the batch has more channels than target_variables, in the INPUT's order
     (np.in1d(channels, targets)); equal counts in another order are a no-op."""
     from srmi.engine import NetSpec
@@ -126,8 +126,12 @@ def test_fused_trainer_apply_network_target_selection_and_refusals():
     assert check_fused_task({"data_downsample": 1, "input_variables": {"SST": "x"}, "target_variables": ["SST"]},
                             1, 1) is None
     assert check_fused_task({"data_downsample": 0.5}, 1, 1) is None  # <= 1: a no-op in the reference
-    with pytest.raises(NotImplementedError, match="data_downsample"):
-        check_fused_task({"data_downsample": 2.0}, 1, 1)
+    assert check_fused_task({"data_downsample": 2.0}, 1, 1) is None  # the trainer downsamples by 2 first
+    assert data_downsample_factor({"data_downsample": 0.5}) == 1
+    assert data_downsample_factor({"data_downsample": 4}) == 4
+    for bad in (3, 1.5):  # the bicubic kernel's half-way form: even integer factors
+        with pytest.raises(NotImplementedError, match="data_downsample"):
+            check_fused_task({"data_downsample": bad}, 1, 1)
     with pytest.raises(NotImplementedError, match="subset"):
         check_fused_task({}, 2, 1)
     two = {"input_variables": {"SSS": "a", "SST": "b"}}
@@ -145,10 +149,14 @@ def test_fused_trainer_apply_network_target_selection_and_refusals():
         FusedTrainer(NetSpec(nchannels_in=3, nchannels_out=2), 2, device=torch.device("cpu"),
                      task={"input_variables": ["A", "B", "C"], "target_variables": ["A", "C"]})
     with pytest.raises(NotImplementedError):
-        FusedTrainer(NetSpec(), 2, device=torch.device("cpu"), task={"data_downsample": 4})
-    with ConfigContext("sres", dict(model="rcan-10-20-64", task="SST-tiles-48"), **{"task.data_downsample": 2}):
-        assert cfg().task.data_downsample == 2
-        with pytest.raises(NotImplementedError):
+        FusedTrainer(NetSpec(), 2, device=torch.device("cpu"), task={"data_downsample": 3})
+    from srmi.inference import TiledInference
+    with pytest.raises(NotImplementedError, match="data_downsample"):  # scored at 1/ds: the trainer only
+        TiledInference(NetSpec(), torch.empty(0), (1, 384, 384), device=torch.device("cpu"),
+                       task={"data_downsample": 2})
+    with ConfigContext("sres", dict(model="rcan-10-20-64", task="SST-tiles-48"), **{"task.data_downsample": 3}):
+        assert cfg().task.data_downsample == 3
+        with pytest.raises(NotImplementedError):  # (read from the active context)
             FusedTrainer(NetSpec(), 2, device=torch.device("cpu"))
 
 
