@@ -345,13 +345,18 @@ def batch_losses(prd: torch.Tensor, tar: torch.Tensor, batch_size: int, loss_fn:
 
 
 def process_region(model, region: np.ndarray, ty: int, tx: int, scale: int, batch_size: Optional[int] = None,
-                   loss_fn: str = "l2"):
+                   loss_fn: str = "l2", data_downsample: int = 1):
     """process_image (dual_trainer.py:396-480) on one region: tiles scored in batches
     of batch_size (None: one batch of all tiles); loss = mean of the batch losses
-    (:443-446).  Returns (images dict, losses dict) with the reference's image types."""
+    (:443-446).  Returns (images dict, losses dict) with the reference's image types.
+    data_downsample > 1: apply_network first downsamples the (normalised) tiles by it
+    (:561-563), so target, model and interpolated are at 1/ds of the tile size."""
     tiles, mean, std, ids, grid = region_to_tiles(region, ty, tx)
     dt = torch.float64 if tiles.dtype == np.float64 else torch.float32
     target = torch.tensor(tiles, dtype=dt)
+    if data_downsample > 1:
+        target = downsample(target, data_downsample)
+        tiles = target.numpy()
     lr = downsample(target, scale)
     with torch.no_grad():
         sr = model(lr)

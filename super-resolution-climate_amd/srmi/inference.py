@@ -81,9 +81,9 @@ class TiledInference:
             from . import config as _config
             task = _config._CURRENT.get("task") if _config._CURRENT is not None else None
         from .config import data_downsample_factor
-        if data_downsample_factor(task) > 1:  # apply_network's pre-downsampling (:561-563)
-            raise NotImplementedError("task.data_downsample > 1 in tiled inference: the tiles would be scored at "
-                                      "1/ds resolution; only the fused trainer implements it")
+        # apply_network's pre-downsampling (:561-563): the normalised tiles are scored
+        # at 1/ds of the tile size (target, model, interpolated and their mosaics)
+        self.ds = data_downsample_factor(task)
         self.loss_kind = LOSS_KINDS[loss_fn]
         self.batch_size = int(batch_size)
         self.spec = spec
@@ -91,12 +91,14 @@ class TiledInference:
         C, H, W = region_chw
         if C != spec.nchannels_in or spec.nchannels_in != spec.nchannels_out:
             raise ValueError("region channels must equal the model's input/output channels")
-        ty, tx = tile_hr
+        ty0, tx0 = tile_hr
         s = spec.scale
-        if ty % s or tx % s:
-            raise ValueError(f"tile {tile_hr} not divisible by the model scale {s}")
+        if ty0 % (s * self.ds) or tx0 % (s * self.ds):
+            raise ValueError(f"tile {tile_hr} not divisible by the model scale {s} x data_downsample {self.ds}")
+        ty, tx = ty0 // self.ds, tx0 // self.ds  # the scored tile (the region's tile at ds = 1)
         self.C, self.H, self.W, self.ty, self.tx, self.s = C, H, W, ty, tx, s
-        self.gy, self.gx = H // ty, W // tx
+        self.ty0, self.tx0 = ty0, tx0
+        self.gy, self.gx = H // ty0, W // tx0
         n = self.gy * self.gx
         if n < 1:
             raise ValueError("region smaller than one tile")
@@ -112,6 +114,7 @@ class TiledInference:
         f32 = dict(dtype=torch.float32, device=d)
         self.region = torch.empty((C, H, W), **f32)
         self.tiles = torch.empty((n, C, ty, tx), **f32)
+        self.tiles0 = torch.empty((n, C, ty0, tx0), **f32) if self.ds > 1 else self.tiles
         self.mean = torch.empty((n, C), **f32)
         self.std = torch.empty((n, C), **f32)
         self.bad = torch.zeros(n, dtype=torch.int32, device=d)
@@ -165,8 +168,10 @@ class TiledInference:
     # ---------------------------------------------------------------- pieces
     def _tile(self):
         st = stream_handle()
-        call("srmi_region_to_tiles", ptr(self.region), self.C, self.H, self.W, self.ty, self.tx, ptr(self.tiles),
+        call("srmi_region_to_tiles", ptr(self.region), self.C, self.H, self.W, self.ty0, self.tx0, ptr(self.tiles0),
              ptr(self.mean), ptr(self.std), ptr(self.bad), st)
+        if self.ds > 1:  # apply_network: downsample(input, scale_factor=ds) of the normalised tiles
+            downsample(self.tiles0, self.ds, out=self.tiles)
 
     def _model_and_mosaic(self, tiles, lr, sr, interp, mean, std, inv, nt):
         st = stream_handle()

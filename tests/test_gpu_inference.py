@@ -96,6 +96,28 @@ def test_tiled_inference_matches_oracle(graph):
     assert rel_l2(images2["model"].cpu().numpy(), ref_img2["model"]) < 2e-2
 
 
+@pytest.mark.parametrize("graph", [True, False])
+def test_tiled_inference_data_downsample_vs_oracle(graph):
+    """apply_network's data_downsample in process_image (dual_trainer.py:423,
+    :561-563): the normalised 384² tiles are downsampled by 2 first, so target, model
+    and interpolated -- and their mosaics -- are at 192² per tile."""
+    d = dev()
+    spec, model, flat = _small_rcan()
+    rng = np.random.RandomState(9)
+    base = rng.randn(1, 2 * 384 + 5, 2 * 384 + 11)
+    region = (base + np.roll(base, 1, 1) + np.roll(base, 1, 2)).astype(np.float32)
+    ti = TiledInference(spec, flat.to(d), region.shape, (384, 384), device=d, graph=graph,
+                        task={"data_downsample": 2})
+    images, losses = ti.process_region(torch.tensor(region, device=d))
+    ref_img, ref_loss = ro.process_region(model, region.astype(np.float64), 384, 384, 4, data_downsample=2)
+    assert images["target"].shape[-1] == 2 * 192 and images["input"].shape[-1] == 2 * 48
+    for k in ("input", "target", "interpolated"):
+        assert rel_l2(images[k].cpu().numpy(), ref_img[k]) < 1e-5, k
+    assert rel_l2(images["model"].cpu().numpy(), ref_img["model"]) < 2e-2
+    assert abs(float(losses["interpolated"]) - ref_loss["interpolated"]) < 1e-5 * ref_loss["interpolated"] + 1e-7
+    assert abs(float(losses["model"]) - ref_loss["model"]) < 2e-3 * ref_loss["model"]
+
+
 def test_tiled_inference_drops_nonfinite_tiles():
     d = dev()
     spec, model, flat = _small_rcan()

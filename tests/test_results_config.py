@@ -151,9 +151,9 @@ def test_fused_trainer_apply_network_target_selection_and_refusals():
     with pytest.raises(NotImplementedError):
         FusedTrainer(NetSpec(), 2, device=torch.device("cpu"), task={"data_downsample": 3})
     from srmi.inference import TiledInference
-    with pytest.raises(NotImplementedError, match="data_downsample"):  # scored at 1/ds: the trainer only
+    with pytest.raises(NotImplementedError, match="data_downsample"):  # odd factors: also in inference
         TiledInference(NetSpec(), torch.empty(0), (1, 384, 384), device=torch.device("cpu"),
-                       task={"data_downsample": 2})
+                       task={"data_downsample": 3})
     with ConfigContext("sres", dict(model="rcan-10-20-64", task="SST-tiles-48"), **{"task.data_downsample": 3}):
         assert cfg().task.data_downsample == 3
         with pytest.raises(NotImplementedError):  # (read from the active context)
