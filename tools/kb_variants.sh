@@ -1,8 +1,8 @@
 #!/bin/bash
-# kbench of the in-tree library and every build/alt/libsrmi_*.so variant
+# kbench of the in-tree library and every alt/libsrmi_*.so variant
 R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R; mkdir -p gpurun_out
 timeout -k 10 120 python tools/kbench.py > gpurun_out/kbv_intree.log 2>&1 || exit 5
-for f in build/alt/libsrmi_*.so; do
+for f in alt/libsrmi_*.so; do
   b=$(basename $f .so)
   SRMI_LIB=$R/$f timeout -k 10 120 python tools/kbench.py > gpurun_out/kbv_$b.log 2>&1 || exit 6
 done
