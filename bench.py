@@ -261,7 +261,8 @@ def inference_bench(dev, side, iters, flags=0, info=None):
     default_init_(params, table, 0)
     region = torch.tensor(synthetic_hr(1, 1, side, 99)[0]).to(dev)
     multi = info is not None and info.enabled
-    ti = TiledInference(spec, params, tuple(region.shape), (192, 192), device=dev, graph=not multi,
+    micro = int(os.environ["SRMI_INFER_MICRO"]) if os.environ.get("SRMI_INFER_MICRO") else None  # A/B only
+    ti = TiledInference(spec, params, tuple(region.shape), (192, 192), device=dev, graph=not multi, micro=micro,
                         info=info if multi else None)
     ti.process_region(region)  # builds + captures the graph
     torch.cuda.synchronize()
