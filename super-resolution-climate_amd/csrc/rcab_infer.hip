@@ -24,8 +24,10 @@
 #ifndef SRMI_INFER_WLDS
 #define SRMI_INFER_WLDS 1
 #endif
+// plain (write-back) stores for this launch's outputs: t is re-read by the workgroup
+// that wrote it, and the pair by the next launch (+1 % C5 against write-through)
 #ifndef SRMI_INFER_WT
-#define SRMI_INFER_WT 1
+#define SRMI_INFER_WT 0
 #endif
 // deferred conv epilogues (conv64_body.hpp SRMI_DEFER) for this launch's convs: an
 // image is one run of 12 strips here, not 3 as in training.  23 = v1's RELU / POOL
