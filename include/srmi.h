@@ -21,6 +21,7 @@
  *   srmi_rmse_*, srmi_loss_*     -> l2loss sres/controller/stats.py:5-8
  *   srmi_charbonnier_partial     -> ModelTrainer.charbonnier dual_trainer.py:196-198
  *   srmi_downsample/_upsample    -> sres/base/util/array.py:72-76 / :84-87
+ *   srmi_interpolate             -> the same with torch_interp_mode, array.py:37-41
  *   srmi_adam_step               -> torch.optim.Adam, dual_trainer.py:126,323
  *   srmi_conv3x3* / srmi_wgrad*  -> nn.Conv2d of default_conv
  *                                   sres/model/common/cnn.py:8-9 (op level)
@@ -171,6 +172,17 @@ int srmi_loss_combine(float* loss4, const float* parts4, int nparts, int kind, v
 /* interp baseline / data path */
 int srmi_downsample(const float* hr, int N, int C, int H, int W, int scale, float* lr, void* stream);
 int srmi_upsample(const float* lr, int N, int C, int h, int w, int scale, float* hr, void* stream);
+/* torch.nn.functional.interpolate(x, scale_factor=f, mode) with align_corners=False,
+ * any factor: the downsample / upsample of array.py:72-76 / :84-87 under
+ * task.downsample_mode / upsample_mode (torch_interp_mode, array.py:37-41: 'linear'
+ * -> SRMI_INTERP_BILINEAR, 'cubic' -> SRMI_INTERP_BICUBIC) and data_downsample's
+ * factors (dual_trainer.py:561-563).  x NCHW [N][C][H][W] -> y [N][C][Ho][Wo] with
+ * Ho = floor(H f), Wo = floor(W f) chosen by the caller and rh = rw = (float)(1 / f),
+ * the source-coordinate scale ATen uses (UpSample.h area_pixel_compute_scale) */
+#define SRMI_INTERP_BILINEAR 1
+#define SRMI_INTERP_BICUBIC 2
+int srmi_interpolate(const float* x, int N, int C, int H, int W, int Ho, int Wo, float rh, float rw, int mode, float* y,
+                     void* stream);
 
 /* Adam on flat buffers, step counted from 1 */
 int srmi_adam_step(float* p, const float* g, float* m, float* v, size_t n, int step, float lr, float beta1,

@@ -189,9 +189,10 @@ def init_params_numpy(model: nn.Module, seed: int) -> None:
 # ---------------------------------------------------------------------------
 # data path pieces on the hot path
 # ---------------------------------------------------------------------------
-def downsample(hr: torch.Tensor, scale: int) -> torch.Tensor:
-    """array.py:72-76: F.interpolate(scale_factor=1/scale, mode='bicubic')."""
-    return F.interpolate(hr, scale_factor=1.0 / scale, mode="bicubic")
+def downsample(hr: torch.Tensor, scale, mode: str = "bicubic") -> torch.Tensor:
+    """array.py:72-76: F.interpolate(scale_factor=1/scale, mode=torch_interp_mode(True))
+    (array.py:37-41: task.downsample_mode 'cubic' -> 'bicubic', 'linear' -> 'bilinear')."""
+    return F.interpolate(hr, scale_factor=1.0 / scale, mode=mode)
 
 
 def downsample_explicit(hr: np.ndarray, scale: int) -> np.ndarray:
@@ -209,9 +210,10 @@ def downsample_explicit(hr: np.ndarray, scale: int) -> np.ndarray:
     return np.einsum("bchwk,k->bchw", rows[:, :, :, xs], w)         # [B,C,h,w]
 
 
-def upsample(lr: torch.Tensor, scale: int) -> torch.Tensor:
-    """array.py:84-87: interp baseline, bicubic xscale."""
-    return F.interpolate(lr, scale_factor=scale, mode="bicubic")
+def upsample(lr: torch.Tensor, scale: int, mode: str = "bicubic") -> torch.Tensor:
+    """array.py:84-87: interp baseline, xscale with torch_interp_mode(False)
+    (task.upsample_mode)."""
+    return F.interpolate(lr, scale_factor=scale, mode=mode)
 
 
 def l2loss(prd: torch.Tensor, tar: torch.Tensor, squared: bool = False) -> torch.Tensor:
@@ -268,19 +270,21 @@ class AdamOracle:
 
 
 def train_step(model: nn.Module, opt: AdamOracle, hr: torch.Tensor, scale: int,
-               interp_loss: bool = False) -> Tuple[float, Optional[float], torch.Tensor]:
+               interp_loss: bool = False, dmode: str = "bicubic",
+               umode: str = "bicubic") -> Tuple[float, Optional[float], torch.Tensor]:
     """One step of dual_trainer.py:310-323 with apply_network (:557-571):
     HR (requires_grad, as array2tensor does) -> downsample -> model -> RMSE ->
-    backward -> Adam.  Returns (loss, interp_loss, output)."""
+    backward -> Adam.  Returns (loss, interp_loss, output).  dmode / umode: the
+    F.interpolate modes of task.downsample_mode / upsample_mode."""
     opt.zero_grad()
     hr = hr.detach().clone().requires_grad_(True)          # array2tensor, array.py:70
-    lr_in = downsample(hr, scale)
+    lr_in = downsample(hr, scale, dmode)
     out = model(lr_in)
     loss = l2loss(out, hr)
     iloss = None
     if interp_loss:
         with torch.no_grad():
-            iloss = float(l2loss(hr, upsample(lr_in, scale)))
+            iloss = float(l2loss(hr, upsample(lr_in, scale, umode)))
     loss.backward()
     opt.step()
     return float(loss), iloss, out.detach()
@@ -345,22 +349,23 @@ def batch_losses(prd: torch.Tensor, tar: torch.Tensor, batch_size: int, loss_fn:
 
 
 def process_region(model, region: np.ndarray, ty: int, tx: int, scale: int, batch_size: Optional[int] = None,
-                   loss_fn: str = "l2", data_downsample: int = 1):
+                   loss_fn: str = "l2", data_downsample=1, dmode: str = "bicubic", umode: str = "bicubic"):
     """process_image (dual_trainer.py:396-480) on one region: tiles scored in batches
     of batch_size (None: one batch of all tiles); loss = mean of the batch losses
     (:443-446).  Returns (images dict, losses dict) with the reference's image types.
     data_downsample > 1: apply_network first downsamples the (normalised) tiles by it
-    (:561-563), so target, model and interpolated are at 1/ds of the tile size."""
+    (:561-563), so target, model and interpolated are at 1/ds of the tile size.
+    dmode / umode: the F.interpolate modes of task.downsample_mode / upsample_mode."""
     tiles, mean, std, ids, grid = region_to_tiles(region, ty, tx)
     dt = torch.float64 if tiles.dtype == np.float64 else torch.float32
     target = torch.tensor(tiles, dtype=dt)
     if data_downsample > 1:
-        target = downsample(target, data_downsample)
+        target = downsample(target, data_downsample, dmode)
         tiles = target.numpy()
-    lr = downsample(target, scale)
+    lr = downsample(target, scale, dmode)
     with torch.no_grad():
         sr = model(lr)
-    interp = upsample(lr, scale)
+    interp = upsample(lr, scale, umode)
     bs = batch_size or target.shape[0]
     bm = batch_losses(sr, target, bs, loss_fn)
     bi = batch_losses(interp, target, bs, loss_fn)

@@ -990,6 +990,11 @@ int srmi_upsample(const float* lr, int N, int C, int h, int w, int scale, float*
   return upsample_launch(lr, N, C, h, w, scale, hr, S_(stream));
 }
 
+int srmi_interpolate(const float* x, int N, int C, int H, int W, int Ho, int Wo, float rh, float rw, int mode, float* y,
+                     void* stream) {
+  return interp_launch(x, N, C, H, W, Ho, Wo, rh, rw, mode, y, S_(stream));
+}
+
 int srmi_adam_step(float* p, const float* g, float* m, float* v, size_t n, int step, float lr, float beta1,
                    float beta2, float eps, float weight_decay, void* stream) {
   if (step < 1) return SRMI_ERR_ARG;

@@ -776,6 +776,63 @@ int upsample_launch(const float* lr, int N, int C, int h, int w, int scale, floa
   return 0;
 }
 
+// F.interpolate(x, scale_factor, mode, align_corners=False) at any factor, the form
+// downsample / upsample take with task.downsample_mode / upsample_mode 'linear' ->
+// bilinear, 'cubic' -> bicubic (torch_interp_mode, array.py:37-41, :72-76, :84-87) and
+// data_downsample's non-even factors (dual_trainer.py:561-563).  As ATen computes it
+// (UpSample.h): source coordinate r (d + 0.5) - 0.5 in fp32 with r = 1 / scale_factor;
+// bilinear clamps it at 0, index i0 = min(floor, n - 1), weight lambda = clamp(src - i0,
+// 0, 1) on i0 and min(i0 + 1, n - 1); bicubic (A = -0.75) reads i0 - 1 .. i0 + 2 clamped
+// to the edge with the cubic weights of lambda.  One thread per output element.
+__device__ __forceinline__ void interp_axis(float r, int d, int n, int mode, int* idx, float* wt) {
+  float src = r * ((float)d + 0.5f) - 0.5f;
+  if (mode == 1 && src < 0.f) src = 0.f;
+  const int i0 = min((int)floorf(src), n - 1);
+  const float t = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  if (mode == 1) {
+    idx[0] = i0;
+    idx[1] = min(i0 + 1, n - 1);
+    wt[0] = 1.f - t;
+    wt[1] = t;
+  } else {
+    cubic_w(t, wt);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) idx[i] = min(max(i0 - 1 + i, 0), n - 1);
+  }
+}
+
+__global__ void interp_kernel(const float* __restrict__ x, int NC, int H, int W, int Ho, int Wo, float rh, float rw,
+                              int mode, float* __restrict__ y) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)NC * Ho * Wo) return;
+  const int ox = idx % Wo, oy = (idx / Wo) % Ho;
+  const size_t nc = idx / ((size_t)Wo * Ho);
+  int iy[4], ix[4];
+  float wy[4], wx[4];
+  interp_axis(rh, oy, H, mode, iy, wy);
+  interp_axis(rw, ox, W, mode, ix, wx);
+  const float* src = x + nc * H * W;
+  const int taps = mode == 1 ? 2 : 4;
+  float acc = 0.f;
+  for (int i = 0; i < taps; ++i) {
+    float rsum = 0.f;
+    for (int j = 0; j < taps; ++j) rsum += wx[j] * src[(size_t)iy[i] * W + ix[j]];
+    acc += wy[i] * rsum;
+  }
+  y[idx] = acc;
+}
+
+int interp_launch(const float* x, int N, int C, int H, int W, int Ho, int Wo, float rh, float rw, int mode, float* y,
+                  hipStream_t st) {
+  if (!x || !y || (mode != 1 && mode != 2)) return SRMI_ERR_ARG;
+  if (N < 1 || C < 1 || H < 1 || W < 1 || Ho < 1 || Wo < 1 || !(rh > 0.f) || !(rw > 0.f)) return SRMI_ERR_SHAPE;
+  const size_t tot = (size_t)N * C * Ho * Wo;
+  hipLaunchKernelGGL(interp_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, x, N * C, H, W, Ho, Wo, rh, rw, mode,
+                     y);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
 // ============================================================================ loss
 __global__ void __launch_bounds__(256) sqerr_partial_kernel(const float* __restrict__ y, const float* __restrict__ t,
                                                             size_t n, float* __restrict__ partial) {

@@ -150,6 +150,8 @@ int tail_wgrad_reduce_launch(const float* slab, int nslab, int C, float* gw, flo
 
 int downsample_launch(const float* hr, int N, int C, int H, int W, int scale, float* lr, hipStream_t st);
 int upsample_launch(const float* lr, int N, int C, int h, int w, int scale, float* hr, hipStream_t st);
+int interp_launch(const float* x, int N, int C, int H, int W, int Ho, int Wo, float rh, float rw, int mode, float* y,
+                  hipStream_t st);
 // loss[0] = sum (y-t)^2 (this rank), loss[1] = element count (global after all-reduce)
 int sqerr_partial_launch(const float* y, const float* t, size_t n, float* partial, int nblk, hipStream_t st);
 int sqerr_finish_launch(const float* partial, int nblk, double count, float* loss, hipStream_t st);

@@ -22,6 +22,8 @@ SRMI_FLAG_NO_RCAB_INFER = 2
 SRMI_DTYPE_F32 = 1
 SRMI_LOSS_RMSE = 0
 SRMI_LOSS_MEAN = 1
+SRMI_INTERP_BILINEAR = 1
+SRMI_INTERP_BICUBIC = 2
 
 ERRORS = {-10001: "SRMI_ERR_ARG", -10002: "SRMI_ERR_SHAPE", -10003: "SRMI_ERR_WORKSPACE",
           -10004: "SRMI_ERR_UNSUPPORTED"}
@@ -60,6 +62,8 @@ _SIGS = {
     "srmi_batch_loss_means": ([P, C.c_int, C.c_longlong, C.c_int, C.c_int, P, P], C.c_int),
     "srmi_downsample": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),
     "srmi_upsample": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),
+    "srmi_interpolate": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, C.c_int, P,
+                          P], C.c_int),
     "srmi_adam_step": ([P, P, P, P, C.c_size_t, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, P],
                        C.c_int),
     "srmi_conv3x3": ([P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P,

@@ -193,25 +193,44 @@ def init_parms(model: str, custom: Dict[str, Any], model_cfg: Optional[Any] = No
     return parms
 
 
-def data_downsample_factor(task) -> int:
+def data_downsample_factor(task):
     """apply_network's pre-downsampling of the HR batch (dual_trainer.py:561-563):
-    ``downsample(input, scale_factor=ds)`` -- F.interpolate(1/ds, bicubic), array.py:72-76
-    -- only when ds > 1.0; any value <= 1 is a no-op there and here (returns 1).  The
-    engine's bicubic kernel is the half-way 4-tap form, exact for EVEN integer factors;
-    other factors raise NotImplementedError."""
+    ``downsample(input, scale_factor=ds)`` -- F.interpolate(scale_factor=1/ds,
+    mode=torch_interp_mode(True)), array.py:72-76 -- only when ds > 1.0; any value
+    <= 1 is a no-op there and here (returns 1).  Any factor > 1: an integer is
+    returned as int, anything else as float (srmi.engine.downsample runs both)."""
     ds = float(task.get("data_downsample", 1.0) or 1.0) if task is not None else 1.0
     if ds <= 1.0:
         return 1
-    if ds != int(ds) or int(ds) % 2:
-        raise NotImplementedError(f"task.data_downsample={ds}: even integer factors only")
-    return int(ds)
+    return int(ds) if ds.is_integer() else ds
+
+
+# torch_interp_mode (sres/base/util/array.py:37-41): 'linear' -> 'bilinear', 'cubic'
+# -> 'bicubic', any other name passed to F.interpolate unchanged
+_INTERP_NAMES = {"linear": "bilinear", "cubic": "bicubic", "bilinear": "bilinear", "bicubic": "bicubic"}
+
+
+def interp_mode(task, downsample: bool) -> str:
+    """The F.interpolate mode of downsample (task.downsample_mode) or upsample
+    (task.upsample_mode), as torch_interp_mode maps them (array.py:37-41).  Absent
+    keys mean 'cubic' (every reference task yaml sets cubic).  The engine runs
+    'bilinear' and 'bicubic'; any other mode (e.g. 'nearest', 'area') raises
+    NotImplementedError instead of silently resampling differently."""
+    key = "downsample_mode" if downsample else "upsample_mode"
+    mode = task.get(key, "cubic") if task is not None else "cubic"
+    mode = "cubic" if mode is None else str(mode)
+    if mode not in _INTERP_NAMES:
+        raise NotImplementedError(f"task.{key}={mode!r}: srmi implements 'linear' (bilinear) and 'cubic' (bicubic)")
+    return _INTERP_NAMES[mode]
 
 
 def check_fused_task(task, nchannels_in: int, nchannels_out: int) -> Optional[List[int]]:
     """What the fused trainer takes from apply_network (dual_trainer.py:557-571).
 
-    * ``task.data_downsample`` (:561-563): ``data_downsample_factor`` (validated here
-      too; the trainer downsamples the HR batch by it first).
+    * ``task.data_downsample`` (:561-563): ``data_downsample_factor`` (the trainer
+      downsamples the HR batch by it first).
+    * ``task.downsample_mode`` / ``task.upsample_mode`` (array.py:37-41): validated
+      by ``interp_mode`` (bilinear / bicubic; anything else raises).
     * The target channels: when the batch has MORE channels than
       ``task.target_variables`` the reference index_selects them (:564-568) with
       ``np.in1d(channels, target_variables).nonzero()`` -- the input's own order.
@@ -221,6 +240,8 @@ def check_fused_task(task, nchannels_in: int, nchannels_out: int) -> Optional[Li
       alone decide: fewer output channels than inputs cannot be resolved, and raise.
     """
     data_downsample_factor(task)
+    interp_mode(task, True)
+    interp_mode(task, False)
     names_in = list(task["input_variables"]) if task is not None and "input_variables" in task else None
     names_out = list(task["target_variables"]) if task is not None and "target_variables" in task else None
     if names_in is None or names_out is None:

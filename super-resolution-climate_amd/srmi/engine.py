@@ -178,18 +178,56 @@ class Engine:
 
 
 # ----------------------------------------------------------------- free ops
-def downsample(hr: torch.Tensor, scale: int, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
-    """bicubic 1/scale (sres/base/util/array.py:72-76), NCHW fp32."""
-    N, Cc, H, W = hr.shape
+INTERP_MODES = {"bilinear": _lib.SRMI_INTERP_BILINEAR, "bicubic": _lib.SRMI_INTERP_BICUBIC}
+
+
+def interp_size(n: int, scale_factor: float) -> int:
+    """F.interpolate's output size floor(n * scale_factor) (ATen compute_output_size)."""
+    return int(math.floor(float(n) * float(scale_factor)))
+
+
+def interpolate(x: torch.Tensor, scale_factor: float, mode: str = "bicubic", out: Optional[torch.Tensor] = None,
+                stream=None) -> torch.Tensor:
+    """torch.nn.functional.interpolate(x, scale_factor=scale_factor, mode=mode) with
+    align_corners=False (mode 'bilinear' | 'bicubic'), NCHW fp32, any factor
+    (srmi_interpolate)."""
+    if mode not in INTERP_MODES:
+        raise _lib.SrmiError(f"interpolation mode {mode!r}: bilinear | bicubic")
+    N, Cc, H, W = x.shape
+    Ho, Wo = interp_size(H, scale_factor), interp_size(W, scale_factor)
     if out is None:
-        out = torch.empty((N, Cc, H // scale, W // scale), dtype=torch.float32, device=hr.device)
-    call("srmi_downsample", ptr(hr), N, Cc, H, W, scale, ptr(out), stream_handle(stream))
+        out = torch.empty((N, Cc, Ho, Wo), dtype=torch.float32, device=x.device)
+    if tuple(out.shape) != (N, Cc, Ho, Wo):
+        raise _lib.SrmiError(f"interpolate: out {tuple(out.shape)} != {(N, Cc, Ho, Wo)}")
+    r = 1.0 / float(scale_factor)  # (float)(1 / scale_factor): ctypes rounds it to fp32 as ATen does
+    call("srmi_interpolate", ptr(x), N, Cc, H, W, Ho, Wo, r, r, INTERP_MODES[mode], ptr(out), stream_handle(stream))
     return out
 
 
-def upsample(lr: torch.Tensor, scale: int, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
-    """bicubic xscale interp baseline (sres/base/util/array.py:84-87), NCHW fp32."""
+def downsample(hr: torch.Tensor, scale, out: Optional[torch.Tensor] = None, stream=None,
+               mode: str = "bicubic") -> torch.Tensor:
+    """downsample (sres/base/util/array.py:72-76): F.interpolate(scale_factor=1/scale,
+    mode), NCHW fp32.  Bicubic at an even integer factor dividing the tile is the
+    separable half-way [-3,19,19,-3]/32 kernel (srmi_downsample); every other factor
+    or mode takes the general F.interpolate kernel (srmi_interpolate)."""
+    N, Cc, H, W = hr.shape
+    fs = float(scale)
+    if mode == "bicubic" and fs.is_integer() and int(fs) % 2 == 0 and H % int(fs) == 0 and W % int(fs) == 0:
+        scale = int(fs)
+        if out is None:
+            out = torch.empty((N, Cc, H // scale, W // scale), dtype=torch.float32, device=hr.device)
+        call("srmi_downsample", ptr(hr), N, Cc, H, W, scale, ptr(out), stream_handle(stream))
+        return out
+    return interpolate(hr, 1.0 / fs, mode, out=out, stream=stream)
+
+
+def upsample(lr: torch.Tensor, scale: int, out: Optional[torch.Tensor] = None, stream=None,
+             mode: str = "bicubic") -> torch.Tensor:
+    """upsample, the interp baseline (sres/base/util/array.py:84-87):
+    F.interpolate(scale_factor=scale, mode), NCHW fp32."""
     N, Cc, h, w = lr.shape
+    if mode != "bicubic":
+        return interpolate(lr, float(scale), mode, out=out, stream=stream)
     if out is None:
         out = torch.empty((N, Cc, h * scale, w * scale), dtype=torch.float32, device=lr.device)
     call("srmi_upsample", ptr(lr), N, Cc, h, w, scale, ptr(out), stream_handle(stream))

@@ -32,7 +32,7 @@ import torch
 
 from ._lib import SRMI_LOSS_MEAN, SRMI_LOSS_RMSE, call, ptr, stream_handle
 from .dist import DistInfo
-from .engine import Engine, NetSpec, downsample, upsample
+from .engine import Engine, NetSpec, downsample, interp_size, upsample
 
 LOSS_KINDS = {"l2": SRMI_LOSS_RMSE, "charbonnier": SRMI_LOSS_MEAN}
 CHARBONNIER_EPS = 1e-6  # dual_trainer.py:122
@@ -80,10 +80,12 @@ class TiledInference:
         if task is None:  # the active srmi ConfigContext's task section, if any
             from . import config as _config
             task = _config._CURRENT.get("task") if _config._CURRENT is not None else None
-        from .config import data_downsample_factor
+        from .config import data_downsample_factor, interp_mode
         # apply_network's pre-downsampling (:561-563): the normalised tiles are scored
         # at 1/ds of the tile size (target, model, interpolated and their mosaics)
         self.ds = data_downsample_factor(task)
+        # task.downsample_mode / upsample_mode (torch_interp_mode, array.py:37-41)
+        self.dmode, self.umode = interp_mode(task, True), interp_mode(task, False)
         self.loss_kind = LOSS_KINDS[loss_fn]
         self.batch_size = int(batch_size)
         self.spec = spec
@@ -93,9 +95,11 @@ class TiledInference:
             raise ValueError("region channels must equal the model's input/output channels")
         ty0, tx0 = tile_hr
         s = spec.scale
-        if ty0 % (s * self.ds) or tx0 % (s * self.ds):
-            raise ValueError(f"tile {tile_hr} not divisible by the model scale {s} x data_downsample {self.ds}")
-        ty, tx = ty0 // self.ds, tx0 // self.ds  # the scored tile (the region's tile at ds = 1)
+        # the scored tile: floor(tile / ds) (F.interpolate's size; the region's tile at ds = 1)
+        ty, tx = (interp_size(ty0, 1.0 / self.ds), interp_size(tx0, 1.0 / self.ds)) if self.ds > 1 else (ty0, tx0)
+        if ty % s or tx % s or ty < s or tx < s:
+            raise ValueError(f"tile {tile_hr} / data_downsample {self.ds} = {(ty, tx)} not divisible by the model "
+                             f"scale {s}")
         self.C, self.H, self.W, self.ty, self.tx, self.s = C, H, W, ty, tx, s
         self.ty0, self.tx0 = ty0, tx0
         self.gy, self.gx = H // ty0, W // tx0
@@ -138,7 +142,9 @@ class TiledInference:
         # engine's launch ramps and tails overlap the other's work
         nl = self.n_local
         if micro is None:
-            micro = 2 if nl >= 32 else 1
+            # multi-rank mode runs its engines one after another on one stream
+            # (_process_region_ranks), so one whole-chip engine there
+            micro = 2 if nl >= 32 and not self.info.enabled else 1
         self.micro = max(1, min(int(micro), max(nl, 1)))
         per = (max(nl, 1) + self.micro - 1) // self.micro
         self.split = [max(1, min(per, nl - k * per)) for k in range(self.micro)]
@@ -171,11 +177,11 @@ class TiledInference:
         call("srmi_region_to_tiles", ptr(self.region), self.C, self.H, self.W, self.ty0, self.tx0, ptr(self.tiles0),
              ptr(self.mean), ptr(self.std), ptr(self.bad), st)
         if self.ds > 1:  # apply_network: downsample(input, scale_factor=ds) of the normalised tiles
-            downsample(self.tiles0, self.ds, out=self.tiles)
+            downsample(self.tiles0, self.ds, out=self.tiles, mode=self.dmode)
 
     def _model_and_mosaic(self, tiles, lr, sr, interp, mean, std, inv, nt):
         st = stream_handle()
-        downsample(tiles, self.s, out=lr)
+        downsample(tiles, self.s, out=lr, mode=self.dmode)
         main = torch.cuda.current_stream(self.device)
         self.ev_fork.record(main)
         for sk in self.streams[1:]:
@@ -193,7 +199,7 @@ class TiledInference:
         for sk, ev in zip(self.streams[1:], self.ev_join):
             ev.record(sk)
             main.wait_event(ev)
-        upsample(lr, self.s, out=interp)
+        upsample(lr, self.s, out=interp, mode=self.umode)
         te = self.C * self.ty * self.tx
         for pred, lo in ((sr, self.loss_m), (interp, self.loss_i)):
             call("srmi_batch_losses", ptr(pred), ptr(tiles), nt, te, self.batch_size, self.loss_kind,
@@ -356,21 +362,23 @@ class TiledInference:
         nl = self.n_local
         if nl > 0:
             torch.index_select(self.tiles, 0, self.idx_local, out=self.sub_tiles[:nl])
-            downsample(self.sub_tiles[:nl], self.s, out=self.sub_lr[:nl])
+            downsample(self.sub_tiles[:nl], self.s, out=self.sub_lr[:nl], mode=self.dmode)
             a = 0
             for e, m in zip(self.engs, self.split):
                 b = min(nl, a + m)
                 if b > a:
                     e.forward(self.params, self.sub_lr[a:b], out=self.sub_sr[a:b])
                 a = b
-            upsample(self.sub_lr[:nl], self.s, out=self.sub_interp[:nl])
+            upsample(self.sub_lr[:nl], self.s, out=self.sub_interp[:nl], mode=self.umode)
         st = stream_handle()
         te = self.C * self.ty * self.tx
         sums = {}
         for name, pred in (("model", self.sub_sr), ("interpolated", self.sub_interp)):
             work = torch.zeros(max(nl, 1), dtype=torch.float32, device=self.device)
-            if nl > 0:  # per-tile sums (srmi_batch_losses' first pass, batches of one tile)
-                call("srmi_batch_losses", ptr(pred), ptr(self.sub_tiles), nl, te, 1, self.loss_kind, CHARBONNIER_EPS,
+            if nl > 0:  # per-tile sums: srmi_batch_losses' first pass into `work`; its mean pass sees
+                # ONE batch of all nl tiles (the pass holds at most 1024 batches, so batches of one
+                # tile would cap a rank at 1024 tiles)
+                call("srmi_batch_losses", ptr(pred), ptr(self.sub_tiles), nl, te, nl, self.loss_kind, CHARBONNIER_EPS,
                      ptr(work), ptr(self.sub_out), st)
             sums[name] = self._gather(work[:, None])[:, 0]
         lr = self._gather(self.sub_lr)

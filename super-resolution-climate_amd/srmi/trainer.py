@@ -25,9 +25,9 @@ import torch
 
 from . import checkpoint as ckpt
 from ._lib import SRMI_LOSS_MEAN, SRMI_LOSS_RMSE
-from .config import check_fused_task, data_downsample_factor
+from .config import check_fused_task, data_downsample_factor, interp_mode
 from .dist import DistInfo, GradReducer, allreduce_sum_
-from .engine import Engine, NetSpec, adam_step, axpy, downsample, upsample
+from .engine import Engine, NetSpec, adam_step, axpy, downsample, interp_size, upsample
 
 LOSS_KINDS = {"l2": SRMI_LOSS_RMSE, "charbonnier": SRMI_LOSS_MEAN}
 CHARBONNIER_EPS = 1e-6  # ModelTrainer.eps, sres/controller/dual_trainer.py:122
@@ -76,8 +76,11 @@ class FusedTrainer:
         task.target_variables names fewer channels than the input, the loss target is
         those HR channels (index_select in the input's order, dual_trainer.py:564-568)
         and the model has that many output channels.  task.data_downsample = ds > 1
-        (even integers) downsamples every HR batch by ds first, as apply_network does
-        (:561-563): step() then takes tiles of lr_hw * scale * ds."""
+        downsamples every HR batch by ds first, as apply_network does (:561-563):
+        step() then takes tiles T with floor(T / ds) = lr_hw * scale.
+        task.downsample_mode / upsample_mode select the resampling of the model input
+        and of the interp baseline ('cubic' -> bicubic, 'linear' -> bilinear,
+        array.py:37-41; others raise)."""
         if loss_fn not in LOSS_KINDS:  # single_product_loss, dual_trainer.py:210-211
             raise ValueError(f"Unknown single-product loss function {loss_fn}")
         if task is None:
@@ -85,6 +88,7 @@ class FusedTrainer:
             task = _config._CURRENT.get("task") if _config._CURRENT is not None else None
         tindx = check_fused_task(task, spec.nchannels_in, spec.nchannels_out)
         self.ds = data_downsample_factor(task)
+        self.dmode, self.umode = interp_mode(task, True), interp_mode(task, False)
         if tindx is not None and interp_loss and spec.nchannels_out != 1:
             # loss(btarget, upsample(binput)) (:315-317) needs equal or broadcastable channels
             raise ValueError(f"interp loss of a {spec.nchannels_out}-channel target against the "
@@ -178,10 +182,11 @@ class FusedTrainer:
             raise ValueError(f"batch {b} outside 1..{self.batch}")
         s = self.spec.scale
         if self.ds > 1:  # apply_network: downsample(input, scale_factor=ds) first (:561-563)
-            want = (self.hrds.shape[2] * self.ds, self.hrds.shape[3] * self.ds)
-            if tuple(hr.shape[2:]) != want:
-                raise ValueError(f"data_downsample={self.ds}: HR tiles {tuple(hr.shape[2:])}, expected {want}")
-            hr = downsample(hr, self.ds, out=self.hrds[:b])
+            got = tuple(interp_size(n, 1.0 / self.ds) for n in hr.shape[2:])
+            if got != tuple(self.hrds.shape[2:]):
+                raise ValueError(f"data_downsample={self.ds}: HR tiles {tuple(hr.shape[2:])} give {got}, "
+                                 f"expected {tuple(self.hrds.shape[2:])}")
+            hr = downsample(hr, self.ds, out=self.hrds[:b], mode=self.dmode)
         mb = (b + self.micro - 1) // self.micro
         sls = [slice(min(b, k * mb), min(b, (k + 1) * mb)) for k in range(self.micro)]
         main = torch.cuda.current_stream(self.device)
@@ -203,12 +208,12 @@ class FusedTrainer:
                 self.miloss4[k].zero_()
                 continue
             with self._ctx(k):
-                downsample(hr[sl], s, out=self.lrbuf[sl])
+                downsample(hr[sl], s, out=self.lrbuf[sl], mode=self.dmode)
                 eng.forward(self.params, self.lrbuf[sl], out=self.sr[sl])
                 self._loss_partial(eng, self.sr[sl], tgt[sl], self.mloss4[k], count,
                                    None if self.dy is None else self.dy[sl])
                 if self.interp_loss:  # self.loss(btarget, binterp), dual_trainer.py:316-317
-                    up = upsample(self.lrbuf[sl], s, out=self.up[sl])
+                    up = upsample(self.lrbuf[sl], s, out=self.up[sl], mode=self.umode)
                     itgt = hr[sl] if self.tgt_b is None else self.tgt_b[sl]
                     self._loss_partial(eng, itgt, up, self.miloss4[k], icount)
         for st in self.streams[1:]:

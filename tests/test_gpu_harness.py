@@ -305,11 +305,21 @@ def test_target_channel_subset_step_vs_oracle():
         assert rel_l2(grads[off:off + n].view(shape), g[name].grad) < 8e-2, name
 
 
-def test_data_downsample_step_vs_oracle():
-    """apply_network's data_downsample (dual_trainer.py:561-563): with
-    task.data_downsample = 2 the HR batch is downsampled by 2 first (bicubic,
-    array.py:72-76) and becomes both the loss target and the source of the model
-    input; the interp metric compares it with the upsampled input (:316-317)."""
+@pytest.mark.parametrize("task,side", [
+    ({"data_downsample": 2}, 384),
+    ({"data_downsample": 3, "downsample_mode": "linear", "upsample_mode": "linear"}, 576),
+    ({"data_downsample": 1.5}, 289),   # floor(289 / 1.5) = 192 (F.interpolate's size)
+    ({"downsample_mode": "linear", "upsample_mode": "cubic"}, 192),
+    ({"downsample_mode": "cubic", "upsample_mode": "linear"}, 192),
+])
+def test_data_downsample_step_vs_oracle(task, side):
+    """apply_network's data_downsample (dual_trainer.py:561-563) at even, odd and
+    fractional factors, and task.downsample_mode / upsample_mode (torch_interp_mode,
+    array.py:37-41: 'linear' -> bilinear, 'cubic' -> bicubic): the HR batch is
+    downsampled by ds first and becomes both the loss target and the source of the
+    model input (downsample_mode); the interp metric compares it with the upsampled
+    input (upsample_mode, :316-317)."""
+    from srmi.config import data_downsample_factor, interp_mode
     d = dev()
     spec = NetSpec(arch="rcan", nchannels_in=2, nchannels_out=2, nfeatures=64, nlayers=1, nblocks=2,
                    cbottleneck=2, scale=4)
@@ -318,19 +328,25 @@ def test_data_downsample_step_vs_oracle():
     table = param_table(spec)
     sd = dict(model.named_parameters())
     flat = torch.cat([sd[n].detach().reshape(-1).float() for n, _, _, _ in table])
-    hr = ro.synthetic_hr(4, 2, 384, 78)
-    tr = FusedTrainer(spec, 4, (48, 48), device=d, params=flat.to(d), task={"data_downsample": 2})
+    hr = ro.synthetic_hr(4, 2, side, 78)
+    tr = FusedTrainer(spec, 4, (48, 48), device=d, params=flat.to(d), task=task)
     res = tr.step(torch.tensor(hr, device=d))
     torch.cuda.synchronize()
-    with pytest.raises(ValueError, match="data_downsample"):  # tiles of the wrong size
-        tr.step(torch.zeros(4, 2, 192, 192, device=d))
+    ds = data_downsample_factor(task)
+    dm, um = interp_mode(task, True), interp_mode(task, False)
+    if ds > 1:
+        with pytest.raises(ValueError, match="data_downsample"):  # tiles of the wrong size
+            tr.step(torch.zeros(4, 2, 192, 192, device=d))
     model = model.double()
-    h = ro.downsample(torch.tensor(hr, dtype=torch.float64), 2)
-    lr_in = ro.downsample(h, 4)
+    h = torch.tensor(hr, dtype=torch.float64)
+    if ds > 1:
+        h = ro.downsample(h, ds, dm)
+    assert tuple(h.shape[2:]) == (192, 192)
+    lr_in = ro.downsample(h, 4, dm)
     out = model(lr_in)
     loss = ro.l2loss(out, h)
     loss.backward()
-    iloss = float(ro.l2loss(h, ro.upsample(lr_in, 4)))
+    iloss = float(ro.l2loss(h, ro.upsample(lr_in, 4, um)))
     assert abs(float(res["loss"]) - float(loss)) < 2e-3 * float(loss)
     assert abs(float(res["interp_loss"]) - iloss) < 1e-5 * iloss
     g = dict(model.named_parameters())

@@ -96,20 +96,28 @@ def test_tiled_inference_matches_oracle(graph):
     assert rel_l2(images2["model"].cpu().numpy(), ref_img2["model"]) < 2e-2
 
 
-@pytest.mark.parametrize("graph", [True, False])
-def test_tiled_inference_data_downsample_vs_oracle(graph):
+@pytest.mark.parametrize("graph,task,tile", [
+    (True, {"data_downsample": 2}, 384),
+    (False, {"data_downsample": 2}, 384),
+    (True, {"data_downsample": 3, "downsample_mode": "linear", "upsample_mode": "linear"}, 576),
+    (False, {"data_downsample": 1.5, "upsample_mode": "linear"}, 289),
+])
+def test_tiled_inference_data_downsample_vs_oracle(graph, task, tile):
     """apply_network's data_downsample in process_image (dual_trainer.py:423,
-    :561-563): the normalised 384² tiles are downsampled by 2 first, so target, model
-    and interpolated -- and their mosaics -- are at 192² per tile."""
+    :561-563) at even, odd and fractional factors, with task.downsample_mode /
+    upsample_mode (array.py:37-41): the normalised tiles are downsampled by ds first,
+    so target, model and interpolated -- and their mosaics -- are at 192² per tile."""
+    from srmi.config import data_downsample_factor, interp_mode
     d = dev()
     spec, model, flat = _small_rcan()
     rng = np.random.RandomState(9)
-    base = rng.randn(1, 2 * 384 + 5, 2 * 384 + 11)
+    base = rng.randn(1, 2 * tile + 5, 2 * tile + 11)
     region = (base + np.roll(base, 1, 1) + np.roll(base, 1, 2)).astype(np.float32)
-    ti = TiledInference(spec, flat.to(d), region.shape, (384, 384), device=d, graph=graph,
-                        task={"data_downsample": 2})
+    ti = TiledInference(spec, flat.to(d), region.shape, (tile, tile), device=d, graph=graph, task=task)
     images, losses = ti.process_region(torch.tensor(region, device=d))
-    ref_img, ref_loss = ro.process_region(model, region.astype(np.float64), 384, 384, 4, data_downsample=2)
+    ref_img, ref_loss = ro.process_region(model, region.astype(np.float64), tile, tile, 4,
+                                          data_downsample=data_downsample_factor(task),
+                                          dmode=interp_mode(task, True), umode=interp_mode(task, False))
     assert images["target"].shape[-1] == 2 * 192 and images["input"].shape[-1] == 2 * 48
     for k in ("input", "target", "interpolated"):
         assert rel_l2(images[k].cpu().numpy(), ref_img[k]) < 1e-5, k

@@ -380,6 +380,55 @@ def test_downsample_upsample_match_reference():
     np.testing.assert_allclose(up.double().cpu().numpy(), gd["up4_out"], rtol=1e-5, atol=1e-5)
 
 
+INTERP_CASES = ["down_linear_4", "down_linear_8", "down_linear_3", "down_linear_1p5", "down_cubic_3",
+                "down_cubic_1p5", "down_cubic_6", "up_linear_4", "up_linear_4b"]
+
+
+@pytest.mark.parametrize("case", INTERP_CASES)
+def test_interpolate_modes_match_reference(case):
+    """srmi_interpolate (through srmi.engine.downsample / upsample) against the
+    reference's own downsample / upsample under task.downsample_mode /
+    upsample_mode 'linear' / 'cubic' (array.py:37-41, :72-76, :84-87) at the model
+    scale and at odd / fractional data_downsample factors: golden vectors of
+    tests/golden/make_golden_interp.py (fp64 reference on the fp32 inputs)."""
+    import os
+    from oracle import rcan_oracle as ro
+    from srmi.engine import downsample, upsample
+    d = dev()
+    gd = np.load(os.path.join(os.path.dirname(__file__), "golden", "interp.npz"))
+    B, C, T = (int(v) for v in gd[f"{case}_shape"][:3])
+    x = ro.synthetic_hr(B, C, T, int(gd[f"{case}_seed"]))
+    assert abs(x.astype(np.float64).sum() - float(gd[f"{case}_in_sum"])) < 1e-6
+    sf = float(gd[f"{case}_sf"])
+    mode = "bilinear" if "linear" in case else "bicubic"
+    xt = torch.tensor(x).to(d)
+    y = downsample(xt, sf, mode=mode) if case.startswith("down") else upsample(xt, int(sf), mode=mode)
+    torch.cuda.synchronize()
+    ref = gd[f"{case}_out"]
+    assert tuple(y.shape) == ref.shape
+    np.testing.assert_allclose(y.double().cpu().numpy(), ref, rtol=1e-5, atol=2e-6)
+
+
+def test_batch_losses_beyond_1024_tiles_one_batch():
+    """Per-tile sums of more than 1024 tiles (a multi-rank tiled-inference rank's
+    share, srmi.inference._process_region_ranks): one batch of all tiles keeps the
+    mean pass within its 1024-batch bound while `work` holds every tile's sum."""
+    d = dev()
+    n, te = 1500, 48
+    g = torch.Generator(device="cpu").manual_seed(3)
+    y = torch.randn(n, te, generator=g).to(d)
+    t = torch.randn(n, te, generator=g).to(d)
+    work = torch.zeros(n, device=d)
+    out = torch.zeros(2, device=d)
+    call("srmi_batch_losses", ptr(y), ptr(t), n, te, n, _lib.SRMI_LOSS_RMSE, 1e-6, ptr(work), ptr(out), S())
+    torch.cuda.synchronize()
+    ref = ((y.double() - t.double()) ** 2).sum(dim=1)
+    assert rel_l2(work, ref) < 1e-6
+    assert abs(float(out[0]) - math.sqrt(float(ref.sum()) / (n * te))) < 1e-5
+    with pytest.raises(_lib.SrmiError):  # batches of one tile exceed the bound
+        call("srmi_batch_losses", ptr(y), ptr(t), n, te, 1, _lib.SRMI_LOSS_RMSE, 1e-6, ptr(work), ptr(out), S())
+
+
 def test_adam_matches_reference():
     import os
     d = dev()

@@ -118,7 +118,8 @@ def test_config_identity_keys_and_derived_paths(tmp_path, monkeypatch):
 
 def test_fused_trainer_apply_network_target_selection_and_refusals():
     """apply_network (dual_trainer.py:557-571): data_downsample only acts when > 1
-    (even integer factors; others refused); the target is index_selected only when
+    (any factor: srmi.engine.downsample runs the general F.interpolate kernel for
+    the odd / fractional ones); the target is index_selected only when
     the batch has more channels than target_variables, in the INPUT's order
     (np.in1d(channels, targets)); equal counts in another order are a no-op."""
     from srmi.engine import NetSpec
@@ -129,9 +130,8 @@ def test_fused_trainer_apply_network_target_selection_and_refusals():
     assert check_fused_task({"data_downsample": 2.0}, 1, 1) is None  # the trainer downsamples by 2 first
     assert data_downsample_factor({"data_downsample": 0.5}) == 1
     assert data_downsample_factor({"data_downsample": 4}) == 4
-    for bad in (3, 1.5):  # the bicubic kernel's half-way form: even integer factors
-        with pytest.raises(NotImplementedError, match="data_downsample"):
-            check_fused_task({"data_downsample": bad}, 1, 1)
+    for ok in (3, 1.5):  # odd and fractional factors: the general interpolation kernel
+        assert check_fused_task({"data_downsample": ok}, 1, 1) is None
     with pytest.raises(NotImplementedError, match="subset"):
         check_fused_task({}, 2, 1)
     two = {"input_variables": {"SSS": "a", "SST": "b"}}
@@ -148,14 +148,13 @@ def test_fused_trainer_apply_network_target_selection_and_refusals():
     with pytest.raises(ValueError, match="broadcast"):  # a 2-of-3 target cannot meet the 3-channel interp input
         FusedTrainer(NetSpec(nchannels_in=3, nchannels_out=2), 2, device=torch.device("cpu"),
                      task={"input_variables": ["A", "B", "C"], "target_variables": ["A", "C"]})
-    with pytest.raises(NotImplementedError):
-        FusedTrainer(NetSpec(), 2, device=torch.device("cpu"), task={"data_downsample": 3})
     from srmi.inference import TiledInference
-    with pytest.raises(NotImplementedError, match="data_downsample"):  # odd factors: also in inference
+    with pytest.raises(ValueError, match="divisible"):  # floor(384 / 5) = 76 is no multiple of the scale 4
         TiledInference(NetSpec(), torch.empty(0), (1, 384, 384), device=torch.device("cpu"),
-                       task={"data_downsample": 3})
-    with ConfigContext("sres", dict(model="rcan-10-20-64", task="SST-tiles-48"), **{"task.data_downsample": 3}):
-        assert cfg().task.data_downsample == 3
+                       task={"data_downsample": 5})
+    with ConfigContext("sres", dict(model="rcan-10-20-64", task="SST-tiles-48"),
+                       **{"task.downsample_mode": "nearest"}):
+        assert cfg().task.downsample_mode == "nearest"
         with pytest.raises(NotImplementedError):  # (read from the active context)
             FusedTrainer(NetSpec(), 2, device=torch.device("cpu"))
 
