@@ -67,6 +67,12 @@ def parse():
                     help="diagnostic: the DP path (RCCL group, reducer stream, bucketed all-reduce) at one rank")
     ap.add_argument("--ca-fold", action="store_true",
                     help="A/B: fold each RCAB's CA backward into the conv launches (SRMI_FLAG_CA_FOLD)")
+    ap.add_argument("--dp-reducer-stream", action="store_true",
+                    help="A/B: the DP all-reduce on a reducer stream of its own (the event-driven schedule)")
+    ap.add_argument("--ca-pass", action="store_true",
+                    help="A/B: the training CA forward as a pass of its own after conv2 (SRMI_FLAG_CA_PASS)")
+    ap.add_argument("--ca-scale-launch", action="store_true",
+                    help="A/B: the training CA scale as a launch of its own (SRMI_FLAG_CA_SCALE_LAUNCH)")
     ap.add_argument("--no-rcab-infer", action="store_true",
                     help="A/B: inference RCABs as three launches (SRMI_FLAG_NO_RCAB_INFER)")
     return ap.parse_args()
@@ -97,25 +103,22 @@ def _pmc_traffic(kernel_prefix):
     return None
 
 
-def _pmc_region_bytes():
-    """Fabric bytes of one C5 region from the committed rocprofv3 --pmc summary of the
-    inference leg (tools/pmc_infer.sh): per-launch FETCH_SIZE x2 + WRITE_SIZE times the
-    launches of that run, over its regions (region_to_tiles_kernel runs once per region)."""
+def _pmc_infer_traffic(side, flags):
+    """HBM bytes per launch of the inference RCAB kernel from the newest committed
+    rocprofv3 --pmc summary of the C5 leg (tools/pmc_infer.sh: FETCH_SIZE x2 +
+    WRITE_SIZE, gfx950-corrected), only when that summary was taken at the same
+    configuration (its "config": region side and engine flags); else None."""
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_infer*.json")), reverse=True):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        kern = {k: v for k, v in d.items() if isinstance(v, dict) and "hbm_bytes_per_launch" in v}
-        regions = [v["dispatches"][0] for k, v in kern.items() if "region_to_tiles" in k]
-        if not regions or not regions[0]:
+        cfg = d.get("config") or {}
+        if cfg.get("infer_region") != side or cfg.get("flags", 0) != flags:
             continue
-        total = sum(v["hbm_bytes_per_launch"] * v["dispatches"][0] for k, v in kern.items()
-                    if "pack_tile" not in k)  # (the filter packs: once per model, not per region)
-        rcab = {k: v["hbm_bytes_per_launch"] for k, v in kern.items()
-                if "rcab_infer2_kernel" in k or "rcab_infer_kernel<false>" in k}
-        return {"bytes": total / regions[0], "source": os.path.relpath(f, ROOT),
-                "rcab_launch_bytes": next(iter(rcab.values()), None)}
+        for k, v in d.items():
+            if isinstance(v, dict) and "hbm_bytes_per_launch" in v and "rcab_infer_kernel" in k:
+                return {"bytes": v["hbm_bytes_per_launch"], "source": os.path.relpath(f, ROOT)}
     return None
 
 
@@ -151,6 +154,34 @@ F2_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE
 FUSED_FLOP_PER_TILE = 2 * CONV64_FLOP_PER_TILE   # one dgrad conv + one filter-gradient conv
 
 
+def _prof_in_step_us(key):
+    """In-step average launch duration (us) of the fused backward kernel `key` (F1 / F2)
+    from the newest committed rocprofv3 kernel-trace summary of the bench
+    (tools/prof_summary.py -> profiles/rNN_prof_summary.json), or None."""
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*prof_summary*.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+            return {"in_step_avg_us": d["fused"][key]["in_step_avg_us"], "source": os.path.relpath(f, ROOT)}
+        except Exception:
+            continue
+    return None
+
+
+def _probe_ms(issue, streams, reps):
+    """Average per-launch duration (ms) on each stream of `reps` launches issued by
+    issue(reps) (after 3 warm-up launches), HIP events on those streams."""
+    issue(3)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in streams]
+    for k, st in enumerate(streams):
+        ev[k][0].record(st)
+    issue(reps)
+    for k, st in enumerate(streams):
+        ev[k][1].record(st)
+    torch.cuda.synchronize()
+    return [ev[k][0].elapsed_time(ev[k][1]) / reps for k in range(len(streams))]
+
+
 def fused_rooflines(tr, step_ms, reps=20):
     # per engine and step: conv2's fused launch (F2) runs once per RCAB; conv1's
     # (F1, EPI_DG_ACC_CA) once per RCAB except the first of each residual group, whose
@@ -158,12 +189,16 @@ def fused_rooflines(tr, step_ms, reps=20):
     # different kernel: engine.cpp backward_impl)
     """Roofline of the dominant kernel AT ITS IN-STEP CONFIGURATION: the bench's own
     trainer engines re-issue their fused backward launch of one RCAB
-    (srmi_engine_probe: same parameters, buffers, grid and CU split as inside the
-    step) `reps` times, every micro-batch engine on its own stream concurrently, as
-    in the step.  HIP events are recorded on each engine's stream; the per-launch
-    average duration is the slowest stream's elapsed / reps (the launches of the
-    engines overlap, so one launch slot moves micro x the per-engine bytes).
-    `achieved` = algorithmic bytes of all launches of one slot / average duration."""
+    (srmi_engine_probe: same parameters, buffers, grid and CU split as inside the step),
+    HIP events on the engines' own streams.  Two measurements:
+    * per launch -- the `roofline` numbers (`frac`): engine 0 alone issues `reps`
+      launches, one at a time, as a rocprofv3 kernel trace of the step sees them (the
+      profiler serialises the streams): achieved = algorithmic bytes of ONE launch / its
+      average duration.  `rocprof_check` recomputes it from the committed kernel-trace
+      summary's in-step average of the same kernel;
+    * concurrent slot (`concurrent`): every micro-batch engine issues its launch on its
+      own stream at once, as in the step; bytes of all launches of a slot / the slowest
+      stream's average -- what the two engines move together, not one launch's roofline."""
     from srmi._lib import call
     main_st = torch.cuda.current_stream()
     n_eng = len(tr.engines)
@@ -172,43 +207,48 @@ def fused_rooflines(tr, step_ms, reps=20):
     nl, nb = tr.spec.nlayers, tr.spec.nblocks
     per_step = {1: nl * (nb - 1), 2: nl * nb}
     fold = bool(tr.spec.flags & 1)
-    for which, name, bpt in ((1, "rcab_bwd_kernel<EPI_DG_ACC_CA>", F1_FOLD_BYTES_PER_TILE if fold else F1_BYTES_PER_TILE),
-                             (2, "rcab_bwd_kernel<EPI_DG_RELUMASK>", F2_BYTES_PER_TILE)):
-        streams = [tr.streams[k] or main_st for k in range(n_eng)]
-
-        def issue(r):
+    streams = [tr.streams[k] or main_st for k in range(n_eng)]
+    for which, key, name, bpt in ((1, "F1", "rcab_bwd_kernel<EPI_DG_ACC_CA>",
+                                   F1_FOLD_BYTES_PER_TILE if fold else F1_BYTES_PER_TILE),
+                                  (2, "F2", "rcab_bwd_kernel<EPI_DG_RELUMASK>", F2_BYTES_PER_TILE)):
+        def issue_all(r):
             for k, eng in enumerate(tr.engines):
                 call("srmi_engine_probe", eng._h, which, r, streams[k].cuda_stream)
 
-        issue(3)
-        torch.cuda.synchronize()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in streams]
-        for k, st in enumerate(streams):
-            ev[k][0].record(st)
-        issue(reps)
-        for k, st in enumerate(streams):
-            ev[k][1].record(st)
-        torch.cuda.synchronize()
-        per_stream = [ev[k][0].elapsed_time(ev[k][1]) / reps for k in range(n_eng)]
+        def issue_one(r):
+            call("srmi_engine_probe", tr.engines[0]._h, which, r, streams[0].cuda_stream)
+
+        ms1 = _probe_ms(issue_one, streams[:1], reps)[0]
+        per_stream = _probe_ms(issue_all, streams, reps)
         ms = max(per_stream)
-        bytes_slot = bpt * tiles_per_engine * n_eng + WGRAD_OUT_BYTES * n_eng
-        flop_slot = FUSED_FLOP_PER_TILE * tiles_per_engine * n_eng
-        ach = bytes_slot / (ms * 1e-3) / 1e9
-        tf = flop_slot / (ms * 1e-3) / 1e12
+        bytes_launch = bpt * tiles_per_engine + WGRAD_OUT_BYTES
+        flop_launch = FUSED_FLOP_PER_TILE * tiles_per_engine
+        ach = bytes_launch / (ms1 * 1e-3) / 1e9
+        tf = flop_launch / (ms1 * 1e-3) / 1e12
+        ach_slot = bytes_launch * n_eng / (ms * 1e-3) / 1e9
         tr_ = _pmc_traffic("rcab_bwd_kernel<%d" % (7 if which == 1 else 4))
+        prof = _prof_in_step_us(key)
+        rc = None
+        if prof:
+            a = bytes_launch / (prof["in_step_avg_us"] * 1e-6) / 1e9
+            rc = {"in_step_avg_us": prof["in_step_avg_us"], "achieved": round(a, 1),
+                  "frac": round(a / HBM_PEAK_GBS, 4), "source": prof["source"]}
         out[which] = {
             "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4),
-            "traffic": (tr_["bytes"] * n_eng if tr_ and tr_["bytes"] is not None else None),
-            "traffic_per_launch": tr_["bytes"] if tr_ else None,
+            "traffic": tr_["bytes"] if tr_ and tr_["bytes"] is not None else None,
             "traffic_source": tr_["source"] if tr_ else None,
             "kernel": "srmi::" + name, "in_step": True, "ca_fold": fold,
-            "config": f"{n_eng} concurrent launch(es) (one per micro-batch engine), {tiles_per_engine} tiles each, "
-                      "in-step grid and CU split",
-            "avg_launch_ms": round(ms, 4), "per_stream_ms": [round(x, 4) for x in per_stream],
-            "bytes_per_launch": bpt * tiles_per_engine + WGRAD_OUT_BYTES, "launches_per_slot": n_eng,
-            "flop_per_launch": FUSED_FLOP_PER_TILE * tiles_per_engine, "mfma_tflops": round(tf, 1),
-            "mfma_frac": round(tf / PEAK_BF16_TFLOPS, 4),
+            "frac_is": "per launch: algorithmic bytes of one launch / its average duration, the launch alone "
+                       "on the chip (engine 0's stream, in-step grid and CU split)",
+            "config": f"one launch of {tiles_per_engine} tiles (micro-batch engine 0), in-step grid and CU split",
+            "avg_launch_ms": round(ms1, 4), "bytes_per_launch": bytes_launch, "flop_per_launch": flop_launch,
+            "mfma_tflops": round(tf, 1), "mfma_frac": round(tf / PEAK_BF16_TFLOPS, 4),
+            "rocprof_check": rc,
+            "concurrent": {"launches_per_slot": n_eng, "per_stream_ms": [round(x, 4) for x in per_stream],
+                           "achieved": round(ach_slot, 1), "frac": round(ach_slot / HBM_PEAK_GBS, 4),
+                           "note": "all micro-batch engines' launches at once, as in the step: bytes of the "
+                                   "slot / slowest stream's average"},
             "launches_per_engine_per_step": per_step[which],
             "share_of_step": round(ms * per_step[which] / step_ms, 3),
         }
@@ -241,6 +281,53 @@ def conv_fwd_roofline(dev, batch):
             "kernel": "srmi::conv64_kernel<48,RELU>", "in_step": False, "config": f"isolated, {N} tiles",
             "avg_launch_ms": round(ms_c, 4), "flop_per_launch": flop,
             "bytes_per_launch": 2 * N * ACT_BF16_PER_TILE + 64 * 576 * 2}
+
+
+RCAB_INFER_BYTES_PER_IMAGE = 48 * 48 * 64 * 10     # h pair in + out (3 + 3 B), t written + read (2 + 2 B)
+RCAB_INFER_FLOP_PER_IMAGE = 2 * CONV64_FLOP_PER_TILE  # conv1 + conv2 (the CA MLP is negligible)
+
+
+def infer_rcab_roofline(ti, side, flags, reps=20):
+    """Roofline of C5's dominant kernel, the one-launch inference RCAB
+    (rcab_infer_kernel: conv1 -> CA scale -> conv2 + h' = h + s u, a workgroup per
+    image), at its in-region configuration: srmi_engine_probe(which = 3) re-issues RCAB
+    (0, 2) of the last forward on the engine's own stream, HIP events there.  Per
+    launch, the launch alone on the chip (as a rocprofv3 trace sees it): algorithmic
+    bytes (RCAB_INFER_BYTES_PER_IMAGE x images) / average duration; the MFMA fraction
+    of the same launch beside it.  `concurrent`: every engine's launch at once, as in the
+    region.  `traffic`: PMC bytes per launch from a committed summary of the SAME
+    configuration, else null."""
+    from srmi._lib import call
+    main_st = torch.cuda.current_stream()
+    streams = [ti.streams[k] or main_st for k in range(len(ti.engs))]
+    n = ti.engs[0].batch
+
+    def issue_one(r):
+        call("srmi_engine_probe", ti.engs[0]._h, 3, r, streams[0].cuda_stream)
+
+    def issue_all(r):
+        for k, e in enumerate(ti.engs):
+            call("srmi_engine_probe", e._h, 3, r, streams[k].cuda_stream)
+
+    ms1 = _probe_ms(issue_one, streams[:1], reps)[0]
+    per_stream = _probe_ms(issue_all, streams, reps)
+    nb = RCAB_INFER_BYTES_PER_IMAGE * n
+    nf = RCAB_INFER_FLOP_PER_IMAGE * n
+    ach = nb / (ms1 * 1e-3) / 1e9
+    tf = nf / (ms1 * 1e-3) / 1e12
+    tot = sum(e.batch for e in ti.engs)
+    ach_slot = RCAB_INFER_BYTES_PER_IMAGE * tot / (max(per_stream) * 1e-3) / 1e9
+    tr_ = _pmc_infer_traffic(side, flags)
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": round(tr_["bytes"]) if tr_ else None, "traffic_source": tr_["source"] if tr_ else None,
+            "kernel": "srmi::rcab_infer_kernel", "images_per_launch": n, "avg_launch_ms": round(ms1, 4),
+            "bytes_per_launch": nb, "flop_per_launch": nf, "mfma_tflops": round(tf, 1),
+            "mfma_frac": round(tf / PEAK_BF16_TFLOPS, 4),
+            "frac_is": "per launch: algorithmic bytes (h pair in/out, t written/read: 10 B per element) / "
+                       "average duration, the launch alone on the chip",
+            "concurrent": {"launches": len(ti.engs), "per_stream_ms": [round(x, 4) for x in per_stream],
+                           "achieved": round(ach_slot, 1), "frac": round(ach_slot / HBM_PEAK_GBS, 4)}}
 
 
 def inference_bench(dev, side, iters, flags=0, info=None):
@@ -286,14 +373,9 @@ def inference_bench(dev, side, iters, flags=0, info=None):
         e1.synchronize()
         ms = e0.elapsed_time(e1) / iters
     mpix = ti.n * 192 * 192 / 1e6
-    tr_ = _pmc_region_bytes()
     roof = None
-    if tr_ and not multi:  # the region's fabric bytes (PMC) over its time: the bound of C5
-        gbs = tr_["bytes"] / (ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": round(tr_["bytes"]),
-                "traffic_rcab_launch": tr_["rcab_launch_bytes"], "traffic_source": tr_["source"],
-                "note": "PMC fabric bytes per region (all kernels) / ms_per_region"}
+    if not multi and not (flags & 2):
+        roof = infer_rcab_roofline(ti, side, flags)
     return {"metric": "inference MPix/sec (HR pixels produced)", "value": round(mpix / (ms * 1e-3), 2),
             "roofline": roof,
             "unit": "MPix/s", "ms_per_region": round(ms, 3), "tiles": ti.n, "hr_mpix_per_region": round(mpix, 3),
@@ -352,8 +434,9 @@ def dp_overhead_probe(args, reps=2):
             "--no-dp-probe", "--steps", str(args.steps), "--warmup", str(args.warmup), "--batch", str(args.batch)]
     if args.micro is not None:
         base += ["--micro", str(args.micro)]
-    if args.ca_fold:
-        base += ["--ca-fold"]
+    for flag in ("ca_fold", "ca_pass", "ca_scale_launch", "dp_reducer_stream"):
+        if getattr(args, flag):
+            base += ["--" + flag.replace("_", "-")]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
     best = {"plain": 0.0, "dp": 0.0}
     micro = None
@@ -367,7 +450,8 @@ def dp_overhead_probe(args, reps=2):
             micro = line.get("micro", micro)
     return {"tiles_per_s_plain": round(best["plain"], 2), "tiles_per_s_dp": round(best["dp"], 2),
             "overhead_frac": round(1.0 - best["dp"] / best["plain"], 4),
-            "streams_per_rank": f"{micro} engine stream(s) + 1 reducer comm stream (+ RCCL internal)",
+            "streams_per_rank": (f"{micro} engine stream(s) + 1 reducer comm stream (+ RCCL internal)"
+                                 if args.dp_reducer_stream else f"{micro} engine stream(s) (+ RCCL internal)"),
             "config": f"1-rank RCCL group, {micro} micro-batch engine(s), same B={args.batch}, child process per "
                       f"leg (one trainer per process, as a rank), best of {reps} interleaved rounds of "
                       f"{args.steps} steps"}
@@ -458,11 +542,13 @@ def main():
                                                                            2 if args.no_rcab_infer else 0)}
         print(json.dumps(rec), flush=True)
         return
-    from srmi._lib import SRMI_FLAG_CA_FOLD
+    from srmi._lib import SRMI_FLAG_CA_FOLD, SRMI_FLAG_CA_PASS, SRMI_FLAG_CA_SCALE_LAUNCH
+    flags = ((SRMI_FLAG_CA_FOLD if args.ca_fold else 0) | (SRMI_FLAG_CA_PASS if args.ca_pass else 0) |
+             (SRMI_FLAG_CA_SCALE_LAUNCH if args.ca_scale_launch else 0))
     spec = NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=10, nblocks=20,
-                   cbottleneck=2, scale=4, flags=SRMI_FLAG_CA_FOLD if args.ca_fold else 0)
+                   cbottleneck=2, scale=4, flags=flags)
     tr = FusedTrainer(spec, B, (48, 48), lr=1e-4, interp_loss=not args.no_interp_loss, info=info, device=dev, seed=0,
-                      micro=args.micro, cu_budget=args.cu_budget)
+                      micro=args.micro, cu_budget=args.cu_budget, dp_reducer_stream=args.dp_reducer_stream)
     hr = torch.tensor(synthetic_hr(B, C, 192, 1234 + info.rank)).to(dev)
 
     micro = tr.micro

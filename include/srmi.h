@@ -88,6 +88,12 @@ typedef struct srmi_model_config {
 /* SRMI_FLAG_NO_RCAB_INFER: inference engines run each RCAB as three launches (conv1,
  * conv2 + pool, CA) instead of one launch with a workgroup per image (A/B, tests) */
 #define SRMI_FLAG_NO_RCAB_INFER 2
+/* training forward (A/B, tests): SRMI_FLAG_CA_PASS runs each RCAB's channel attention as
+ * a pass of its own after conv2 (conv1, conv2 + pool writing u, CA pass) instead of inside
+ * conv2's launch; SRMI_FLAG_CA_SCALE_LAUNCH computes the CA scale s in a launch of its
+ * own between conv1 and conv2 instead of in every conv2 workgroup's prologue */
+#define SRMI_FLAG_CA_PASS 4
+#define SRMI_FLAG_CA_SCALE_LAUNCH 8
 
 typedef struct srmi_param_info {
   long long offset; /* element offset in the flat fp32 parameter buffer     */
@@ -126,12 +132,23 @@ int srmi_forward(srmi_engine* e, const float* params, const float* lr, float* sr
 int srmi_backward(srmi_engine* e, const float* params, const float* lr, const float* sr, const float* hr,
                   const float* loss4, const float* dy, float* grads, void** group_events, void* stream);
 
+/* the same backward in stages, so that a caller can enqueue work between them (a
+ * residual group's gradient all-reduce right behind that group, srmi.trainer): stages
+ * 0 = tail conv, upsamplers and body tail; 1 .. nlayers = residual groups nlayers-1 ..
+ * 0; nlayers + 1 = head (RCAN; EDSR has one stage).  srmi_backward_stages runs stages
+ * first .. last (in order, each exactly once per backward); group_events as above. */
+int srmi_backward_stage_count(srmi_engine* e);
+int srmi_backward_stages(srmi_engine* e, const float* params, const float* lr, const float* sr, const float* hr,
+                         const float* loss4, const float* dy, float* grads, void** group_events, int first, int last,
+                         void* stream);
+
 /* diagnostic (bench roofline): re-issue `reps` times on `stream` the fused backward
  * launch of RCAB (0, 2) exactly as srmi_backward issues it (same shapes, CU split,
  * row chunks) -- which = 1: dgrad of conv1 accumulating into the gradient stream
  * (+ CA sums) beside conv1's filter gradient; which = 2: the ReLU-mask dgrad of
  * conv2 beside conv2's filter gradient -- on the buffers of the last backward
- * (their contents are overwritten).  RCAN train engines only. */
+ * (their contents are overwritten).  RCAN train engines; which = 3: an RCAN
+ * inference engine's one-launch RCAB (0, 2) on the buffers of the last forward. */
 int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream);
 
 /* RMSE (l2loss, squared=False).  loss4[0] = sum of squares (this rank),

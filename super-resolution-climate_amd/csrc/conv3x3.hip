@@ -356,6 +356,22 @@ static int launch_tw(const ConvParams& p, hipStream_t st) {
   return 0;
 }
 
+// the epilogues only the 8-wave persistent-run body has (48-wide tiles, Cin = 64):
+// conv1 with t's per-strip sums and the training conv2 with the CA residual update
+template <int EPI>
+static int launch_v2_only(const ConvParams& p, hipStream_t st) {
+  if (p.Cin != 64 || p.Cout != 64 || p.in_mode != IN_PLAIN || p.W % 48 || p.H % kTH || SRMI_CONV_NW8 != 1)
+    return SRMI_ERR_SHAPE;
+  const int run_len = conv64_run_len(p, 48, p.cu_budget > 0 ? p.cu_budget : 256);
+  ConvParams q = p;
+  q.stamps = g_debug_stamps;
+  size_t lds = Conv2Smem<48>::TOTAL;
+  if (EPI == EPI_CA_RESID_U && p.cas_on) lds += kCaScaleFloats * sizeof(float);  // the scale's scratch
+  hipLaunchKernelGGL((conv64_kernel<48, EPI, 8>), dim3(conv64_blocks(p, 48, run_len)), dim3(512), lds, st, q, run_len);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int EPI>
 static int launch_epi(const ConvParams& p, hipStream_t st) {
   if (p.W % 48 == 0 && p.H % kTH == 0) return launch_tw<48, EPI>(p, st);
@@ -390,6 +406,17 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
     case EPI_DG_ACC:
       if (!p.yf || (p.part && !p.aux)) return SRMI_ERR_ARG;
       break;
+    case EPI_RELU_POOL:
+      if (!p.yb || !p.part || p.f32) return SRMI_ERR_ARG;
+      break;
+    case EPI_CA_RESID_U:
+      if (!p.yb || !p.yph || !p.ypl || (!p.r1 && (!p.r1h || !p.r1l)) || p.f32) return SRMI_ERR_ARG;
+      if (p.cas_on ? (!p.cas.t || !p.cas.part || !p.cas.w1 || !p.cas.b1 || !p.cas.w2 || !p.cas.b2 || !p.cas.bc2 ||
+                      !p.cas.rec || p.cas.CR < 4 || p.cas.CR > 32 || p.cas.CR % 4 ||
+                      p.cas.nstrips != conv3x3_nstrips(p.H, p.W))
+                   : !p.escale)
+        return SRMI_ERR_ARG;
+      break;
     default:
       break;
   }
@@ -414,6 +441,8 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
     case EPI_DG_ACC: return launch_epi<EPI_DG_ACC>(p, st);
     case EPI_PLAIN_BF16: return launch_epi<EPI_PLAIN_BF16>(p, st);
     case EPI_DG_ACC_CA: return launch_epi<EPI_DG_ACC_CA>(p, st);
+    case EPI_RELU_POOL: return launch_v2_only<EPI_RELU_POOL>(p, st);
+    case EPI_CA_RESID_U: return launch_v2_only<EPI_CA_RESID_U>(p, st);
     default: return SRMI_ERR_ARG;
   }
 }

@@ -5,6 +5,7 @@
 #include <type_traits>
 
 #include "ca_fold.hpp"
+#include "ca_scale.hpp"
 
 // the pair codec of the inference RCAB's CA_RESID epilogue (common.hpp: the fast form
 // by default; SRMI_PAIR_FAST=0 for the reference form, bit-identical to ca_fwd's)
@@ -79,9 +80,15 @@ struct EpiPre {
 #ifndef SRMI_DGACC_RUN
 #define SRMI_DGACC_RUN 1
 #endif
+// h' = h + s u into the residual pair: the inference RCAB's conv2 (u never stored) and
+// the training one's (u stored for backward, and rounded to bf16 before the product)
+template <int EPI>
+constexpr bool epi_cr() {
+  return EPI == EPI_CA_RESID || EPI == EPI_CA_RESID_U;
+}
 template <int EPI>
 constexpr bool epi_run() {
-  return EPI == EPI_DG_ACC_CA || (SRMI_DGACC_RUN && EPI == EPI_DG_ACC) || EPI == EPI_CA_RESID;
+  return EPI == EPI_DG_ACC_CA || (SRMI_DGACC_RUN && EPI == EPI_DG_ACC) || epi_cr<EPI>();
 }
 
 // one (pt, c) element (idx = pt * NCT + c), issued one or two per K-step
@@ -89,7 +96,7 @@ template <int NPT, int EPI, int NCT>
 __device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT, EPI, NCT>& e, int n, int cb, int y,
                                                  int x0, int fr, int fk, int ct0, int idx) {
   if constexpr (EPI == EPI_RESID || EPI == EPI_DG_ACC || EPI == EPI_DG_RELUMASK || EPI == EPI_DG_ACC_CA ||
-                EPI == EPI_CA_RESID) {
+                epi_cr<EPI>()) {
     const int pt = idx / NCT, c = idx % NCT;
     const size_t HW = (size_t)p.H * p.W;
     const size_t pix = (size_t)n * HW + (size_t)y * p.W + x0 + pt * 16 + fr;
@@ -110,7 +117,7 @@ __device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT
       const int i = kSh ? 2 * j + (ct0 >> 1) : j;
       const int lin = i * 1024 + lane * 16, lpx = lin >> 8, ch = (lin >> 4) & 15;
       const size_t oc = ((size_t)n * HW + (size_t)y * p.W + x0 + h * HALF + lpx) * p.Cout + cb * 64 + ch * 4;
-      if constexpr (EPI == EPI_CA_RESID) {  // h: the pair's raw bits (decoded in the store loop) or fp32
+      if constexpr (epi_cr<EPI>()) {  // h: the pair's raw bits (decoded in the store loop) or fp32
         if (p.r1h) {
           const uint2 hh = *reinterpret_cast<const uint2*>(p.r1h + oc);
           const uint32_t ll = *reinterpret_cast<const uint32_t*>(p.r1l + oc);
@@ -191,7 +198,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       const size_t o = pix * p.Cout + co;
       f32x4 v = acc[pt][c];
       if constexpr (EPI == EPI_RELU_BF16 || EPI == EPI_POOL_BF16 || EPI == EPI_RESID || EPI == EPI_PS_BF16 ||
-                    EPI == EPI_PLAIN_BF16 || EPI == EPI_RELU_POOL || EPI == EPI_CA_RESID) {
+                    EPI == EPI_PLAIN_BF16 || EPI == EPI_RELU_POOL || epi_cr<EPI>()) {
         v[0] += bias[c].x; v[1] += bias[c].y; v[2] += bias[c].z; v[3] += bias[c].w;
       }
       if constexpr (EPI == EPI_RELU_BF16 || EPI == EPI_RELU_POOL) {
@@ -236,10 +243,15 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
         fv[pt][c] = make_float4(v[0], v[1], v[2], v[3]);  // dx; g is added in the store loop
         continue;  // no bf16 copy
       }
-      if constexpr (kPart1) {
+      if constexpr (EPI == EPI_POOL_BF16) {  // the pooled mean of the fp32 conv output
         ps0[c][0] += v[0]; ps0[c][1] += v[1]; ps0[c][2] += v[2]; ps0[c][3] += v[3];
       }
       bv[pt][c] = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      if constexpr (EPI == EPI_RELU_POOL) {  // sums of the bf16 t conv2 reads (ca_scale.hpp)
+        const uint2 b = bv[pt][c];
+        ps0[c][0] += bf2f(b.x & 0xFFFFu); ps0[c][1] += bf2f(b.x >> 16);
+        ps0[c][2] += bf2f(b.y & 0xFFFFu); ps0[c][3] += bf2f(b.y >> 16);
+      }
     }
   }
   const int lane = tid & 63;
@@ -275,15 +287,20 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
           const int i = kShared ? 2 * j + half_id : j;
           const int lin = i * 1024 + lane * 16, lpx = lin >> 8, c = (lin >> 4) & 15;
           float4 val = *reinterpret_cast<const float4*>(stage + lpx * 256 + ((c ^ (lpx & 15)) << 4));
-          if constexpr (EPI == EPI_CA_RESID) {
+          if constexpr (epi_cr<EPI>()) {
             // h' = h + s u in the run layout (the lane's channels 4c..4c+3: s in fs), out as the pair
             const int q = h * (kShared ? RUNS / 2 : RUNS) + j;
             float4 hh = e.r1[q / NCT][q % NCT];
             if (p.r1h)
               hh = PAIR_DEC4(make_uint2(__float_as_uint(hh.x), __float_as_uint(hh.y)), __float_as_uint(hh.z));
+            const uint32_t oe = (uint32_t)((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4);  // element
+            if constexpr (EPI == EPI_CA_RESID_U) {  // u to bf16 (backward reads it), the product of bf16(u)
+              const uint2 ub = make_uint2(pack2(val.x, val.y), pack2(val.z, val.w));
+              st_wt8(rbb, p.yb, oe * 2, ub);
+              val = make_float4(bf2f(ub.x & 0xFFFFu), bf2f(ub.x >> 16), bf2f(ub.y & 0xFFFFu), bf2f(ub.y >> 16));
+            }
             const float o0 = fmaf(val.x, fs.x, hh.x), o1 = fmaf(val.y, fs.y, hh.y);
             const float o2 = fmaf(val.z, fs.z, hh.z), o3 = fmaf(val.w, fs.w, hh.w);
-            const uint32_t oe = (uint32_t)((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4);  // element
             uint2 hi;
             const uint32_t lo = PAIR_ENC4(o0, o1, o2, o3, hi);
             st_wt8(rph, p.yph, oe * 2, hi);
@@ -440,6 +457,7 @@ constexpr bool conv64_defers() {
   return ((SRMI_DEFER & 1) && EPI == EPI_RELU_BF16) || ((SRMI_DEFER & 2) && EPI == EPI_POOL_BF16) ||
          ((SRMI_DEFER & 4) && EPI == EPI_DG_RELUMASK) || ((SRMI_DEFER & 8) && EPI == EPI_DG_ACC_CA) ||
          ((SRMI_DEFER & 16) && EPI == EPI_RELU_POOL) || ((SRMI_DEFER & 32) && EPI == EPI_CA_RESID);
+  // (EPI_CA_RESID_U: the non-deferred body only)
 }
 template <int TW, int EPI, bool FOLD = false>
 __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_len, int bid, char* smem, int tail,
@@ -501,6 +519,13 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   STAMP(0);
 
   const bf16_t* xn = p.x + (size_t)n * p.H * p.W * 64;
+  // the training conv2 (EPI_CA_RESID_U, cas_on): its image's CA scale in the prologue;
+  // the scale's global operands are issued first, to land under the DMA wait
+  [[maybe_unused]] CaScalePre cq;
+  if constexpr (EPI == EPI_CA_RESID_U) {
+    static_assert(NW == 8, "the CA scale needs 512 threads");
+    if (p.cas_on) ca_scale_load(p.cas, n, p.H, p.W, cq);
+  }
 
   // LDS-DMA of one 4-row input group into its ring slot: one wave instruction per
   // 8 pixels (1 KiB), swizzle applied on the source side, halo lanes read the zero
@@ -576,12 +601,24 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   float4 fs = float4{0.f, 0.f, 0.f, 0.f};
   if constexpr (EPI == EPI_CA_RESID)
     fs = *reinterpret_cast<const float4*>(p.escale + (size_t)n * p.escale_stride + 4 * (lane & 15));
+  if constexpr (EPI == EPI_CA_RESID_U) {
+    if (!p.cas_on) fs = *reinterpret_cast<const float4*>(p.escale + (size_t)n * p.escale_stride + 4 * (lane & 15));
+  }
   if constexpr ((EPI == EPI_DG_ACC_CA && FOLD) || (EPI == EPI_DG_ACC && epi_run<EPI>())) {
     if (p.fold.du_out)
       fs = *reinterpret_cast<const float4*>(p.fold.s_rec + (size_t)n * (128 + p.fold.CR) + 64 + p.fold.CR +
                                             4 * (lane & 15));
   }
   __syncthreads();
+  if constexpr (EPI == EPI_CA_RESID_U) {
+    if (p.cas_on) {  // (the barrier above published every wave's filter DMA)
+      // scratch beyond the body's LDS (the launch adds kCaScaleFloats floats); the first
+      // workgroup of the image writes its record m | z1 | s for backward
+      float* sm = reinterpret_cast<float*>(smem + S::TOTAL);
+      ca_scale_finish<false>(p.cas, cq, n, p.H, p.W, sm, wl, ry == 0 && sx == 0 && cb == 0 && !tail_part);
+      fs = *reinterpret_cast<const float4*>(sm + kCaScaleS + 4 * (lane & 15));
+    }
+  }
 
 #pragma unroll 1
   for (int k = k0; k < k1; ++k) {
@@ -982,10 +1019,7 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
         for (int rr = 0; rr < 4; ++rr) {
           float x = v[rr];
           if constexpr (EPI == EPI_RELU_BF16) x = fmaxf(x + b[rr], 0.f);
-          if constexpr (EPI == EPI_RELU_POOL) {
-            x = fmaxf(x + b[rr], 0.f);
-            ps0[c][rr] += x;
-          }
+          if constexpr (EPI == EPI_RELU_POOL) x = fmaxf(x + b[rr], 0.f);  // (summed as bf16 below)
           if constexpr (EPI == EPI_POOL_BF16) {
             x += b[rr];
             ps0[c][rr] += x;
@@ -999,6 +1033,11 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
         }
       }
       const uint4 val = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+      if constexpr (EPI == EPI_RELU_POOL) {  // sums of the bf16 t conv2 reads (ca_scale.hpp)
+        const uint32_t w[4] = {val.x, val.y, val.z, val.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ps0[i >> 2][i & 3] += bf2f((i & 1) ? (w[i >> 1] >> 16) : (w[i >> 1] & 0xFFFFu));
+      }
       st_defer(rout, p.yb, (uint32_t)((pix * p.Cout + cb * 64 + chan(0, 0)) * 2), val);
     } else {
 #pragma unroll

@@ -215,7 +215,7 @@ struct srmi_engine {
   int max_cob = 0, max_cib = 0;  // largest Cout / 64, Cin / 64 of the packed convs
   bool tables_uploaded = false;
   int last_n = 0;
-  const float* probe_prm = nullptr;  // the parameters of the last backward (srmi_engine_probe)
+  const float* probe_prm = nullptr;  // the parameters of the last backward / inference forward (srmi_engine_probe)
 
   bf16_t* at(bf16_t* base, size_t elems) const {
     return reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(base) + elems * esz);
@@ -601,6 +601,26 @@ static bool use_rcab_infer(const srmi_engine* e) {
          e->P.cfg.arch == SRMI_ARCH_RCAN && e->w == 48 && e->h % 4 == 0 && CR >= 4 && CR <= 32 && CR % 4 == 0;
 }
 
+// training forward: the CA forward of an RCAB (CALayer, sres/model/rcan/network.py:
+// 31-47, 61-64) without a pass of its own.  conv1 writes t and its per-strip sums
+// (EPI_RELU_POOL); conv2 (EPI_CA_RESID_U) stores u for backward and adds s bf16(u) into
+// the residual pair in its epilogue, with s = the CA MLP of mean(u), and mean(u) from t's
+// statistics and conv2's bf16 filter image (ca_scale.hpp) -- computed by every conv2
+// workgroup in its prologue (1), or by a launch of its own between the convs (2).
+// 0: conv1, conv2 + pool writing u, the CA pass (ca_fwd) -- the exact-fp32 mode and tiles
+// other than 48 wide always run this form; SRMI_FLAG_CA_PASS selects it at run time.
+// bf16, 48-wide tiles, a bottleneck the scale code handles.
+#ifndef SRMI_CA_FWD
+#define SRMI_CA_FWD 1
+#endif
+static int ca_fwd_mode(const srmi_engine* e) {
+  const int CR = 64 / e->P.cfg.reduction;
+  if (!e->train || e->f32 || e->P.cfg.arch != SRMI_ARCH_RCAN || e->w != 48 || e->h % 4 || CR < 4 || CR > 32 ||
+      CR % 4 || (e->P.cfg.flags & SRMI_FLAG_CA_PASS))
+    return 0;
+  return (e->P.cfg.flags & SRMI_FLAG_CA_SCALE_LAUNCH) ? 2 : SRMI_CA_FWD;
+}
+
 // ------------------------------------------------------------------ forward
 static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float* sr, int n, hipStream_t st) {
   const Plan& P = e->P;
@@ -619,7 +639,30 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
           const ConvParams c2 = fwd_params(e, r.c2, e->Tm(g, b), n, h, w, e->Um(g, b), nullptr, nullptr, e->ppool, 1.f);
           RC(rcab_infer_launch(c1, c2, e->ppool, nstrips, prm + r.ca_w1, prm + r.ca_b1, prm + r.ca_w2, prm + r.ca_b2,
                                64 / R, b == 1 ? rin : nullptr, b == 1 ? nullptr : e->hb(g, b - 1),
-                               b == 1 ? nullptr : lo, e->hb(g, b), lo, e->recp(g, b), st, prm + r.c2.w, prm + r.c2.b));
+                               b == 1 ? nullptr : lo, e->hb(g, b), lo, e->recp(g, b), st));
+          continue;
+        }
+        if (const int mode = ca_fwd_mode(e)) {  // training: the CA forward inside conv2
+          uint8_t* lo = reinterpret_cast<uint8_t*>(e->Hf);  // the pair's lo8 remainder (as below)
+          RC(conv_fwd(e, r.c1, e->hb(g, b - 1), n, h, w, EPI_RELU_POOL, e->Tm(g, b), nullptr, nullptr, e->ppool, 1.f,
+                      st));
+          ConvParams c2 = fwd_params(e, r.c2, e->Tm(g, b), n, h, w, e->Um(g, b), nullptr, b == 1 ? rin : nullptr,
+                                     nullptr, 1.f);
+          c2.r1h = b == 1 ? nullptr : e->hb(g, b - 1);
+          c2.r1l = b == 1 ? nullptr : lo;
+          c2.yph = e->hb(g, b);
+          c2.ypl = lo;
+          const CaScale cas{e->Tm(g, b), e->ppool, nstrips, prm + r.ca_w1, prm + r.ca_b1, prm + r.ca_w2,
+                            prm + r.ca_b2, e->pbias + r.c2.pb_off, 64 / R, e->recp(g, b)};
+          if (mode == 2) {
+            RC(ca_scale_launch(cas, e->at(e->packs, r.c2.f_off), n, h, w, st));
+            c2.escale = e->recp(g, b) + 64 + 64 / R;  // s of the record m | z1 | s
+            c2.escale_stride = 128 + 64 / R;
+          } else {
+            c2.cas = cas;
+            c2.cas_on = 1;
+          }
+          RC(conv3x3_launch(c2, EPI_CA_RESID_U, st));
           continue;
         }
         RC(conv_fwd(e, r.c1, e->hb(g, b - 1), n, h, w, EPI_RELU_BF16, e->Tm(g, b), nullptr, nullptr, nullptr, 1.f, st));
@@ -661,48 +704,65 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
   }
   RC(tail_fwd_launch(cur, prm + P.tail.w, prm + P.tail.b, n, e->Co, H, W, sr, e->f32, st));
   e->last_n = n;
+  if (!e->train) e->probe_prm = prm;  // (srmi_engine_probe which = 3)
   return 0;
 }
 
 // ----------------------------------------------------------------- backward
+// Stages of the RCAN backward, in order: 0 = tail conv, upsamplers and body tail;
+// 1 .. nlayers = residual groups nlayers-1 .. 0; nlayers + 1 = the head.  backward_impl
+// runs stages s_lo .. s_hi (EDSR: all of them at once), so that a caller can enqueue a
+// group's gradient all-reduce right behind that group (srmi_backward_stages).
+static int backward_stages(const srmi_engine* e) { return e->P.cfg.arch == SRMI_ARCH_RCAN ? e->P.cfg.nlayers + 2 : 1; }
+
 static int backward_impl(srmi_engine* e, const float* prm, const float* lr, const float* sr, const float* hr,
-                         const float* loss4, const float* dy, float* grads, void** group_events, hipStream_t st) {
+                         const float* loss4, const float* dy, float* grads, void** group_events, hipStream_t st,
+                         int s_lo = 0, int s_hi = 1 << 30) {
   const Plan& P = e->P;
   const int n = e->last_n, h = e->h, w = e->w, HW = h * w;
   const int nstrips = conv3x3_nstrips(h, w);
   int H = h << P.nups, W = w << P.nups;
   e->probe_prm = prm;
-  // tail conv 64 -> C
-  const bf16_t* xlast = e->PS[P.nups - 1];
-  const float* yv = dy ? dy : sr;
-  const float* tv = dy ? nullptr : hr;
-  const float* lv = dy ? nullptr : loss4;
-  RC(tail_dgrad_launch(yv, tv, lv, prm + P.tail.w, n, e->Co, H, W, e->dPS[P.nups - 1], e->f32, st));
-  int nsl = 0;
-  RC(tail_wgrad_launch(yv, tv, lv, xlast, n, e->Co, H, W, e->slab, &nsl, e->f32, st));
-  RC(tail_wgrad_reduce_launch(e->slab, nsl, e->Co, grads + P.tail.w, grads + P.tail.b, st));
-  // upsamplers, last to first
-  for (int k = P.nups - 1; k >= 0; --k) {
-    H /= 2;
-    W /= 2;
-    const bf16_t* xin = k == 0 ? e->RESb : e->PS[k - 1];
-    RC(conv_wgrad(e, P.ups[k], xin, e->dPS[k], n, H, W, grads, true, 1.f, st));
-    if (k > 0)
-      RC(conv_dgrad(e, P.ups[k], e->dPS[k], n, H, W, EPI_PLAIN_BF16, e->dPS[k - 1], nullptr, nullptr, nullptr, nullptr,
-                    nullptr, nullptr, 1.f, st));
-    else
-      RC(conv_dgrad(e, P.ups[k], e->dPS[k], n, H, W, EPI_DG_ACC, e->dRESb, e->dRESf, nullptr, nullptr, nullptr,
-                    nullptr, nullptr, 1.f, st));
+  const bool rcan = P.cfg.arch == SRMI_ARCH_RCAN;
+  if (!rcan) {
+    s_lo = 0;
+    s_hi = 1 << 30;
+  }
+  const int nl = P.cfg.nlayers;
+  if (s_lo <= 0) {
+    // tail conv 64 -> C
+    const bf16_t* xlast = e->PS[P.nups - 1];
+    const float* yv = dy ? dy : sr;
+    const float* tv = dy ? nullptr : hr;
+    const float* lv = dy ? nullptr : loss4;
+    RC(tail_dgrad_launch(yv, tv, lv, prm + P.tail.w, n, e->Co, H, W, e->dPS[P.nups - 1], e->f32, st));
+    int nsl = 0;
+    RC(tail_wgrad_launch(yv, tv, lv, xlast, n, e->Co, H, W, e->slab, &nsl, e->f32, st));
+    RC(tail_wgrad_reduce_launch(e->slab, nsl, e->Co, grads + P.tail.w, grads + P.tail.b, st));
+    // upsamplers, last to first
+    for (int k = P.nups - 1; k >= 0; --k) {
+      H /= 2;
+      W /= 2;
+      const bf16_t* xin = k == 0 ? e->RESb : e->PS[k - 1];
+      RC(conv_wgrad(e, P.ups[k], xin, e->dPS[k], n, H, W, grads, true, 1.f, st));
+      if (k > 0)
+        RC(conv_dgrad(e, P.ups[k], e->dPS[k], n, H, W, EPI_PLAIN_BF16, e->dPS[k - 1], nullptr, nullptr, nullptr,
+                      nullptr, nullptr, nullptr, 1.f, st));
+      else
+        RC(conv_dgrad(e, P.ups[k], e->dPS[k], n, H, W, EPI_DG_ACC, e->dRESb, e->dRESf, nullptr, nullptr, nullptr,
+                      nullptr, nullptr, 1.f, st));
+    }
   }
   // body tail: res = conv(hb_last) + x0
-  const int nl = P.cfg.nlayers;
   float *gRf = e->GAf, *ghf = e->GBf;
   bf16_t *gRb = e->GAb, *ghb = e->GBb;
-  if (P.cfg.arch == SRMI_ARCH_RCAN) {
+  if (rcan) {
     const int nb = P.cfg.nblocks, R = P.cfg.reduction;
-    RC(conv_wgrad(e, P.body_tail, e->hb(nl, 0), e->dRESb, n, h, w, grads, true, 1.f, st));
-    RC(conv_dgrad(e, P.body_tail, e->dRESb, n, h, w, EPI_DG_ACC, gRb, gRf, nullptr, nullptr, nullptr, nullptr, nullptr,
-                  1.f, st));
+    if (s_lo <= 0) {
+      RC(conv_wgrad(e, P.body_tail, e->hb(nl, 0), e->dRESb, n, h, w, grads, true, 1.f, st));
+      RC(conv_dgrad(e, P.body_tail, e->dRESb, n, h, w, EPI_DG_ACC, gRb, gRf, nullptr, nullptr, nullptr, nullptr,
+                    nullptr, 1.f, st));
+    }
     // One stream, three launches per RCAB:
     //   [CA backward -> du (+ the slab reductions of the previous RCAB)]
     //   [dgrad conv2 -> dz  ||  filter gradient conv2 (t, du)]
@@ -715,8 +775,16 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
     // above (F1) instead of a CA-backward pass; its conv2 backward (F2) adds the
     // constant dm / HW itself.  bf16 engine, fused-launch shapes only.
     const bool fold = use_ca_fold(e, n);
-    int it = 0;  // RCAB counter (slab-set parity)
     for (int g = nl - 1; g >= 0; --g) {
+      const int stage = nl - g;
+      // the gradient streams swap after every group: the state group g starts from
+      const bool sw = ((nl - 1 - g) & 1) != 0;
+      gRf = sw ? e->GBf : e->GAf;
+      ghf = sw ? e->GAf : e->GBf;
+      gRb = sw ? e->GBb : e->GAb;
+      ghb = sw ? e->GAb : e->GBb;
+      if (stage < s_lo || stage > s_hi) continue;
+      int it = (nl - 1 - g) * nb;  // RCAB counter (slab-set parity)
       const ConvRef& gt = P.group_tail[g];
       RC(conv_wgrad(e, gt, e->hb(g, nb), gRb, n, h, w, grads, true, 1.f, st));
       // the group tail's dgrad is the fold producer of the group's last RCAB (du' of RCAB nb)
@@ -779,12 +847,12 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
       RC(wgrad_reduce2_launch(prev2, prev1, st));
       RC(ca_param_grads_batched_launch(e->recp(g, 1), e->brecp(g, 1), nb, n, e->N, 64, R, e->d_caoffs + (size_t)g * nb * 5,
                                        grads, st));
-      std::swap(gRf, ghf);
-      std::swap(gRb, ghb);
       // the group's gradients are final here (one stream): the hook for a bucketed
       // all-reduce overlapped with the rest of backward
       if (group_events && group_events[g]) HC(hipEventRecord(reinterpret_cast<hipEvent_t>(group_events[g]), st));
     }
+    // after all nl groups: the group-0 input gradient (the head's upstream)
+    gRf = (nl & 1) ? e->GBf : e->GAf;
   } else {
     const float rsc = P.cfg.res_scale;
     RC(conv_wgrad(e, P.body_tail, e->hb(nl, 0), e->dRESb, n, h, w, grads, true, 1.f, st));
@@ -803,8 +871,11 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
     }
   }
   // head: only the weight gradient (the input gradient is never read)
-  RC(head_wgrad_launch(lr, gRf, n, e->C, h, w, e->slab, &nsl, st));
-  RC(head_wgrad_reduce_launch(e->slab, nsl, e->C, grads + P.head.w, grads + P.head.b, st));
+  if (s_hi >= (rcan ? nl + 1 : 0)) {
+    int nsl = 0;
+    RC(head_wgrad_launch(lr, gRf, n, e->C, h, w, e->slab, &nsl, st));
+    RC(head_wgrad_reduce_launch(e->slab, nsl, e->C, grads + P.head.w, grads + P.head.b, st));
+  }
   return 0;
 }
 
@@ -885,7 +956,35 @@ int srmi_backward(srmi_engine* e, const float* params, const float* lr, const fl
   return backward_impl(e, params, lr, sr, hr, loss4, dy, grads, group_events, S_(stream));
 }
 
+int srmi_backward_stage_count(srmi_engine* e) { return e ? backward_stages(e) : SRMI_ERR_ARG; }
+
+int srmi_backward_stages(srmi_engine* e, const float* params, const float* lr, const float* sr, const float* hr,
+                         const float* loss4, const float* dy, float* grads, void** group_events, int first, int last,
+                         void* stream) {
+  if (!e || !e->train || !params || !lr || !grads || e->last_n < 1) return SRMI_ERR_ARG;
+  if (!dy && (!sr || !hr || !loss4)) return SRMI_ERR_ARG;
+  const int ns = backward_stages(e);
+  if (first < 0 || last >= ns || first > last || (ns == 1 && (first != 0 || last != 0))) return SRMI_ERR_ARG;
+  return backward_impl(e, params, lr, sr, hr, loss4, dy, grads, group_events, S_(stream), first, last);
+}
+
 int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
+  if (which == 3) {  // inference engines: the one-launch RCAB (0, 2) of the last forward
+    if (!e || e->train || !use_rcab_infer(e) || e->last_n < 1 || reps < 1 || e->P.cfg.nblocks < 2)
+      return SRMI_ERR_ARG;
+    const int n = e->last_n, R = e->P.cfg.reduction;
+    const RCABRef& r = e->P.groups[0][1];
+    const float* prm = e->probe_prm;
+    if (!prm) return SRMI_ERR_ARG;
+    uint8_t* lo = reinterpret_cast<uint8_t*>(e->Hf);
+    const ConvParams c1 = fwd_params(e, r.c1, e->hb(0, 1), n, e->h, e->w, e->Tm(0, 2), nullptr, nullptr, nullptr, 1.f);
+    const ConvParams c2 = fwd_params(e, r.c2, e->Tm(0, 2), n, e->h, e->w, e->Um(0, 2), nullptr, nullptr, e->ppool, 1.f);
+    for (int i = 0; i < reps; ++i)
+      RC(rcab_infer_launch(c1, c2, e->ppool, conv3x3_nstrips(e->h, e->w), prm + r.ca_w1, prm + r.ca_b1,
+                           prm + r.ca_w2, prm + r.ca_b2, 64 / R, nullptr, e->hb(0, 1), lo, e->hb(0, 2), lo,
+                           e->recp(0, 2), S_(stream)));
+    return 0;
+  }
   if (!e || !e->train || e->P.cfg.arch != SRMI_ARCH_RCAN || e->last_n < 1 || reps < 1) return SRMI_ERR_ARG;
   if (which != 1 && which != 2) return SRMI_ERR_ARG;
   const int n = e->last_n, h = e->h, w = e->w;

@@ -26,6 +26,22 @@ enum Epi {
   EPI_RELU_POOL = 8,   // t = relu(acc + b) -> bf16, + per-strip channel sums of t
   EPI_CA_RESID = 9,    // h' = h + s[c] (acc + b): h in as fp32 r1 or the pair r1h / r1l,
                        // h' out as the pair yph / ypl, s = escale[n * escale_stride + c]
+  // the training RCAB's conv2 (the CA forward without a pass of its own):
+  EPI_CA_RESID_U = 10, // u = acc + b -> bf16 yb (saved for backward), h' = h + s[c] bf16(u) as
+                       // in EPI_CA_RESID; s computed in the prologue from conv1's t (cas_on,
+                       // ca_scale.hpp) or read from escale
+};
+
+// The CA scale of an RCAB from its conv1 output t (ca_scale.hpp): mean(u) of u =
+// conv2(t) + b2 from t's statistics and conv2's bf16 filter image, then the MLP.
+struct CaScale {
+  const bf16_t* t;    // conv1 output [N][H][W][64] bf16
+  const float* part;  // conv1's per-strip channel sums of t [N][nstrips][64] (EPI_RELU_POOL)
+  int nstrips;
+  const float *w1, *b1, *w2, *b2;  // conv_du.0 [CR][64] + [CR], conv_du.2 [64][CR] + [64]
+  const float* bc2;   // conv2's bias [64]
+  int CR;
+  float* rec;         // out: m | z1 | s per image [N][128 + CR]
 };
 
 // The CA-backward fold of the bf16 RCAB backward (engine.cpp backward_impl).  du =
@@ -77,6 +93,10 @@ struct ConvParams {
   uint8_t* ypl;
   const float* escale;         // per-image channel scale s [N][escale_stride]
   int escale_stride;
+  // EPI_CA_RESID_U with cas_on: every workgroup computes its image's s in the prologue
+  // (and the first one of the image writes cas.rec); cas_on = 0: s from escale
+  CaScale cas;
+  int cas_on;
 };
 
 void conv3x3_set_debug_stamps(unsigned long long* buf);
@@ -177,12 +197,16 @@ int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1
 int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
                      const float* w2, int N, int HW, int C, int R, void* du, float* brec, int f32, hipStream_t st,
                      const ReduceSet* red0 = nullptr, const ReduceSet* red1 = nullptr);
-// inference RCAB, one launch (rcab_infer.hip): c1 = conv1 (RELU, yb = t), c2 = conv2
-// (POOL, yb = u, part), then the CA MLP and the residual pair update per image
+// inference RCAB, one launch with a workgroup per image (rcab_infer.hip): c1 = conv1
+// (yb = t), c2 = conv2 (its bias = the CA's bc2); t's per-strip sums into part, the CA
+// scale into rec, h' = h + s u into the pair hi_out / lo_out (h from h_in or the pair)
 int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* part, int nstrips, const float* w1,
                       const float* b1, const float* w2, const float* b2, int CR, const float* h_in, const void* hi_in,
-                      const void* lo_in, void* hi_out, void* lo_out, float* rec, hipStream_t st,
-                      const float* wc2 = nullptr, const float* bc2 = nullptr);  // v2: conv2's fp32 weight, bias
+                      const void* lo_in, void* hi_out, void* lo_out, float* rec, hipStream_t st);
+// the CA scale of every image of an RCAB as its own launch (a 512-thread workgroup per
+// image; conv2's filter pack wpack, forward layout): the A/B alternative to computing it
+// in the conv2 prologue
+int ca_scale_launch(const CaScale& c, const bf16_t* wpack, int N, int H, int W, hipStream_t st);
 // records of consecutive RCABs Ncap images apart (the engine capacity), N summed
 int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int Ncap, int C, int R,
                                   const long long* offs, float* grads, hipStream_t st);

@@ -19,6 +19,8 @@ SRMI_ARCH_EDSR = 1
 SRMI_DTYPE_BF16 = 0
 SRMI_FLAG_CA_FOLD = 1
 SRMI_FLAG_NO_RCAB_INFER = 2
+SRMI_FLAG_CA_PASS = 4
+SRMI_FLAG_CA_SCALE_LAUNCH = 8
 SRMI_DTYPE_F32 = 1
 SRMI_LOSS_RMSE = 0
 SRMI_LOSS_MEAN = 1
@@ -52,6 +54,8 @@ _SIGS = {
     "srmi_pack_weights": ([P, P, P], C.c_int),
     "srmi_forward": ([P, P, P, P, C.c_int, P], C.c_int),
     "srmi_backward": ([P, P, P, P, P, P, P, P, C.POINTER(P), P], C.c_int),
+    "srmi_backward_stage_count": ([P], C.c_int),
+    "srmi_backward_stages": ([P, P, P, P, P, P, P, P, C.POINTER(P), C.c_int, C.c_int, P], C.c_int),
     "srmi_engine_probe": ([P, C.c_int, C.c_int, P], C.c_int),
     "srmi_rmse_partial": ([P, P, P, C.c_size_t, C.c_double, P, P], C.c_int),
     "srmi_rmse_finalize": ([P, P], C.c_int),

@@ -14,8 +14,8 @@ the MI355X-native addition, designed for exact single-process semantics:
 * parameter gradients are then SUMMED over ranks (no 1/world factor: the
   global count already normalises), bucket by bucket in the order backward
   finalises them (one bucket per residual group, tail/upsampler first, head
-  last), each bucket launched on a communication stream as soon as its
-  group's HIP event fires, overlapping with the rest of backward.
+  last), each bucket's all-reduce launched right behind the backward stage that
+  finalises it, overlapping with the rest of backward (GradReducer).
 """
 from __future__ import annotations
 
@@ -121,17 +121,60 @@ def grad_buckets(table, arch: str, nlayers: int) -> List[Bucket]:
     return buckets
 
 
-class GradReducer:
-    """Bucketed, event-driven SUM all-reduce of the flat gradient buffer."""
+def bucket_stage(b: Bucket, nlayers: int, nstages: int) -> int:
+    """The backward stage (srmi_backward_stages) after which bucket b is final: residual
+    group g is stage nlayers - g; the head bucket (and EDSR's) the last stage."""
+    return nlayers - b.event_index if b.event_index is not None else nstages - 1
 
-    def __init__(self, table, arch: str, nlayers: int, info: DistInfo, device: torch.device):
+
+class GradReducer:
+    """Bucketed SUM all-reduce of the flat gradient buffer, overlapped with backward.
+
+    Two schedules (srmi.trainer.FusedTrainer):
+    * staged (the default; `reduce_stage`): the trainer enqueues the engines' backward
+      stage by stage and, behind the stage that finalises a bucket, the bucket's
+      gradient add and all-reduce on the last engine's stream -- no stream of the
+      reducer's own;
+    * event-driven (`reduce`; stream=True): the whole backward is enqueued first and a
+      communication stream of the reducer's own waits for each group's HIP event."""
+
+    def __init__(self, table, arch: str, nlayers: int, info: DistInfo, device: torch.device, stream: bool = True):
         self.info = info
+        self.nlayers = nlayers
         self.buckets = grad_buckets(table, arch, nlayers)
         self.n_events = max([b.event_index for b in self.buckets if b.event_index is not None], default=-1) + 1
         self.cuda = device.type == "cuda"
         self.device = device
-        self.stream = torch.cuda.Stream(device=device) if self.cuda else None
-        self.events = self.new_events()
+        self.stream = torch.cuda.Stream(device=device) if self.cuda and stream else None
+        self.events = self.new_events() if self.stream is not None else []
+
+    def stage_buckets(self, nstages: int) -> List[List[Bucket]]:
+        """Buckets final after each backward stage (srmi_backward_stages)."""
+        out: List[List[Bucket]] = [[] for _ in range(nstages)]
+        for b in self.buckets:
+            out[bucket_stage(b, self.nlayers, nstages)].append(b)
+        return out
+
+    def reduce_stage(self, buckets: Sequence[Bucket], grads: torch.Tensor, extra: Sequence[torch.Tensor] = (),
+                     works: Optional[list] = None):
+        """Enqueue, on the CURRENT stream, the micro-batch gradient adds and the
+        asynchronous all-reduce of `buckets` (the caller has made the current stream
+        wait for every engine's part of them); the all-reduce handles go to `works`."""
+        if not self.info.enabled:
+            return
+        from .engine import axpy
+        for b in buckets:
+            for off, n in b.ranges:
+                for x in extra:
+                    if self.cuda:
+                        axpy(grads[off:off + n], x[off:off + n], 1.0)
+                    else:
+                        grads[off:off + n].add_(x[off:off + n])
+                w = dist.all_reduce(grads[off:off + n], op=dist.ReduceOp.SUM, async_op=True)
+                if works is not None:
+                    works.append(w)
+                else:
+                    w.wait()
 
     def covered(self) -> int:
         return sum(n for b in self.buckets for _, n in b.ranges)
@@ -144,7 +187,7 @@ class GradReducer:
         `Stream.wait_event` on it is a no-op -- the bucket all-reduce would not wait
         for backward at all.  So each event is created here by one record on the
         reducer's stream."""
-        if not self.cuda:
+        if not self.cuda or self.stream is None:
             return []
         evs = [torch.cuda.Event() for _ in range(max(self.n_events, 0))]
         for ev in evs:

@@ -166,13 +166,25 @@ class Engine:
         assert parts.is_contiguous() and parts.shape[-1] == 4
         call("srmi_loss_combine", ptr(loss4), ptr(parts), parts.numel() // 4, int(kind), stream_handle(stream))
 
+    @property
+    def stage_count(self) -> int:
+        """Stages of srmi_backward_stages: 0 = tail / upsamplers / body tail, 1..nlayers =
+        residual groups nlayers-1..0, nlayers + 1 = head (RCAN); EDSR: 1."""
+        return call("srmi_backward_stage_count", self._h)
+
     def backward(self, params: torch.Tensor, lr: torch.Tensor, grads: torch.Tensor, sr=None, hr=None, loss4=None,
-                 dy=None, events: Optional[Sequence] = None, stream=None):
+                 dy=None, events: Optional[Sequence] = None, stream=None, stages: Optional[Tuple[int, int]] = None):
+        """The whole backward of the last forward, or (stages = (first, last)) those
+        stages of it -- each stage exactly once per backward, in order."""
         evp = None
         if events is not None:
             if any(e is not None and not e.cuda_event for e in events):
                 raise RuntimeError("backward: group event not created yet (record it once before passing it)")
             evp = (C.c_void_p * len(events))(*[e.cuda_event if e is not None else None for e in events])
+        if stages is not None:
+            call("srmi_backward_stages", self._h, ptr(params), ptr(lr), ptr(sr), ptr(hr), ptr(loss4), ptr(dy),
+                 ptr(grads), evp, int(stages[0]), int(stages[1]), stream_handle(stream))
+            return
         call("srmi_backward", self._h, ptr(params), ptr(lr), ptr(sr), ptr(hr), ptr(loss4), ptr(dy), ptr(grads), evp,
              stream_handle(stream))
 

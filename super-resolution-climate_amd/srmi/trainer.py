@@ -70,7 +70,7 @@ class FusedTrainer:
                  eps: float = 1e-8, weight_decay: float = 0.0, interp_loss: bool = True,
                  info: Optional[DistInfo] = None, device: Optional[torch.device] = None, seed: int = 0,
                  params: Optional[torch.Tensor] = None, micro: Optional[int] = None, loss_fn: str = "l2",
-                 cu_budget: Optional[int] = None, task=None):
+                 cu_budget: Optional[int] = None, task=None, dp_reducer_stream: bool = False):
         """task: the task config section (default: the active srmi ConfigContext's,
         if any).  apply_network's target selection is followed: when
         task.target_variables names fewer channels than the input, the loss target is
@@ -78,6 +78,10 @@ class FusedTrainer:
         and the model has that many output channels.  task.data_downsample = ds > 1
         downsamples every HR batch by ds first, as apply_network does (:561-563):
         step() then takes tiles T with floor(T / ds) = lr_hw * scale.
+        dp_reducer_stream (data parallel, A/B): the gradient all-reduce on a reducer
+        stream of its own that waits for each residual group's event of the whole
+        enqueued backward, instead of (the default) enqueuing the backward stage by stage
+        with each bucket's all-reduce behind its stage on an engine stream.
         task.downsample_mode / upsample_mode select the resampling of the model input
         and of the interp baseline ('cubic' -> bicubic, 'linear' -> bilinear,
         array.py:37-41; others raise)."""
@@ -147,9 +151,17 @@ class FusedTrainer:
         self.mloss4 = torch.zeros((micro, 4), dtype=torch.float32, device=self.device)   # per micro-batch
         self.miloss4 = torch.zeros((micro, 4), dtype=torch.float32, device=self.device)
         self.streams = [None] + [torch.cuda.Stream(device=self.device) for _ in range(micro - 1)]
-        self.reducer = GradReducer(self.eng.table, spec.arch, spec.nlayers, self.info, self.device)
+        self.dp_staged = not dp_reducer_stream
+        self.reducer = GradReducer(self.eng.table, spec.arch, spec.nlayers, self.info, self.device,
+                                   stream=self.info.enabled and not self.dp_staged)
         # group events of engines 1.. (engine 0 records into reducer.events)
         self.xevents = [self.reducer.new_events() for _ in range(micro - 1)]
+        # staged DP backward: the stages, the buckets final after each, and per engine
+        # (but the last, which reduces) an event per stage
+        self.nstages = self.eng.stage_count if self.info.enabled and self.dp_staged else 0
+        self.stage_buckets = self.reducer.stage_buckets(self.nstages) if self.nstages else []
+        self.stage_ev = ([[torch.cuda.Event() for _ in range(self.nstages)] for _ in range(micro - 1)]
+                         if self.nstages and self.device.type == "cuda" else [])
         for e in self.engines:
             e.pack(self.params)
 
@@ -223,11 +235,14 @@ class FusedTrainer:
             self._reduce_loss(self.iloss4, self.miloss4)
         for st in self.streams[1:]:
             st.wait_stream(main)
-        # backward per micro-batch with the global loss scale.  Data parallel: every
-        # engine records its residual-group events; the reducer adds the engines'
-        # gradients bucket by bucket on its stream and all-reduces each bucket as
-        # soon as all engines are past it (overlapped with the rest of backward).
+        # backward per micro-batch with the global loss scale.  Data parallel: the
+        # engines' gradients are added and all-reduced bucket by bucket as soon as every
+        # engine is past the bucket, overlapped with the rest of backward
+        # (_backward_dp_staged, or the reducer stream waiting on the engines' residual-group events).
         dp = self.info.enabled and self.reducer.cuda
+        if dp and self.dp_staged:
+            self._backward_dp_staged(sls, tgt)
+            return self._finish_step(main)
         evs = [self.reducer.events] + self.xevents if dp else [None] * self.micro
         for k, eng in enumerate(self.engines):
             sl = sls[k]
@@ -250,6 +265,46 @@ class FusedTrainer:
         else:
             for g in self.mgrads[1:]:
                 axpy(self.grads, g, 1.0)  # exact gradient of the whole batch
+        return self._finish_step(main)
+
+    def _backward_dp_staged(self, sls, tgt):
+        """Data-parallel backward without a reducer stream: with two micro-batch engines
+        a rank runs 3 streams (the engines' and RCCL's) instead of 4.  The engines'
+        backward is enqueued stage by stage (srmi_backward_stages: tail / upsamplers,
+        each residual group, head); behind the stage that finalises a bucket, the LAST
+        engine's stream waits for the other engines' events of that stage, adds their
+        gradients into engine 0's (the exact whole-batch gradient) and launches the
+        bucket's asynchronous all-reduce.  RCCL's stream waits for that point; no engine
+        stream waits for RCCL until Adam."""
+        red_k = self.micro - 1
+        works = []
+        for s in range(self.nstages):
+            for k, eng in enumerate(self.engines):
+                sl = sls[k]
+                with self._ctx(k):
+                    if sl.stop == sl.start:  # no tiles: a zero gradient
+                        if s == 0:
+                            self.mgrads[k].zero_()
+                    elif self.dy is not None:
+                        eng.backward(self.params, self.lrbuf[sl], self.mgrads[k], dy=self.dy[sl], stages=(s, s))
+                    else:
+                        eng.backward(self.params, self.lrbuf[sl], self.mgrads[k], sr=self.sr[sl], hr=tgt[sl],
+                                     loss4=self.loss4, stages=(s, s))
+                    if k != red_k:
+                        self.stage_ev[k][s].record()
+            if self.stage_buckets[s]:
+                with self._ctx(red_k):
+                    cur = torch.cuda.current_stream(self.device)
+                    for k in range(self.micro):
+                        if k != red_k:
+                            cur.wait_event(self.stage_ev[k][s])
+                    self.reducer.reduce_stage(self.stage_buckets[s], self.grads, self.mgrads[1:], works)
+        for w in works:
+            w.wait()  # the current (main) stream waits for the all-reduces
+
+    def _finish_step(self, main):
+        for st in self.streams[1:]:
+            main.wait_stream(st)
         self.t += 1
         adam_step(self.params, self.grads, self.m, self.v, self.t, self.lr, self.betas, self.eps, self.wd)
         for k, eng in enumerate(self.engines):

@@ -12,8 +12,9 @@ run as unfold + rocBLAS GEMM) and no reduced-precision math.
   its backward dx = conv^T(bf16(dy), bf16(w)), dw = corr(bf16(x), bf16(dy)) (the
   engine's MFMA operands and its bf16 activation / gradient maps t, u, hb, dz, du);
 * in every RCAB the channel-attention product uses the stored bf16 u while the
-  pooled mean is taken from the fp32 conv output (the conv2 POOL epilogue sums
-  before rounding): out = bf16(u) * s(mean(u));
+  pooled mean is that of the fp32 conv output (training's conv2 derives it from the
+  statistics of the bf16 t and conv2's bf16 filters, csrc/ca_scale.hpp -- the same
+  quantity up to fp32 summation order): out = bf16(u) * s(mean(u));
 * the residual stream INSIDE a residual group is the pair hi + lo (bf16 hi plus an
   8-bit remainder in units of ulp(hi) / 256, common.hpp lo8 codec): 16 significant
   bits, rounded after every CA add (h = pair16(h + out)); the group input, the

@@ -24,7 +24,7 @@ def _spec():
                    scale=4)
 
 
-def _worker(rank, port, q):
+def _worker(rank, port, q, reducer_stream=False):
     import sys
     sys.path[:0] = [os.path.join(ROOT, "super-resolution-climate_amd"), ROOT]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
@@ -43,14 +43,19 @@ def _worker(rank, port, q):
     default_init_(flat, table, seed=5)
     hr_all = torch.tensor(ro.synthetic_hr(16, 2, 192, 17)).to(d)
     a, b = shard_range(16, info)
-    tr = FusedTrainer(spec, b - a, (48, 48), device=d, params=flat, micro=2, info=info)
+    tr = FusedTrainer(spec, b - a, (48, 48), device=d, params=flat, micro=2, info=info,
+                      dp_reducer_stream=reducer_stream)
     out = tr.step(hr_all[a:b].contiguous())
     torch.cuda.synchronize()
     q.put((rank, float(out["loss"]), float(out["interp_loss"]), tr.grads.cpu().numpy(), tr.params.cpu().numpy()))
     dist.destroy_process_group()
 
 
-def test_dp_world2_micro2_matches_single_process():
+@pytest.mark.parametrize("reducer_stream", [False, True])
+def test_dp_world2_micro2_matches_single_process(reducer_stream):
+    """Both DP schedules: the default staged one (backward enqueued stage by stage,
+    each bucket's gradient add and all-reduce behind its stage on engine 1's stream)
+    and the reducer stream waiting on the group events (dp_reducer_stream)."""
     import multiprocessing as mp
     from oracle import rcan_oracle as ro
     from srmi.engine import param_table
@@ -58,7 +63,7 @@ def test_dp_world2_micro2_matches_single_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 31000 + random.randint(0, 2000)
-    ps = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, port, q, reducer_stream)) for r in range(2)]
     for p in ps:
         p.start()
     res = sorted([q.get(timeout=100) for _ in ps], key=lambda t: t[0])
@@ -104,7 +109,7 @@ def test_group_events_exist_before_backward():
         Engine.backward(None, None, None, None, events=[torch.cuda.Event()])
 
 
-def _force_dp_rccl_worker(port, q):
+def _force_dp_rccl_worker(port, q, reducer_stream=False):
     import sys
     sys.path[:0] = [os.path.join(ROOT, "super-resolution-climate_amd"), ROOT]
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
@@ -123,7 +128,8 @@ def _force_dp_rccl_worker(port, q):
     flat = torch.empty(sum(t[2] for t in table), device=d)
     default_init_(flat, table, seed=6)
     hr = torch.tensor(ro.synthetic_hr(16, 2, 192, 23)).to(d)
-    dp = FusedTrainer(spec, 16, (48, 48), device=d, params=flat, micro=2, info=info)
+    dp = FusedTrainer(spec, 16, (48, 48), device=d, params=flat, micro=2, info=info,
+                      dp_reducer_stream=reducer_stream)
     ref = FusedTrainer(spec, 16, (48, 48), device=d, params=flat, micro=2)
     out = []
     for _ in range(2):
@@ -135,17 +141,19 @@ def _force_dp_rccl_worker(port, q):
     dist.destroy_process_group()
 
 
-def test_force_dp_rccl_bucketed_allreduce_waits_for_backward():
+@pytest.mark.parametrize("reducer_stream", [False, True])
+def test_force_dp_rccl_bucketed_allreduce_waits_for_backward(reducer_stream):
     """The DP path over a real RCCL communicator (backend "nccl", one rank): every
-    bucket's micro-batch gradient sum and all-reduce run on the reducer stream
-    behind the engines' group events.  At one rank the SUM all-reduce is the
-    identity, so the gradients must equal the non-DP step's bit for bit -- a
-    bucket that did not wait for its backward group would read unfinished
-    gradients and differ."""
+    bucket's micro-batch gradient sum and all-reduce run behind the backward stage
+    that finalises it (the default: on engine 1's stream after engine 0's stage
+    event) or on the reducer stream behind the engines' group events.  At one rank the
+    SUM all-reduce is the identity, so the gradients must equal the non-DP step's bit
+    for bit -- a bucket that did not wait for its backward group would read
+    unfinished gradients and differ."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_force_dp_rccl_worker, args=(33000 + random.randint(0, 2000), q))
+    p = ctx.Process(target=_force_dp_rccl_worker, args=(33000 + random.randint(0, 2000), q, reducer_stream))
     p.start()
     out, params_equal = q.get(timeout=240)
     p.join(timeout=60)

@@ -169,12 +169,12 @@ def test_tiled_inference_micro_engines_bit_identical(graph):
 
 @pytest.mark.parametrize("C,nl,nb,hw,N", [(1, 2, 3, (48, 48), 5), (2, 1, 2, (32, 48), 3), (1, 1, 1, (8, 48), 2)])
 def test_fused_inference_rcab_matches_three_launches_and_oracle(C, nl, nb, hw, N):
-    """The inference RCAB as one launch with a workgroup per image (rcab_infer.hip v2:
-    conv1 + sums of t -> mean(u) from t's statistics and the CA MLP -> conv2 whose
-    epilogue writes h + s u; u is never stored) against the three launches
-    (SRMI_FLAG_NO_RCAB_INFER: conv1, conv2 + pool, CA pass) and the fp64 oracle
-    forward.  v2 differs from the three launches only in summation order, in using the
-    fp32 conv2 weights for mean(u) and in adding u to h in fp32 instead of bf16, so
+    """The inference RCAB as one launch with a workgroup per image (rcab_infer.hip:
+    conv1 + sums of the bf16 t -> mean(u) from t's statistics with conv2's bf16 filter
+    image and the CA MLP -> conv2 whose epilogue writes h + s u; u is never stored)
+    against the three launches (SRMI_FLAG_NO_RCAB_INFER: conv1, conv2 + pool, CA pass)
+    and the fp64 oracle forward.  The one launch differs from the three only in the
+    summation order of mean(u) and in adding the fp32 u to h instead of bf16(u), so
     both sit within bf16 noise of the oracle and of each other."""
     from srmi._lib import SRMI_FLAG_NO_RCAB_INFER
     from srmi.engine import Engine

@@ -151,9 +151,17 @@ def test_grad_buckets_partition_every_parameter_once():
         groups = {int(names[off].split(".")[1]) for off, _ in bk.ranges
                   if names[off].startswith("body.") and names[off].split(".")[2] == "body"}
         assert groups == {bk.event_index}
+    # the staged schedule (srmi_backward_stages: 0 tail/upsamplers/body tail, 1..nl
+    # groups nl-1..0, nl+1 head): group g's bucket after stage nl - g, the head's last
+    r = GradReducer(tab, "rcan", 3, DistInfo(), torch.device("cpu"), stream=False)
+    sb = r.stage_buckets(3 + 2)
+    assert [[x.event_index for x in st] for st in sb] == [[], [2], [1], [0], [None]]
+    tab_e = param_table(NetSpec(arch="edsr", nchannels_in=4, nchannels_out=4, nlayers=16, scale=8))
+    sb = GradReducer(tab_e, "edsr", 16, DistInfo(), torch.device("cpu"), stream=False).stage_buckets(1)
+    assert len(sb) == 1 and len(sb[0]) == 2
 
 
-def _dp_rank(rank, world, port, q, micro=1):
+def _dp_rank(rank, world, port, q, micro=1, staged=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import sys
@@ -185,23 +193,32 @@ def _dp_rank(rank, world, port, q, micro=1):
         o = model(ro.downsample(hr[k * per:(k + 1) * per], 4))
         o.backward(dy[k * per:(k + 1) * per])
         mg.append(torch.cat([sd[n].grad.reshape(-1) for n, _, _, _ in table]))
-    GradReducer(table, "rcan", 1, info, torch.device("cpu")).reduce(mg[0], extra=mg[1:])
+    red = GradReducer(table, "rcan", 1, info, torch.device("cpu"), stream=not staged)
+    if staged:  # the trainer's default schedule: each bucket behind its backward stage
+        works = []
+        for bk in red.stage_buckets(1 + 2):
+            red.reduce_stage(bk, mg[0], mg[1:], works)
+        for w in works:
+            w.wait()
+    else:
+        red.reduce(mg[0], extra=mg[1:])
     grads = mg[0]
     q.put((rank, float(L), grads.numpy()))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("micro", [1, 2])
-def test_data_parallel_semantics_gloo_world2(micro):
+@pytest.mark.parametrize("micro,staged", [(1, False), (2, False), (1, True), (2, True)])
+def test_data_parallel_semantics_gloo_world2(micro, staged):
     """2 ranks x 2 tiles == 1 process x 4 tiles: global RMSE and summed grads
     (micro=2: each rank's 2 tiles as 2 micro-batch gradients, summed per bucket
-    by the reducer before its all-reduce)."""
+    by the reducer before its all-reduce; staged: bucket by bucket in backward-stage
+    order, as FusedTrainer's default DP schedule issues them)."""
     import multiprocessing as mp
     import random
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29500 + random.randint(0, 2000)
-    ps = [ctx.Process(target=_dp_rank, args=(r, 2, port, q, micro)) for r in range(2)]
+    ps = [ctx.Process(target=_dp_rank, args=(r, 2, port, q, micro, staged)) for r in range(2)]
     for p in ps:
         p.start()
     res = sorted([q.get(timeout=300) for _ in ps], key=lambda t: t[0])

@@ -13,7 +13,7 @@ for rep in 1 2; do
     SRMI_LIB=${lib:+$R/$lib} timeout -k 10 200 python bench.py --no-cpu-baseline --no-edsr --steps 20 --warmup 3 > gpurun_out/abk.log 2>>gpurun_out/abk.err || exit 2
     python -c "
 import json; d=json.loads(open('gpurun_out/abk.log').read().strip().splitlines()[-1])
-print('${lib:-main}', d['value'], d['ms_per_step'], 'F1', d['roofline']['per_stream_ms'], 'F2', d['roofline_f2']['per_stream_ms'], 'inf', d['inference']['value'])" >> gpurun_out/ab_kb.log
+print('${lib:-main}', d['value'], d['ms_per_step'], 'F1', d['roofline']['avg_launch_ms'], d['roofline']['concurrent']['per_stream_ms'], 'F2', d['roofline_f2']['avg_launch_ms'], d['roofline_f2']['concurrent']['per_stream_ms'], 'inf', d['inference']['value'])" >> gpurun_out/ab_kb.log
   done
 done
 cat gpurun_out/ab_kb.log

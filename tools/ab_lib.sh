@@ -9,7 +9,7 @@ for m in $MICROS; do
     SRMI_LIB=${lib:+$R/$lib} timeout -k 10 200 python bench.py --no-cpu-baseline --no-inference --no-edsr --steps 20 --warmup 3 --micro $m > gpurun_out/abl.log 2>>gpurun_out/abl.err || exit 2
     python -c "
 import json; d=json.loads(open('gpurun_out/abl.log').read().strip().splitlines()[-1])
-print('micro $m ${lib:-main}', d['value'], d['ms_per_step'], 'F1', d['roofline']['per_stream_ms'], 'F2', d['roofline_f2']['per_stream_ms'])" | tee -a gpurun_out/ab_lib.log
+print('micro $m ${lib:-main}', d['value'], d['ms_per_step'], 'F1', d['roofline']['avg_launch_ms'], d['roofline']['concurrent']['per_stream_ms'], 'F2', d['roofline_f2']['avg_launch_ms'], d['roofline_f2']['concurrent']['per_stream_ms'])" | tee -a gpurun_out/ab_lib.log
   done
 done
 done

@@ -11,7 +11,7 @@ for rep in $(seq $REPS); do
       --steps 20 --warmup 3 $flags > $O/abv.json 2>> $O/abv.err || { echo "variant $name failed"; exit 2; }
     python -c "
 import json; d=json.loads(open('$O/abv.json').read().strip().splitlines()[-1])
-print('$name', d['value'], d['ms_per_step'], d['step_times']['median_ms'], 'F1', d['roofline']['per_stream_ms'], 'F2', d['roofline_f2']['per_stream_ms'])" | tee -a $O/ab_var.log
+print('$name', d['value'], d['ms_per_step'], d['step_times']['median_ms'], 'F1', d['roofline']['avg_launch_ms'], d['roofline']['concurrent']['per_stream_ms'], 'F2', d['roofline_f2']['avg_launch_ms'], d['roofline_f2']['concurrent']['per_stream_ms'])" | tee -a $O/ab_var.log
   done
 done
 echo done

@@ -2,9 +2,9 @@
 
 Reports the kernel table of the run (dispatches, average and total duration per
 kernel), and for the two fused RCAB-backward kernels the average duration of the
-roofline-phase dispatches (bench.py fused_rooflines: 3 warm-up + 20 timed launches
-per micro-batch engine, after the timed steps) next to the bench's HIP-event
-average, plus the average over the in-step dispatches.
+roofline-phase dispatches (bench.py fused_rooflines, after the timed steps: engine 0
+alone, 3 warm-up + 20 timed launches, then every engine at once) next to the bench's
+HIP-event per-launch average, plus the average over the in-step dispatches.
 
     python tools/prof_summary.py <kernel_trace.csv> <bench_log_with_json_line> <out.json>
 """
@@ -34,15 +34,18 @@ def main(trace, bench_log, out):
                                    "total_ms": round(sum(v) / 1e6, 3), "share": round(sum(v) / tot, 4)}
     n_eng = 1
     if line and line.get("roofline"):
-        n_eng = line["roofline"].get("launches_per_slot", 1)
+        n_eng = line["roofline"].get("concurrent", {}).get("launches_per_slot", 1)
     for key, pat, rk in (("F1", "rcab_bwd_kernel<7", "roofline"), ("F2", "rcab_bwd_kernel<4", "roofline_f2")):
         d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows if pat in r["Kernel_Name"]]
         if not d:
             continue
-        probe = d[-REPS * n_eng:]
-        instep = d[:-(REPS + WARM) * n_eng]
+        # bench.fused_rooflines after the timed steps: engine 0 alone (WARM + REPS launches),
+        # then every engine at once (WARM + REPS each)
+        tail = d[-(REPS + WARM) * (1 + n_eng):]
+        alone = tail[WARM:WARM + REPS]
+        instep = d[:-(REPS + WARM) * (1 + n_eng)]
         rec = {"name_contains": pat, "dispatches": len(d),
-               "roofline_phase_avg_us": round(sum(probe) / len(probe) / 1e3, 3),
+               "roofline_phase_avg_us": round(sum(alone) / len(alone) / 1e3, 3),
                "in_step_avg_us": round(sum(instep) / len(instep) / 1e3, 3) if instep else None}
         if line and line.get(rk):
             rec["bench_event_avg_us"] = round(line[rk]["avg_launch_ms"] * 1e3, 3)
