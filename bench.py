@@ -69,6 +69,8 @@ def parse():
                     help="A/B: fold each RCAB's CA backward into the conv launches (SRMI_FLAG_CA_FOLD)")
     ap.add_argument("--dp-reducer-stream", action="store_true",
                     help="A/B: the DP all-reduce on a reducer stream of its own (the event-driven schedule)")
+    ap.add_argument("--wgrad-full-co", action="store_true",
+                    help="A/B: RCAB filter gradients on whole co blocks over half-image chunks (SRMI_FLAG_WGRAD_FULL_CO)")
     ap.add_argument("--ca-pass", action="store_true",
                     help="A/B: the training CA forward as a pass of its own after conv2 (SRMI_FLAG_CA_PASS)")
     ap.add_argument("--ca-scale-launch", action="store_true",
@@ -434,7 +436,7 @@ def dp_overhead_probe(args, reps=2):
             "--no-dp-probe", "--steps", str(args.steps), "--warmup", str(args.warmup), "--batch", str(args.batch)]
     if args.micro is not None:
         base += ["--micro", str(args.micro)]
-    for flag in ("ca_fold", "ca_pass", "ca_scale_launch", "dp_reducer_stream"):
+    for flag in ("ca_fold", "ca_pass", "ca_scale_launch", "dp_reducer_stream", "wgrad_full_co"):
         if getattr(args, flag):
             base += ["--" + flag.replace("_", "-")]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
@@ -542,9 +544,10 @@ def main():
                                                                            2 if args.no_rcab_infer else 0)}
         print(json.dumps(rec), flush=True)
         return
-    from srmi._lib import SRMI_FLAG_CA_FOLD, SRMI_FLAG_CA_PASS, SRMI_FLAG_CA_SCALE_LAUNCH
+    from srmi._lib import SRMI_FLAG_CA_FOLD, SRMI_FLAG_CA_PASS, SRMI_FLAG_CA_SCALE_LAUNCH, SRMI_FLAG_WGRAD_FULL_CO
     flags = ((SRMI_FLAG_CA_FOLD if args.ca_fold else 0) | (SRMI_FLAG_CA_PASS if args.ca_pass else 0) |
-             (SRMI_FLAG_CA_SCALE_LAUNCH if args.ca_scale_launch else 0))
+             (SRMI_FLAG_CA_SCALE_LAUNCH if args.ca_scale_launch else 0) |
+             (SRMI_FLAG_WGRAD_FULL_CO if args.wgrad_full_co else 0))
     spec = NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=10, nblocks=20,
                    cbottleneck=2, scale=4, flags=flags)
     tr = FusedTrainer(spec, B, (48, 48), lr=1e-4, interp_loss=not args.no_interp_loss, info=info, device=dev, seed=0,

@@ -94,6 +94,10 @@ typedef struct srmi_model_config {
  * own between conv1 and conv2 instead of in every conv2 workgroup's prologue */
 #define SRMI_FLAG_CA_PASS 4
 #define SRMI_FLAG_CA_SCALE_LAUNCH 8
+/* SRMI_FLAG_WGRAD_FULL_CO: the RCAB filter gradients on whole 64-channel co blocks over
+ * half-image row chunks instead of (the default) co halves over whole images, which
+ * write half the partial slabs (A/B, tests) */
+#define SRMI_FLAG_WGRAD_FULL_CO 16
 
 typedef struct srmi_param_info {
   long long offset; /* element offset in the flat fp32 parameter buffer     */

@@ -328,12 +328,6 @@ __global__ void __launch_bounds__(kThreads, 2) conv3x3_kernel(ConvParams p) {
                           wave, tid);
 }
 
-#ifndef SRMI_CONV_NW8
-#define SRMI_CONV_NW8 1
-#endif
-#ifndef SRMI_DGRAD_NW8
-#define SRMI_DGRAD_NW8 1
-#endif
 template <int TW, int EPI>
 static int launch_tw(const ConvParams& p, hipStream_t st) {
   if (p.Cin == 64 && p.in_mode == IN_PLAIN) {
@@ -343,9 +337,7 @@ static int launch_tw(const ConvParams& p, hipStream_t st) {
     ConvParams q = p;
     q.stamps = g_debug_stamps;
     // 8 waves (two per SIMD, a wave per row and channel half) at TW = 48
-    constexpr bool kFwd = EPI == EPI_RELU_BF16 || EPI == EPI_POOL_BF16 || EPI == EPI_RESID || EPI == EPI_PS_BF16 ||
-                          EPI == EPI_PLAIN_BF16;
-    constexpr int NW = (TW == 48 && (kFwd ? SRMI_CONV_NW8 : SRMI_DGRAD_NW8)) ? 8 : 4;
+    constexpr int NW = TW == 48 ? 8 : 4;
     hipLaunchKernelGGL((conv64_kernel<TW, EPI, NW>), grid, dim3(NW * 64), Conv2Smem<TW>::TOTAL, st, q, run_len);
   } else {
     constexpr int E1 = EPI == EPI_DG_ACC_CA ? EPI_DG_ACC : EPI;  // v1 handles the general form
@@ -360,7 +352,7 @@ static int launch_tw(const ConvParams& p, hipStream_t st) {
 // conv1 with t's per-strip sums and the training conv2 with the CA residual update
 template <int EPI>
 static int launch_v2_only(const ConvParams& p, hipStream_t st) {
-  if (p.Cin != 64 || p.Cout != 64 || p.in_mode != IN_PLAIN || p.W % 48 || p.H % kTH || SRMI_CONV_NW8 != 1)
+  if (p.Cin != 64 || p.Cout != 64 || p.in_mode != IN_PLAIN || p.W % 48 || p.H % kTH)
     return SRMI_ERR_SHAPE;
   const int run_len = conv64_run_len(p, 48, p.cu_budget > 0 ? p.cu_budget : 256);
   ConvParams q = p;

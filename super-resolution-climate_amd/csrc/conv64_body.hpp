@@ -7,18 +7,10 @@
 #include "ca_fold.hpp"
 #include "ca_scale.hpp"
 
-// the pair codec of the inference RCAB's CA_RESID epilogue (common.hpp: the fast form
-// by default; SRMI_PAIR_FAST=0 for the reference form, bit-identical to ca_fwd's)
-#ifndef SRMI_PAIR_FAST
-#define SRMI_PAIR_FAST 1
-#endif
-#if SRMI_PAIR_FAST
+// the pair codec of the CA_RESID / CA_RESID_U epilogues: the fast form (common.hpp; the
+// same quantisation as ca_fwd's reference form for every normal hi, in fewer VALU ops)
 #define PAIR_DEC4 pair_decode4_fast
 #define PAIR_ENC4 pair_encode4_fast
-#else
-#define PAIR_DEC4 pair_decode4
-#define PAIR_ENC4 pair_encode4
-#endif
 #include "common.hpp"
 #include "srmi_internal.hpp"
 
@@ -77,9 +69,6 @@ struct EpiPre {
 
 // the gradient-stream epilogues (DG_ACC_CA, DG_ACC) add their fp32 operands to the
 // staged dgrad in the 1 KiB run layout of the stores instead of the MFMA layout
-#ifndef SRMI_DGACC_RUN
-#define SRMI_DGACC_RUN 1
-#endif
 // h' = h + s u into the residual pair: the inference RCAB's conv2 (u never stored) and
 // the training one's (u stored for backward, and rounded to bf16 before the product)
 template <int EPI>
@@ -88,7 +77,7 @@ constexpr bool epi_cr() {
 }
 template <int EPI>
 constexpr bool epi_run() {
-  return EPI == EPI_DG_ACC_CA || (SRMI_DGACC_RUN && EPI == EPI_DG_ACC) || epi_cr<EPI>();
+  return EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC || epi_cr<EPI>();
 }
 
 // one (pt, c) element (idx = pt * NCT + c), issued one or two per K-step
@@ -441,13 +430,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
   }
 }
 
-#ifndef SRMI_CONV_FRAGBUF
-#define SRMI_CONV_FRAGBUF 2
-#endif
-constexpr int kFragBuf = SRMI_CONV_FRAGBUF;
-#ifndef SRMI_CONV_ILV
-#define SRMI_CONV_ILV 1
-#endif  // register buffers of A/B fragments (K-steps)
+constexpr int kFragBuf = 2;  // register buffers of A/B fragments (K-steps)
 
 #ifndef SRMI_DEFER
 #define SRMI_DEFER 4  // bit mask: 1 RELU, 2 POOL, 4 DG_RELUMASK, 8 DG_ACC_CA (in-step A/B: only 4 gains)
@@ -679,7 +662,6 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
 #pragma unroll
         for (int c = 0; c < NCT; ++c)
           acc[pt][c] = mfma16(A[s % kFragBuf][c], B[s % kFragBuf][pt], acc[pt][c]);
-#if SRMI_CONV_ILV
       // one fragment read issued behind each MFMA: the reads' issue time hides under
       // the MFMA pipe instead of stalling it between K-steps
       if (ld) {
@@ -690,7 +672,6 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
         }
         if constexpr (NCT * NPT > NCT + NPT) __builtin_amdgcn_sched_group_barrier(0x008, NCT * NPT - (NCT + NPT), 0);
       }
-#endif
       __builtin_amdgcn_sched_barrier(0);
     }
     // group k+2's DMA, the epilogue operands and the previous strip's stores had the
@@ -754,20 +735,10 @@ __device__ __forceinline__ void pin4(f32x4& v) {
 __device__ __forceinline__ void pin4f(float4& v) { pin(v.x); pin(v.y); pin(v.z); pin(v.w); }
 __device__ __forceinline__ void pin4u(uint4& v) { pin(v.x); pin(v.y); pin(v.z); pin(v.w); }
 
-#ifndef SRMI_DEFER_WT
-#define SRMI_DEFER_WT 1  // deferred epilogue stores: 1 write-through (sc1), 0 plain
-#endif
-#ifndef SRMI_DEFER_PRIO
-#define SRMI_DEFER_PRIO 0
-#endif
+// deferred epilogue stores: write-through (sc1) like the others (SRMI_WT)
 template <typename V>
 __device__ __forceinline__ void st_defer(__amdgpu_buffer_rsrc_t r, void* base, uint32_t off, const V& v) {
-#if SRMI_DEFER_WT
   st_wt16(r, base, off, v);
-#else
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
-  (void)base;
-#endif
 }
 
 template <int NPT>
@@ -1204,11 +1175,6 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
   };
   using T = std::true_type;
   using F = std::false_type;
-#if SRMI_DEFER_PRIO
-  // the second-dispatched half (waves 4-7) loses every MFMA arbitration to its older
-  // partner and reaches the strip barrier ~1.2 K cycles later: static priority
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
   if (k1 - k0 == 1) {
     strip(k0, F{}, T{});
   } else {

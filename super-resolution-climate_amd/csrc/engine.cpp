@@ -242,17 +242,21 @@ static int engine_cus(const srmi_engine* e) { return e->cu_budget > 0 ? e->cu_bu
 // CU shares of the two parts of a fused launch, in percent of the engine budget taken
 // by the filter gradient: after the ReLU-mask dgrad of conv2 (FUSE_WG2) and after the
 // gradient-accumulating dgrad of conv1 (FUSE_WG1, the heavier conv epilogue)
-#ifndef SRMI_FUSE_WG2
-#define SRMI_FUSE_WG2 50
-#endif
-#ifndef SRMI_FUSE_WG1
-#define SRMI_FUSE_WG1 50
-#endif
 static int fuse_wg_cus(const srmi_engine* e, int which) {
-  return engine_cus(e) * (which == 2 ? SRMI_FUSE_WG2 : SRMI_FUSE_WG1) / 100;
+  (void)which;  // half the budget for both fused launches (44 / 56 % measured within noise)
+  return engine_cus(e) / 2;
+}
+// The RCAB filter gradients in co halves (WgradParams.co_split = 2): a workgroup
+// computes half of the 64 output channels over chunks of twice the rows, so each
+// fused launch writes (and the next one reduces) half the partial slabs.
+// SRMI_FLAG_WGRAD_FULL_CO: whole co blocks (A/B); the CA fold needs them.
+static int rcab_co_split(const srmi_engine* e) {
+  const int f = e->P.cfg.flags;
+  return (!e->f32 && e->P.cfg.arch == SRMI_ARCH_RCAN && e->w == 48 && !(f & SRMI_FLAG_WGRAD_FULL_CO) &&
+          !(f & SRMI_FLAG_CA_FOLD)) ? 2 : 1;
 }
 static int rcab_row_splits(const srmi_engine* e, int n, int which) {
-  return choose_row_splits(n, e->h, 64, fuse_wg_cus(e, which));
+  return choose_row_splits(n * rcab_co_split(e), e->h, 64, fuse_wg_cus(e, which));
 }
 
 static size_t carve(srmi_engine* e, char* base) {
@@ -398,9 +402,6 @@ static inline hipStream_t S_(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 // --------------------------------------------------------------- conv helpers
 // forward convs sized for this share of the engine's CU budget (A/B: fewer, longer runs)
-#ifndef SRMI_FWD_CUS_PCT
-#define SRMI_FWD_CUS_PCT 100
-#endif
 static ConvParams fwd_params(srmi_engine* e, const ConvRef& c, const bf16_t* x, int n, int H, int W, bf16_t* yb,
                              float* yf, const float* r1, float* part, float alpha) {
   ConvParams p{};
@@ -421,7 +422,7 @@ static ConvParams fwd_params(srmi_engine* e, const ConvRef& c, const bf16_t* x, 
   p.part_stride = 64;
   p.alpha = alpha;
   p.zeros = e->zeros;
-  p.cu_budget = e->cu_budget > 0 ? e->cu_budget * SRMI_FWD_CUS_PCT / 100 : e->cu_budget;
+  p.cu_budget = e->cu_budget;
   return p;
 }
 
@@ -592,12 +593,9 @@ static int upload_tables(srmi_engine* e, hipStream_t st) {
 
 // inference (no saved activations): each RCAB as one launch with a workgroup per image
 // (rcab_infer.hip) -- bf16, 48-wide tiles, a CA bottleneck the MLP code handles
-#ifndef SRMI_RCAB_INFER
-#define SRMI_RCAB_INFER 1
-#endif
 static bool use_rcab_infer(const srmi_engine* e) {
   const int CR = 64 / e->P.cfg.reduction;
-  return SRMI_RCAB_INFER && !(e->P.cfg.flags & SRMI_FLAG_NO_RCAB_INFER) && !e->train && !e->f32 &&
+  return !(e->P.cfg.flags & SRMI_FLAG_NO_RCAB_INFER) && !e->train && !e->f32 &&
          e->P.cfg.arch == SRMI_ARCH_RCAN && e->w == 48 && e->h % 4 == 0 && CR >= 4 && CR <= 32 && CR % 4 == 0;
 }
 
@@ -817,6 +815,7 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
                                      nullptr, 1.f);
         RC(wgrad_params(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, rs2, e->slab_r[q][0], e->bslab_r[q][0],
                         e->slab_r_floats, e->bslab_r_floats, &wp, &red2));
+        wp.co_split = rcab_co_split(e);
         if (folded) {
           cp.fold = fold_consumer(e, prm, r, g, b, nstrips);
           wp.fold = cp.fold;
@@ -839,6 +838,7 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         }
         RC(wgrad_params(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, rs1, e->slab_r[q][1],
                         e->bslab_r[q][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red1));
+        wp.co_split = rcab_co_split(e);
         RC(dgrad_with_wgrad(e, cp, epi, wp, 1, st));
         prev2 = red2;
         prev1 = red1;
@@ -1004,6 +1004,7 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
                       1.f);
     RC(wgrad_params(e, r.c2, e->Tm(0, b), e->DU, n, h, w, grads, false, 1.f, rcab_row_splits(e, n, 2),
                     e->slab_r[0][0], e->bslab_r[0][0], e->slab_r_floats, e->bslab_r_floats, &wp, &red));
+    wp.co_split = rcab_co_split(e);
     if (fold) {
       cp.fold = fold_consumer(e, e->probe_prm, r, 0, b, conv3x3_nstrips(h, w));
       wp.fold = cp.fold;
@@ -1030,6 +1031,7 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
                       nullptr, last ? nullptr : e->Um(0, b - 1), last ? nullptr : e->pacc, 1.f);
     RC(wgrad_params(e, r.c1, e->hb(0, b - 1), e->DZ, n, h, w, grads, true, 1.f, rcab_row_splits(e, n, 1),
                     e->slab_r[0][1], e->bslab_r[0][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red));
+    wp.co_split = rcab_co_split(e);
     if (use_ca_fold(e, n) && !last) {
       cp.fold.du_out = e->DU;
       cp.fold.s_rec = e->recp(0, b - 1);

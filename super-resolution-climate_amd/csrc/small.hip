@@ -1081,16 +1081,8 @@ constexpr int kCaVec = SRMI_CA_VEC;
 // instead of 12 with an fp32 stream (10 with a bf16 lo).
 enum CaMode { CA_F32 = 0, CA_F32LO = 1, CA_LO = 2 };
 // the training pass's codec: the reference form (1: the fast form of common.hpp)
-#ifndef SRMI_CA_PAIR_FAST
-#define SRMI_CA_PAIR_FAST 0
-#endif
-#if SRMI_CA_PAIR_FAST
-#define CA_DEC4 pair_decode4_fast
-#define CA_ENC4 pair_encode4_fast
-#else
 #define CA_DEC4 pair_decode4
 #define CA_ENC4 pair_encode4
-#endif
 
 // (lo8_encode / lo8_decode, the pair codec: common.hpp)
 template <typename T, int MODE>

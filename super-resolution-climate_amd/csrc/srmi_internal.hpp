@@ -132,6 +132,9 @@ struct WgradParams {
   // after their own chunk (nred = 0: none)
   ReduceSet red[2];
   int nred;
+  // 2: every workgroup computes half of a co block's output channels over its chunk
+  // (wgrad48 only; the engine then takes chunks of twice the rows: half the slabs)
+  int co_split;
 };
 void wgrad3x3_set_debug_stamps(unsigned long long* buf);
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st);  // dispatches p.f32

@@ -244,9 +244,6 @@ constexpr int kFoldOff = Conv2Smem<48>::TOTAL;
 static_assert(Conv2Smem<48>::TOTAL >= v4::LDS, "fold scratch must not overlap the rings");
 static_assert(kFoldOff + kFoldBytes <= 160 * 1024, "LDS");
 
-#ifndef SRMI_SLAB_WT
-#define SRMI_SLAB_WT 1  // partial slabs stored write-through (in-step A/B +1.1 %)
-#endif
 
 // The body is instantiated once per wave (WV = wave index): the wave's DMA groups,
 // taps and tile rotation are compile-time constants (no SGPR pressure, no branches).
@@ -375,19 +372,24 @@ __device__ __forceinline__ void add_fold_c(bf16x8 (&a)[4], const float (&fc)[4])
 #ifndef SRMI_FOLD_WG
 #define SRMI_FOLD_WG 2
 #endif
-template <int WV, int NW = 4, bool FOLD = false>
-__device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, int chunk, int cb) {
+// HALF (co_split = 2): the workgroup computes one half (`half`: output-channel tiles
+// 2 half, 2 half + 1) of the co block's filter gradient over a chunk of twice the
+// rows -- a whole image -- so that a launch writes half the partial slabs for the
+// same MFMA work per workgroup; the two halves of an image write disjoint tiles of
+// one slab (layout 1 unchanged, the reduction too).  The dY rows are still DMA'd
+// whole (the other half's channels ride along, L2 hits).
+template <int WV, int NW = 4, bool FOLD = false, bool HALF = false>
+__device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, int chunk, int cb, int half = 0) {
   constexpr bool FOLD_A = FOLD && SRMI_FOLD_WG == 2;
   using namespace v4;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-#ifndef SRMI_WG_OLD5
-#define SRMI_WG_OLD5 0  // 1: the older half (waves 0-3, the MFMA-arbitration winners) takes 5 tiles
-#endif
-  constexpr int NT = NW == 4 ? 9 : ((WV < 4) == (SRMI_WG_OLD5 != 0) ? 5 : 4);  // N tiles of this wave
-  constexpr int J0 = NW == 4 ? 9 * WV
-                             : (SRMI_WG_OLD5 ? (WV < 4 ? 5 * WV : 20 + 4 * (WV - 4))
-                                             : (WV < 4 ? 4 * WV : 16 + 5 * (WV - 4)));  // its first N tile
-  constexpr bool kMain = WV < 4;  // DMA + bias gradient
+  static_assert(!(FOLD && HALF), "the fold runs on whole co blocks");
+  constexpr int NCA = HALF ? 2 : 4;  // output-channel (A) tiles of this workgroup's waves
+  // N tiles of this wave and its first one (8 waves: the younger half, waves 4-7, takes 5)
+  constexpr int NT = NW == 4 ? 9 : (WV < 4 ? 4 : 5);
+  constexpr int J0 = NW == 4 ? 9 * WV : (WV < 4 ? 4 * WV : 16 + 5 * (WV - 4));
+  constexpr bool kMain = WV < 4;  // DMA (+ the bias gradient: waves 0-3, or 0-1 of a half)
+  constexpr bool kBias = HALF ? WV < 2 : WV < 4;
   const int tid = threadIdx.x, lane = tid & 63;
   constexpr int wave = WV & 3, wave_s = WV & 3;
   // chunk = (image, row band, 48-column block): W may be any multiple of 48 (the
@@ -475,11 +477,13 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
     }
   };
 
-  f32x4 acc[4][NT];
+  f32x4 acc[NCA][NT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NCA; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the output-channel tile of A slot ct: rotated by the wave (LDS banks), within the half
+  auto ctile = [&](int ct) -> int { return HALF ? 2 * half + ((ct + wave) & 1) : (ct + wave) & 3; };
   f32x4 bacc = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 ones;
 #pragma unroll
@@ -488,19 +492,19 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   // transposed-read lane coordinates (see v3); row parts are added per pair
   const int g4 = lane >> 4, li = lane & 15, lq = li >> 2, lp = li & 3;
   const int prow = g4 >> 1, pcol = 8 * (g4 & 1) + lq;
-  const uint32_t half = (lp & 1) * 8;
-  uint32_t acol[4][2], bcol[NT][2];
+  const uint32_t hoff = (lp & 1) * 8;
+  uint32_t acol[NCA][2], bcol[NT][2];
   int bky[NT];
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct)
+  for (int ct = 0; ct < NCA; ++ct)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) acol[ct][h] = swz128t(pcol + 4 * h, 2 * ((ct + wave) & 3) + (lp >> 1)) + half;
+    for (int h = 0; h < 2; ++h) acol[ct][h] = swz128t(pcol + 4 * h, 2 * ctile(ct) + (lp >> 1)) + hoff;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int j = J0 + t, tap = j >> 2, it = j & 3, kx = tap % 3;
     bky[t] = tap / 3;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) bcol[t][h] = DY_RING + swz128t(pcol + kx + 4 * h, 2 * it + (lp >> 1)) + half;
+    for (int h = 0; h < 2; ++h) bcol[t][h] = DY_RING + swz128t(pcol + kx + 4 * h, 2 * it + (lp >> 1)) + hoff;
   }
 
   // slot offsets: dY row r -> slot r & (RD-1); input row r -> slot (r + 1) % RX.
@@ -518,9 +522,9 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
       rb[t] = (uint32_t)(sl * XSLOT);
     }
   };
-  auto load_a = [&](uint32_t ra, int kc, bf16x8 (&a)[4]) __attribute__((always_inline)) {
+  auto load_a = [&](uint32_t ra, int kc, bf16x8 (&a)[NCA]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
+    for (int ct = 0; ct < NCA; ++ct)
       a[ct] = cat_tr(lds_tr(smem, ra + acol[ct][0] + kc * 2048), lds_tr(smem, ra + acol[ct][1] + kc * 2048));
   };
   auto load_b = [&](const uint32_t (&rb)[NT], int kc, bf16x8 (&b)[NT]) __attribute__((always_inline)) {
@@ -528,10 +532,10 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
     for (int t = 0; t < NT; ++t)
       b[t] = cat_tr(lds_tr(smem, rb[t] + bcol[t][0] + kc * 2048), lds_tr(smem, rb[t] + bcol[t][1] + kc * 2048));
   };
-  auto load_step = [&](uint32_t ra, const uint32_t (&rb)[NT], int kc, bf16x8 (&a)[4], bf16x8 (&b)[NT])
+  auto load_step = [&](uint32_t ra, const uint32_t (&rb)[NT], int kc, bf16x8 (&a)[NCA], bf16x8 (&b)[NT])
       __attribute__((always_inline)) {
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
+    for (int ct = 0; ct < NCA; ++ct)
       a[ct] = cat_tr(lds_tr(smem, ra + acol[ct][0] + kc * 2048), lds_tr(smem, ra + acol[ct][1] + kc * 2048));
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -572,16 +576,17 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
     for (int ct = 0; ct < 4; ++ct) fc[ct] = fsm[kFoldC + ((ct + wave) & 3) * 16 + (lane & 15)];
   }
   WSTAMP(1);
-#ifdef SRMI_WG_PRIO
-  if constexpr (NW == 8 && WV >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
 
   // fragments double-buffered across K-steps; a pair has 3 K-steps, so the pair loop
   // is unrolled by two (np is even) to keep the buffer parity compile-time.  8 waves
   // (256 registers a wave): B single-buffered, each tile reloaded right behind its
   // MFMAs (the partner wave on the SIMD covers the read latency).
-  constexpr int NB = NW == 8 ? 1 : 2;
-  bf16x8 A[2][4], B[NB][NT];
+  // (co halves hold half the accumulators: room for double-buffered B, SRMI_HALF_NB = 2)
+#ifndef SRMI_HALF_NB
+#define SRMI_HALF_NB 1
+#endif
+  constexpr int NB = (NW == 8 && !(HALF && SRMI_HALF_NB == 2)) ? 1 : 2;
+  bf16x8 A[2][NCA], B[NB][NT];
   uint32_t ra, rb[NT];
   slots(0, ra, rb);
   load_step(ra, rb, 0, A[0], B[0]);
@@ -614,14 +619,14 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
-          for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(A[cur][ct], B[cur % NB][t], acc[ct][t]);
-        if constexpr (kMain) bacc = mfma16(A[cur][0], ones, bacc);  // slot 0 = this wave's own co tile
+          for (int ct = 0; ct < NCA; ++ct) acc[ct][t] = mfma16(A[cur][ct], B[cur % NB][t], acc[ct][t]);
+        if constexpr (kBias) bacc = mfma16(A[cur][0], ones, bacc);  // slot 0 = this wave's own co tile
         if constexpr (NB == 1) {
           if (kc < 2) load_b(rb, kc + 1, B[0]);
           else if (more) load_b(rbn, 0, B[0]);
         }
         // the next K-step's transposed reads issued behind the MFMAs, one per MFMA
-        constexpr int NRD = 2 * (4 + NT), NMF = 4 * NT + (kMain ? 1 : 0);
+        constexpr int NRD = 2 * (NCA + NT), NMF = NCA * NT + (kBias ? 1 : 0);
         constexpr int NPAIR = NRD < NMF ? NRD : NMF;
         if (ld) {
 #pragma unroll
@@ -671,51 +676,59 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      const int J = J0 + t, w4 = J / 9, t4 = J % 9, s4 = (ct + wave - w4) & 3;
+    for (int ct = 0; ct < NCA; ++ct) {
+      const int J = J0 + t, w4 = J / 9, t4 = J % 9, s4 = (ctile(ct) - w4) & 3;
       const float4 v = make_float4(acc[ct][t][0], acc[ct][t][1], acc[ct][t][2], acc[ct][t][3]);
       const size_t o = soff + (size_t)w4 * (9 * 4 * 256) + ((t4 * 4 + s4) * 64 + lane) * 4;
-#if SRMI_SLAB_WT
       st_wt16(rsl, p.slab, (uint32_t)(o * 4), v);
-#else
-      *reinterpret_cast<float4*>(p.slab + o) = v;
-#endif
     }
-  if (kMain && (lane & 15) == 0) {
+  if (kBias && (lane & 15) == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      p.bslab[(size_t)chunk * Cout + cb * 64 + wave * 16 + 4 * (lane >> 4) + r] = bacc[r];
+      p.bslab[(size_t)chunk * Cout + cb * 64 + ctile(0) * 16 + 4 * (lane >> 4) + r] = bacc[r];
   }
   WSTAMP(63);
 }
 
-template <int NW = 4, bool FOLD = false>
-__device__ __forceinline__ void wgrad48_dispatch(const WgradParams& p, char* smem, int chunk, int cb) {
+template <int NW = 4, bool FOLD = false, bool HALF = false>
+__device__ __forceinline__ void wgrad48_dispatch(const WgradParams& p, char* smem, int chunk, int cb, int half = 0) {
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: wgrad48_body<0, NW, FOLD>(p, smem, chunk, cb); break;
-    case 1: wgrad48_body<1, NW, FOLD>(p, smem, chunk, cb); break;
-    case 2: wgrad48_body<2, NW, FOLD>(p, smem, chunk, cb); break;
-    case 3: wgrad48_body<3, NW, FOLD>(p, smem, chunk, cb); break;
+    case 0: wgrad48_body<0, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
+    case 1: wgrad48_body<1, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
+    case 2: wgrad48_body<2, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
+    case 3: wgrad48_body<3, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
     default:
       if constexpr (NW == 8) {
         switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-          case 4: wgrad48_body<4, NW, FOLD>(p, smem, chunk, cb); break;
-          case 5: wgrad48_body<5, NW, FOLD>(p, smem, chunk, cb); break;
-          case 6: wgrad48_body<6, NW, FOLD>(p, smem, chunk, cb); break;
-          default: wgrad48_body<7, NW, FOLD>(p, smem, chunk, cb); break;
+          case 4: wgrad48_body<4, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
+          case 5: wgrad48_body<5, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
+          case 6: wgrad48_body<6, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
+          default: wgrad48_body<7, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
         }
       }
       break;
   }
 }
 
-#ifndef SRMI_WGRAD_NW
-#define SRMI_WGRAD_NW 8
-#endif
-constexpr int kWgradNW = SRMI_WGRAD_NW;  // waves per workgroup of the standalone filter gradient
+// workgroup index w of a filter-gradient grid -> (chunk, co block, half): with
+// co halves, w = 2 (cb nch + chunk) + half, so the two halves of a chunk are
+// neighbours (and conv run w of a paired fused launch covers the same image)
+__device__ __forceinline__ void wgrad_unit(const WgradParams& p, int w, int& chunk, int& cb, int& half) {
+  const int nch = p.N * p.row_splits * (p.W / 48);
+  const int cs = p.co_split == 2 ? 2 : 1;
+  half = w % cs;
+  const int r = w / cs;
+  chunk = r % nch;
+  cb = r / nch;
+}
+
+constexpr int kWgradNW = 8;  // waves per workgroup of the standalone filter gradient (two per SIMD)
+template <bool HALF>
 __global__ void __launch_bounds__(kWgradNW * 64, 1) wgrad48_kernel(WgradParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  wgrad48_dispatch<kWgradNW>(p, smem, blockIdx.x, blockIdx.y);
+  int chunk, cb, half;
+  wgrad_unit(p, blockIdx.x, chunk, cb, half);
+  wgrad48_dispatch<kWgradNW, false, HALF>(p, smem, chunk, cb, half);
 }
 
 // ---------------------------------------------------------------------------
@@ -740,7 +753,7 @@ __global__ void __launch_bounds__(kWgradNW * 64, 1) wgrad48_kernel(WgradParams p
 // dgrad half (F1: 24.7 vs 36.9 us at C2), so the last `tail` strips of dgrad run k
 // move to the workgroup of chunk k, which runs them after its chunk (same rows, same
 // XCD), with its own filter prologue.
-template <int EPI, int NW, bool FOLD = false>
+template <int EPI, int NW, bool FOLD = false, bool HALF = false>
 __global__ void __launch_bounds__(NW * 64, 1) rcab_bwd_kernel(ConvParams cp, int run_len, int nconv, WgradParams wp,
                                                               int nwg, int paired, int tail) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -767,8 +780,11 @@ __global__ void __launch_bounds__(NW * 64, 1) rcab_bwd_kernel(ConvParams cp, int
     if (!(SRMI_FUSE_DIAG & 2)) conv64_body<48, EPI, NW, kFoldConv>(cp, run_len, conv, smem, tail, false);
     return;
   }
-  const int nch = wp.N * wp.row_splits;
-  if (!(SRMI_FUSE_DIAG & 1)) wgrad48_dispatch<NW, kFoldWg>(wp, smem, w % nch, w / nch);
+  if (!(SRMI_FUSE_DIAG & 1)) {
+    int chunk, cb, half;
+    wgrad_unit(wp, w, chunk, cb, half);
+    wgrad48_dispatch<NW, kFoldWg, HALF>(wp, smem, chunk, cb, half);
+  }
   if constexpr (kF2 && FOLD) {
     if (wp.nred > 0) {  // the previous RCAB's slab reductions, shared over this launch's filter-gradient workgroups
       static_assert(NW * 64 == 512, "slab_reduce_share runs on 512 threads");
@@ -784,14 +800,11 @@ __global__ void __launch_bounds__(NW * 64, 1) rcab_bwd_kernel(ConvParams cp, int
 int rcab_bwd_fusable(const ConvParams& cp, const WgradParams& wp) {
   return !cp.f32 && !wp.f32 && cp.Cin == 64 && cp.Cout == 64 && cp.in_mode == IN_PLAIN && cp.W == 48 &&
          cp.H % 4 == 0 && wp.W == 48 && wp.Cout == 64 && wp.dy_mode == IN_PLAIN && wp.row_splits > 0 &&
-         wp.H % wp.row_splits == 0 && (wp.H / wp.row_splits) % 4 == 0;
+         wp.H % wp.row_splits == 0 && (wp.H / wp.row_splits) % 4 == 0 && (wp.co_split == 2 ? !wp.fold.on : true);
 }
 
 // waves per workgroup of the fused launch (8: two per SIMD in both roles)
-#ifndef SRMI_FUSE_NW
-#define SRMI_FUSE_NW 8
-#endif
-constexpr int kFuseNW = SRMI_FUSE_NW;
+constexpr int kFuseNW = 8;
 
 // the partial slabs are stored through a buffer resource with a 32-bit byte range
 static bool slab_range_ok(const WgradParams& p, int nslabs) {
@@ -803,7 +816,8 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
   if (!slab_range_ok(wp, wp.N * wp.row_splits)) return SRMI_ERR_SHAPE;
   const int run_len = conv64_run_len(cp, 48, conv_cus);
   const int nconv = conv64_blocks(cp, 48, run_len);
-  const int nwg = wp.N * wp.row_splits * (wp.Cout / 64);
+  const int cs = wp.co_split == 2 ? 2 : 1;
+  const int nwg = wp.N * wp.row_splits * (wp.Cout / 64) * cs;
   const bool fold = cp.fold.on != 0;
   if (fold && (epi != EPI_DG_RELUMASK || !wp.fold.on || !cp.fold.part || !cp.fold.rec || !cp.fold.w1 ||
                !cp.fold.w2 || !cp.fold.brec || cp.fold.CR < 4 || cp.fold.CR > 32 || cp.fold.CR % 4 ||
@@ -822,22 +836,41 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
   WgradParams w = wp;
   w.stamps = nullptr;
   const dim3 grid(nconv + nwg);
-#ifndef SRMI_FUSE_PAIR
-#define SRMI_FUSE_PAIR 1
-#endif
   // conv run k and wgrad chunk k cover the same rows of the same image
   const int runs_per_col = (cp.H / kTH + run_len - 1) / run_len;
-  const int paired = SRMI_FUSE_PAIR && nconv == nwg && cp.N == wp.N && runs_per_col == wp.row_splits &&
-                     run_len * kTH == wp.H / wp.row_splits;
+  // (co halves: conv run k and filter-gradient workgroup k cover the same image)
+  const int paired = nconv == nwg && cp.N == wp.N &&
+                     (cs == 2 ? runs_per_col == 2 * wp.row_splits
+                              : runs_per_col == wp.row_splits && run_len * kTH == wp.H / wp.row_splits);
   // dgrad strips per run handed to the paired filter-gradient workgroup (see the kernel)
-#ifndef SRMI_TAIL_F1
-#define SRMI_TAIL_F1 1
-#endif
-#ifndef SRMI_TAIL_F2
-#define SRMI_TAIL_F2 0
-#endif
-  const int tail = !paired ? 0 : std::min(run_len - 1, epi == EPI_DG_RELUMASK ? SRMI_TAIL_F2 : SRMI_TAIL_F1);
+  // (one strip in F1; none in F2, whose ReLU-mask strip is cheaper than the extra
+  // filter prologue: DESIGN.md section 3)
+  const int tail = !paired ? 0 : std::min(run_len - 1, epi == EPI_DG_RELUMASK ? 0 : 1);
   if (wp.nred > 0 && tail > 0) return SRMI_ERR_ARG;  // (the reduction share uses the ring LDS the tail needs)
+  if (cs == 2) {  // co halves (no fold)
+    if (fold || c.fold.du_out) return SRMI_ERR_ARG;
+    switch (epi) {
+      case EPI_DG_RELUMASK:
+        if (!c.aux) return SRMI_ERR_ARG;
+        hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_RELUMASK, kFuseNW, false, true>), grid, dim3(kFuseNW * 64), lds, st,
+                           c, run_len, nconv, w, nwg, paired, tail);
+        break;
+      case EPI_DG_ACC_CA:
+        if (!c.r1 || !c.aux || !c.part || c.yb || c.r2 || c.r3 || !c.yf) return SRMI_ERR_ARG;
+        hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA, kFuseNW, false, true>), grid, dim3(kFuseNW * 64), lds, st,
+                           c, run_len, nconv, w, nwg, paired, tail);
+        break;
+      case EPI_DG_ACC:
+        if (!c.yf || (c.part && !c.aux)) return SRMI_ERR_ARG;
+        hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC, kFuseNW, false, true>), grid, dim3(kFuseNW * 64), lds, st, c,
+                           run_len, nconv, w, nwg, paired, tail);
+        break;
+      default:
+        return SRMI_ERR_ARG;
+    }
+    SRMI_CHECK_LAUNCH();
+    return 0;
+  }
   switch (epi) {
     case EPI_DG_RELUMASK:
       if (!c.aux) return SRMI_ERR_ARG;
@@ -891,7 +924,12 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
   WgradParams q = p;
   q.stamps = g_wg_stamps;
   if (use_wgrad48(p)) {
-    hipLaunchKernelGGL(wgrad48_kernel, grid, dim3(kWgradNW * 64), v4::LDS, st, q);
+    const int cs = p.co_split == 2 ? 2 : 1;
+    const dim3 g48(wgrad3x3_nslabs(p) * (p.Cout / 64) * cs);
+    if (cs == 2)
+      hipLaunchKernelGGL(wgrad48_kernel<true>, g48, dim3(kWgradNW * 64), v4::LDS, st, q);
+    else
+      hipLaunchKernelGGL(wgrad48_kernel<false>, g48, dim3(kWgradNW * 64), v4::LDS, st, q);
   } else if (p.W % 48 == 0) {
     hipLaunchKernelGGL(wgrad3x3_kernel<48>, grid, dim3(256), Wg3<48>::TOTAL, st, q);
   } else if (p.W % 32 == 0) {

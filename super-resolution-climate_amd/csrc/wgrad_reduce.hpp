@@ -125,11 +125,8 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab
 __device__ __forceinline__ void slab_reduce_share(const ReduceSet& ra, const ReduceSet& rb, int nred, int part,
                                                   int nparts, float4* lds) {
   constexpr int PERQ = 64 * 576 / 4;  // output quads per set
-#ifndef SRMI_RED_LOADS
-#define SRMI_RED_LOADS 16
-#endif
   // QR quads per round x NPH slab phases, up to NL loads in flight per thread
-  constexpr int NL = SRMI_RED_LOADS, NPH = NL == 32 ? 2 : 4, QR = 512 / NPH;
+  constexpr int NL = 16, NPH = 4, QR = 512 / NPH;
   const int tid = threadIdx.x, qi = tid % QR, ph = tid / QR;
   const int total = nred * PERQ;
   const int q0 = (int)((long long)total * part / nparts), q1 = (int)((long long)total * (part + 1) / nparts);

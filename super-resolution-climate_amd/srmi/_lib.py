@@ -21,6 +21,7 @@ SRMI_FLAG_CA_FOLD = 1
 SRMI_FLAG_NO_RCAB_INFER = 2
 SRMI_FLAG_CA_PASS = 4
 SRMI_FLAG_CA_SCALE_LAUNCH = 8
+SRMI_FLAG_WGRAD_FULL_CO = 16
 SRMI_DTYPE_F32 = 1
 SRMI_LOSS_RMSE = 0
 SRMI_LOSS_MEAN = 1

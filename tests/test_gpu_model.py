@@ -375,3 +375,14 @@ def test_ca_scale_launch_bit_identical_to_prologue_scale(lr_hw):
     scale in conv2's prologue: bit-identical forward and gradients."""
     from srmi._lib import SRMI_FLAG_CA_SCALE_LAUNCH
     _engine_variants_agree(lr_hw, (0, SRMI_FLAG_CA_SCALE_LAUNCH), 0)
+
+
+@pytest.mark.parametrize("lr_hw", [(48, 48), (32, 48), (8, 48)])
+def test_wgrad_co_halves_match_full_co_blocks(lr_hw):
+    """The RCAB filter gradients in co halves over whole-image chunks (the default:
+    half the partial slabs per fused launch; wgrad3x3.hip HALF) against whole
+    64-channel co blocks over half-image chunks (SRMI_FLAG_WGRAD_FULL_CO): the forward
+    is untouched, the gradients differ only in how the fp32 partial sums are grouped
+    into slabs."""
+    from srmi._lib import SRMI_FLAG_WGRAD_FULL_CO
+    _engine_variants_agree(lr_hw, (0, SRMI_FLAG_WGRAD_FULL_CO), 1e-5)

@@ -5,4 +5,4 @@ R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R; O=$R/gpurun_out; mkdir -p $O; rm -f $O/
 timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_model.py \
   tests/test_gpu_inference.py tests/test_gpu_fullsize.py > $O/t2.log 2>&1
 rc=$?; tail -40 $O/t2.log; [ $rc -eq 0 ] || exit $rc
-REPS=${REPS:-2} bash tools/ab_var.sh "prologue::" "launch::--ca-scale-launch" "pass::--ca-pass"
+REPS=${REPS:-2} bash tools/ab_var.sh "default::" "fullco::--wgrad-full-co" "launch::--ca-scale-launch" "pass::--ca-pass" "fold::--ca-fold" "halfnb2:alt/libsrmi_halfnb2.so:"
