@@ -185,6 +185,15 @@ int srmi_batch_losses(const float* pred, const float* target, int ntiles, long l
  * (process_image's np.array(batch_losses).mean(), dual_trainer.py:443-446) */
 int srmi_batch_loss_means(const float* sums, int ntiles, long long tile_elems, int batch_size, int kind, float* out,
                           void* stream);
+/* loss sums that do not depend on how a batch is split over calls / micro-batch
+ * engines: srmi_tile_loss_parts writes parts[ntiles][16] (per tile, 16 fixed slices,
+ * fixed reduction order; kind RMSE: (p - t)^2, MEAN: sqrt((p - t)^2 + eps)) -- each
+ * call writes its tiles' rows of one batch-wide array; srmi_loss_from_parts then sums
+ * the ntiles x 16 parts in order (fp64) into loss4 ([0] = S, [1] = count_global) and
+ * finalises it as `kind` (-1: not finalised, before a data-parallel all-reduce) */
+int srmi_tile_loss_parts(const float* pred, const float* target, int ntiles, long long tile_elems, int kind,
+                         float eps, float* parts, void* stream);
+int srmi_loss_from_parts(const float* parts, int ntiles, double count_global, int kind, float* loss4, void* stream);
 /* loss4 = the sum over nparts micro-batch records parts4[k][4] (S summed in a fixed
  * order, the count of part 0), then finalised as `kind` (-1: not finalised, e.g.
  * before a data-parallel all-reduce of loss4[0]) */

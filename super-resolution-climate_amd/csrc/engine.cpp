@@ -1072,6 +1072,17 @@ int srmi_batch_losses(const float* pred, const float* target, int ntiles, long l
   return batch_losses_launch(pred, target, ntiles, tile_elems, batch_size, kind, eps, work, out, S_(stream));
 }
 
+int srmi_tile_loss_parts(const float* pred, const float* target, int ntiles, long long tile_elems, int kind,
+                         float eps, float* parts, void* stream) {
+  if (!pred || !target || !parts || (kind != SRMI_LOSS_RMSE && kind != SRMI_LOSS_MEAN)) return SRMI_ERR_ARG;
+  return tile_loss_parts_launch(pred, target, ntiles, tile_elems, kind, eps, parts, S_(stream));
+}
+
+int srmi_loss_from_parts(const float* parts, int ntiles, double count_global, int kind, float* loss4, void* stream) {
+  if (!parts || !loss4 || kind < -1 || kind > SRMI_LOSS_MEAN) return SRMI_ERR_ARG;
+  return loss_from_parts_launch(parts, ntiles * kTileSub, count_global, kind, loss4, S_(stream));
+}
+
 int srmi_batch_loss_means(const float* sums, int ntiles, long long tile_elems, int batch_size, int kind, float* out,
                           void* stream) {
   if (!sums || !out || (kind != SRMI_LOSS_RMSE && kind != SRMI_LOSS_MEAN)) return SRMI_ERR_ARG;

@@ -1005,6 +1005,70 @@ int batch_losses_launch(const float* y, const float* t, int ntiles, long long ti
   return 0;
 }
 
+// Loss sums invariant to how the batch is split over micro-batch engines (and over
+// calls): every tile's elements are summed by kTileSub blocks over fixed slices with a
+// fixed reduction tree, into parts[tile][kTileSub]; the whole batch's S is then the sum
+// of all parts in tile order, in fp64 (loss_from_parts).  So one engine of B tiles and
+// two of B/2 give a bit-identical loss -- and loss scale 1/(count L), which the bf16
+// gradient maps would otherwise turn from a 1-ulp difference into 1e-5-level noise.
+__global__ void __launch_bounds__(256) tile_loss_parts_kernel(const float* __restrict__ y, const float* __restrict__ t,
+                                                              long long tile_elems, int kind, float eps,
+                                                              float* __restrict__ parts) {
+  __shared__ float red[4];
+  const int sub = blockIdx.x, tile = blockIdx.y;
+  const long long per = (tile_elems + kTileSub - 1) / kTileSub;
+  const long long i0 = (long long)sub * per, i1 = min(tile_elems, i0 + per);
+  const size_t base = (size_t)tile * (size_t)tile_elems;
+  float s = 0.f;
+  for (long long i = i0 + threadIdx.x; i < i1; i += 256) {
+    const float d = y[base + i] - t[base + i];
+    s += kind == LOSS_MEAN ? sqrtf(d * d + eps) : d * d;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) parts[(size_t)tile * kTileSub + sub] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+int tile_loss_parts_launch(const float* y, const float* t, int ntiles, long long tile_elems, int kind, float eps,
+                           float* parts, hipStream_t st) {
+  if (ntiles < 1 || tile_elems < 1) return SRMI_ERR_SHAPE;
+  hipLaunchKernelGGL(tile_loss_parts_kernel, dim3(kTileSub, ntiles), dim3(256), 0, st, y, t, tile_elems, kind, eps,
+                     parts);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// loss4 from the parts of loss_from_parts' tiles: [0] = S (fp64 sum in part order),
+// [1] = count; finalised as `kind` when kind >= 0 (-1: before a data-parallel
+// all-reduce of loss4[0])
+__global__ void __launch_bounds__(256) loss_from_parts_kernel(const float* __restrict__ parts, int nparts, double count,
+                                                              int kind, float* loss) {
+  __shared__ double red[256];
+  const int tid = threadIdx.x;
+  const int per = (nparts + 255) / 256, i0 = tid * per, i1 = min(nparts, i0 + per);
+  double a = 0.0;
+  for (int i = i0; i < i1; ++i) a += parts[i];
+  red[tid] = a;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    loss[0] = (float)red[0];
+    loss[1] = (float)count;
+    if (kind >= 0) loss_finalize_one(loss, kind);
+  }
+}
+
+int loss_from_parts_launch(const float* parts, int nparts, double count, int kind, float* loss, hipStream_t st) {
+  if (nparts < 1 || count <= 0) return SRMI_ERR_ARG;
+  hipLaunchKernelGGL(loss_from_parts_kernel, dim3(1), dim3(256), 0, st, parts, nparts, count, kind, loss);
+  SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
 int batch_loss_means_launch(const float* sums, int ntiles, long long tile_elems, int bs, int kind, float* out,
                             hipStream_t st) {
   if (ntiles < 1 || tile_elems < 1 || bs < 1 || (ntiles + bs - 1) / bs > 1024) return SRMI_ERR_SHAPE;

@@ -185,6 +185,12 @@ int batch_losses_launch(const float* y, const float* t, int ntiles, long long ti
                         float* work, float* out, hipStream_t st);
 int batch_loss_means_launch(const float* sums, int ntiles, long long tile_elems, int bs, int kind, float* out,
                             hipStream_t st);
+// split-invariant loss sums (small.hip): parts[tile][kTileSub] of every tile, then S in
+// fixed order (fp64) into loss4, finalised as kind (>= 0)
+constexpr int kTileSub = 16;
+int tile_loss_parts_launch(const float* y, const float* t, int ntiles, long long tile_elems, int kind, float eps,
+                           float* parts, hipStream_t st);
+int loss_from_parts_launch(const float* parts, int nparts, double count, int kind, float* loss, hipStream_t st);
 int charb_partial_launch(const float* y, const float* t, size_t n, float eps, double count, float* dy,
                          float* partial, int nblk, hipStream_t st);
 

@@ -27,6 +27,7 @@ SRMI_LOSS_RMSE = 0
 SRMI_LOSS_MEAN = 1
 SRMI_INTERP_BILINEAR = 1
 SRMI_INTERP_BICUBIC = 2
+TILE_LOSS_SUB = 16  # parts per tile of srmi_tile_loss_parts
 
 ERRORS = {-10001: "SRMI_ERR_ARG", -10002: "SRMI_ERR_SHAPE", -10003: "SRMI_ERR_WORKSPACE",
           -10004: "SRMI_ERR_UNSUPPORTED"}
@@ -63,6 +64,8 @@ _SIGS = {
     "srmi_charbonnier_partial": ([P, P, P, C.c_size_t, C.c_double, C.c_float, P, P, P], C.c_int),
     "srmi_loss_finalize": ([P, C.c_int, P], C.c_int),
     "srmi_loss_combine": ([P, P, C.c_int, C.c_int, P], C.c_int),
+    "srmi_tile_loss_parts": ([P, P, C.c_int, C.c_longlong, C.c_int, C.c_float, P, P], C.c_int),
+    "srmi_loss_from_parts": ([P, C.c_int, C.c_double, C.c_int, P, P], C.c_int),
     "srmi_batch_losses": ([P, P, C.c_int, C.c_longlong, C.c_int, C.c_int, C.c_float, P, P, P], C.c_int),
     "srmi_batch_loss_means": ([P, C.c_int, C.c_longlong, C.c_int, C.c_int, P, P], C.c_int),
     "srmi_downsample": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P], C.c_int),

@@ -24,7 +24,7 @@ from typing import Dict, Optional
 import torch
 
 from . import checkpoint as ckpt
-from ._lib import SRMI_LOSS_MEAN, SRMI_LOSS_RMSE
+from ._lib import SRMI_LOSS_MEAN, SRMI_LOSS_RMSE, TILE_LOSS_SUB, call, ptr
 from .config import check_fused_task, data_downsample_factor, interp_mode
 from .dist import DistInfo, GradReducer, allreduce_sum_
 from .engine import Engine, NetSpec, adam_step, axpy, downsample, interp_size, upsample
@@ -149,7 +149,10 @@ class FusedTrainer:
         self.loss4 = torch.zeros(4, dtype=torch.float32, device=self.device)
         self.iloss4 = torch.zeros(4, dtype=torch.float32, device=self.device)
         self.mloss4 = torch.zeros((micro, 4), dtype=torch.float32, device=self.device)   # per micro-batch
-        self.miloss4 = torch.zeros((micro, 4), dtype=torch.float32, device=self.device)
+        # the loss sums as per-tile parts (srmi_tile_loss_parts): the step's loss -- and the
+        # gradient scale 1/(count L) -- does not depend on the micro-batch split
+        self.lparts = torch.zeros(batch * TILE_LOSS_SUB, dtype=torch.float32, device=self.device)
+        self.iparts = torch.zeros(batch * TILE_LOSS_SUB, dtype=torch.float32, device=self.device)
         self.streams = [None] + [torch.cuda.Stream(device=self.device) for _ in range(micro - 1)]
         self.dp_staged = not dp_reducer_stream
         self.reducer = GradReducer(self.eng.table, spec.arch, spec.nlayers, self.info, self.device,
@@ -169,21 +172,23 @@ class FusedTrainer:
         st = self.streams[k]
         return torch.cuda.stream(st) if st is not None else _Null()
 
-    def _loss_partial(self, eng: Engine, pred, target, loss4, count, dy=None):
-        if self.loss_kind == SRMI_LOSS_MEAN:
-            eng.charbonnier_partial(pred, target, loss4, count, CHARBONNIER_EPS, dy=dy)
-        else:
-            eng.rmse_partial(pred, target, loss4, count)
+    def _loss_parts(self, pred, target, parts, t0):
+        """This micro-batch's tiles' loss parts (rows t0.. of the batch-wide parts array)."""
+        nt = pred.shape[0]
+        te = pred[0].numel()
+        call("srmi_tile_loss_parts", ptr(pred), ptr(target), nt, te, self.loss_kind, CHARBONNIER_EPS,
+             ptr(parts[t0 * TILE_LOSS_SUB:]), torch.cuda.current_stream(self.device).cuda_stream)
 
-    def _reduce_loss(self, loss4, parts):
-        """loss4 of the whole (global) batch: micro-batch partials summed, all-reduced
-        over ranks, finalised -- one launch without data parallelism."""
+    def _reduce_loss(self, loss4, parts, b, count):
+        """loss4 of the whole (global) batch from its b tiles' parts in tile order,
+        all-reduced over ranks, finalised -- one launch without data parallelism."""
+        st = torch.cuda.current_stream(self.device).cuda_stream
         if self.info.enabled:
-            Engine.loss_combine(loss4, parts, -1)
+            call("srmi_loss_from_parts", ptr(parts), b, float(count), -1, ptr(loss4), st)
             allreduce_sum_(loss4[0:1], self.info)
             Engine.loss_finalize(loss4, self.loss_kind)
         else:
-            Engine.loss_combine(loss4, parts, self.loss_kind)
+            call("srmi_loss_from_parts", ptr(parts), b, float(count), self.loss_kind, ptr(loss4), st)
 
     def step(self, hr: torch.Tensor) -> Dict[str, torch.Tensor]:
         """hr: this rank's HR tiles [b, C, H, W] fp32 on the device (already normalised),
@@ -216,23 +221,23 @@ class FusedTrainer:
         for k, eng in enumerate(self.engines):
             sl = sls[k]
             if sl.stop == sl.start:
-                self.mloss4[k].zero_()
-                self.miloss4[k].zero_()
                 continue
             with self._ctx(k):
                 downsample(hr[sl], s, out=self.lrbuf[sl], mode=self.dmode)
                 eng.forward(self.params, self.lrbuf[sl], out=self.sr[sl])
-                self._loss_partial(eng, self.sr[sl], tgt[sl], self.mloss4[k], count,
-                                   None if self.dy is None else self.dy[sl])
+                if self.dy is not None:  # Charbonnier: the elementwise upstream gradient
+                    eng.charbonnier_partial(self.sr[sl], tgt[sl], self.mloss4[k], count, CHARBONNIER_EPS,
+                                            dy=self.dy[sl])
+                self._loss_parts(self.sr[sl], tgt[sl], self.lparts, sl.start)
                 if self.interp_loss:  # self.loss(btarget, binterp), dual_trainer.py:316-317
                     up = upsample(self.lrbuf[sl], s, out=self.up[sl], mode=self.umode)
                     itgt = hr[sl] if self.tgt_b is None else self.tgt_b[sl]
-                    self._loss_partial(eng, itgt, up, self.miloss4[k], icount)
+                    self._loss_parts(itgt, up, self.iparts, sl.start)
         for st in self.streams[1:]:
             main.wait_stream(st)
-        self._reduce_loss(self.loss4, self.mloss4)
+        self._reduce_loss(self.loss4, self.lparts, b, count)
         if self.interp_loss:
-            self._reduce_loss(self.iloss4, self.miloss4)
+            self._reduce_loss(self.iloss4, self.iparts, b, icount)
         for st in self.streams[1:]:
             st.wait_stream(main)
         # backward per micro-batch with the global loss scale.  Data parallel: the

@@ -244,8 +244,10 @@ def test_plugin_module_reference_style_step():
 
 def test_micro_batch_step_matches_single_engine():
     """FusedTrainer(micro=2) -- two half-batch engines on two streams -- computes the
-    same step as one engine: the loss partials and gradients are summed exactly (up
-    to fp32 summation order)."""
+    same step as one engine: the loss comes from per-tile parts summed in tile order
+    (srmi_tile_loss_parts / srmi_loss_from_parts), so it is bit-identical whatever the
+    split, and the gradients agree up to fp32 summation order.  (A 1-ulp loss
+    difference would scale the bf16 gradient maps and flip roundings: 4e-5.)"""
     d = dev()
     spec = spec_of("rcan", 2, 2, 3)
     table = _table(spec)
@@ -260,8 +262,7 @@ def test_micro_batch_step_matches_single_engine():
         res.append((float(out["loss"]), float(out["interp_loss"]), tr.grads.clone(), tr.params.clone()))
         del tr
     (l1, i1, g1, p1), (l2, i2, g2, p2) = res
-    assert abs(l1 - l2) <= 1e-6 * abs(l1)
-    assert abs(i1 - i2) <= 1e-6 * abs(i1)
+    assert l1 == l2 and i1 == i2
     assert rel_l2(g2, g1) < 1e-5
     assert rel_l2(p2 - flat, p1 - flat) < 1e-4
 
