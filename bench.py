@@ -65,16 +65,10 @@ def parse():
     ap.add_argument("--no-dp-probe", action="store_true", help="skip the dp_overhead_1rank measurement")
     ap.add_argument("--force-dp", action="store_true",
                     help="diagnostic: the DP path (RCCL group, reducer stream, bucketed all-reduce) at one rank")
-    ap.add_argument("--ca-fold", action="store_true",
-                    help="A/B: fold each RCAB's CA backward into the conv launches (SRMI_FLAG_CA_FOLD)")
     ap.add_argument("--dp-reducer-stream", action="store_true",
                     help="A/B: the DP all-reduce on a reducer stream of its own (the event-driven schedule)")
-    ap.add_argument("--wgrad-full-co", action="store_true",
-                    help="A/B: RCAB filter gradients on whole co blocks over half-image chunks (SRMI_FLAG_WGRAD_FULL_CO)")
     ap.add_argument("--ca-pass", action="store_true",
                     help="A/B: the training CA forward as a pass of its own after conv2 (SRMI_FLAG_CA_PASS)")
-    ap.add_argument("--ca-scale-launch", action="store_true",
-                    help="A/B: the training CA scale as a launch of its own (SRMI_FLAG_CA_SCALE_LAUNCH)")
     ap.add_argument("--no-rcab-infer", action="store_true",
                     help="A/B: inference RCABs as three launches (SRMI_FLAG_NO_RCAB_INFER)")
     return ap.parse_args()
@@ -147,11 +141,7 @@ WGRAD_OUT_BYTES = 64 * 577 * 4           # dW (64x64x9) + db, fp32, once per lau
 #  F2 = rcab_bwd_kernel<DG_RELUMASK>: conv2's dgrad (reads du bf16, reads the ReLU
 #       output t bf16 as the mask, writes dz bf16) and conv2's filter gradient (t, du
 #       already counted)
-#  with the CA-backward fold (opt-in, --ca-fold) F1 also writes du' = bf16(g s) of the next
-#  RCAB (one more bf16 map; the CA-backward pass that read g and wrote du is gone) and
-#  F2 reads du' instead of du (same bytes)
 F1_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE + 2 * ACT_F32_PER_TILE
-F1_FOLD_BYTES_PER_TILE = F1_BYTES_PER_TILE + ACT_BF16_PER_TILE
 F2_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE
 FUSED_FLOP_PER_TILE = 2 * CONV64_FLOP_PER_TILE   # one dgrad conv + one filter-gradient conv
 
@@ -208,10 +198,8 @@ def fused_rooflines(tr, step_ms, reps=20):
     out = {}
     nl, nb = tr.spec.nlayers, tr.spec.nblocks
     per_step = {1: nl * (nb - 1), 2: nl * nb}
-    fold = bool(tr.spec.flags & 1)
     streams = [tr.streams[k] or main_st for k in range(n_eng)]
-    for which, key, name, bpt in ((1, "F1", "rcab_bwd_kernel<EPI_DG_ACC_CA>",
-                                   F1_FOLD_BYTES_PER_TILE if fold else F1_BYTES_PER_TILE),
+    for which, key, name, bpt in ((1, "F1", "rcab_bwd_kernel<EPI_DG_ACC_CA>", F1_BYTES_PER_TILE),
                                   (2, "F2", "rcab_bwd_kernel<EPI_DG_RELUMASK>", F2_BYTES_PER_TILE)):
         def issue_all(r):
             for k, eng in enumerate(tr.engines):
@@ -240,7 +228,7 @@ def fused_rooflines(tr, step_ms, reps=20):
             "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": tr_["bytes"] if tr_ and tr_["bytes"] is not None else None,
             "traffic_source": tr_["source"] if tr_ else None,
-            "kernel": "srmi::" + name, "in_step": True, "ca_fold": fold,
+            "kernel": "srmi::" + name, "in_step": True,
             "frac_is": "per launch: algorithmic bytes of one launch / its average duration, the launch alone "
                        "on the chip (engine 0's stream, in-step grid and CU split)",
             "config": f"one launch of {tiles_per_engine} tiles (micro-batch engine 0), in-step grid and CU split",
@@ -436,7 +424,7 @@ def dp_overhead_probe(args, reps=2):
             "--no-dp-probe", "--steps", str(args.steps), "--warmup", str(args.warmup), "--batch", str(args.batch)]
     if args.micro is not None:
         base += ["--micro", str(args.micro)]
-    for flag in ("ca_fold", "ca_pass", "ca_scale_launch", "dp_reducer_stream", "wgrad_full_co"):
+    for flag in ("ca_pass", "dp_reducer_stream"):
         if getattr(args, flag):
             base += ["--" + flag.replace("_", "-")]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
@@ -544,10 +532,8 @@ def main():
                                                                            2 if args.no_rcab_infer else 0)}
         print(json.dumps(rec), flush=True)
         return
-    from srmi._lib import SRMI_FLAG_CA_FOLD, SRMI_FLAG_CA_PASS, SRMI_FLAG_CA_SCALE_LAUNCH, SRMI_FLAG_WGRAD_FULL_CO
-    flags = ((SRMI_FLAG_CA_FOLD if args.ca_fold else 0) | (SRMI_FLAG_CA_PASS if args.ca_pass else 0) |
-             (SRMI_FLAG_CA_SCALE_LAUNCH if args.ca_scale_launch else 0) |
-             (SRMI_FLAG_WGRAD_FULL_CO if args.wgrad_full_co else 0))
+    from srmi._lib import SRMI_FLAG_CA_PASS
+    flags = SRMI_FLAG_CA_PASS if args.ca_pass else 0
     spec = NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=10, nblocks=20,
                    cbottleneck=2, scale=4, flags=flags)
     tr = FusedTrainer(spec, B, (48, 48), lr=1e-4, interp_loss=not args.no_interp_loss, info=info, device=dev, seed=0,
@@ -640,7 +626,7 @@ def main():
         rec = {
             "metric": METRIC, "value": round(value, 2), "unit": "tiles/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "step_times": step_stats,
-            "ca_fold": bool(args.ca_fold),
+            "ca_pass": bool(args.ca_pass),
             "host_enqueue_ms_per_step": round(1000 * t_host / args.steps, 3),
             "host_enqueue_idle_ms_per_step": round(host_idle_ms, 3), "micro": micro, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",

@@ -81,23 +81,15 @@ typedef struct srmi_model_config {
   int dtype;         /* SRMI_DTYPE_BF16 | SRMI_DTYPE_F32                    */
   int flags;         /* SRMI_FLAG_* (0 = defaults)                           */
 } srmi_model_config;
-/* flags: SRMI_FLAG_CA_FOLD folds every RCAB's channel-attention backward into the
- * conv launches (du never materialised) instead of its own pass.  Opt-in:
- * parity-green but measured slower than the materialised path on MI355X (A/B, tests) */
-#define SRMI_FLAG_CA_FOLD 1
+/* flags (bits 0 and 3 are retired: the CA-backward fold and the separate CA-scale
+ * launch, both measured slower on MI355X and removed) */
 /* SRMI_FLAG_NO_RCAB_INFER: inference engines run each RCAB as three launches (conv1,
  * conv2 + pool, CA) instead of one launch with a workgroup per image (A/B, tests) */
 #define SRMI_FLAG_NO_RCAB_INFER 2
 /* training forward (A/B, tests): SRMI_FLAG_CA_PASS runs each RCAB's channel attention as
  * a pass of its own after conv2 (conv1, conv2 + pool writing u, CA pass) instead of inside
- * conv2's launch; SRMI_FLAG_CA_SCALE_LAUNCH computes the CA scale s in a launch of its
- * own between conv1 and conv2 instead of in every conv2 workgroup's prologue */
+ * conv2's launch */
 #define SRMI_FLAG_CA_PASS 4
-#define SRMI_FLAG_CA_SCALE_LAUNCH 8
-/* SRMI_FLAG_WGRAD_FULL_CO: the RCAB filter gradients on whole 64-channel co blocks over
- * half-image row chunks instead of (the default) co halves over whole images, which
- * write half the partial slabs (A/B, tests) */
-#define SRMI_FLAG_WGRAD_FULL_CO 16
 
 typedef struct srmi_param_info {
   long long offset; /* element offset in the flat fp32 parameter buffer     */

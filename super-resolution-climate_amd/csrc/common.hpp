@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tuning.hpp"
+
 namespace srmi {
 
 typedef uint16_t bf16_t;                                        // raw bf16 bits
@@ -100,9 +102,6 @@ __device__ __forceinline__ uint32_t pair_encode4_fast(float a, float b, float c,
 // kernel boundary: ~1.8 us + dirty bytes / 6 TB/s); stores that write through
 // reach memory while the kernel still computes, so the boundary finds nothing
 // to flush.  Used for the large outputs (activations, gradient streams, slabs).
-#ifndef SRMI_WT
-#define SRMI_WT 1
-#endif
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);

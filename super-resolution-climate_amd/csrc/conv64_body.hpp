@@ -4,7 +4,6 @@
 #pragma once
 #include <type_traits>
 
-#include "ca_fold.hpp"
 #include "ca_scale.hpp"
 
 // the pair codec of the CA_RESID / CA_RESID_U epilogues: the fast form (common.hpp; the
@@ -142,9 +141,7 @@ __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 // channel halves) share the row's LDS staging, so their writes and the full-line
 // stores that read them are separated by workgroup barriers and each wave stores
 // every other 1 KiB run.
-// FP: the CA-fold producer's du' store may be on (DG_ACC_CA: a template switch of the
-// fused launch, so the default kernel carries none of it; DG_ACC: a runtime check)
-template <int NPT, int EPI, int NCT = 4, bool FP = true>
+template <int NPT, int EPI, int NCT = 4>
 __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)[NPT][NCT],
                                                const EpiPre<NPT, EPI, NCT>& e, const float4 (&bias)[NCT], int n,
                                                int cb, int y, int x0, int strip, int nstrips, float* red, int fr,
@@ -252,9 +249,6 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       constexpr int RUNS = HALF / 4;  // 1 KiB runs per half
       const auto rf = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
       [[maybe_unused]] const auto rbb = wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
-      // CA-backward fold producer (EPI_DG_ACC_CA): du' = bf16(g * s) of the next RCAB
-      [[maybe_unused]] const bool fold_out = FP && (EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC) && p.fold.du_out != nullptr;
-      [[maybe_unused]] const auto rdu = wt_rsrc(p.fold.du_out, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
       [[maybe_unused]] const auto rph = wt_rsrc(p.yph, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
       [[maybe_unused]] const auto rpl = wt_rsrc(p.ypl, (uint32_t)((size_t)p.N * HW * p.Cout));
       const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
@@ -319,11 +313,6 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             ps1[0][3] += val.w * bf2f(uu.y >> 16);
           }
           st_wt16(rf, p.yf, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 4), val);
-          if constexpr (FP && (EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC)) {
-            if (fold_out)  // the lane's channels 4c..4c+3 are the same in every run: s in fs
-              st_wt8(rdu, p.fold.du_out, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 2),
-                     make_uint2(pack2(val.x * fs.x, val.y * fs.y), pack2(val.z * fs.z, val.w * fs.w)));
-          }
           if constexpr (EPI == EPI_DG_ACC) {
             if (p.yb)  // its bf16 copy: 512 contiguous bytes per instruction
               st_wt8(rbb, p.yb, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 2),
@@ -432,9 +421,6 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
 
 constexpr int kFragBuf = 2;  // register buffers of A/B fragments (K-steps)
 
-#ifndef SRMI_DEFER
-#define SRMI_DEFER 4  // bit mask: 1 RELU, 2 POOL, 4 DG_RELUMASK, 8 DG_ACC_CA (in-step A/B: only 4 gains)
-#endif
 template <int EPI>
 constexpr bool conv64_defers() {
   return ((SRMI_DEFER & 1) && EPI == EPI_RELU_BF16) || ((SRMI_DEFER & 2) && EPI == EPI_POOL_BF16) ||
@@ -442,7 +428,7 @@ constexpr bool conv64_defers() {
          ((SRMI_DEFER & 16) && EPI == EPI_RELU_POOL) || ((SRMI_DEFER & 32) && EPI == EPI_CA_RESID);
   // (EPI_CA_RESID_U: the non-deferred body only)
 }
-template <int TW, int EPI, bool FOLD = false>
+template <int TW, int EPI>
 __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_len, int bid, char* smem, int tail,
                                                   bool tail_part);
 
@@ -456,21 +442,13 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
 // NW = waves per workgroup: 4 (one per output row of the strip, all 64 output
 // channels) or 8 (a wave per row and channel half: two waves per SIMD, so one wave's
 // LDS / memory waits overlap the other's MFMAs; same LDS footprint)
-// FOLD (EPI_DG_RELUMASK, deferred form only): the consumer side of the CA-backward
-// fold (srmi_internal.hpp CaFold, ca_fold.hpp); the producer side (EPI_DG_ACC_CA) is
-// the runtime p.fold.du_out.
 // WRES: the filter image is already resident in LDS (the caller loaded it): no filter DMA
-template <int TW, int EPI, int NW = 4, bool FOLD = false, bool WRES = false>
+template <int TW, int EPI, int NW = 4, bool WRES = false>
 __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, int bid, char* smem, int tail = 0,
                                             bool tail_part = false) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  // FOLD: the CA-fold consumer (the deferred 8-wave ReLU-mask dgrad) or producer
-  // (the non-deferred DG_ACC_CA epilogue's du' store)
-  static_assert(!FOLD || (EPI == EPI_DG_RELUMASK && NW == 8 && conv64_defers<EPI>()) ||
-                    (EPI == EPI_DG_ACC_CA && !(NW == 8 && conv64_defers<EPI>())),
-                "fold: the deferred ReLU-mask dgrad (consumer) or the non-deferred DG_ACC_CA (producer)");
   if constexpr (NW == 8 && conv64_defers<EPI>()) {
-    conv64_body_defer<TW, EPI, FOLD>(p, run_len, bid, smem, tail, tail_part);
+    conv64_body_defer<TW, EPI>(p, run_len, bid, smem, tail, tail_part);
     return;
   }
   constexpr int NCT = NW == 8 ? 2 : 4;  // 16-wide output-channel tiles per wave
@@ -580,17 +558,12 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
     for (int c = 0; c < NCT; ++c) aoff[kk][c] = swz128((ct0 + c) * 16 + fr, kk * 4 + fk);
-  // fold producer: s of the next RCAB for the lane's 4 run-layout channels (conv_epilogue2)
+  // CA_RESID(_U): s for the lane's 4 run-layout channels (conv_epilogue2)
   float4 fs = float4{0.f, 0.f, 0.f, 0.f};
   if constexpr (EPI == EPI_CA_RESID)
     fs = *reinterpret_cast<const float4*>(p.escale + (size_t)n * p.escale_stride + 4 * (lane & 15));
   if constexpr (EPI == EPI_CA_RESID_U) {
     if (!p.cas_on) fs = *reinterpret_cast<const float4*>(p.escale + (size_t)n * p.escale_stride + 4 * (lane & 15));
-  }
-  if constexpr ((EPI == EPI_DG_ACC_CA && FOLD) || (EPI == EPI_DG_ACC && epi_run<EPI>())) {
-    if (p.fold.du_out)
-      fs = *reinterpret_cast<const float4*>(p.fold.s_rec + (size_t)n * (128 + p.fold.CR) + 64 + p.fold.CR +
-                                            4 * (lane & 15));
   }
   __syncthreads();
   if constexpr (EPI == EPI_CA_RESID_U) {
@@ -686,7 +659,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    conv_epilogue2<NPT, EPI, NCT, (EPI != EPI_DG_ACC_CA || FOLD)>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx,
+    conv_epilogue2<NPT, EPI, NCT>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx,
                                                                nsy * nsx, red, fr, fk, row, ct0,
                                   tid, ring + (k % 3) * S::GROUPB + row * TW * 128, fs);
     STAMP(sj + 3);
@@ -748,7 +721,7 @@ struct DeferOps {
   uint2 u[NPT][2];   // DG_ACC_CA: the CA input u
 };
 
-template <int TW, int EPI, bool FOLD>
+template <int TW, int EPI>
 __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_len, int bid, char* smem, int tail,
                                                   bool tail_part) {
   constexpr int NW = 8, NCT = 2;
@@ -826,8 +799,6 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
 #pragma unroll
     for (int c = 0; c < NCT; ++c) bias[c] = *reinterpret_cast<const float4*>(bp + cb * 64 + chan(c, 0));
   }
-  [[maybe_unused]] CaFoldRegs fregs;
-  if constexpr (FOLD) ca_fold_mlp_load(p.fold, n, fregs);  // in flight under the DMA prologue
   {
     const uint32_t wbase = lds_u32(wl);
     // the filter image uses the swz128t chunk swizzle (c ^ (bit1, bit3 of the row)):
@@ -842,14 +813,6 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     group_dma(k0);
     group_dma(k0 + 1);
     wait_vm<0>();
-  }
-  // fold consumer: the image's CA MLP backward (c = dm / HW) and the border-class
-  // dgrad of c, from the filter image just landed (the first barrier inside makes
-  // every wave's DMA visible); the first run of the image writes its brec
-  float* const fsm = reinterpret_cast<float*>(smem + S::TOTAL);
-  if constexpr (FOLD) {
-    ca_fold_mlp_compute(p.fold, n, p.N, (int)HW, fsm, ry == 0 && sx == 0 && cb == 0 && !tail_part, fregs);
-    ca_fold_corr(wl, fsm);
   }
   STAMP(1);
   // A-fragment rows: lane fr of tile c reads the filter row of the channel its
@@ -901,22 +864,6 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
         ops.g[i][0] = *reinterpret_cast<const float4*>(p.r1 + o);
         ops.g[i][1] = *reinterpret_cast<const float4*>(p.r1 + o + 4);
       }
-    }
-  };
-  // fold: the border-class corrections of strip kp's row for this lane (LDS, issued
-  // early in a strip so the epilogue K-steps find them in registers)
-  [[maybe_unused]] float fb[8], fd[8];
-  [[maybe_unused]] const int fpt = (fr == 0 && x0 == 0) ? 0 : ((fr == 15 && x0 + TW == p.W) ? NPT - 1 : -1);
-  auto fold_corr_load = [&](int kp) __attribute__((always_inline)) {
-    if constexpr (FOLD) {
-      const int yy = 4 * kp + row, cy = yy == 0 ? 0 : (yy == p.H - 1 ? 2 : 1);
-      const float* cb1 = fsm + kFoldCorr + (cy * 3 + 1) * 64 + ct0 * 16 + 8 * fk;
-      const float* cbx = fsm + kFoldCorr + (cy * 3 + (fpt == 0 ? 0 : (fpt > 0 ? 2 : 1))) * 64 + ct0 * 16 + 8 * fk;
-      const float4 b0 = *reinterpret_cast<const float4*>(cb1), b1 = *reinterpret_cast<const float4*>(cb1 + 4);
-      const float4 x0v = *reinterpret_cast<const float4*>(cbx), x1v = *reinterpret_cast<const float4*>(cbx + 4);
-      fb[0] = b0.x; fb[1] = b0.y; fb[2] = b0.z; fb[3] = b0.w; fb[4] = b1.x; fb[5] = b1.y; fb[6] = b1.z; fb[7] = b1.w;
-      fd[0] = x0v.x - b0.x; fd[1] = x0v.y - b0.y; fd[2] = x0v.z - b0.z; fd[3] = x0v.w - b0.w;
-      fd[4] = x1v.x - b1.x; fd[5] = x1v.y - b1.y; fd[6] = x1v.z - b1.z; fd[7] = x1v.w - b1.w;
     }
   };
   // epilogue of pixel tile pt of strip kp from accp
@@ -974,14 +921,6 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
       st_wt8(rpl, p.ypl, oe, make_uint2(l0, l1));
     } else if constexpr (kPerm) {
       float o[8];
-      // fold: + the dgrad of the constant c for this pixel's border class (8 contiguous
-      // channels ct0*16 + 8fk ..), before the ReLU mask: the row class's x-inner value
-      // fb, plus fd on the lane's x-border pixel (fold_corr_load)
-      [[maybe_unused]] float cv[8];
-      if constexpr (FOLD) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) cv[i] = fb[i] + (pt == fpt ? fd[i] : 0.f);
-      }
 #pragma unroll
       for (int c = 0; c < NCT; ++c) {
         const f32x4 v = accp[pt][c];
@@ -997,7 +936,6 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
           }
           if constexpr (EPI == EPI_DG_RELUMASK) {
             const uint32_t w = (c ? (rr < 2 ? ops.t[pt].z : ops.t[pt].w) : (rr < 2 ? ops.t[pt].x : ops.t[pt].y));
-            if constexpr (FOLD) x += cv[4 * c + rr];
             x = p.alpha * relu_mask((rr & 1) ? (w >> 16) : (w & 0xFFFFu), x);
           }
           o[4 * c + rr] = x;
@@ -1110,8 +1048,6 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
           if (st < 3 && st * PER + i < NLD) op_load(k - 1, st * PER + i);
       }
       if (st < NGW && pf && wv_s + NW * st < NGRP) group_dma_one(k + 2, st);
-      if constexpr (FOLD && PREV)
-        if (st == 0) fold_corr_load(k - 1);
       __builtin_amdgcn_sched_barrier(0);
       const bool ld = st + LA < 18;
       if (ld) load_step(st + LA, A[(st + LA) % kFragBuf], B[(st + LA) % kFragBuf]);
@@ -1186,7 +1122,6 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
   // the last strip's epilogue, exposed
   if constexpr (kPart)
     if (k1 - 2 >= k0) part_store(k1 - 2);
-  fold_corr_load(k1 - 1);
   zero_ps();
 #pragma unroll
   for (int pt = 0; pt < NPT; ++pt) epi_tile(k1 - 1, pt);

@@ -278,9 +278,6 @@ __global__ void __launch_bounds__(NW * 64, 1) conv3x3_f32_kernel(ConvParams p) {
                               fk, row, ct0, tid);
 }
 
-#ifndef SRMI_F32_NW
-#define SRMI_F32_NW 8
-#endif
 constexpr int kF32NW = SRMI_F32_NW;  // waves per workgroup of the fp32 conv
 
 template <int TW, int EPI>

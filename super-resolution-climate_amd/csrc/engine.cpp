@@ -84,6 +84,7 @@ int build_plan(const srmi_model_config* cfg, Plan& P) {
   if (c.arch == SRMI_ARCH_RCAN && (c.nblocks < 1 || c.reduction < 1 || 64 % c.reduction)) return SRMI_ERR_ARG;
   if (c.arch != SRMI_ARCH_RCAN && c.arch != SRMI_ARCH_EDSR) return SRMI_ERR_ARG;
   if (c.dtype != SRMI_DTYPE_BF16 && c.dtype != SRMI_DTYPE_F32) return SRMI_ERR_ARG;
+  if (c.flags & ~(SRMI_FLAG_NO_RCAB_INFER | SRMI_FLAG_CA_PASS)) return SRMI_ERR_ARG;  // (retired bits refused)
   P = Plan();
   P.cfg = c;
   const int F = 64;
@@ -246,17 +247,8 @@ static int fuse_wg_cus(const srmi_engine* e, int which) {
   (void)which;  // half the budget for both fused launches (44 / 56 % measured within noise)
   return engine_cus(e) / 2;
 }
-// The RCAB filter gradients in co halves (WgradParams.co_split = 2): a workgroup
-// computes half of the 64 output channels over chunks of twice the rows, so each
-// fused launch writes (and the next one reduces) half the partial slabs.
-// SRMI_FLAG_WGRAD_FULL_CO: whole co blocks (A/B); the CA fold needs them.
-static int rcab_co_split(const srmi_engine* e) {
-  const int f = e->P.cfg.flags;
-  return (!e->f32 && e->P.cfg.arch == SRMI_ARCH_RCAN && e->w == 48 && !(f & SRMI_FLAG_WGRAD_FULL_CO) &&
-          !(f & SRMI_FLAG_CA_FOLD)) ? 2 : 1;
-}
 static int rcab_row_splits(const srmi_engine* e, int n, int which) {
-  return choose_row_splits(n * rcab_co_split(e), e->h, 64, fuse_wg_cus(e, which));
+  return choose_row_splits(n, e->h, 64, fuse_wg_cus(e, which));
 }
 
 static size_t carve(srmi_engine* e, char* base) {
@@ -464,9 +456,8 @@ static ConvParams dgrad_params(srmi_engine* e, const ConvRef& c, const bf16_t* d
 
 static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n, int H, int W, int epi, bf16_t* yb,
                       float* yf, const float* r1, const float* r2, const float* r3, const bf16_t* aux, float* part,
-                      float alpha, hipStream_t st, const CaFold* fold = nullptr) {
+                      float alpha, hipStream_t st) {
   ConvParams p = dgrad_params(e, c, dy, n, H, W, &epi, yb, yf, r1, r2, r3, aux, part, alpha);
-  if (fold) p.fold = *fold;
   return conv3x3_launch(p, epi, st);
 }
 
@@ -522,40 +513,6 @@ static int dgrad_with_wgrad(srmi_engine* e, const ConvParams& cp, int epi, const
   return conv3x3_launch(cp, epi, st);
 }
 
-// the CA-backward fold runs where both halves of the RCAB backward are fused launches
-// (bf16, 48-wide tiles) and the producer's epilogue is the specialised DG_ACC_CA
-// (opt-in per engine: SRMI_FLAG_CA_FOLD; SRMI_CA_FOLD=0 compiles it out)
-#ifndef SRMI_CA_FOLD
-#define SRMI_CA_FOLD 1
-#endif
-// folded RCABs: the previous RCAB's two slab reductions run in the conv2 backward
-// launch's filter-gradient workgroups after their chunk (0: a reduction launch)
-#ifndef SRMI_RED_IN_F2
-#define SRMI_RED_IN_F2 1
-#endif
-static bool use_ca_fold(const srmi_engine* e, int n) {
-  if (!SRMI_CA_FOLD || !(e->P.cfg.flags & SRMI_FLAG_CA_FOLD) || e->f32 || e->P.cfg.arch != SRMI_ARCH_RCAN ||
-      e->w != 48 || e->h % 4)
-    return false;
-  const int R = e->P.cfg.reduction, CR = 64 / R;
-  if (CR < 4 || CR > 32 || CR % 4) return false;
-  const int rs2 = rcab_row_splits(e, n, 2);
-  return (e->h / rs2) % 4 == 0;
-}
-
-static CaFold fold_consumer(const srmi_engine* e, const float* prm, const RCABRef& r, int g, int b, int nstrips) {
-  CaFold f{};
-  f.part = e->pacc;
-  f.nstrips = nstrips;
-  f.CR = 64 / e->P.cfg.reduction;
-  f.rec = e->recp(g, b);
-  f.w1 = prm + r.ca_w1;
-  f.w2 = prm + r.ca_w2;
-  f.brec = e->brecp(g, b);
-  f.on = 1;
-  return f;
-}
-
 // SRMI_TRACE_ERRORS=1 in the environment: every failing step prints its line
 static int trace_rc(int rc, int line) {
   static const bool on = std::getenv("SRMI_TRACE_ERRORS") != nullptr;
@@ -603,20 +560,17 @@ static bool use_rcab_infer(const srmi_engine* e) {
 // 31-47, 61-64) without a pass of its own.  conv1 writes t and its per-strip sums
 // (EPI_RELU_POOL); conv2 (EPI_CA_RESID_U) stores u for backward and adds s bf16(u) into
 // the residual pair in its epilogue, with s = the CA MLP of mean(u), and mean(u) from t's
-// statistics and conv2's bf16 filter image (ca_scale.hpp) -- computed by every conv2
-// workgroup in its prologue (1), or by a launch of its own between the convs (2).
+// statistics and conv2's bf16 filter image (ca_scale.hpp), computed by every conv2
+// workgroup in its prologue (1; its own launch between the convs measured -2.5 %).
 // 0: conv1, conv2 + pool writing u, the CA pass (ca_fwd) -- the exact-fp32 mode and tiles
 // other than 48 wide always run this form; SRMI_FLAG_CA_PASS selects it at run time.
 // bf16, 48-wide tiles, a bottleneck the scale code handles.
-#ifndef SRMI_CA_FWD
-#define SRMI_CA_FWD 1
-#endif
 static int ca_fwd_mode(const srmi_engine* e) {
   const int CR = 64 / e->P.cfg.reduction;
   if (!e->train || e->f32 || e->P.cfg.arch != SRMI_ARCH_RCAN || e->w != 48 || e->h % 4 || CR < 4 || CR > 32 ||
       CR % 4 || (e->P.cfg.flags & SRMI_FLAG_CA_PASS))
     return 0;
-  return (e->P.cfg.flags & SRMI_FLAG_CA_SCALE_LAUNCH) ? 2 : SRMI_CA_FWD;
+  return SRMI_CA_FWD;
 }
 
 // ------------------------------------------------------------------ forward
@@ -640,7 +594,7 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
                                b == 1 ? nullptr : lo, e->hb(g, b), lo, e->recp(g, b), st));
           continue;
         }
-        if (const int mode = ca_fwd_mode(e)) {  // training: the CA forward inside conv2
+        if (ca_fwd_mode(e)) {  // training: the CA forward inside conv2
           uint8_t* lo = reinterpret_cast<uint8_t*>(e->Hf);  // the pair's lo8 remainder (as below)
           RC(conv_fwd(e, r.c1, e->hb(g, b - 1), n, h, w, EPI_RELU_POOL, e->Tm(g, b), nullptr, nullptr, e->ppool, 1.f,
                       st));
@@ -652,14 +606,8 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
           c2.ypl = lo;
           const CaScale cas{e->Tm(g, b), e->ppool, nstrips, prm + r.ca_w1, prm + r.ca_b1, prm + r.ca_w2,
                             prm + r.ca_b2, e->pbias + r.c2.pb_off, 64 / R, e->recp(g, b)};
-          if (mode == 2) {
-            RC(ca_scale_launch(cas, e->at(e->packs, r.c2.f_off), n, h, w, st));
-            c2.escale = e->recp(g, b) + 64 + 64 / R;  // s of the record m | z1 | s
-            c2.escale_stride = 128 + 64 / R;
-          } else {
-            c2.cas = cas;
-            c2.cas_on = 1;
-          }
+          c2.cas = cas;
+          c2.cas_on = 1;
           RC(conv3x3_launch(c2, EPI_CA_RESID_U, st));
           continue;
         }
@@ -768,11 +716,6 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
     // The filter gradients write the slab set of their RCAB's parity; the last
     // RCAB of a group reduces its own slabs before the group's event.
     const int rs2 = rcab_row_splits(e, n, 2), rs1 = rcab_row_splits(e, n, 1);
-    // The CA-backward fold (srmi_internal.hpp CaFold): every RCAB but the first one of
-    // a group in backward order gets du' = bf16(g * s) from the conv1 dgrad of the RCAB
-    // above (F1) instead of a CA-backward pass; its conv2 backward (F2) adds the
-    // constant dm / HW itself.  bf16 engine, fused-launch shapes only.
-    const bool fold = use_ca_fold(e, n);
     for (int g = nl - 1; g >= 0; --g) {
       const int stage = nl - g;
       // the gradient streams swap after every group: the state group g starts from
@@ -785,15 +728,8 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
       int it = (nl - 1 - g) * nb;  // RCAB counter (slab-set parity)
       const ConvRef& gt = P.group_tail[g];
       RC(conv_wgrad(e, gt, e->hb(g, nb), gRb, n, h, w, grads, true, 1.f, st));
-      // the group tail's dgrad is the fold producer of the group's last RCAB (du' of RCAB nb)
-      CaFold tail_fold{};
-      if (fold) {
-        tail_fold.du_out = e->DU;
-        tail_fold.s_rec = e->recp(g, nb);
-        tail_fold.CR = 64 / R;
-      }
       RC(conv_dgrad(e, gt, gRb, n, h, w, EPI_DG_ACC, nullptr, ghf, nullptr, nullptr, nullptr, e->Um(g, nb), e->pacc,
-                    1.f, st, fold ? &tail_fold : nullptr));
+                    1.f, st));
       ReduceSet prev2{}, prev1{};
       bool have_prev = false;
       for (int b = nb; b >= 1; --b) {
@@ -801,13 +737,8 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         const int q = it++ & 1;
         bf16_t* du = e->DU;
         bf16_t* dz = e->DZ;
-        const bool folded = fold;  // du' came from the previous F1 (the group tail's dgrad for b == nb)
-        if (!folded) {
-          RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
-                              e->brecp(g, b), e->f32, st, have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
-        } else if (!SRMI_RED_IN_F2 && have_prev) {
-          RC(wgrad_reduce2_launch(prev2, prev1, st));
-        }
+        RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
+                            e->brecp(g, b), e->f32, st, have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
         ReduceSet red2, red1;
         WgradParams wp;
         int epi = EPI_DG_RELUMASK;
@@ -815,30 +746,14 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
                                      nullptr, 1.f);
         RC(wgrad_params(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, rs2, e->slab_r[q][0], e->bslab_r[q][0],
                         e->slab_r_floats, e->bslab_r_floats, &wp, &red2));
-        wp.co_split = rcab_co_split(e);
-        if (folded) {
-          cp.fold = fold_consumer(e, prm, r, g, b, nstrips);
-          wp.fold = cp.fold;
-          if (SRMI_RED_IN_F2 && have_prev) {  // the previous RCAB's slab reductions ride in this launch
-            wp.red[0] = prev2;
-            wp.red[1] = prev1;
-            wp.nred = 2;
-          }
-        }
         RC(dgrad_with_wgrad(e, cp, epi, wp, 2, st));
         const bool last = (b == 1);
         epi = EPI_DG_ACC;
         cp = dgrad_params(e, r.c1, dz, n, h, w, &epi, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
                           (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
                           last ? nullptr : e->pacc, 1.f);
-        if (fold && !last) {  // du' of RCAB b - 1
-          cp.fold.du_out = e->DU;
-          cp.fold.s_rec = e->recp(g, b - 1);
-          cp.fold.CR = 64 / R;
-        }
         RC(wgrad_params(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, rs1, e->slab_r[q][1],
                         e->bslab_r[q][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red1));
-        wp.co_split = rcab_co_split(e);
         RC(dgrad_with_wgrad(e, cp, epi, wp, 1, st));
         prev2 = red2;
         prev1 = red1;
@@ -996,34 +911,12 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
   ReduceSet red;
   ConvParams cp;
   int epi;
-  const bool fold = use_ca_fold(e, n) && b < e->P.cfg.nblocks && e->probe_prm;  // (as backward_impl has it)
-  // (b < nblocks: the probe's in-launch reductions read the slabs of RCAB b + 1)
   if (which == 2) {
     epi = EPI_DG_RELUMASK;
     cp = dgrad_params(e, r.c2, e->DU, n, h, w, &epi, e->DZ, nullptr, nullptr, nullptr, nullptr, e->Tm(0, b), nullptr,
                       1.f);
     RC(wgrad_params(e, r.c2, e->Tm(0, b), e->DU, n, h, w, grads, false, 1.f, rcab_row_splits(e, n, 2),
                     e->slab_r[0][0], e->bslab_r[0][0], e->slab_r_floats, e->bslab_r_floats, &wp, &red));
-    wp.co_split = rcab_co_split(e);
-    if (fold) {
-      cp.fold = fold_consumer(e, e->probe_prm, r, 0, b, conv3x3_nstrips(h, w));
-      wp.fold = cp.fold;
-      // and, as in the step, the previous RCAB's two slab reductions (the other slab
-      // parity; results into GAf -- scratch after the timed region -- when they fit)
-      const RCABRef& rp = e->P.groups[0][b];
-      float* gs = e->GAf - rp.c1.w;
-      ReduceSet r2, r1;
-      WgradParams tmp;
-      if (SRMI_RED_IN_F2 && rp.c1.b + 64 <= (long long)e->mapn && rp.c2.w + 64 * 576 <= (long long)e->mapn &&
-          wgrad_params(e, rp.c2, e->Tm(0, b + 1), e->DU, n, h, w, gs, false, 1.f, rcab_row_splits(e, n, 2),
-                       e->slab_r[1][0], e->bslab_r[1][0], e->slab_r_floats, e->bslab_r_floats, &tmp, &r2) == 0 &&
-          wgrad_params(e, rp.c1, e->hb(0, b), e->DZ, n, h, w, gs, true, 1.f, rcab_row_splits(e, n, 1),
-                       e->slab_r[1][1], e->bslab_r[1][1], e->slab_r_floats, e->bslab_r_floats, &tmp, &r1) == 0) {
-        wp.red[0] = r2;
-        wp.red[1] = r1;
-        wp.nred = 2;
-      }
-    }
   } else {
     const bool last = (b == 1);
     epi = EPI_DG_ACC;
@@ -1031,12 +924,6 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
                       nullptr, last ? nullptr : e->Um(0, b - 1), last ? nullptr : e->pacc, 1.f);
     RC(wgrad_params(e, r.c1, e->hb(0, b - 1), e->DZ, n, h, w, grads, true, 1.f, rcab_row_splits(e, n, 1),
                     e->slab_r[0][1], e->bslab_r[0][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red));
-    wp.co_split = rcab_co_split(e);
-    if (use_ca_fold(e, n) && !last) {
-      cp.fold.du_out = e->DU;
-      cp.fold.s_rec = e->recp(0, b - 1);
-      cp.fold.CR = 64 / e->P.cfg.reduction;
-    }
   }
   for (int i = 0; i < reps; ++i) RC(dgrad_with_wgrad(e, cp, epi, wp, which, S_(stream)));
   return 0;

@@ -15,20 +15,8 @@
 // instead of the pooled fp32 u) and in adding the fp32 u to h (the three launches add
 // bf16(u)): both within bf16 noise of the fp64 oracle
 // (test_fused_inference_rcab_matches_three_launches_and_oracle).
-// plain (write-back) stores for this launch's outputs: t is re-read by the workgroup
-// that wrote it, and the pair by the next launch (+1 % C5 against write-through)
-#ifndef SRMI_INFER_WT
-#define SRMI_INFER_WT 0
-#endif
-// deferred conv epilogues (conv64_body.hpp SRMI_DEFER) for this launch's convs: an
-// image is one run of 12 strips here, not 3 as in training.  16 = conv1's RELU_POOL;
-// conv2's CA_RESID epilogue (32) measured 5 % slower deferred (its pair codec then
-// competes with the next strip's MFMA issue)
-#ifndef SRMI_INFER_DEFER
-#define SRMI_INFER_DEFER 16
-#endif
-#define SRMI_WT SRMI_INFER_WT
-#define SRMI_DEFER SRMI_INFER_DEFER
+// (write-back stores and the deferred conv1 epilogue: tuning.hpp SRMI_INFER_*)
+#define SRMI_TU_INFER 1
 #include "conv64_body.hpp"
 #include "ca_scale.hpp"
 #include "srmi_internal.hpp"
@@ -65,7 +53,7 @@ __global__ void __launch_bounds__(512, 1) rcab_infer_kernel(ConvParams c1, ConvP
   }
   own_stores_visible();  // s in the record, read by conv2's epilogue
   // h' = h + s (conv2(t) + b2); its filter image is resident from the scale phase
-  conv64_body<48, EPI_CA_RESID, 8, false, true>(c2, nsy, n, smem);
+  conv64_body<48, EPI_CA_RESID, 8, true>(c2, nsy, n, smem);
 }
 
 int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* part, int nstrips, const float* w1,
@@ -104,33 +92,6 @@ int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* p
   b.escale = rec + 64 + CR;  // s of the record m | z1 | s
   b.escale_stride = 128 + CR;
   hipLaunchKernelGGL(rcab_infer_kernel, dim3(c1.N), dim3(512), Conv2Smem<48>::TOTAL, st, a, b, ca);
-  SRMI_CHECK_LAUNCH();
-  return 0;
-}
-
-// the CA scale as its own launch (training A/B): a workgroup per image loads conv2's
-// filter image and runs the scale phase of the inference RCAB
-__global__ void __launch_bounds__(512, 1) ca_scale_kernel(CaScale ca, const bf16_t* __restrict__ wpack, int H, int W) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int n = blockIdx.x;
-  CaScalePre q;
-  ca_scale_load(ca, n, H, W, q);
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t wbase = lds_u32(smem);
-  for (int i = wv; i < 72; i += 8) {
-    const int tap = i >> 3, row = 8 * (i & 7) + (lane >> 3), ch = (lane & 7) ^ (row & 7);
-    glds16(wpack + ((size_t)(tap * 64 + row)) * 64 + ch * 8, wbase + (uint32_t)i * 1024u);
-  }
-  wait_vm<0>();
-  ca_scale_finish<false>(ca, q, n, H, W, reinterpret_cast<float*>(smem + 9 * 8192), smem, true);
-}
-
-int ca_scale_launch(const CaScale& c, const bf16_t* wpack, int N, int H, int W, hipStream_t st) {
-  if (!c.t || !c.part || !c.w1 || !c.b1 || !c.w2 || !c.b2 || !c.bc2 || !c.rec || !wpack || N < 1 || H % kTH ||
-      W % 48 || c.CR < 4 || c.CR > 32 || c.CR % 4 || c.nstrips != (H / kTH) * (W / 48))
-    return SRMI_ERR_ARG;
-  hipLaunchKernelGGL(ca_scale_kernel, dim3(N), dim3(512), 9 * 8192 + kCaScaleFloats * sizeof(float), st, c, wpack, H,
-                     W);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

@@ -400,9 +400,6 @@ __global__ void __launch_bounds__(256) tail_fwd_f32_kernel(const float* __restri
   }
 }
 
-#ifndef SRMI_TAIL_FWD_BLOCKS
-#define SRMI_TAIL_FWD_BLOCKS 512
-#endif
 constexpr int kTailFwdBlocks = SRMI_TAIL_FWD_BLOCKS;
 
 int tail_fwd_launch(const void* xv, const float* w, const float* b, int N, int C, int H, int W, float* y, int f32,
@@ -1128,9 +1125,6 @@ struct Unit4<float> {
 // per-block MLP is amortised over 2x the data of the former 2; 18 blocks per
 // 48x48 image, every block resident at once; ca_fwd 22.6 -> 20.0 us, ca_bwd
 // 15.1 -> 13.7 us against the former separate MLP launches)
-#ifndef SRMI_CA_VEC
-#define SRMI_CA_VEC 4
-#endif
 constexpr int kCaVec = SRMI_CA_VEC;
 
 // h_out = u * s + h_in; grid (chunks, N).  Residual-stream forms (MODE):

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/srmi.h"
+#include "tuning.hpp"
 
 namespace srmi {
 
@@ -44,27 +45,6 @@ struct CaScale {
   float* rec;         // out: m | z1 | s per image [N][128 + CR]
 };
 
-// The CA-backward fold of the bf16 RCAB backward (engine.cpp backward_impl).  du =
-// g * s + dm / HW (CALayer backward, sres/model/rcan/network.py:44-47) is never
-// materialised: the producer (the conv1 dgrad of the RCAB above, EPI_DG_ACC_CA) writes
-// du' = bf16(g * s) beside the gradient stream, and the consumer (the conv2 dgrad,
-// EPI_DG_RELUMASK, and its filter gradient) recomputes the image's MLP backward from
-// the producer's CA sums and adds the spatially constant c = dm / HW exactly: the
-// dgrad as a per-border-class epilogue term conv2^T(c), the filter gradient as
-// c (x) (window sums of t) added to each partial slab.
-struct CaFold {
-  bf16_t* du_out;       // producer: du' output (null: no fold output)
-  const float* s_rec;   // producer: the next RCAB's forward record (m | z1 | s per image)
-  const float* part;    // consumer: CA sums [N][nstrips][128] (sum g, sum g*u) of this RCAB
-  int nstrips;
-  int CR;               // bottleneck width (C / reduction)
-  const float* rec;     // consumer: this RCAB's forward record
-  const float* w1;      // consumer: conv_du.0.weight [CR][C]
-  const float* w2;      // consumer: conv_du.2.weight [C][CR]
-  float* brec;          // consumer: backward record [N][2C+CR] (+ dm [N][C]) for ca_param_grads
-  int on;               // consumer: 1 = add the constant term
-};
-
 struct ConvParams {
   const bf16_t* x;     // input (logical NHWC [N][H][W][Cin])
   const bf16_t* w;     // packed filters [Cin/64][9][Cout][64]
@@ -85,7 +65,6 @@ struct ConvParams {
   int cu_budget;               // CUs a launch should fill (0 = all 256)
   int f32;                     // exact-fp32 mode: x, w, yb, aux point at fp32 data
                                // (the bf16_t* fields are plain addresses then)
-  CaFold fold;                 // zero-initialised: no fold
   // EPI_CA_RESID: the residual stream as the pair (bf16 hi + lo8 remainder, common.hpp)
   const bf16_t* r1h;
   const uint8_t* r1l;
@@ -126,15 +105,6 @@ struct WgradParams {
   const void* zeros;   // >= 16 zero bytes in global memory (DMA source for padding)
   unsigned long long* stamps;  // diagnostic (null in production)
   int f32;             // exact-fp32 mode: x, dy point at fp32 data
-  CaFold fold;         // consumer side (the conv2 filter gradient of a folded RCAB)
-  // fused launch only: two slab reductions of an earlier launch (the previous RCAB's
-  // filter gradients) shared out over this launch's filter-gradient workgroups,
-  // after their own chunk (nred = 0: none)
-  ReduceSet red[2];
-  int nred;
-  // 2: every workgroup computes half of a co block's output channels over its chunk
-  // (wgrad48 only; the engine then takes chunks of twice the rows: half the slabs)
-  int co_split;
 };
 void wgrad3x3_set_debug_stamps(unsigned long long* buf);
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st);  // dispatches p.f32
@@ -215,7 +185,6 @@ int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* p
 // the CA scale of every image of an RCAB as its own launch (a 512-thread workgroup per
 // image; conv2's filter pack wpack, forward layout): the A/B alternative to computing it
 // in the conv2 prologue
-int ca_scale_launch(const CaScale& c, const bf16_t* wpack, int N, int H, int W, hipStream_t st);
 // records of consecutive RCABs Ncap images apart (the engine capacity), N summed
 int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int Ncap, int C, int R,
                                   const long long* offs, float* grads, hipStream_t st);

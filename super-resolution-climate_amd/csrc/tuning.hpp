@@ -1,0 +1,62 @@
+// Every compile-time switch of the srmi kernels, in one place.  The values below are
+// the production build (the measured winners, DESIGN.md sections 3-4); a variant build
+// for an A/B overrides one with -DNAME=value (tools/build_variant.sh) and never ships.
+// Run-time choices (A/B and tests) are the srmi_model_config.flags bits, include/srmi.h.
+#pragma once
+
+// Write-through (sc1) stores for the large outputs (common.hpp st_wt*): the kernel
+// boundary then finds no dirty lines to flush (the slabs alone: +1.1 % in the step).
+#ifndef SRMI_TRAIN_WT
+#define SRMI_TRAIN_WT 1
+#endif
+// the one-launch inference RCAB (rcab_infer.hip): write-back stores -- t is re-read by
+// the workgroup that wrote it and the pair by the next launch (+1 % C5 over write-through)
+#ifndef SRMI_INFER_WT
+#define SRMI_INFER_WT 0
+#endif
+
+// Deferred conv epilogues (conv64_body.hpp conv64_defers), a bit mask: 1 RELU, 2 POOL,
+// 4 DG_RELUMASK, 8 DG_ACC_CA, 16 RELU_POOL, 32 CA_RESID.  Training: only DG_RELUMASK
+// gains in the step; inference (an image is one run of 12 strips): conv1's RELU_POOL
+// (CA_RESID deferred measured 5 % slower: its pair codec competes with the next strip's
+// MFMA issue).
+#ifndef SRMI_TRAIN_DEFER
+#define SRMI_TRAIN_DEFER 4
+#endif
+#ifndef SRMI_INFER_DEFER
+#define SRMI_INFER_DEFER 16
+#endif
+
+// rcab_infer.hip defines SRMI_TU_INFER before its includes: the inference policies
+#ifdef SRMI_TU_INFER
+#define SRMI_WT SRMI_INFER_WT
+#define SRMI_DEFER SRMI_INFER_DEFER
+#else
+#define SRMI_WT SRMI_TRAIN_WT
+#define SRMI_DEFER SRMI_TRAIN_DEFER
+#endif
+
+// Training CA forward (engine.cpp ca_fwd_mode): 1 = inside conv2's launch (the scale in
+// every conv2 workgroup's prologue, +1.1 % over the CA pass), 0 = the CA pass of its own.
+#ifndef SRMI_CA_FWD
+#define SRMI_CA_FWD 1
+#endif
+
+// waves per workgroup of the exact-fp32 conv (conv_f32.hip)
+#ifndef SRMI_F32_NW
+#define SRMI_F32_NW 8
+#endif
+
+// workgroups of the tail conv's forward (small.hip tail_fwd_launch)
+#ifndef SRMI_TAIL_FWD_BLOCKS
+#define SRMI_TAIL_FWD_BLOCKS 512
+#endif
+
+// 8-channel groups per thread of the CA elementwise passes (small.hip): 4 amortises the
+// per-block MLP over twice the data of 2 (ca_fwd 22.6 -> 20.0 us, ca_bwd 15.1 -> 13.7 us)
+#ifndef SRMI_CA_VEC
+#define SRMI_CA_VEC 4
+#endif
+
+// SRMI_STAMPS (undefined in production): s_memtime stamps per workgroup phase into
+// ConvParams / WgradParams .stamps (srmi_debug_conv_stamps, tools/stamps_run.sh)

@@ -235,15 +235,6 @@ constexpr int NGP = 2 * GD + 2 * GX;                             // groups per p
 }  // namespace v4
 
 
-#ifndef SRMI_FOLD_PARTS
-#define SRMI_FOLD_PARTS 3  // diagnostic: 1 = only the dgrad side of the fold consumer, 2 = only the filter gradient's
-#endif
-// the fold's LDS scratch in the fused launch: after the conv body's own LDS (which
-// is larger than the filter gradient's rings)
-constexpr int kFoldOff = Conv2Smem<48>::TOTAL;
-static_assert(Conv2Smem<48>::TOTAL >= v4::LDS, "fold scratch must not overlap the rings");
-static_assert(kFoldOff + kFoldBytes <= 160 * 1024, "LDS");
-
 
 // The body is instantiated once per wave (WV = wave index): the wave's DMA groups,
 // taps and tile rotation are compile-time constants (no SGPR pressure, no branches).
@@ -253,143 +244,16 @@ static_assert(kFoldOff + kFoldBytes <= 160 * 1024, "LDS");
 // 0-3 also issue the DMA (the 4-wave schedule) and the bias gradient; every wave
 // keeps all four output-channel tiles and writes its partial slab in the 4-wave
 // layout, so wgrad_reduce is unchanged.
-// The fold's filter-gradient term for one chunk (rows ybase .. ybase + Hr - 1 of image
-// n, W == 48): T[tap][ci] = sum over the chunk's pixels p of x[p + off(tap)][ci]
-// (zero outside the image), then acc += c[co] T[tap][ci] (c = dm / HW, ca_fold_mlp).
-// Runs after the K-loop (every wave): the rings are free, the input rows are L2-hot.
-//   T[ky][kx] = sum over input rows r of the ky window (ky 0: rows -1 .. Hr-2, 1: 0 ..
-//   Hr-1, 2: 1 .. Hr) of the row sum over the kx window (kx 0: columns 0 .. 46, 1:
-//   all, 2: 1 .. 47).  Thread (pixel pg, 8-channel chunk cc) sums its pixel over the
-//   rows into the three ky windows; the pixel partials are combined in LDS in a fixed
-//   order (deterministic), the kx windows by subtracting the pixel-0 / pixel-47 parts.
-template <int NT, int J0>
-__device__ __forceinline__ void wgrad48_fold_correction(const WgradParams& p, char* smem, f32x4 (&acc)[4][NT], int n,
-                                                        int ybase, int Hr, int wave, int lane) {
-  constexpr int Wd = 48;
-  float* const fsm = reinterpret_cast<float*>(smem + kFoldOff);
-  float* const tpart = reinterpret_cast<float*>(smem);              // [48 pg][3 ky][64 ci] (ring: free now)
-  float* const tsum = reinterpret_cast<float*>(smem + 48 * 3 * 64 * 4);  // [9 taps][64 ci]
-  const int tid = threadIdx.x;
-  fold_barrier();  // every wave is past its last ring read
-  {
-    // the chunk's input rows -1 .. Hr: the first (up to) 16 rows' loads are issued
-    // before the MLP's, so the two latencies overlap; then the rest
-    const int cc = tid & 7, pg = tid >> 3;
-    const bool act = pg < Wd;
-    const bf16_t* xr = p.x + ((size_t)n * p.H * Wd + (act ? pg : 0)) * 64 + cc * 8;
-    float a[3][8];
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) a[k][e] = 0.f;
-    auto row_batch = [&](int r0, auto issue_mlp) __attribute__((always_inline)) {
-      uint4 v[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {  // clamped unconditional loads, zeroed outside the rows / image
-        const int y = min(max(ybase + r0 + i, 0), p.H - 1);
-        v[i] = *reinterpret_cast<const uint4*>(xr + (size_t)y * Wd * 64);
-      }
-      if constexpr (decltype(issue_mlp)::value) ca_fold_mlp(p.fold, n, p.N, p.H * Wd, fsm, false);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int r = r0 + i, y = ybase + r;
-        const bool in = act && r <= Hr && y >= 0 && y < p.H;
-        const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-        const bool k0 = in && r <= Hr - 2, k1 = in && r >= 0 && r <= Hr - 1, k2 = in && r >= 1;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float x0 = __uint_as_float(w[e] << 16), x1 = __uint_as_float(w[e] & 0xFFFF0000u);
-          a[0][2 * e] += k0 ? x0 : 0.f;
-          a[0][2 * e + 1] += k0 ? x1 : 0.f;
-          a[1][2 * e] += k1 ? x0 : 0.f;
-          a[1][2 * e + 1] += k1 ? x1 : 0.f;
-          a[2][2 * e] += k2 ? x0 : 0.f;
-          a[2][2 * e + 1] += k2 ? x1 : 0.f;
-        }
-      }
-    };
-    row_batch(-1, std::true_type{});
-    for (int r0 = 15; r0 <= Hr; r0 += 16) row_batch(r0, std::false_type{});
-    if (act) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        float4* d = reinterpret_cast<float4*>(tpart + (pg * 3 + k) * 64 + cc * 8);
-        d[0] = make_float4(a[k][0], a[k][1], a[k][2], a[k][3]);
-        d[1] = make_float4(a[k][4], a[k][5], a[k][6], a[k][7]);
-      }
-    }
-  }
-  fold_barrier();
-  if (tid < 192) {  // (ky, ci): the pixel partials in order, then the three kx windows
-    const int ky = tid >> 6, ci = tid & 63;
-    float sum = 0.f;
-    for (int pg = 0; pg < Wd; ++pg) sum += tpart[(pg * 3 + ky) * 64 + ci];
-    tsum[(ky * 3 + 0) * 64 + ci] = sum - tpart[((Wd - 1) * 3 + ky) * 64 + ci];
-    tsum[(ky * 3 + 1) * 64 + ci] = sum;
-    tsum[(ky * 3 + 2) * 64 + ci] = sum - tpart[ky * 64 + ci];
-  }
-  fold_barrier();
-  // acc[ct][t]: rows 4 (lane >> 4) + r of co tile (ct + wave) & 3, column ci of N tile
-  // J0 + t (tap = J >> 2, ci = 16 (J & 3) + (lane & 15))
-  float tv[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int J = J0 + t;
-    tv[t] = tsum[(J >> 2) * 64 + (J & 3) * 16 + (lane & 15)];
-  }
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    const float4 cv = *reinterpret_cast<const float4*>(fsm + kFoldC + ((ct + wave) & 3) * 16 + 4 * (lane >> 4));
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      acc[ct][t][0] += cv.x * tv[t];
-      acc[ct][t][1] += cv.y * tv[t];
-      acc[ct][t][2] += cv.z * tv[t];
-      acc[ct][t][3] += cv.w * tv[t];
-    }
-  }
-}
-
-// FOLD (the conv2 filter gradient of a folded RCAB, fused launch only, W == 48):
-// before the slab store the partial gains c[co] T[tap][ci] (wgrad48_fold_correction):
-// the filter gradient of du = du' + c, exactly.
-// du' + c on one K-step's dY fragments: lane l of co tile ct holds 8 pixels of row co
-// = tile (ct + wave) & 3, l & 15 -- one c per fragment, rounded back to bf16
-__device__ __forceinline__ void add_fold_c(bf16x8 (&a)[4], const float (&fc)[4]) {
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    u32x4 q = __builtin_bit_cast(u32x4, a[ct]);
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      q[e] = pack2(__uint_as_float(q[e] << 16) + fc[ct], __uint_as_float(q[e] & 0xFFFF0000u) + fc[ct]);
-    a[ct] = __builtin_bit_cast(bf16x8, q);
-  }
-}
-
-// SRMI_FOLD_WG: 2 = c added to the dY fragments in the K-loop (the filter gradient of
-// bf16(du' + c), as the materialised path rounds du); 1 = c (x) T added to the partial
-// after the K-loop (exact; its row-sum pass after the chunk measured +7-11 us in F2)
-#ifndef SRMI_FOLD_WG
-#define SRMI_FOLD_WG 2
-#endif
-// HALF (co_split = 2): the workgroup computes one half (`half`: output-channel tiles
-// 2 half, 2 half + 1) of the co block's filter gradient over a chunk of twice the
-// rows -- a whole image -- so that a launch writes half the partial slabs for the
-// same MFMA work per workgroup; the two halves of an image write disjoint tiles of
-// one slab (layout 1 unchanged, the reduction too).  The dY rows are still DMA'd
-// whole (the other half's channels ride along, L2 hits).
-template <int WV, int NW = 4, bool FOLD = false, bool HALF = false>
-__device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, int chunk, int cb, int half = 0) {
-  constexpr bool FOLD_A = FOLD && SRMI_FOLD_WG == 2;
+template <int WV, int NW = 4>
+__device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, int chunk, int cb) {
   using namespace v4;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  static_assert(!(FOLD && HALF), "the fold runs on whole co blocks");
-  constexpr int NCA = HALF ? 2 : 4;  // output-channel (A) tiles of this workgroup's waves
+  constexpr int NCA = 4;  // output-channel (A) tiles of every wave
   // N tiles of this wave and its first one (8 waves: the younger half, waves 4-7, takes 5)
   constexpr int NT = NW == 4 ? 9 : (WV < 4 ? 4 : 5);
   constexpr int J0 = NW == 4 ? 9 * WV : (WV < 4 ? 4 * WV : 16 + 5 * (WV - 4));
-  constexpr bool kMain = WV < 4;  // DMA (+ the bias gradient: waves 0-3, or 0-1 of a half)
-  constexpr bool kBias = HALF ? WV < 2 : WV < 4;
+  constexpr bool kMain = WV < 4;  // DMA + bias gradient
+  constexpr bool kBias = kMain;
   const int tid = threadIdx.x, lane = tid & 63;
   constexpr int wave = WV & 3, wave_s = WV & 3;
   // chunk = (image, row band, 48-column block): W may be any multiple of 48 (the
@@ -482,8 +346,8 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   for (int i = 0; i < NCA; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // the output-channel tile of A slot ct: rotated by the wave (LDS banks), within the half
-  auto ctile = [&](int ct) -> int { return HALF ? 2 * half + ((ct + wave) & 1) : (ct + wave) & 3; };
+  // the output-channel tile of A slot ct: rotated by the wave (LDS banks)
+  auto ctile = [&](int ct) -> int { return (ct + wave) & 3; };
   f32x4 bacc = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 ones;
 #pragma unroll
@@ -554,9 +418,6 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
     else wait_vm<0>();
   };
 
-  // fold (A-operand form): the MLP's operands in flight under the DMA prologue
-  [[maybe_unused]] CaFoldRegs fregs;
-  if constexpr (FOLD_A) ca_fold_mlp_load(p.fold, n, fregs);
   // prologue: input rows -1, 0 and pairs 0 .. PF-1; wait for the rows and pair 0
   if constexpr (kMain) {
 #pragma unroll
@@ -566,31 +427,17 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   }
   wait_groups(min(PF, np) - 1, 0);
   __syncthreads();
-  // fold, A-operand form: c = dm / HW of the image for the lane's A rows (co =
-  // tile (ct + wave) & 3, row lane & 15), added to every dY fragment before its MFMAs
-  [[maybe_unused]] float fc[4];
-  if constexpr (FOLD_A) {
-    float* const fsm = reinterpret_cast<float*>(smem + kFoldOff);
-    ca_fold_mlp_compute(p.fold, n, p.N, H * Wd, fsm, false, fregs);
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) fc[ct] = fsm[kFoldC + ((ct + wave) & 3) * 16 + (lane & 15)];
-  }
   WSTAMP(1);
 
   // fragments double-buffered across K-steps; a pair has 3 K-steps, so the pair loop
   // is unrolled by two (np is even) to keep the buffer parity compile-time.  8 waves
   // (256 registers a wave): B single-buffered, each tile reloaded right behind its
   // MFMAs (the partner wave on the SIMD covers the read latency).
-  // (co halves hold half the accumulators: room for double-buffered B, SRMI_HALF_NB = 2)
-#ifndef SRMI_HALF_NB
-#define SRMI_HALF_NB 1
-#endif
-  constexpr int NB = (NW == 8 && !(HALF && SRMI_HALF_NB == 2)) ? 1 : 2;
+  constexpr int NB = NW == 8 ? 1 : 2;
   bf16x8 A[2][NCA], B[NB][NT];
   uint32_t ra, rb[NT];
   slots(0, ra, rb);
   load_step(ra, rb, 0, A[0], B[0]);
-  if constexpr (FOLD_A) add_fold_c(A[0], fc);
 
 #pragma unroll 1
   for (int j0 = 0; j0 < np; j0 += 2) {
@@ -638,12 +485,6 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
           if constexpr (NRD > NPAIR) __builtin_amdgcn_sched_group_barrier(0x100, NRD - NPAIR, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (FOLD_A) {
-          // du = du' + c on the NEXT K-step's dY fragments (loaded during these MFMAs):
-          // the VALU runs while the MFMA pipe drains instead of ahead of it
-          if (kc < 2 || more) add_fold_c(A[nxt], fc);
-          __builtin_amdgcn_sched_barrier(0);
-        }
         if (kc == 1) {
           // pair j+1 must have landed before K-step 2 reads its first fragments.  In
           // flight may stay: pair j+2 (whole) and the 5 groups of pair j+PF issued above.
@@ -668,7 +509,6 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   // other way round in round 2: the launch 0.9 us shorter, the reduce 1.9 us longer)
   // (N tile J, slot ct of rotation `wave`) -> the 4-wave position (wave J / 9, tile
   // J % 9, the slot of the same output-channel tile under that wave's rotation)
-  if constexpr (FOLD && !FOLD_A) wgrad48_fold_correction<NT, J0>(p, smem, acc, n, ybase, Hr, wave, lane);
   const size_t soff = (size_t)chunk * Cout * 576 + (size_t)cb * (64 * 576);
   // (write-through: the slab leaves the XCD's L2 while the other waves still
   //  compute, instead of in the dirty-line flush at the end of the launch)
@@ -690,45 +530,30 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   WSTAMP(63);
 }
 
-template <int NW = 4, bool FOLD = false, bool HALF = false>
-__device__ __forceinline__ void wgrad48_dispatch(const WgradParams& p, char* smem, int chunk, int cb, int half = 0) {
+template <int NW = 4>
+__device__ __forceinline__ void wgrad48_dispatch(const WgradParams& p, char* smem, int chunk, int cb) {
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: wgrad48_body<0, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
-    case 1: wgrad48_body<1, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
-    case 2: wgrad48_body<2, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
-    case 3: wgrad48_body<3, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
+    case 0: wgrad48_body<0, NW>(p, smem, chunk, cb); break;
+    case 1: wgrad48_body<1, NW>(p, smem, chunk, cb); break;
+    case 2: wgrad48_body<2, NW>(p, smem, chunk, cb); break;
+    case 3: wgrad48_body<3, NW>(p, smem, chunk, cb); break;
     default:
       if constexpr (NW == 8) {
         switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-          case 4: wgrad48_body<4, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
-          case 5: wgrad48_body<5, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
-          case 6: wgrad48_body<6, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
-          default: wgrad48_body<7, NW, FOLD, HALF>(p, smem, chunk, cb, half); break;
+          case 4: wgrad48_body<4, NW>(p, smem, chunk, cb); break;
+          case 5: wgrad48_body<5, NW>(p, smem, chunk, cb); break;
+          case 6: wgrad48_body<6, NW>(p, smem, chunk, cb); break;
+          default: wgrad48_body<7, NW>(p, smem, chunk, cb); break;
         }
       }
       break;
   }
 }
 
-// workgroup index w of a filter-gradient grid -> (chunk, co block, half): with
-// co halves, w = 2 (cb nch + chunk) + half, so the two halves of a chunk are
-// neighbours (and conv run w of a paired fused launch covers the same image)
-__device__ __forceinline__ void wgrad_unit(const WgradParams& p, int w, int& chunk, int& cb, int& half) {
-  const int nch = p.N * p.row_splits * (p.W / 48);
-  const int cs = p.co_split == 2 ? 2 : 1;
-  half = w % cs;
-  const int r = w / cs;
-  chunk = r % nch;
-  cb = r / nch;
-}
-
 constexpr int kWgradNW = 8;  // waves per workgroup of the standalone filter gradient (two per SIMD)
-template <bool HALF>
 __global__ void __launch_bounds__(kWgradNW * 64, 1) wgrad48_kernel(WgradParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  int chunk, cb, half;
-  wgrad_unit(p, blockIdx.x, chunk, cb, half);
-  wgrad48_dispatch<kWgradNW, false, HALF>(p, smem, chunk, cb, half);
+  wgrad48_dispatch<kWgradNW>(p, smem, blockIdx.x, blockIdx.y);
 }
 
 // ---------------------------------------------------------------------------
@@ -753,14 +578,11 @@ __global__ void __launch_bounds__(kWgradNW * 64, 1) wgrad48_kernel(WgradParams p
 // dgrad half (F1: 24.7 vs 36.9 us at C2), so the last `tail` strips of dgrad run k
 // move to the workgroup of chunk k, which runs them after its chunk (same rows, same
 // XCD), with its own filter prologue.
-template <int EPI, int NW, bool FOLD = false, bool HALF = false>
+template <int EPI, int NW>
 __global__ void __launch_bounds__(NW * 64, 1) rcab_bwd_kernel(ConvParams cp, int run_len, int nconv, WgradParams wp,
                                                               int nwg, int paired, int tail) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x, tot = nconv + nwg;
-#ifndef SRMI_FUSE_DIAG
-#define SRMI_FUSE_DIAG 0  // diagnostic builds only (wrong results): 1 = skip the wgrad part, 2 = skip the conv part
-#endif
   int conv = -1, w;
   if (paired) {
     const int base = (b >> 4) << 3, i = b & 15, m = min(8, nconv - base);
@@ -771,36 +593,22 @@ __global__ void __launch_bounds__(NW * 64, 1) rcab_bwd_kernel(ConvParams cp, int
     if (c1 > c0) conv = c0;
     else w = b - c0;
   }
-  // FOLD: in F2 (DG_RELUMASK) the fold consumer -- its dgrad, its filter gradient and the
-  // previous RCAB's slab reductions; in F1 (DG_ACC_CA) the producer's du' store only
-  constexpr bool kF2 = EPI == EPI_DG_RELUMASK;
-  constexpr bool kFoldConv = kF2 ? (FOLD && (SRMI_FOLD_PARTS & 1)) : FOLD;
-  constexpr bool kFoldWg = kF2 && FOLD && (SRMI_FOLD_PARTS & 2);
   if (conv >= 0) {
-    if (!(SRMI_FUSE_DIAG & 2)) conv64_body<48, EPI, NW, kFoldConv>(cp, run_len, conv, smem, tail, false);
+    conv64_body<48, EPI, NW>(cp, run_len, conv, smem, tail, false);
     return;
   }
-  if (!(SRMI_FUSE_DIAG & 1)) {
-    int chunk, cb, half;
-    wgrad_unit(wp, w, chunk, cb, half);
-    wgrad48_dispatch<NW, kFoldWg, HALF>(wp, smem, chunk, cb, half);
-  }
-  if constexpr (kF2 && FOLD) {
-    if (wp.nred > 0) {  // the previous RCAB's slab reductions, shared over this launch's filter-gradient workgroups
-      static_assert(NW * 64 == 512, "slab_reduce_share runs on 512 threads");
-      slab_reduce_share(wp.red[0], wp.red[1], wp.nred, w, nwg, reinterpret_cast<float4*>(smem));
-    }
-  }
-  if (tail > 0 && !(SRMI_FUSE_DIAG & 2)) {
+  const int nch = wp.N * wp.row_splits;
+  wgrad48_dispatch<NW>(wp, smem, w % nch, w / nch);
+  if (tail > 0) {
     __syncthreads();  // every wave is past its last LDS read of the chunk
-    conv64_body<48, EPI, NW, kFoldConv>(cp, run_len, w, smem, tail, true);
+    conv64_body<48, EPI, NW>(cp, run_len, w, smem, tail, true);
   }
 }
 
 int rcab_bwd_fusable(const ConvParams& cp, const WgradParams& wp) {
   return !cp.f32 && !wp.f32 && cp.Cin == 64 && cp.Cout == 64 && cp.in_mode == IN_PLAIN && cp.W == 48 &&
          cp.H % 4 == 0 && wp.W == 48 && wp.Cout == 64 && wp.dy_mode == IN_PLAIN && wp.row_splits > 0 &&
-         wp.H % wp.row_splits == 0 && (wp.H / wp.row_splits) % 4 == 0 && (wp.co_split == 2 ? !wp.fold.on : true);
+         wp.H % wp.row_splits == 0 && (wp.H / wp.row_splits) % 4 == 0;
 }
 
 // waves per workgroup of the fused launch (8: two per SIMD in both roles)
@@ -816,21 +624,8 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
   if (!slab_range_ok(wp, wp.N * wp.row_splits)) return SRMI_ERR_SHAPE;
   const int run_len = conv64_run_len(cp, 48, conv_cus);
   const int nconv = conv64_blocks(cp, 48, run_len);
-  const int cs = wp.co_split == 2 ? 2 : 1;
-  const int nwg = wp.N * wp.row_splits * (wp.Cout / 64) * cs;
-  const bool fold = cp.fold.on != 0;
-  if (fold && (epi != EPI_DG_RELUMASK || !wp.fold.on || !cp.fold.part || !cp.fold.rec || !cp.fold.w1 ||
-               !cp.fold.w2 || !cp.fold.brec || cp.fold.CR < 4 || cp.fold.CR > 32 || cp.fold.CR % 4 ||
-               cp.alpha != 1.f))
-    return SRMI_ERR_ARG;
-  if (epi == EPI_DG_ACC_CA && cp.fold.du_out && (!cp.fold.s_rec || cp.fold.CR < 4 || cp.fold.CR > 32))
-    return SRMI_ERR_ARG;
-  if (wp.nred < 0 || wp.nred > 2 || (wp.nred > 0 && (!fold || epi != EPI_DG_RELUMASK))) return SRMI_ERR_ARG;
-  for (int k = 0; k < wp.nred; ++k)
-    if (!wp.red[k].slab || !wp.red[k].gw || wp.red[k].Cout != 64 || wp.red[k].layout != 1 || wp.red[k].ps ||
-        wp.red[k].nslab < 1 || (wp.red[k].gb && !wp.red[k].bslab))
-      return SRMI_ERR_ARG;
-  const int lds = (Conv2Smem<48>::TOTAL > v4::LDS ? Conv2Smem<48>::TOTAL : v4::LDS) + (fold ? kFoldBytes : 0);
+  const int nwg = wp.N * wp.row_splits * (wp.Cout / 64);
+  const int lds = Conv2Smem<48>::TOTAL > v4::LDS ? Conv2Smem<48>::TOTAL : v4::LDS;
   ConvParams c = cp;
   c.stamps = nullptr;
   WgradParams w = wp;
@@ -838,60 +633,22 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
   const dim3 grid(nconv + nwg);
   // conv run k and wgrad chunk k cover the same rows of the same image
   const int runs_per_col = (cp.H / kTH + run_len - 1) / run_len;
-  // (co halves: conv run k and filter-gradient workgroup k cover the same image)
-  const int paired = nconv == nwg && cp.N == wp.N &&
-                     (cs == 2 ? runs_per_col == 2 * wp.row_splits
-                              : runs_per_col == wp.row_splits && run_len * kTH == wp.H / wp.row_splits);
+  const int paired =
+      nconv == nwg && cp.N == wp.N && runs_per_col == wp.row_splits && run_len * kTH == wp.H / wp.row_splits;
   // dgrad strips per run handed to the paired filter-gradient workgroup (see the kernel)
   // (one strip in F1; none in F2, whose ReLU-mask strip is cheaper than the extra
   // filter prologue: DESIGN.md section 3)
   const int tail = !paired ? 0 : std::min(run_len - 1, epi == EPI_DG_RELUMASK ? 0 : 1);
-  if (wp.nred > 0 && tail > 0) return SRMI_ERR_ARG;  // (the reduction share uses the ring LDS the tail needs)
-  if (cs == 2) {  // co halves (no fold)
-    if (fold || c.fold.du_out) return SRMI_ERR_ARG;
-    switch (epi) {
-      case EPI_DG_RELUMASK:
-        if (!c.aux) return SRMI_ERR_ARG;
-        hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_RELUMASK, kFuseNW, false, true>), grid, dim3(kFuseNW * 64), lds, st,
-                           c, run_len, nconv, w, nwg, paired, tail);
-        break;
-      case EPI_DG_ACC_CA:
-        if (!c.r1 || !c.aux || !c.part || c.yb || c.r2 || c.r3 || !c.yf) return SRMI_ERR_ARG;
-        hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA, kFuseNW, false, true>), grid, dim3(kFuseNW * 64), lds, st,
-                           c, run_len, nconv, w, nwg, paired, tail);
-        break;
-      case EPI_DG_ACC:
-        if (!c.yf || (c.part && !c.aux)) return SRMI_ERR_ARG;
-        hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC, kFuseNW, false, true>), grid, dim3(kFuseNW * 64), lds, st, c,
-                           run_len, nconv, w, nwg, paired, tail);
-        break;
-      default:
-        return SRMI_ERR_ARG;
-    }
-    SRMI_CHECK_LAUNCH();
-    return 0;
-  }
   switch (epi) {
     case EPI_DG_RELUMASK:
       if (!c.aux) return SRMI_ERR_ARG;
-      if (fold)
-        hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_RELUMASK, kFuseNW, true>), grid, dim3(kFuseNW * 64), lds, st, c,
-                           run_len, nconv, w, nwg, paired, tail);
-      else
-        hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_RELUMASK, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len,
-                           nconv, w, nwg, paired, tail);
+      hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_RELUMASK, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len,
+                         nconv, w, nwg, paired, tail);
       break;
     case EPI_DG_ACC_CA:
       if (!c.r1 || !c.aux || !c.part || c.yb || c.r2 || c.r3 || !c.yf) return SRMI_ERR_ARG;
-      if (c.fold.du_out) {  // the fold producer (du' beside g): the non-deferred epilogue only
-        if constexpr (!(kFuseNW == 8 && conv64_defers<EPI_DG_ACC_CA>()))
-          hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA, kFuseNW, true>), grid, dim3(kFuseNW * 64), lds, st, c,
-                             run_len, nconv, w, nwg, paired, tail);
-        else
-          return SRMI_ERR_ARG;
-      } else
-        hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len,
-                           nconv, w, nwg, paired, tail);
+      hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len,
+                         nconv, w, nwg, paired, tail);
       break;
     case EPI_DG_ACC:
       if (!c.yf || (c.part && !c.aux)) return SRMI_ERR_ARG;
@@ -924,12 +681,7 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
   WgradParams q = p;
   q.stamps = g_wg_stamps;
   if (use_wgrad48(p)) {
-    const int cs = p.co_split == 2 ? 2 : 1;
-    const dim3 g48(wgrad3x3_nslabs(p) * (p.Cout / 64) * cs);
-    if (cs == 2)
-      hipLaunchKernelGGL(wgrad48_kernel<true>, g48, dim3(kWgradNW * 64), v4::LDS, st, q);
-    else
-      hipLaunchKernelGGL(wgrad48_kernel<false>, g48, dim3(kWgradNW * 64), v4::LDS, st, q);
+    hipLaunchKernelGGL(wgrad48_kernel, grid, dim3(kWgradNW * 64), v4::LDS, st, q);
   } else if (p.W % 48 == 0) {
     hipLaunchKernelGGL(wgrad3x3_kernel<48>, grid, dim3(256), Wg3<48>::TOTAL, st, q);
   } else if (p.W % 32 == 0) {

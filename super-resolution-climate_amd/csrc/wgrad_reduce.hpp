@@ -113,102 +113,4 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab
   }
 }
 
-// The share `part` of `nparts` of nred (1 or 2) slab reductions of 64->64 convs
-// (wgrad48 layout 1, no pixel-shuffle permutation), run by ONE 512-thread workgroup
-// inside another launch: the fused RCAB backward's filter-gradient workgroups reduce
-// the previous RCAB's slabs after their own chunk (no reduction launch of its own).
-// Output quads of the concatenated sets are split evenly over the parts; per round a
-// thread sums one quad over half of the slabs (up to 32 loads in flight, clamped and
-// zeroed past the end), the two halves are combined in LDS in a fixed order:
-// deterministic, independent of placement.  The conv1 bias (r.gb) is reduced by the
-// last part.  lds: >= 512 float4 scratch.  Every thread of the workgroup calls this.
-__device__ __forceinline__ void slab_reduce_share(const ReduceSet& ra, const ReduceSet& rb, int nred, int part,
-                                                  int nparts, float4* lds) {
-  constexpr int PERQ = 64 * 576 / 4;  // output quads per set
-  // QR quads per round x NPH slab phases, up to NL loads in flight per thread
-  constexpr int NL = 16, NPH = 4, QR = 512 / NPH;
-  const int tid = threadIdx.x, qi = tid % QR, ph = tid / QR;
-  const int total = nred * PERQ;
-  const int q0 = (int)((long long)total * part / nparts), q1 = (int)((long long)total * (part + 1) / nparts);
-  for (int qb = q0; qb < q1; qb += QR) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // the previous round's (or the caller's) LDS reads are done
-    const int q = min(qb + qi, q1 - 1);
-    const int set = q >= PERQ;
-    const float* slab = set ? rb.slab : ra.slab;
-    const int nslab = set ? rb.nslab : ra.nslab;
-    const int o4 = (q - set * PERQ) * 4;
-    const int S = (nslab + NPH - 1) / NPH, s0 = ph * S, s1 = min(nslab, s0 + S);
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int sb = s0; sb < s1; sb += NL) {
-      float4 v[NL];
-#pragma unroll
-      for (int i = 0; i < NL; ++i) {
-        const int sl = sb + i;
-        v[i] = *reinterpret_cast<const float4*>(slab + (size_t)min(sl, nslab - 1) * (64 * 576) + o4);
-        if (sl >= s1) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int i = 0; i < NL; ++i) {
-        acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w;
-      }
-    }
-    lds[ph * QR + qi] = acc;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (ph == 0 && qb + qi < q1) {
-      float4 r = lds[qi];
-#pragma unroll
-      for (int k = 1; k < NPH; ++k) {
-        const float4 t = lds[k * QR + qi];
-        r.x += t.x; r.y += t.y; r.z += t.z; r.w += t.w;
-      }
-      const float alpha = set ? rb.alpha : ra.alpha;
-      float* gw = set ? rb.gw : ra.gw;
-      const float s4[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {  // layout 1: [wave][t][ct][lane][4] (wgrad_reduce_body)
-        const int l = o4 + e;
-        const int rr = l & 3, lane = (l >> 2) & 63, ct = (l >> 8) & 3, wt = l >> 10;
-        const int wave = wt / 9, tap = wt >> 2, ci = (wt & 3) * 16 + (lane & 15);
-        const int co = ((ct + wave) & 3) * 16 + 4 * (lane >> 4) + rr;
-        gw[((size_t)co * 64 + ci) * 9 + tap] = alpha * s4[e];
-      }
-    }
-  }
-  if (part == nparts - 1) {  // the biases: 64 outputs x 8 slab phases
-    float* lf = reinterpret_cast<float*>(lds);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      if (k >= nred) break;
-      const ReduceSet& r = k ? rb : ra;
-      if (!r.gb) continue;  // (uniform)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      const int c = tid & 63, bp = tid >> 6, S = (r.nslab + 7) >> 3, s0 = bp * S, s1 = min(r.nslab, s0 + S);
-      float a = 0.f;
-      for (int sb = s0; sb < s1; sb += 8) {
-        float v[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int sl = sb + i;
-          v[i] = r.bslab[(size_t)min(sl, r.nslab - 1) * 64 + c];
-          if (sl >= s1) v[i] = 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) a += v[i];
-      }
-      lf[bp * 64 + c] = a;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (tid < 64) {
-        float b = lf[tid];
-#pragma unroll
-        for (int k2 = 1; k2 < 8; ++k2) b += lf[k2 * 64 + tid];
-        r.gb[tid] = r.alpha * b;
-      }
-    }
-  }
-}
-
 }  // namespace srmi

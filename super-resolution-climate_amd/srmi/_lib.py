@@ -17,11 +17,8 @@ LIB_PATH = os.environ.get("SRMI_LIB") or LIB_PATH_DEFAULT  # SRMI_LIB: diagnosti
 SRMI_ARCH_RCAN = 0
 SRMI_ARCH_EDSR = 1
 SRMI_DTYPE_BF16 = 0
-SRMI_FLAG_CA_FOLD = 1
 SRMI_FLAG_NO_RCAB_INFER = 2
 SRMI_FLAG_CA_PASS = 4
-SRMI_FLAG_CA_SCALE_LAUNCH = 8
-SRMI_FLAG_WGRAD_FULL_CO = 16
 SRMI_DTYPE_F32 = 1
 SRMI_LOSS_RMSE = 0
 SRMI_LOSS_MEAN = 1

@@ -343,19 +343,6 @@ def _engine_variants_agree(lr_hw, flags, grad_tol, fwd_tol=None):
 
 
 @pytest.mark.parametrize("lr_hw", [(48, 48), (32, 48), (8, 48)])
-def test_ca_fold_matches_materialised_du(lr_hw):
-    """The CA-backward fold (du never materialised; srmi_internal.hpp CaFold, DESIGN.md
-    §3) against the materialised path (the default; the fold is SRMI_FLAG_CA_FOLD):
-    every gradient -- the conv2 filter gradients with their c term, the conv1 chain
-    through the dgrad's border-class correction, the CA MLP parameter gradients from
-    the fold's backward record -- agrees to the bf16 rounding of du (the materialised
-    path rounds g s + dm/HW once, the fold rounds g s and adds dm/HW in fp32).  Three
-    tile heights move the border rows between strips and runs."""
-    from srmi._lib import SRMI_FLAG_CA_FOLD
-    _engine_variants_agree(lr_hw, (SRMI_FLAG_CA_FOLD, 0), 5e-3)
-
-
-@pytest.mark.parametrize("lr_hw", [(48, 48), (32, 48), (8, 48)])
 def test_ca_forward_in_conv2_matches_ca_pass(lr_hw):
     """The training CA forward inside conv2's launch (the default: conv1 writes t and
     the per-strip sums of the bf16 t, every conv2 workgroup derives its image's mean(u)
@@ -367,23 +354,3 @@ def test_ca_forward_in_conv2_matches_ca_pass(lr_hw):
     oracle's drift bounds.  Three tile heights move the border rows between strips."""
     from srmi._lib import SRMI_FLAG_CA_PASS
     _engine_variants_agree(lr_hw, (0, SRMI_FLAG_CA_PASS), 5e-3, fwd_tol=1e-3)
-
-
-@pytest.mark.parametrize("lr_hw", [(48, 48), (8, 48)])
-def test_ca_scale_launch_bit_identical_to_prologue_scale(lr_hw):
-    """The CA scale as a launch of its own between conv1 and conv2
-    (SRMI_FLAG_CA_SCALE_LAUNCH) runs the same arithmetic on the same operands as the
-    scale in conv2's prologue: bit-identical forward and gradients."""
-    from srmi._lib import SRMI_FLAG_CA_SCALE_LAUNCH
-    _engine_variants_agree(lr_hw, (0, SRMI_FLAG_CA_SCALE_LAUNCH), 0)
-
-
-@pytest.mark.parametrize("lr_hw", [(48, 48), (32, 48), (8, 48)])
-def test_wgrad_co_halves_match_full_co_blocks(lr_hw):
-    """The RCAB filter gradients in co halves over whole-image chunks (the default:
-    half the partial slabs per fused launch; wgrad3x3.hip HALF) against whole
-    64-channel co blocks over half-image chunks (SRMI_FLAG_WGRAD_FULL_CO): the forward
-    is untouched, the gradients differ only in how the fp32 partial sums are grouped
-    into slabs."""
-    from srmi._lib import SRMI_FLAG_WGRAD_FULL_CO
-    _engine_variants_agree(lr_hw, (0, SRMI_FLAG_WGRAD_FULL_CO), 1e-5)

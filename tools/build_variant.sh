@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build the working tree's libsrmi.so with extra compile-time switches into
 # alt/libsrmi_<name>.so (for the interleaved A/Bs of tools/ab_lib.sh / ab_kb.sh):
-#   bash tools/build_variant.sh halfnb2 "-DSRMI_HALF_NB=2"
+#   bash tools/build_variant.sh nowt "-DSRMI_TRAIN_WT=0"   (switches: csrc/tuning.hpp)
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; shift
