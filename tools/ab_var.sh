@@ -1,6 +1,6 @@
 #!/bin/bash
 # Interleaved bench A/B of library builds and engine flags on ONE box (training leg only):
-#   bash tools/ab_var.sh "main::" "redl:alt/libsrmi_redl.so:" "fold::--ca-fold"
+#   bash tools/ab_var.sh "main::" "redl:alt/libsrmi_redl.so:" "pass::--ca-pass"
 # each variant = name:library (empty = in-tree):extra bench flags[:VAR=x,VAR2=y env]
 R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R; O=$R/gpurun_out; mkdir -p $O
 REPS=${REPS:-2}
