@@ -29,6 +29,7 @@ namespace srmi {
 
 static unsigned long long* g_debug_stamps = nullptr;
 void conv3x3_set_debug_stamps(unsigned long long* buf) { g_debug_stamps = buf; }
+unsigned long long* conv3x3_debug_stamps() { return g_debug_stamps; }
 
 template <int TW>
 struct ConvSmem {

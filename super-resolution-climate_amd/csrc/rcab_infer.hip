@@ -31,12 +31,28 @@ __device__ __forceinline__ void own_stores_visible() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// diagnostic build (SRMI_STAMPS): the launch's phase stamps after the two conv bodies'
+#ifdef SRMI_STAMPS
+#define ISTAMP(i)                                                                                    \
+  do {                                                                                               \
+    if (c1.stamps && threadIdx.x == 0)                                                               \
+      c1.stamps[(size_t)2 * gridDim.x * 64 + blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memtime();  \
+  } while (0)
+#else
+#define ISTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+
 __global__ void __launch_bounds__(512, 1) rcab_infer_kernel(ConvParams c1, ConvParams c2, CaScale ca) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = blockIdx.x;
   const int nsy = c1.H / kTH;
+  ISTAMP(0);
   conv64_body<48, EPI_RELU_POOL, 8>(c1, nsy, n, smem);  // t and its per-strip sums: the whole image, one run
+  ISTAMP(1);
   own_stores_visible();
+  ISTAMP(2);
   {
     // conv2's filter image into the filter slot (conv1 is done with it): the mean's
     // matvec reads it there, and conv2 computes on it; scratch in the ring
@@ -49,11 +65,15 @@ __global__ void __launch_bounds__(512, 1) rcab_infer_kernel(ConvParams c1, ConvP
       glds16(c2.w + ((size_t)(tap * 64 + row)) * 64 + ch * 8, wbase + (uint32_t)i * 1024u);
     }
     wait_vm<0>();  // the DMA and the scale's operands (its barriers publish the DMA)
+    ISTAMP(3);
     ca_scale_finish<false>(ca, q, n, c1.H, c1.W, reinterpret_cast<float*>(smem + Conv2Smem<48>::WB), smem, true);
   }
+  ISTAMP(4);
   own_stores_visible();  // s in the record, read by conv2's epilogue
+  ISTAMP(5);
   // h' = h + s (conv2(t) + b2); its filter image is resident from the scale phase
   conv64_body<48, EPI_CA_RESID, 8, true>(c2, nsy, n, smem);
+  ISTAMP(6);
 }
 
 int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* part, int nstrips, const float* w1,
@@ -78,7 +98,9 @@ int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* p
   ca.CR = CR;
   ca.rec = rec;
   ConvParams a = c1, b = c2;
-  a.stamps = b.stamps = nullptr;
+  // (diagnostic: [3][N][64] stamps -- conv1's body, conv2's body, the launch's phases)
+  a.stamps = conv3x3_debug_stamps();
+  b.stamps = a.stamps ? a.stamps + (size_t)c1.N * 64 : nullptr;
   a.part = const_cast<float*>(part);  // conv1's per-strip sums of t
   a.part_stride = 64;
   b.yb = nullptr;  // u is never stored

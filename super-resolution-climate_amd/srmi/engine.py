@@ -189,6 +189,21 @@ class Engine:
              stream_handle(stream))
 
 
+def engine_stream(device) -> "torch.cuda.Stream":
+    """The stream of a second (third, ...) micro-batch engine: a HIGH-priority stream.
+
+    HIP maps a process's streams onto GPU_MAX_HW_QUEUES (4) hardware queues per
+    priority, and two streams on one queue run one after the other.  Which normal-
+    priority queue a new stream lands on depends on what the process used before: with
+    an RCCL group up, the second engine's stream shared the default stream's queue and
+    the one-rank DP step lost its two-engine overlap (44.1 vs 26.2 ms/step, every
+    stream-creation offset; tools/dbg_dp.py, tools/dbg_queues.py).  High-priority
+    streams come from a separate pool of queues that neither the default stream
+    (engine 0) nor RCCL's streams use, so the engines never share a queue."""
+    lo, hi = torch.cuda.Stream.priority_range()
+    return torch.cuda.Stream(device=device, priority=hi)
+
+
 # ----------------------------------------------------------------- free ops
 INTERP_MODES = {"bilinear": _lib.SRMI_INTERP_BILINEAR, "bicubic": _lib.SRMI_INTERP_BICUBIC}
 

@@ -32,7 +32,7 @@ import torch
 
 from ._lib import SRMI_LOSS_MEAN, SRMI_LOSS_RMSE, call, ptr, stream_handle
 from .dist import DistInfo
-from .engine import Engine, NetSpec, downsample, interp_size, upsample
+from .engine import Engine, NetSpec, downsample, engine_stream, interp_size, upsample
 
 LOSS_KINDS = {"l2": SRMI_LOSS_RMSE, "charbonnier": SRMI_LOSS_MEAN}
 CHARBONNIER_EPS = 1e-6  # dual_trainer.py:122
@@ -164,7 +164,7 @@ class TiledInference:
         self.eng = self.engs[0]
         for e in self.engs:
             e.pack(params)
-        self.streams = [None] + [torch.cuda.Stream(device=d) for _ in range(self.micro - 1)]
+        self.streams = [None] + [engine_stream(d) for _ in range(self.micro - 1)]
         # fork / join events, created once (also valid inside a graph capture)
         self.ev_fork = torch.cuda.Event()
         self.ev_join = [torch.cuda.Event() for _ in range(self.micro - 1)]

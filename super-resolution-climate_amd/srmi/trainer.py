@@ -27,7 +27,7 @@ from . import checkpoint as ckpt
 from ._lib import SRMI_LOSS_MEAN, SRMI_LOSS_RMSE, TILE_LOSS_SUB, call, ptr
 from .config import check_fused_task, data_downsample_factor, interp_mode
 from .dist import DistInfo, GradReducer, allreduce_sum_
-from .engine import Engine, NetSpec, adam_step, axpy, downsample, interp_size, upsample
+from .engine import Engine, NetSpec, adam_step, axpy, downsample, engine_stream, interp_size, upsample
 
 LOSS_KINDS = {"l2": SRMI_LOSS_RMSE, "charbonnier": SRMI_LOSS_MEAN}
 CHARBONNIER_EPS = 1e-6  # ModelTrainer.eps, sres/controller/dual_trainer.py:122
@@ -153,7 +153,7 @@ class FusedTrainer:
         # gradient scale 1/(count L) -- does not depend on the micro-batch split
         self.lparts = torch.zeros(batch * TILE_LOSS_SUB, dtype=torch.float32, device=self.device)
         self.iparts = torch.zeros(batch * TILE_LOSS_SUB, dtype=torch.float32, device=self.device)
-        self.streams = [None] + [torch.cuda.Stream(device=self.device) for _ in range(micro - 1)]
+        self.streams = [None] + [engine_stream(self.device) for _ in range(micro - 1)]
         self.dp_staged = not dp_reducer_stream
         self.reducer = GradReducer(self.eng.table, spec.arch, spec.nlayers, self.info, self.device,
                                    stream=self.info.enabled and not self.dp_staged)
