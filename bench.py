@@ -118,6 +118,29 @@ def _pmc_infer_traffic(side, flags):
     return None
 
 
+def _pmc_mfma(kernel_prefix, infer_cfg=None):
+    """MFMA busy fraction of a kernel (SQ_VALU_MFMA_BUSY_CYCLES / (median duration x
+    2.4 GHz x 1024 SIMDs): a lower bound, the chip runs at or below 2.4 GHz) and the
+    kernel-trace median duration of the same pass, from the newest committed summary
+    (tools/pmc_mfma_parse.py: profiles/rNN_pmc_mfma.json for training,
+    rNN_pmc_infer_mfma.json for C5 -- the latter only at the same configuration)."""
+    pat = "*pmc_infer_mfma*.json" if infer_cfg is not None else "*pmc_mfma*.json"
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", pat)), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if infer_cfg is not None:
+            cfg = d.get("config") or {}
+            if cfg.get("infer_region") != infer_cfg[0] or cfg.get("flags", 0) != infer_cfg[1]:
+                continue
+        for k, v in d.items():
+            if isinstance(v, dict) and kernel_prefix in k and "mfma_frac_at_max_clock" in v:
+                return {"mfma_frac_at_max_clock": v["mfma_frac_at_max_clock"], "median_us": v.get("median_us"),
+                        "source": os.path.relpath(f, ROOT)}
+    return None
+
+
 def _time_launches(launch, stream, n=50, warm=5):
     for _ in range(warm):
         launch()
@@ -235,6 +258,7 @@ def fused_rooflines(tr, step_ms, reps=20):
             "avg_launch_ms": round(ms1, 4), "bytes_per_launch": bytes_launch, "flop_per_launch": flop_launch,
             "mfma_tflops": round(tf, 1), "mfma_frac": round(tf / PEAK_BF16_TFLOPS, 4),
             "rocprof_check": rc,
+            "mfma_pmc": _pmc_mfma("rcab_bwd_kernel<%d" % (7 if which == 1 else 4)),
             "concurrent": {"launches_per_slot": n_eng, "per_stream_ms": [round(x, 4) for x in per_stream],
                            "achieved": round(ach_slot, 1), "frac": round(ach_slot / HBM_PEAK_GBS, 4),
                            "note": "all micro-batch engines' launches at once, as in the step: bytes of the "
@@ -308,7 +332,14 @@ def infer_rcab_roofline(ti, side, flags, reps=20):
     tot = sum(e.batch for e in ti.engs)
     ach_slot = RCAB_INFER_BYTES_PER_IMAGE * tot / (max(per_stream) * 1e-3) / 1e9
     tr_ = _pmc_infer_traffic(side, flags)
+    mp = _pmc_mfma("rcab_infer_kernel", (side, flags))
+    rc = None
+    if mp and mp.get("median_us"):
+        a = nb / (mp["median_us"] * 1e-6) / 1e9
+        rc = {"median_us": mp["median_us"], "achieved": round(a, 1), "frac": round(a / HBM_PEAK_GBS, 4),
+              "source": mp["source"]}
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "rocprof_check": rc, "mfma_pmc": mp,
             "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": round(tr_["bytes"]) if tr_ else None, "traffic_source": tr_["source"] if tr_ else None,
             "kernel": "srmi::rcab_infer_kernel", "images_per_launch": n, "avg_launch_ms": round(ms1, 4),

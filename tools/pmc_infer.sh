@@ -19,9 +19,11 @@ timeout -s KILL 200 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM
 python3 $R/tools/pmc_parse.py $OUT $R/gpurun_out/pmc_infer.json > /dev/null
 python3 $R/tools/pmc_mfma_parse.py $OUT/MFMA $R/gpurun_out/pmc_infer_mfma.json > /dev/null
 python3 -c "
-import json; p='$R/gpurun_out/pmc_infer.json'; d=json.load(open(p))
-d['config'] = {'infer_region': $SIDE, 'flags': $FLAGS, 'command': 'bench.py --no-train --no-edsr --infer-iters 1 $*'}
-json.dump(d, open(p, 'w'), indent=1)
+import json
+for p in ('$R/gpurun_out/pmc_infer_mfma.json', '$R/gpurun_out/pmc_infer.json'):
+  d=json.load(open(p))
+  d['config'] = {'infer_region': $SIDE, 'flags': $FLAGS, 'command': 'bench.py --no-train --no-edsr --infer-iters 1 $*'}
+  json.dump(d, open(p, 'w'), indent=1)
 for k,v in d.items():
   if isinstance(v,dict) and 'hbm_bytes_per_launch' in v: print(round(v['hbm_bytes_per_launch']/1e6,2),'MB', round(v['fetch_bytes']/1e6,2), round(v['write_bytes']/1e6,2), k[:60])"
 echo pmc_infer done
