@@ -101,6 +101,7 @@ int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* p
   // (diagnostic: [3][N][64] stamps -- conv1's body, conv2's body, the launch's phases)
   a.stamps = conv3x3_debug_stamps();
   b.stamps = a.stamps ? a.stamps + (size_t)c1.N * 64 : nullptr;
+  ca.stamps = a.stamps ? a.stamps + (size_t)3 * c1.N * 64 : nullptr;
   a.part = const_cast<float*>(part);  // conv1's per-strip sums of t
   a.part_stride = 64;
   b.yb = nullptr;  // u is never stored

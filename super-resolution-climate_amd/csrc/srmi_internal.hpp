@@ -43,6 +43,7 @@ struct CaScale {
   const float* bc2;   // conv2's bias [64]
   int CR;
   float* rec;         // out: m | z1 | s per image [N][128 + CR]
+  unsigned long long* stamps;  // diagnostic build only: phase stamps of ca_scale_finish (null)
 };
 
 struct ConvParams {

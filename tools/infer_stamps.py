@@ -36,17 +36,17 @@ def main():
     lr = torch.randn(N, 1, 48, 48, device=d)
     out = eng.forward(params, lr)
     torch.cuda.synchronize()
-    buf = torch.zeros(3 * N * 64, dtype=torch.int64, device=d)
+    buf = torch.zeros(4 * N * 64, dtype=torch.int64, device=d)
     call("srmi_debug_conv_stamps", ptr(buf))
     # one launch of the RCAB (0, 2) of the last forward alone (srmi_engine_probe 3): no
     # other conv launch writes the stamps buffer after it
     call("srmi_engine_probe", eng._h, 3, 1, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     call("srmi_debug_conv_stamps", None)
-    st = buf.view(3, N, 64).cpu().numpy().astype(np.int64)
-    c1, c2, k = st[0], st[1], st[2]
+    st = buf.view(4, N, 64).cpu().numpy().astype(np.int64)
+    c1, c2, k, cs = st[0], st[1], st[2], st[3]
     ok = (k[:, 0] != 0) & (k[:, 6] != 0)
-    c1, c2, k = c1[ok], c2[ok], k[ok]
+    c1, c2, k, cs = c1[ok], c2[ok], k[ok], cs[ok]
     print(f"workgroups with stamps: {ok.sum()} of {N}")
     rt = c1[:, 62:64].astype(np.float64)
     clk = np.median((c1[:, 61] - c1[:, 0]) / np.maximum(rt[:, 1] - rt[:, 0], 1)) * 100.0
@@ -63,6 +63,9 @@ def main():
     row("own_stores_visible #1", k[:, 2] - k[:, 1])
     row("scale loads + conv2 filter DMA", k[:, 3] - k[:, 2])
     row("ca_scale_finish", k[:, 4] - k[:, 3])
+    for i, nm in enumerate(("T partials + border lines", "barrier 1", "S_tap + matvec (LDS filters)", "barrier 2",
+                            "z1 + s (waves 0-3)", "barrier 3")):
+        row("    " + nm, cs[:, i + 1] - cs[:, i])
     row("own_stores_visible #2", k[:, 5] - k[:, 4])
     row("conv2 body", k[:, 6] - k[:, 5])
     row("  conv2 prologue", c2[:, 1] - c2[:, 0])

@@ -1,0 +1,77 @@
+"""Phase timing of the training forward convs (conv1 EPI_RELU_POOL = 8, conv2
+EPI_CA_RESID_U = 10) inside the C2 step, from s_memtime stamps (diagnostic build:
+make stamps -> libsrmi_stamps.so).
+
+The bench's trainer (rcan-10-20-64, B = 64, two micro-batch engines) runs a few steps,
+then one step with the stamps on for ONE epilogue (SRMI_STAMP_EPI); the buffer keeps
+the last such launch of the step.  Per workgroup: prologue (incl. conv2's CA scale,
+whose own sub-phases follow the body's stamps), the run's strips.
+    python tools/train_stamps.py
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "super-resolution-climate_amd"), ROOT]
+os.environ.setdefault("SRMI_LIB", os.path.join(ROOT, "super-resolution-climate_amd", "srmi", "libsrmi_stamps.so"))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from srmi._lib import call, ptr  # noqa: E402
+from srmi.dist import DistInfo  # noqa: E402
+from srmi.engine import NetSpec  # noqa: E402
+from srmi.trainer import FusedTrainer  # noqa: E402
+
+
+def main():
+    d = torch.device("cuda", 0)
+    spec = NetSpec(arch="rcan", nchannels_in=2, nchannels_out=2, nfeatures=64, nlayers=10, nblocks=20,
+                   cbottleneck=2, scale=4)
+    tr = FusedTrainer(spec, 64, (48, 48), lr=1e-4, info=DistInfo(), device=d, seed=0, micro=2)
+    hr = torch.tensor(bench.synthetic_hr(64, 2, 192, 1234)).to(d)
+    for _ in range(3):
+        tr.step(hr)
+    torch.cuda.synchronize()
+    for epi, name in ((8, "conv1 RELU_POOL"), (10, "conv2 CA_RESID_U")):
+        buf = torch.zeros(2 * 4096 * 64, dtype=torch.int64, device=d)
+        os.environ["SRMI_STAMP_EPI"] = str(epi)
+        call("srmi_debug_conv_stamps", ptr(buf))
+        tr.step(hr)
+        torch.cuda.synchronize()
+        call("srmi_debug_conv_stamps", None)
+        flat = buf.view(-1, 64).cpu().numpy().astype(np.int64)
+        nwg = int((flat[:4096, 0] != 0).sum())  # (the scale's stamps follow the body's [grid][64])
+        body, cs = flat[:nwg], flat[nwg:2 * nwg]
+        ok = (body[:, 0] != 0) & (body[:, 61] != 0)
+        body, cs = body[ok], cs[ok]
+        tot = body[:, 61] - body[:, 0]
+        print(f"{name}: {ok.sum()} workgroups, span median {np.median(tot):.0f} cycles")
+
+        def row(nm, v):
+            print(f"  {nm:30s} median {np.median(v):8.0f}  p90 {np.percentile(v, 90):8.0f}  "
+                  f"share {np.median(v) / np.median(tot):6.3f}")
+        row("prologue", body[:, 1] - body[:, 0])
+        if epi == 10:
+            for i, nm in enumerate(("  scale: T + border lines", "  scale: barrier 1", "  scale: S_tap + matvec",
+                                    "  scale: barrier 2", "  scale: z1 + s", "  scale: barrier 3")):
+                row(nm, cs[:, i + 1] - cs[:, i])
+            row("  body start -> scale start", cs[:, 0] - body[:, 0])
+        for j in range(3):
+            base = 2 + 5 * j
+            if not np.all(body[:, base + 4]):
+                break
+            prev = body[:, base - 1] if j else body[:, 1]
+            parts = []
+            for i, nm in enumerate(("issue", "mfma", "gstore", "epi", "barrier")):
+                cur = body[:, base + i]
+                parts.append(f"{nm} {np.median(cur - prev):6.0f}")
+                prev = cur
+            print(f"  strip {j}: " + "  ".join(parts))
+    os.environ.pop("SRMI_STAMP_EPI", None)
+
+
+if __name__ == "__main__":
+    main()
