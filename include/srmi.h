@@ -243,10 +243,11 @@ int srmi_ca_forward(const void* u, const float* part, int nstrips, const float* 
                     const float* b2, int N, int HW, int C, int R, const float* h_in, float* h_out, void* hb_out,
                     float* rec, int dtype, void* stream);
 /* the same CALayer forward on the bf16 engine's residual-stream pair: h = h_in
- * (fp32, when non-NULL) or the pair hi_in (bf16) + lo_in (int8 remainder); out:
- * hi = bf16(h + s*u), lo = rint((h + s*u - hi) * 2^(15 - E(hi))) in [-127, 127]
- * (E = hi's binary exponent; 0 for |hi| < 2^-111, inf, nan), i.e. 16 significant
- * bits (in place allowed: lo_out == lo_in) */
+ * (fp32, when non-NULL) or the pair hi_in (bf16) + lo_in (int8 remainder); out, for
+ * the fp32 bit pattern A of h + s*u: hi = (A + 0x8000) >> 16 (bf16, rounded half away
+ * from zero), lo = byte 1 of A; the pair's value has the bits ((hi << 16) | 0x80) +
+ * (sext8(lo) << 8), i.e. h + s*u to within 128 fp32 steps (16 significant bits) (in
+ * place allowed: lo_out == lo_in) */
 int srmi_ca_forward_pair(const void* u, const float* part, int nstrips, const float* w1, const float* b1,
                          const float* w2, const float* b2, int N, int HW, int C, int R, const float* h_in,
                          const void* hi_in, const void* lo_in, void* hi_out, void* lo_out, float* rec, void* stream);

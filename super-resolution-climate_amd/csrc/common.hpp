@@ -38,63 +38,32 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
 }
 
-// The pair: a value as hi = bf16(h) plus an 8-bit remainder lo in units of 1/256 of
-// hi's ulp -- 16 significant bits in 3 bytes (the bf16 engine's residual stream and
-// its filter-gradient partial slabs).
-// lo8 codec: s = 2^(15 - E) for hi = m * 2^E (1 <= |m| < 2), biased exponent e =
-// E + 127; 2^(E - 15) has biased exponent e - 15.  hi that is zero, subnormal, tiny
-// (e <= 15), inf or nan carries no remainder.
-__device__ __forceinline__ uint32_t lo8_encode(float h, float hi) {
-  const uint32_t e = (__float_as_uint(hi) >> 23) & 0xFFu;
-  const float s = __uint_as_float((269u - e) << 23);
-  float q = rintf((h - hi) * s);
-  q = fminf(fmaxf(q, -127.f), 127.f);
-  return (e > 15u && e < 255u) ? ((uint32_t)(int)q & 0xFFu) : 0u;
-}
-__device__ __forceinline__ float lo8_decode(float hi, uint32_t byte) {
-  const uint32_t e = (__float_as_uint(hi) >> 23) & 0xFFu;
-  const float q = (float)(int)(int8_t)(uint8_t)byte;
-  return (e > 15u && e < 255u) ? fmaf(q, __uint_as_float((e - 15u) << 23), hi) : hi;
-}
-
-// four elements: hi as 4 bf16 (uint2), lo as 4 bytes (uint32, element 0 lowest)
+// The pair: a value as hi = bf16(h) plus an 8-bit remainder lo -- 16 significant bits
+// in 3 bytes (the bf16 engine's residual stream inside a residual group).  In the fp32
+// bit pattern A = (T << 16) + L of h (bit patterns of one sign are monotonic integers):
+//   hi = (A + 0x8000) >> 16      bf16 of h rounded half away from zero (= T + [L >= 2^15])
+//   lo = (A >> 8) & 0xFF         byte 1 of A
+//   A' = ((hi << 16) | 0x80) + (sext8(lo) << 8)  =  A - (L & 0xFF) + 128
+// so the decoded value is h moved by at most 128 fp32 steps of its binade (2^-16
+// relative), centred, across binade boundaries too, and bf16_rne(A') == hi exactly (the
+// decoded low half is never a tie): the next conv1's operand is the stored hi.  Encode
+// and decode are byte permutes, shifts and adds -- no exponent arithmetic (the former
+// ldexp form of the same precision cost 2.4 % in C5: DESIGN.md section 3).
 __device__ __forceinline__ float4 pair_decode4(uint2 hi, uint32_t lo) {
-  return make_float4(lo8_decode(bf2f(hi.x & 0xFFFFu), lo & 0xFFu), lo8_decode(bf2f(hi.x >> 16), (lo >> 8) & 0xFFu),
-                     lo8_decode(bf2f(hi.y & 0xFFFFu), (lo >> 16) & 0xFFu), lo8_decode(bf2f(hi.y >> 16), lo >> 24));
+  const int q0 = (int)(int8_t)(lo & 0xFFu), q1 = (int)(int8_t)((lo >> 8) & 0xFFu);
+  const int q2 = (int)(int8_t)((lo >> 16) & 0xFFu), q3 = (int)(int8_t)(lo >> 24);
+  return make_float4(__uint_as_float(((hi.x << 16) | 0x80u) + (uint32_t)(q0 << 8)),
+                     __uint_as_float(((hi.x & 0xFFFF0000u) | 0x80u) + (uint32_t)(q1 << 8)),
+                     __uint_as_float(((hi.y << 16) | 0x80u) + (uint32_t)(q2 << 8)),
+                     __uint_as_float(((hi.y & 0xFFFF0000u) | 0x80u) + (uint32_t)(q3 << 8)));
 }
 __device__ __forceinline__ uint32_t pair_encode4(float a, float b, float c, float d, uint2& hi) {
-  hi = make_uint2(pack2(a, b), pack2(c, d));
-  return lo8_encode(a, bf2f(hi.x & 0xFFFFu)) | (lo8_encode(b, bf2f(hi.x >> 16)) << 8) |
-         (lo8_encode(c, bf2f(hi.y & 0xFFFFu)) << 16) | (lo8_encode(d, bf2f(hi.y >> 16)) << 24);
-}
-
-// The pair codec in fewer VALU operations, for the one-launch inference RCAB (its
-// pairs are written and read only by its own conv2 epilogue): the same quantisation
-// for normal hi (the power-of-two scaling by ldexp is exact, like the multiply by
-// 2^(15 - E) above), without the range guards -- a zero / tiny / non-finite hi then
-// carries a remainder that is negligible (zero / tiny hi) or absorbed (inf, nan).
-// In a conv epilogue the codec, not the memory traffic, bounds the pass.
-__device__ __forceinline__ uint32_t lo8_encode_fast(float h, float hi) {
-  const int e = (int)((__float_as_uint(hi) >> 23) & 0xFFu);
-  const float x = fminf(fmaxf(__builtin_ldexpf(h - hi, 142 - e), -127.f), 127.f);
-  // + 1.5 * 2^23 rounds x to the nearest integer (ties to even, as rintf) into the low
-  // mantissa bits: their low byte is that integer's two's-complement byte
-  return __float_as_uint(x + 12582912.0f) & 0xFFu;
-}
-__device__ __forceinline__ float lo8_decode_fast(float hi, uint32_t byte) {
-  const int e = (int)((__float_as_uint(hi) >> 23) & 0xFFu);
-  return hi + __builtin_ldexpf((float)(int)(int8_t)(uint8_t)byte, e - 142);
-}
-__device__ __forceinline__ float4 pair_decode4_fast(uint2 hi, uint32_t lo) {
-  return make_float4(lo8_decode_fast(bf2f(hi.x & 0xFFFFu), lo & 0xFFu),
-                     lo8_decode_fast(bf2f(hi.x >> 16), (lo >> 8) & 0xFFu),
-                     lo8_decode_fast(bf2f(hi.y & 0xFFFFu), (lo >> 16) & 0xFFu),
-                     lo8_decode_fast(bf2f(hi.y >> 16), lo >> 24));
-}
-__device__ __forceinline__ uint32_t pair_encode4_fast(float a, float b, float c, float d, uint2& hi) {
-  hi = make_uint2(pack2(a, b), pack2(c, d));
-  return lo8_encode_fast(a, bf2f(hi.x & 0xFFFFu)) | (lo8_encode_fast(b, bf2f(hi.x >> 16)) << 8) |
-         (lo8_encode_fast(c, bf2f(hi.y & 0xFFFFu)) << 16) | (lo8_encode_fast(d, bf2f(hi.y >> 16)) << 24);
+  const uint32_t A = __float_as_uint(a), B = __float_as_uint(b), C = __float_as_uint(c), D = __float_as_uint(d);
+  hi = make_uint2(__builtin_amdgcn_perm(B + 0x8000u, A + 0x8000u, 0x07060302u),
+                  __builtin_amdgcn_perm(D + 0x8000u, C + 0x8000u, 0x07060302u));
+  // byte 1 of each: [A.1, B.1] and [C.1, D.1] in the low halves, then the two halves
+  const uint32_t ab = __builtin_amdgcn_perm(B, A, 0x0C0C0501u), cd = __builtin_amdgcn_perm(D, C, 0x0C0C0501u);
+  return ab | (cd << 16);
 }
 
 // Write-through (sc1) 16-byte stores.  A kernel's end-of-launch release writes

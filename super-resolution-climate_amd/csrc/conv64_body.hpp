@@ -6,10 +6,6 @@
 
 #include "ca_scale.hpp"
 
-// the pair codec of the CA_RESID / CA_RESID_U epilogues: the fast form (common.hpp; the
-// same quantisation as ca_fwd's reference form for every normal hi, in fewer VALU ops)
-#define PAIR_DEC4 pair_decode4_fast
-#define PAIR_ENC4 pair_encode4_fast
 #include "common.hpp"
 #include "srmi_internal.hpp"
 
@@ -275,7 +271,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             const int q = h * (kShared ? RUNS / 2 : RUNS) + j;
             float4 hh = e.r1[q / NCT][q % NCT];
             if (p.r1h)
-              hh = PAIR_DEC4(make_uint2(__float_as_uint(hh.x), __float_as_uint(hh.y)), __float_as_uint(hh.z));
+              hh = pair_decode4(make_uint2(__float_as_uint(hh.x), __float_as_uint(hh.y)), __float_as_uint(hh.z));
             const uint32_t oe = (uint32_t)((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4);  // element
             if constexpr (EPI == EPI_CA_RESID_U) {  // u to bf16 (backward reads it), the product of bf16(u)
               const uint2 ub = make_uint2(pack2(val.x, val.y), pack2(val.z, val.w));
@@ -285,7 +281,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             const float o0 = fmaf(val.x, fs.x, hh.x), o1 = fmaf(val.y, fs.y, hh.y);
             const float o2 = fmaf(val.z, fs.z, hh.z), o3 = fmaf(val.w, fs.w, hh.w);
             uint2 hi;
-            const uint32_t lo = PAIR_ENC4(o0, o1, o2, o3, hi);
+            const uint32_t lo = pair_encode4(o0, o1, o2, o3, hi);
             st_wt8(rph, p.yph, oe * 2, hi);
             st_wt4(rpl, p.ypl, oe, lo);
             continue;
@@ -899,7 +895,7 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
       if (p.r1h) {
         const uint4 th = ops.t[pt];
         const uint2 tl = ops.u[pt][0];
-        const float4 a = PAIR_DEC4(make_uint2(th.x, th.y), tl.x), b = PAIR_DEC4(make_uint2(th.z, th.w), tl.y);
+        const float4 a = pair_decode4(make_uint2(th.x, th.y), tl.x), b = pair_decode4(make_uint2(th.z, th.w), tl.y);
         hv[0] = a.x; hv[1] = a.y; hv[2] = a.z; hv[3] = a.w; hv[4] = b.x; hv[5] = b.y; hv[6] = b.z; hv[7] = b.w;
       } else {
         const float4 a = ops.g[pt][0], b = ops.g[pt][1];
@@ -914,8 +910,8 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
         for (int rr = 0; rr < 4; ++rr) o[4 * c + rr] = fmaf(v[rr] + b[rr], sv[4 * c + rr], hv[4 * c + rr]);
       }
       uint2 h0, h1;
-      const uint32_t l0 = PAIR_ENC4(o[0], o[1], o[2], o[3], h0);
-      const uint32_t l1 = PAIR_ENC4(o[4], o[5], o[6], o[7], h1);
+      const uint32_t l0 = pair_encode4(o[0], o[1], o[2], o[3], h0);
+      const uint32_t l1 = pair_encode4(o[4], o[5], o[6], o[7], h1);
       const uint32_t oe = (uint32_t)(pix * p.Cout + cb * 64 + chan(0, 0));
       st_wt16(rph, p.yph, oe * 2, make_uint4(h0.x, h0.y, h1.x, h1.y));
       st_wt8(rpl, p.ypl, oe, make_uint2(l0, l1));

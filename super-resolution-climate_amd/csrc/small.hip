@@ -1131,18 +1131,14 @@ constexpr int kCaVec = SRMI_CA_VEC;
 //   CA_F32   fp32 h in, fp32 h + operand-type copy out (the exact-fp32 engine mode)
 //   CA_F32LO fp32 h in (the group input), h out as a pair hi + lo
 //   CA_LO    pair in and out
-// The pair: hi = bf16(h) -- the next conv's operand, stored anyway -- and an 8-bit
-// remainder lo = rint((h - hi) * 256 / ulp(hi)) (ulp of hi's binade, |h - hi| <=
-// ulp / 2, so |lo| <= 128, clamped to 127), so hi + lo * ulp / 256 keeps h to 16
-// significant bits (8 of hi + 8 of lo; the bf16 operands the convs see carry 8)
-// while the pass moves 8 B per element (u 2 + hi 2 + lo 1 in, hi 2 + lo 1 out)
-// instead of 12 with an fp32 stream (10 with a bf16 lo).
+// The pair (common.hpp pair_encode4 / pair_decode4): hi = bf16(h) -- the next conv's
+// operand, stored anyway -- and an 8-bit remainder lo, h to 16 significant bits, while
+// the pass moves 8 B per element (u 2 + hi 2 + lo 1 in, hi 2 + lo 1 out) instead of 12
+// with an fp32 stream.
 enum CaMode { CA_F32 = 0, CA_F32LO = 1, CA_LO = 2 };
-// the training pass's codec: the reference form (1: the fast form of common.hpp)
 #define CA_DEC4 pair_decode4
 #define CA_ENC4 pair_encode4
 
-// (lo8_encode / lo8_decode, the pair codec: common.hpp)
 template <typename T, int MODE>
 __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, const float* __restrict__ part,
                                                      int nstrips, int HW, const float* __restrict__ w1,

@@ -16,8 +16,8 @@ run as unfold + rocBLAS GEMM) and no reduced-precision math.
   statistics of the bf16 t and conv2's bf16 filters, csrc/ca_scale.hpp -- the same
   quantity up to fp32 summation order): out = bf16(u) * s(mean(u));
 * the residual stream INSIDE a residual group is the pair hi + lo (bf16 hi plus an
-  8-bit remainder in units of ulp(hi) / 256, common.hpp lo8 codec): 16 significant
-  bits, rounded after every CA add (h = pair16(h + out)); the group input, the
+  8-bit remainder, common.hpp pair codec): 16 significant bits, rounded after every
+  CA add (h = pair16(h + out)); the group input, the
   group-tail / body-tail outputs and the whole gradient stream stay fp32.
 Rounding is straight-through in backward, as in the engine (the stored values are
 what backward reads; the gradient of an add is the identity).  The model's drift
@@ -78,20 +78,18 @@ class _StraightBf16(torch.autograd.Function):
 
 
 def pair16(h: torch.Tensor) -> torch.Tensor:
-    """The lo8 pair codec (csrc/common.hpp lo8_encode / lo8_decode): hi = bf16(h)
-    (round to nearest even), q = rint((h - hi) * 2^(15 - E)) clamped to +-127 for
-    hi = m 2^E (1 <= |m| < 2), value = hi + q 2^(E - 15); hi zero, subnormal, tiny
-    (biased exponent <= 15), inf or nan carries no remainder."""
+    """The pair codec (csrc/common.hpp pair_encode4 / pair_decode4) on fp32 bit
+    patterns A: hi = (A + 0x8000) >> 16, lo = byte 1 of A, value bits
+    ((hi << 16) | 0x80) + (sext8(lo) << 8) = A - (A & 0xFF) + 128: h to within 128 fp32
+    steps of its binade, and bf16(value) == hi (round to nearest even never ties)."""
     hf = h.float()
-    hi = hf.to(torch.bfloat16).float()
-    bits = hi.view(torch.int32)
-    e = (bits >> 23) & 0xFF
-    ok = (e > 15) & (e < 255)
-    scale = torch.ldexp(torch.ones_like(hi), (142 - e).clamp(-126, 127))  # 2^(15 - E), E = e - 127
-    q = torch.round((hf - hi) * scale).clamp(-127.0, 127.0)
-    unit = torch.ldexp(torch.ones_like(hi), (e - 142).clamp(-149, 127))    # 2^(E - 15)
-    val = torch.where(ok, hi + q * unit, hi)
-    return val.to(h.dtype)
+    a = hf.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    hi = ((a + 0x8000) >> 16) & 0xFFFF
+    q = (a >> 8) & 0xFF
+    q = torch.where(q >= 128, q - 256, q)
+    bits = (((hi << 16) | 0x80) + (q << 8)) & 0xFFFFFFFF
+    bits = torch.where(bits >= 2 ** 31, bits - 2 ** 32, bits).to(torch.int32)
+    return bits.view(torch.float32).to(h.dtype)
 
 
 class _StraightPair16(torch.autograd.Function):

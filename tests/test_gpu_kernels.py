@@ -314,13 +314,13 @@ def test_channel_attention_fwd_bwd(dt):
 
 
 def lo8_decode(hi: torch.Tensor, lo: torch.Tensor) -> torch.Tensor:
-    """The residual pair's value hi + lo * 2^(E - 15) (E = hi's binary exponent;
-    no remainder for |hi| < 2^-111, inf, nan) -- include/srmi.h srmi_ca_forward_pair."""
-    h = hi.double().cpu()
-    q = lo.cpu().view(torch.int8).double()
-    e = torch.frexp(h.float())[1].double() - 1  # hi = m * 2^e, 1 <= |m| < 2
-    ok = torch.isfinite(h) & (h.abs() >= 2.0 ** -111)
-    return torch.where(ok, h + q * torch.pow(2.0, e - 15), h)
+    """The residual pair's value (csrc/common.hpp pair_decode4, include/srmi.h
+    srmi_ca_forward_pair): fp32 bits ((hi << 16) | 0x80) + (sext8(lo) << 8)."""
+    hb = hi.cpu().view(torch.int16).to(torch.int64) & 0xFFFF
+    q = lo.cpu().view(torch.int8).to(torch.int64)
+    bits = (((hb << 16) | 0x80) + (q << 8)) & 0xFFFFFFFF
+    bits = torch.where(bits >= 2 ** 31, bits - 2 ** 32, bits).to(torch.int32)
+    return bits.view(torch.float32).double()
 
 
 def test_channel_attention_forward_residual_pair():
@@ -354,8 +354,8 @@ def test_channel_attention_forward_residual_pair():
         s = torch.sigmoid(torch.relu(m @ w1.double().cpu().T + b1.double().cpu()) @ w2.double().cpu().T + b2.double().cpu())
         h_ref = h_ref + u.double().cpu() * s[:, None, None, :]
         got = lo8_decode(hi[step % 2], lo)
-        # lo resolves 1/256 of hi's ulp: the pair's rounding error is 2^-16 of each
-        # element (the fp32 arithmetic of the adds is in the same range)
+        # the pair keeps h to within 128 fp32 steps of its binade: a rounding error of
+        # 2^-16 of each element (the fp32 arithmetic of the adds is in the same range)
         assert rel_l2(got, h_ref) < 2 ** -16
         assert float((got - h_ref).abs().max()) <= 2 ** -14 * float(h_ref.abs().max())
         # hi is within half a bf16 ulp (plus lo's rounding) of h: the conv operand
