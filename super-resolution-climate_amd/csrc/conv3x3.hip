@@ -33,7 +33,7 @@ static unsigned long long* g_debug_stamps = nullptr;
 void conv3x3_set_debug_stamps(unsigned long long* buf) { g_debug_stamps = buf; }
 unsigned long long* conv3x3_debug_stamps() { return g_debug_stamps; }
 // diagnostic build: SRMI_STAMP_EPI=<epilogue> stamps only that epilogue's launches
-static unsigned long long* stamps_for(int epi) {
+unsigned long long* conv3x3_stamps_for(int epi) {
 #ifdef SRMI_STAMPS
   const char* only = std::getenv("SRMI_STAMP_EPI");
   if (only && std::atoi(only) != epi) return nullptr;
@@ -347,7 +347,7 @@ static int launch_tw(const ConvParams& p, hipStream_t st) {
     const int run_len = conv64_run_len(p, TW, p.cu_budget > 0 ? p.cu_budget : 256);
     dim3 grid(conv64_blocks(p, TW, run_len));
     ConvParams q = p;
-    q.stamps = stamps_for(EPI);
+    q.stamps = conv3x3_stamps_for(EPI);
     // 8 waves (two per SIMD, a wave per row and channel half) at TW = 48
     constexpr int NW = TW == 48 ? 8 : 4;
     hipLaunchKernelGGL((conv64_kernel<TW, EPI, NW>), grid, dim3(NW * 64), Conv2Smem<TW>::TOTAL, st, q, run_len);
@@ -368,7 +368,7 @@ static int launch_v2_only(const ConvParams& p, hipStream_t st) {
     return SRMI_ERR_SHAPE;
   const int run_len = conv64_run_len(p, 48, p.cu_budget > 0 ? p.cu_budget : 256);
   ConvParams q = p;
-  q.stamps = stamps_for(EPI);
+  q.stamps = conv3x3_stamps_for(EPI);
   size_t lds = Conv2Smem<48>::TOTAL;
   // (diagnostic: the scale's phase stamps after the body's, [grid][64] each)
   if (q.stamps && EPI == EPI_CA_RESID_U) q.cas.stamps = q.stamps + (size_t)conv64_blocks(p, 48, run_len) * 64;

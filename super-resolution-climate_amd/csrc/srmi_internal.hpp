@@ -81,6 +81,7 @@ struct ConvParams {
 
 void conv3x3_set_debug_stamps(unsigned long long* buf);
 unsigned long long* conv3x3_debug_stamps();  // (null unless a diagnostic run set it)
+unsigned long long* conv3x3_stamps_for(int epi);  // (diagnostic build: SRMI_STAMP_EPI selects one epilogue)
 int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st);  // dispatches p.f32
 int conv3x3_f32_launch(const ConvParams& p, int epi, hipStream_t st);
 int conv3x3_nstrips(int H, int W);

@@ -627,7 +627,7 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
   const int nwg = wp.N * wp.row_splits * (wp.Cout / 64);
   const int lds = Conv2Smem<48>::TOTAL > v4::LDS ? Conv2Smem<48>::TOTAL : v4::LDS;
   ConvParams c = cp;
-  c.stamps = nullptr;
+  c.stamps = conv3x3_stamps_for(epi);  // (null in production; the dgrad runs' phase stamps in diagnostic builds)
   WgradParams w = wp;
   w.stamps = nullptr;
   const dim3 grid(nconv + nwg);

@@ -35,7 +35,8 @@ def main():
     for _ in range(3):
         tr.step(hr)
     torch.cuda.synchronize()
-    for epi, name in ((8, "conv1 RELU_POOL"), (10, "conv2 CA_RESID_U")):
+    for epi, name in ((8, "conv1 RELU_POOL"), (10, "conv2 CA_RESID_U"), (7, "F1 dgrad runs (DG_ACC_CA)"),
+                      (4, "F2 dgrad runs (DG_RELUMASK, deferred)")):
         buf = torch.zeros(2 * 4096 * 64, dtype=torch.int64, device=d)
         os.environ["SRMI_STAMP_EPI"] = str(epi)
         call("srmi_debug_conv_stamps", ptr(buf))
@@ -43,8 +44,18 @@ def main():
         torch.cuda.synchronize()
         call("srmi_debug_conv_stamps", None)
         flat = buf.view(-1, 64).cpu().numpy().astype(np.int64)
-        nwg = int((flat[:4096, 0] != 0).sum())  # (the scale's stamps follow the body's [grid][64])
-        body, cs = flat[:nwg], flat[nwg:2 * nwg]
+        if epi in (4, 7):  # fused launch: the dgrad runs' blocks among the filter-gradient ones
+            body = flat[:4096][flat[:4096, 0] != 0]
+            nst = np.array([sum(1 for j in range(11) if r[2 + 5 * j + 4] != 0) for r in body])
+            if epi == 7 and (nst == 1).any() and (nst > 1).any():
+                t = body[nst == 1]
+                print(f"  (F1 tail strips run by the filter-gradient workgroups: {len(t)}, span median "
+                      f"{np.median(t[:, 61] - t[:, 0]):.0f}, prologue {np.median(t[:, 1] - t[:, 0]):.0f})")
+                body = body[nst == nst.max()]
+            cs = body
+        else:
+            nwg = int((flat[:4096, 0] != 0).sum())  # (the scale's stamps follow the body's [grid][64])
+            body, cs = flat[:nwg], flat[nwg:2 * nwg]
         ok = (body[:, 0] != 0) & (body[:, 61] != 0)
         body, cs = body[ok], cs[ok]
         tot = body[:, 61] - body[:, 0]
@@ -59,7 +70,7 @@ def main():
                                     "  scale: barrier 2", "  scale: z1 + s", "  scale: barrier 3")):
                 row(nm, cs[:, i + 1] - cs[:, i])
             row("  body start -> scale start", cs[:, 0] - body[:, 0])
-        for j in range(3):
+        for j in range(6):
             base = 2 + 5 * j
             if not np.all(body[:, base + 4]):
                 break
