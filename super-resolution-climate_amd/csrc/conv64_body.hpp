@@ -476,13 +476,12 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   STAMP(0);
 
   const bf16_t* xn = p.x + (size_t)n * p.H * p.W * 64;
-  // the training conv2 (EPI_CA_RESID_U, cas_on): its image's CA scale in the prologue;
-  // the scale's global operands are issued first, to land under the DMA wait
+  // the training conv2 (EPI_CA_RESID_U, cas_on): its image's CA scale, computed after
+  // the first strip's MFMAs (only that strip's epilogue needs it): its global operands
+  // (t's border lines from other workgroups' conv1 output) are issued after the
+  // prologue's wait and land under those MFMAs
   [[maybe_unused]] CaScalePre cq;
-  if constexpr (EPI == EPI_CA_RESID_U) {
-    static_assert(NW == 8, "the CA scale needs 512 threads");
-    if (p.cas_on) ca_scale_load(p.cas, n, p.H, p.W, cq);
-  }
+  static_assert(EPI != EPI_CA_RESID_U || NW == 8, "the CA scale needs 512 threads");
 
   // LDS-DMA of one 4-row input group into its ring slot: one wave instruction per
   // 8 pixels (1 KiB), swizzle applied on the source side, halo lanes read the zero
@@ -563,13 +562,12 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   }
   __syncthreads();
   if constexpr (EPI == EPI_CA_RESID_U) {
-    if (p.cas_on) {  // (the barrier above published every wave's filter DMA)
-      // scratch beyond the body's LDS (the launch adds kCaScaleFloats floats); the first
-      // workgroup of the image writes its record m | z1 | s for backward
-      float* sm = reinterpret_cast<float*>(smem + S::TOTAL);
-      ca_scale_finish<false>(p.cas, cq, n, p.H, p.W, sm, wl, ry == 0 && sx == 0 && cb == 0 && !tail_part);
-      fs = *reinterpret_cast<const float4*>(sm + kCaScaleS + 4 * (lane & 15));
-    }
+    if (p.cas_on) ca_scale_load_t(p.cas, n, p.H, p.W, cq);
+#ifdef SRMI_TLAT  // diagnostic: the latency of the scale's t operands alone (scale stamps 8, 9)
+    if (p.cas.stamps && tid == 0) p.cas.stamps[blockIdx.x * 64 + 8] = __builtin_amdgcn_s_memtime();
+    wait_vm<0>();
+    if (p.cas.stamps && tid == 0) p.cas.stamps[blockIdx.x * 64 + 9] = __builtin_amdgcn_s_memtime();
+#endif
   }
 
 #pragma unroll 1
@@ -648,6 +646,16 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     // the end of the strip then publishes group k+2 to every wave)
     wait_vm<0>();
     STAMP(sj + 1);
+    if constexpr (EPI == EPI_CA_RESID_U) {
+      if (p.cas_on && k == k0) {  // the image's scale (every wave: uniform), before the first epilogue
+        // scratch beyond the body's LDS (the launch adds kCaScaleFloats floats); the first
+        // workgroup of the image writes its record m | z1 | s for backward
+        ca_scale_load_params(p.cas, cq);  // (L2-resident; consumed after the finish's first barriers)
+        float* sm = reinterpret_cast<float*>(smem + S::TOTAL);
+        ca_scale_finish<false>(p.cas, cq, n, p.H, p.W, sm, wl, ry == 0 && sx == 0 && cb == 0 && !tail_part);
+        fs = *reinterpret_cast<const float4*>(sm + kCaScaleS + 4 * (lane & 15));
+      }
+    }
     STAMP(sj + 2);
     // every wave is past its last read of input group k: its ring slot stages the
     // strip's bf16 output rows (slot k%3 is next written by group k+3's DMA,

@@ -54,8 +54,13 @@ def main():
                 body = body[nst == nst.max()]
             cs = body
         else:
-            nwg = int((flat[:4096, 0] != 0).sum())  # (the scale's stamps follow the body's [grid][64])
+            # the scale's stamps follow the body's [grid][64] (grid: the last row with a
+            # run-end stamp, the scale's rows hold stamps 0..6 only)
+            nwg = int(np.nonzero(flat[:, 61])[0][-1]) + 1
             body, cs = flat[:nwg], flat[nwg:2 * nwg]
+            if os.environ.get("TS_DEBUG"):
+                nz = np.nonzero(flat[:, 0])[0]
+                print("  (nonzero stamp rows:", nz[:4], "...", nz[-4:], len(nz), "of", len(flat), ")")
         ok = (body[:, 0] != 0) & (body[:, 61] != 0)
         body, cs = body[ok], cs[ok]
         tot = body[:, 61] - body[:, 0]
@@ -70,6 +75,9 @@ def main():
                                     "  scale: barrier 2", "  scale: z1 + s", "  scale: barrier 3")):
                 row(nm, cs[:, i + 1] - cs[:, i])
             row("  body start -> scale start", cs[:, 0] - body[:, 0])
+            if np.all(cs[:, 9]):  # (diagnostic build SRMI_TLAT: the t operands' latency alone)
+                row("  t loads: barrier + issue", cs[:, 8] - body[:, 1])
+                row("  t loads: latency", cs[:, 9] - cs[:, 8])
         for j in range(6):
             base = 2 + 5 * j
             if not np.all(body[:, base + 4]):
