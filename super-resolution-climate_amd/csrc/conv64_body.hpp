@@ -221,6 +221,10 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
           ps1[c][3] += v[3] * bf2f(uu.y >> 16);
         }
       }
+      if constexpr (EPI == EPI_CA_RESID_U) {  // u in bf16: stored for backward, and the product's operand
+        bv[pt][c] = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        continue;
+      }
       if constexpr (kRun) {
         fv[pt][c] = make_float4(v[0], v[1], v[2], v[3]);  // dx; g is added in the store loop
         continue;  // no bf16 copy
@@ -237,6 +241,48 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
     }
   }
   const int lane = tid & 63;
+  // the training conv2 (EPI_CA_RESID_U): u is rounded to bf16 before anything reads it,
+  // so the row is staged once as bf16 (128 B per pixel, chunk-swizzled: one barrier, not
+  // the fp32 path's two halves and four) and read back in the pair's run layout
+  if constexpr (EPI == EPI_CA_RESID_U) {
+    constexpr int HALF = NPT * 8, RUNS = HALF / 4;
+    static_assert(kShared, "the 8-wave body");
+#pragma unroll
+    for (int pt = 0; pt < NPT; ++pt)
+#pragma unroll
+      for (int c = 0; c < NCT; ++c) {
+        const int px = pt * 16 + fr, c16 = (ct0 + c) * 2 + (fk >> 1);
+        *reinterpret_cast<uint2*>(stage + px * 128 + ((c16 ^ (px & 7)) << 4) + (fk & 1) * 8) = bv[pt][c];
+      }
+    stage_sync();
+    const auto rbb = wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
+    const auto rph = wt_rsrc(p.yph, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
+    const auto rpl = wt_rsrc(p.ypl, (uint32_t)((size_t)p.N * HW * p.Cout));
+    const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < RUNS / 2; ++j) {
+        // run i of the half: pixels 4 (i & ..) -- lane = channels 4c..4c+3 of pixel px
+        const int i = 2 * j + half_id;
+        const int lin = i * 1024 + lane * 16, px = h * HALF + (lin >> 8), c = (lin >> 4) & 15;
+        const uint2 ub = *reinterpret_cast<const uint2*>(stage + px * 128 + (((c >> 1) ^ (px & 7)) << 4) + (c & 1) * 8);
+        const int q = h * (RUNS / 2) + j;
+        float4 hh = e.r1[q / NCT][q % NCT];
+        if (p.r1h) hh = pair_decode4(make_uint2(__float_as_uint(hh.x), __float_as_uint(hh.y)), __float_as_uint(hh.z));
+        const uint32_t oe = (uint32_t)((pix0 + px) * p.Cout + cb * 64 + c * 4);  // element
+        st_wt8(rbb, p.yb, oe * 2, ub);
+        const float o0 = fmaf(bf2f(ub.x & 0xFFFFu), fs.x, hh.x), o1 = fmaf(bf2f(ub.x >> 16), fs.y, hh.y);
+        const float o2 = fmaf(bf2f(ub.y & 0xFFFFu), fs.z, hh.z), o3 = fmaf(bf2f(ub.y >> 16), fs.w, hh.w);
+        uint2 hi;
+        const uint32_t lo = pair_encode4(o0, o1, o2, o3, hi);
+        st_wt8(rph, p.yph, oe * 2, hi);
+        st_wt4(rpl, p.ypl, oe, lo);
+      }
+    // (no closing barrier: the body's barrier after the epilogue orders the staging
+    //  slot's reuse by group k+3's DMA)
+    return;
+  }
   // fp32 output: staged in LDS in two halves of the row (256 B per pixel,
   // chunk-swizzled) and written back as 1 KiB contiguous runs (full lines)
   if constexpr (kF) {
@@ -266,18 +312,13 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
           const int i = kShared ? 2 * j + half_id : j;
           const int lin = i * 1024 + lane * 16, lpx = lin >> 8, c = (lin >> 4) & 15;
           float4 val = *reinterpret_cast<const float4*>(stage + lpx * 256 + ((c ^ (lpx & 15)) << 4));
-          if constexpr (epi_cr<EPI>()) {
+          if constexpr (epi_cr<EPI>()) {  // (EPI_CA_RESID: the inference conv2, fp32 u)
             // h' = h + s u in the run layout (the lane's channels 4c..4c+3: s in fs), out as the pair
             const int q = h * (kShared ? RUNS / 2 : RUNS) + j;
             float4 hh = e.r1[q / NCT][q % NCT];
             if (p.r1h)
               hh = pair_decode4(make_uint2(__float_as_uint(hh.x), __float_as_uint(hh.y)), __float_as_uint(hh.z));
             const uint32_t oe = (uint32_t)((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4);  // element
-            if constexpr (EPI == EPI_CA_RESID_U) {  // u to bf16 (backward reads it), the product of bf16(u)
-              const uint2 ub = make_uint2(pack2(val.x, val.y), pack2(val.z, val.w));
-              st_wt8(rbb, p.yb, oe * 2, ub);
-              val = make_float4(bf2f(ub.x & 0xFFFFu), bf2f(ub.x >> 16), bf2f(ub.y & 0xFFFFu), bf2f(ub.y >> 16));
-            }
             const float o0 = fmaf(val.x, fs.x, hh.x), o1 = fmaf(val.y, fs.y, hh.y);
             const float o2 = fmaf(val.z, fs.z, hh.z), o3 = fmaf(val.w, fs.w, hh.w);
             uint2 hi;

@@ -37,7 +37,7 @@
 #endif
 
 // Training CA forward (engine.cpp ca_fwd_mode): 1 = inside conv2's launch (the scale in
-// every conv2 workgroup's prologue, +1.1 % over the CA pass), 0 = the CA pass of its own.
+// every conv2 workgroup, after its first strip's MFMAs), 0 = the CA pass of its own.
 #ifndef SRMI_CA_FWD
 #define SRMI_CA_FWD 1
 #endif
