@@ -517,12 +517,13 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   STAMP(0);
 
   const bf16_t* xn = p.x + (size_t)n * p.H * p.W * 64;
-  // the training conv2 (EPI_CA_RESID_U, cas_on): its image's CA scale, computed after
+  // conv2 with its CA scale (cas_on: the training EPI_CA_RESID_U, the inference RCAB's
+  // EPI_CA_RESID): its image's CA scale, computed after
   // the first strip's MFMAs (only that strip's epilogue needs it): its global operands
   // (t's border lines from other workgroups' conv1 output) are issued after the
   // prologue's wait and land under those MFMAs
   [[maybe_unused]] CaScalePre cq;
-  static_assert(EPI != EPI_CA_RESID_U || NW == 8, "the CA scale needs 512 threads");
+  constexpr bool kCas = epi_cr<EPI>() && NW == 8;  // (the scale needs 512 threads)
 
   // LDS-DMA of one 4-row input group into its ring slot: one wave instruction per
   // 8 pixels (1 KiB), swizzle applied on the source side, halo lanes read the zero
@@ -596,13 +597,11 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     for (int c = 0; c < NCT; ++c) aoff[kk][c] = swz128((ct0 + c) * 16 + fr, kk * 4 + fk);
   // CA_RESID(_U): s for the lane's 4 run-layout channels (conv_epilogue2)
   float4 fs = float4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (EPI == EPI_CA_RESID)
-    fs = *reinterpret_cast<const float4*>(p.escale + (size_t)n * p.escale_stride + 4 * (lane & 15));
-  if constexpr (EPI == EPI_CA_RESID_U) {
-    if (!p.cas_on) fs = *reinterpret_cast<const float4*>(p.escale + (size_t)n * p.escale_stride + 4 * (lane & 15));
+  if constexpr (epi_cr<EPI>()) {
+    if (!kCas || !p.cas_on) fs = *reinterpret_cast<const float4*>(p.escale + (size_t)n * p.escale_stride + 4 * (lane & 15));
   }
   __syncthreads();
-  if constexpr (EPI == EPI_CA_RESID_U) {
+  if constexpr (kCas) {
     if (p.cas_on) ca_scale_load_t(p.cas, n, p.H, p.W, cq);
 #ifdef SRMI_TLAT  // diagnostic: the latency of the scale's t operands alone (scale stamps 8, 9)
     if (p.cas.stamps && tid == 0) p.cas.stamps[blockIdx.x * 64 + 8] = __builtin_amdgcn_s_memtime();
@@ -687,7 +686,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     // the end of the strip then publishes group k+2 to every wave)
     wait_vm<0>();
     STAMP(sj + 1);
-    if constexpr (EPI == EPI_CA_RESID_U) {
+    if constexpr (kCas) {
       if (p.cas_on && k == k0) {  // the image's scale (every wave: uniform), before the first epilogue
         // scratch beyond the body's LDS (the launch adds kCaScaleFloats floats); the first
         // workgroup of the image writes its record m | z1 | s for backward

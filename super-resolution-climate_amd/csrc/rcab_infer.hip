@@ -5,10 +5,10 @@
 // CA pool needs only mean(u), which follows from t's statistics (ca_scale.hpp), so s is
 // known before conv2 runs:
 //   phase A  t = relu(conv1(h) + b1), + per-strip channel sums of the bf16 t   conv64_body<RELU_POOL>
-//   phase S  border rows / columns / corners of t, S_tap, mean(u) with conv2's bf16
-//            filter image (loaded here and kept for phase B), the CA MLP -> s  ca_scale_finish
-//   phase B  h' = h + s (conv2(t) + b2) in conv2's epilogue, on the resident filters
-//                                                                             conv64_body<CA_RESID>
+//   phase B  h' = h + s (conv2(t) + b2) in conv2's epilogue                    conv64_body<CA_RESID>
+//            with s computed inside it after its first strip's MFMAs (as the training
+//            conv2 does): border rows / columns / corners of t, S_tap, mean(u) with
+//            conv2's bf16 filter image in LDS, the CA MLP                      ca_scale_finish
 // against the three launches of the training forward (conv1; conv2 + pool writing u;
 // the CA pass reading u, h and writing h'): per image 0.6 MB less traffic and no
 // elementwise pass.  It differs from them in summation order (m from t's statistics
@@ -44,7 +44,7 @@ __device__ __forceinline__ void own_stores_visible() {
   } while (0)
 #endif
 
-__global__ void __launch_bounds__(512, 1) rcab_infer_kernel(ConvParams c1, ConvParams c2, CaScale ca) {
+__global__ void __launch_bounds__(512, 1) rcab_infer_kernel(ConvParams c1, ConvParams c2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = blockIdx.x;
   const int nsy = c1.H / kTH;
@@ -53,27 +53,9 @@ __global__ void __launch_bounds__(512, 1) rcab_infer_kernel(ConvParams c1, ConvP
   ISTAMP(1);
   own_stores_visible();
   ISTAMP(2);
-  {
-    // conv2's filter image into the filter slot (conv1 is done with it): the mean's
-    // matvec reads it there, and conv2 computes on it; scratch in the ring
-    CaScalePre q;
-    ca_scale_load(ca, n, c1.H, c1.W, q);
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t wbase = lds_u32(smem);
-    for (int i = wv; i < 72; i += 8) {
-      const int tap = i >> 3, row = 8 * (i & 7) + (lane >> 3), ch = (lane & 7) ^ (row & 7);
-      glds16(c2.w + ((size_t)(tap * 64 + row)) * 64 + ch * 8, wbase + (uint32_t)i * 1024u);
-    }
-    wait_vm<0>();  // the DMA and the scale's operands (its barriers publish the DMA)
-    ISTAMP(3);
-    ca_scale_finish<false>(ca, q, n, c1.H, c1.W, reinterpret_cast<float*>(smem + Conv2Smem<48>::WB), smem, true);
-  }
-  ISTAMP(4);
-  own_stores_visible();  // s in the record, read by conv2's epilogue
-  ISTAMP(5);
-  // h' = h + s (conv2(t) + b2); its filter image is resident from the scale phase
-  conv64_body<48, EPI_CA_RESID, 8, true>(c2, nsy, n, smem);
-  ISTAMP(6);
+  // h' = h + s (conv2(t) + b2), s from t inside the body (c2.cas_on)
+  conv64_body<48, EPI_CA_RESID, 8>(c2, nsy, n, smem);
+  ISTAMP(3);
 }
 
 int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* part, int nstrips, const float* w1,
@@ -112,9 +94,10 @@ int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* p
   b.r1l = h_in ? nullptr : static_cast<const uint8_t*>(lo_in);
   b.yph = static_cast<bf16_t*>(hi_out);
   b.ypl = static_cast<uint8_t*>(lo_out);
-  b.escale = rec + 64 + CR;  // s of the record m | z1 | s
-  b.escale_stride = 128 + CR;
-  hipLaunchKernelGGL(rcab_infer_kernel, dim3(c1.N), dim3(512), Conv2Smem<48>::TOTAL, st, a, b, ca);
+  b.cas = ca;  // conv2 computes its s (and the record m | z1 | s) itself
+  b.cas_on = 1;
+  hipLaunchKernelGGL(rcab_infer_kernel, dim3(c1.N), dim3(512), Conv2Smem<48>::TOTAL + kCaScaleFloats * sizeof(float),
+                     st, a, b);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

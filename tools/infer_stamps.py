@@ -45,13 +45,13 @@ def main():
     call("srmi_debug_conv_stamps", None)
     st = buf.view(4, N, 64).cpu().numpy().astype(np.int64)
     c1, c2, k, cs = st[0], st[1], st[2], st[3]
-    ok = (k[:, 0] != 0) & (k[:, 6] != 0)
+    ok = (k[:, 0] != 0) & (k[:, 3] != 0)
     c1, c2, k, cs = c1[ok], c2[ok], k[ok], cs[ok]
     print(f"workgroups with stamps: {ok.sum()} of {N}")
     rt = c1[:, 62:64].astype(np.float64)
     clk = np.median((c1[:, 61] - c1[:, 0]) / np.maximum(rt[:, 1] - rt[:, 0], 1)) * 100.0
     print(f"shader clock ~{clk:.0f} MHz (s_memtime vs s_memrealtime over conv1)")
-    tot = k[:, 6] - k[:, 0]
+    tot = k[:, 3] - k[:, 0]
     print(f"launch span per workgroup: median {np.median(tot):.0f} cycles ({np.median(tot) / clk:.2f} us)")
 
     def row(name, v):
@@ -60,16 +60,14 @@ def main():
     row("conv1 body", k[:, 1] - k[:, 0])
     row("  conv1 prologue", c1[:, 1] - c1[:, 0])
     row("  conv1 strips", c1[:, 61] - c1[:, 1])
-    row("own_stores_visible #1", k[:, 2] - k[:, 1])
-    row("scale loads + conv2 filter DMA", k[:, 3] - k[:, 2])
-    row("ca_scale_finish", k[:, 4] - k[:, 3])
-    for i, nm in enumerate(("T partials + border lines", "barrier 1", "S_tap + matvec (LDS filters)", "barrier 2",
-                            "z1 + s (waves 0-3)", "barrier 3")):
-        row("    " + nm, cs[:, i + 1] - cs[:, i])
-    row("own_stores_visible #2", k[:, 5] - k[:, 4])
-    row("conv2 body", k[:, 6] - k[:, 5])
+    row("own_stores_visible", k[:, 2] - k[:, 1])
+    row("conv2 body (the scale inside)", k[:, 3] - k[:, 2])
     row("  conv2 prologue", c2[:, 1] - c2[:, 0])
     row("  conv2 strips", c2[:, 61] - c2[:, 1])
+    row("  ca_scale_finish (after strip 0's MFMAs)", cs[:, 7] - cs[:, 0])
+    for i, nm in enumerate(("T partials + border lines", "barrier 1", "S_tap + matvec (LDS filters)", "barrier 2",
+                            "z1", "barrier 3 + s", "barrier 4")):
+        row("    " + nm, cs[:, i + 1] - cs[:, i])
     # conv2's per-strip phases (non-deferred body: issue, mfma, gstore, epi, barrier)
     names = ("issue", "mfma", "gstore", "epi", "barrier")
     for j in (0, 5, 10):
