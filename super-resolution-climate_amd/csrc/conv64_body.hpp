@@ -70,6 +70,12 @@ template <int EPI>
 constexpr bool epi_cr() {
   return EPI == EPI_CA_RESID || EPI == EPI_CA_RESID_U;
 }
+// conv2's h' = h + s u with u rounded to bf16 first (staged once as bf16): the training
+// conv2 always (it stores that u for backward), the inference one per SRMI_INFER_BF16U
+template <int EPI>
+constexpr bool epi_cr_bf16() {
+  return EPI == EPI_CA_RESID_U || (EPI == EPI_CA_RESID && SRMI_INFER_BF16U);
+}
 template <int EPI>
 constexpr bool epi_run() {
   return EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC || epi_cr<EPI>();
@@ -221,7 +227,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
           ps1[c][3] += v[3] * bf2f(uu.y >> 16);
         }
       }
-      if constexpr (EPI == EPI_CA_RESID_U) {  // u in bf16: stored for backward, and the product's operand
+      if constexpr (epi_cr_bf16<EPI>()) {  // u in bf16: the product's operand (and stored for backward)
         bv[pt][c] = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         continue;
       }
@@ -241,10 +247,10 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
     }
   }
   const int lane = tid & 63;
-  // the training conv2 (EPI_CA_RESID_U): u is rounded to bf16 before anything reads it,
-  // so the row is staged once as bf16 (128 B per pixel, chunk-swizzled: one barrier, not
-  // the fp32 path's two halves and four) and read back in the pair's run layout
-  if constexpr (EPI == EPI_CA_RESID_U) {
+  // conv2 with u rounded to bf16 before anything reads it (epi_cr_bf16): the row is
+  // staged once as bf16 (128 B per pixel, chunk-swizzled: one barrier, not the fp32
+  // path's two halves and four) and read back in the pair's run layout
+  if constexpr (epi_cr_bf16<EPI>()) {
     constexpr int HALF = NPT * 8, RUNS = HALF / 4;
     static_assert(kShared, "the 8-wave body");
 #pragma unroll
@@ -255,7 +261,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
         *reinterpret_cast<uint2*>(stage + px * 128 + ((c16 ^ (px & 7)) << 4) + (fk & 1) * 8) = bv[pt][c];
       }
     stage_sync();
-    const auto rbb = wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
+    [[maybe_unused]] const auto rbb = wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
     const auto rph = wt_rsrc(p.yph, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
     const auto rpl = wt_rsrc(p.ypl, (uint32_t)((size_t)p.N * HW * p.Cout));
     const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
@@ -271,7 +277,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
         float4 hh = e.r1[q / NCT][q % NCT];
         if (p.r1h) hh = pair_decode4(make_uint2(__float_as_uint(hh.x), __float_as_uint(hh.y)), __float_as_uint(hh.z));
         const uint32_t oe = (uint32_t)((pix0 + px) * p.Cout + cb * 64 + c * 4);  // element
-        st_wt8(rbb, p.yb, oe * 2, ub);
+        if constexpr (EPI == EPI_CA_RESID_U) st_wt8(rbb, p.yb, oe * 2, ub);  // u for backward
         const float o0 = fmaf(bf2f(ub.x & 0xFFFFu), fs.x, hh.x), o1 = fmaf(bf2f(ub.x >> 16), fs.y, hh.y);
         const float o2 = fmaf(bf2f(ub.y & 0xFFFFu), fs.z, hh.z), o3 = fmaf(bf2f(ub.y >> 16), fs.w, hh.w);
         uint2 hi;
@@ -312,7 +318,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
           const int i = kShared ? 2 * j + half_id : j;
           const int lin = i * 1024 + lane * 16, lpx = lin >> 8, c = (lin >> 4) & 15;
           float4 val = *reinterpret_cast<const float4*>(stage + lpx * 256 + ((c ^ (lpx & 15)) << 4));
-          if constexpr (epi_cr<EPI>()) {  // (EPI_CA_RESID: the inference conv2, fp32 u)
+          if constexpr (epi_cr<EPI>()) {  // (EPI_CA_RESID with SRMI_INFER_BF16U = 0: fp32 u)
             // h' = h + s u in the run layout (the lane's channels 4c..4c+3: s in fs), out as the pair
             const int q = h * (kShared ? RUNS / 2 : RUNS) + j;
             float4 hh = e.r1[q / NCT][q % NCT];

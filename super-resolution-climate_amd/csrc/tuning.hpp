@@ -27,6 +27,13 @@
 #define SRMI_INFER_DEFER 16
 #endif
 
+// the inference conv2's h' = h + s u with u rounded to bf16 (as the training conv2 and
+// the round-3 three-launch inference did; staged once as bf16, one barrier), 0 = fp32 u
+// (staged as fp32 in two halves, four barriers)
+#ifndef SRMI_INFER_BF16U
+#define SRMI_INFER_BF16U 1
+#endif
+
 // rcab_infer.hip defines SRMI_TU_INFER before its includes: the inference policies
 #ifdef SRMI_TU_INFER
 #define SRMI_WT SRMI_INFER_WT
