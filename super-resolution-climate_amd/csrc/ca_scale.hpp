@@ -46,6 +46,7 @@ struct CaScalePre {
   float b1;                // b1[j]
   float w2[4];             // W2 row c = tid >> 3, inputs (tid & 7) + 8 i (s)
   float b2, bc2;
+  float bcm;               // (the partial-mean path) conv2's bias of channel tid & 63
 };
 
 // (unconditional loads at clamped indices: no divergent branches around them, so the
@@ -99,12 +100,146 @@ __device__ __forceinline__ void ca_scale_load(const CaScale& c, int n, int H, in
   ca_scale_load_params(c, q);
 }
 
+// The partial-mean path (training, SRMI_CA_MPART): conv1's workgroups leave their share of
+// the matvec in c.mpart [N][nruns][64]; conv2 issues the first kCaPreStrips of them (and
+// its bias) ahead, in q.tp / q.bcm (channel tid & 63)
+__device__ __forceinline__ void ca_mpart_load(const CaScale& c, int n, CaScalePre& q) {
+  const int ch = threadIdx.x & 63;
+  const float* mp = c.mpart + (size_t)n * c.nruns * 64 + ch;
+#pragma unroll
+  for (int i = 0; i < kCaPreStrips; ++i) q.tp[i] = mp[(size_t)min(i, c.nruns - 1) * 64];
+  q.bcm = c.bc2[ch];
+}
+
 // sum over the 8 lanes of an aligned group (DPP: quad swaps, then the half-row mirror)
 __device__ __forceinline__ float sum8(float v) {
   v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
   v += dpp_mov<0x141>(v);  // row_half_mirror
   return v;
+}
+
+// sum_{ci, tap} W2[co][ci][tap] S_tap[ci], co = tid >> 3 (8 lanes per co, 8 ci each, in
+// two halves of 4 ci: the training conv2 runs this with a strip's accumulators live, a
+// half's operands are 36 registers), summed over those 8 lanes.  S_tap from T (four
+// partials, summed in fixed order), the border-line sums bs (row 0, row H-1, column 0,
+// column W-1) and the corners cn ((0,0) (0,W-1) (H-1,0) (H-1,W-1)), each [64] in LDS;
+// wl: conv2's bf16 filter image in LDS (swz128, or swz128t with TSW).
+template <bool TSW>
+__device__ __forceinline__ float ca_matvec(const float* red, const float* bs, const float* cn, const char* wl,
+                                           int tid) {
+  {
+    const int co = tid >> 3, pc = tid & 7;
+    const uint32_t off = TSW ? swz128t(co, pc) : swz128(co, pc);
+    float a = 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c0 = pc * 8 + 4 * h;
+      float T[4], b[4][4], k[4][4];  // T; border sums of row 0, row H-1, column 0, column W-1; corners
+      auto ld4 = [&](const float* src, float (&d)[4]) __attribute__((always_inline)) {
+        const float4 x = *reinterpret_cast<const float4*>(src);
+        d[0] = x.x; d[1] = x.y; d[2] = x.z; d[3] = x.w;
+      };
+      {
+        float r[4][4];  // the 4 phases, fixed order
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) ld4(red + ph * 64 + c0, r[ph]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) T[e] = (r[0][e] + r[1][e]) + (r[2][e] + r[3][e]);
+      }
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        ld4(bs + l * 64 + c0, b[l]);
+        ld4(cn + l * 64 + c0, k[l]);
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {  // tap (dy, dx) reads t[y + dy][x + dx]
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        const uint2 v = *reinterpret_cast<const uint2*>(wl + tap * 8192 + off + 8 * h);
+        const uint32_t w[2] = {v.x, v.y};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float sv = T[e];
+          if (dy == -1) sv -= b[1][e];  // row H-1 is never read
+          if (dy == 1) sv -= b[0][e];   // row 0
+          if (dx == -1) sv -= b[3][e];  // column W-1
+          if (dx == 1) sv -= b[2][e];   // column 0
+          if (dy != 0 && dx != 0) sv += k[(dy == -1 ? 2 : 0) + (dx == -1 ? 1 : 0)][e];
+          const float wv = (e & 1) ? bf2f(w[e >> 1] >> 16) : bf2f(w[e >> 1] & 0xFFFFu);
+          a += wv * sv;
+        }
+      }
+    }
+    return sum8(a);
+  }
+}
+
+// z1 = W1 m + b1 (16 lanes per row j, 4 inputs each, DPP row sum), a barrier, then
+// s = sigmoid(W2 relu(z1) + b2) (8 lanes per channel c): m, z1, s in LDS, q's MLP slices
+__device__ __forceinline__ void ca_mlp(const CaScale& c, const CaScalePre& q, const float* m, float* z1, float* s,
+                                       int tid) {
+  const int CR = c.CR;
+  {
+    const int j = tid >> 4, i4 = 4 * (tid & 15);
+    const float4 mv = *reinterpret_cast<const float4*>(m + i4);
+    float a = q.w1[0] * mv.x + q.w1[1] * mv.y + q.w1[2] * mv.z + q.w1[3] * mv.w;
+    a = sum16(a);
+    if ((tid & 15) == 0 && j < CR) z1[j] = a + q.b1;
+  }
+  CSTAMP(5);
+  __syncthreads();
+  {
+    const int q8 = tid & 7;
+    float b = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (q8 + 8 * i < CR) b += q.w2[i] * fmaxf(z1[q8 + 8 * i], 0.f);
+    b = sum8(b);
+    if (q8 == 0) s[tid >> 3] = 1.f / (1.f + expf(-(b + q.b2)));
+  }
+}
+
+// The scale of image n from conv1's partial means (q from ca_mpart_load and
+// ca_scale_load_params): m = b2 + (1/HW) sum over the runs in run order, then the MLP;
+// three barriers, s left at sm + kCaScaleS, the record m | z1 | s when `write_rec`.
+__device__ __forceinline__ void ca_scale_from_mpart(const CaScale& c, const CaScalePre& q0, int n, int HW, float* sm,
+                                                    bool write_rec) {
+  CaScalePre q = q0;  // (opaque: see ca_scale_finish)
+#pragma unroll
+  for (int i = 0; i < kCaPreStrips; ++i) asm volatile("" : "+v"(q.tp[i]));
+  asm volatile("" : "+v"(q.bcm));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(q.w1[i]), "+v"(q.w2[i]));
+  asm volatile("" : "+v"(q.b1), "+v"(q.b2));
+  constexpr int C = 64;
+  const int tid = opaque_tid(), CR = c.CR;
+  float* m = sm + 768;
+  float* z1 = sm + 832;
+  float* s = sm + kCaScaleS;
+  CSTAMP(0);
+  if (tid < C) {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < kCaPreStrips; ++i)
+      if (i < c.nruns) a += q.tp[i];
+    for (int r = kCaPreStrips; r < c.nruns; ++r) a += c.mpart[((size_t)n * c.nruns + r) * C + tid];
+    m[tid] = q.bcm + a / (float)HW;
+  }
+  CSTAMP(3);
+  __syncthreads();
+  CSTAMP(4);
+  ca_mlp(c, q, m, z1, s, tid);
+  CSTAMP(6);
+  __syncthreads();
+  CSTAMP(7);
+  if (write_rec) {
+    float* r = c.rec + (size_t)n * (2 * C + CR);
+    if (tid < C) {
+      r[tid] = m[tid];
+      r[C + CR + tid] = s[tid];
+    }
+    if (tid < CR) r[C + tid] = z1[tid];
+  }
 }
 
 // The scale of image n from the preloaded operands, 512 threads (sm >= kCaScaleFloats

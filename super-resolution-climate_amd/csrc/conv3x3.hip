@@ -373,6 +373,10 @@ static int launch_v2_only(const ConvParams& p, hipStream_t st) {
   // (diagnostic: the scale's phase stamps after the body's, [grid][64] each)
   if (q.stamps && EPI == EPI_CA_RESID_U) q.cas.stamps = q.stamps + (size_t)conv64_blocks(p, 48, run_len) * 64;
   if (EPI == EPI_CA_RESID_U && p.cas_on) lds += kCaScaleFloats * sizeof(float);  // the scale's scratch
+  if (EPI == EPI_RELU_POOL && p.cas_on) {  // conv1's partial CA means: the matvec's scratch
+    if (!p.cas.mpart || !p.cas.wimg || p.cas.nruns != conv64_runs_per_image(p)) return SRMI_ERR_ARG;
+    lds += kCaScaleFloats * sizeof(float);
+  }
   hipLaunchKernelGGL((conv64_kernel<48, EPI, 8>), dim3(conv64_blocks(p, 48, run_len)), dim3(512), lds, st, q, run_len);
   SRMI_CHECK_LAUNCH();
   return 0;
@@ -417,11 +421,17 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
       break;
     case EPI_CA_RESID_U:
       if (!p.yb || !p.yph || !p.ypl || (!p.r1 && (!p.r1h || !p.r1l)) || p.f32) return SRMI_ERR_ARG;
-      if (p.cas_on ? (!p.cas.t || !p.cas.part || !p.cas.w1 || !p.cas.b1 || !p.cas.w2 || !p.cas.b2 || !p.cas.bc2 ||
-                      !p.cas.rec || p.cas.CR < 4 || p.cas.CR > 32 || p.cas.CR % 4 ||
-                      p.cas.nstrips != conv3x3_nstrips(p.H, p.W))
-                   : !p.escale)
+      if (p.cas_on) {
+        if (!p.cas.w1 || !p.cas.b1 || !p.cas.w2 || !p.cas.b2 || !p.cas.bc2 || !p.cas.rec || p.cas.CR < 4 ||
+            p.cas.CR > 32 || p.cas.CR % 4)
+          return SRMI_ERR_ARG;
+        // SRMI_CA_MPART: s from conv1's partial means; else from t's border lines
+        if (SRMI_CA_MPART ? (!p.cas.mpart || p.cas.nruns < 1)
+                          : (!p.cas.t || !p.cas.part || p.cas.nstrips != conv3x3_nstrips(p.H, p.W)))
+          return SRMI_ERR_ARG;
+      } else if (!p.escale) {
         return SRMI_ERR_ARG;
+      }
       break;
     default:
       break;
@@ -451,6 +461,11 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
     case EPI_CA_RESID_U: return launch_v2_only<EPI_CA_RESID_U>(p, st);
     default: return SRMI_ERR_ARG;
   }
+}
+
+int conv64_runs_per_image(const ConvParams& p) {
+  const int run_len = conv64_run_len(p, 48, p.cu_budget > 0 ? p.cu_budget : 256);
+  return (p.W / 48) * ((p.H / kTH + run_len - 1) / run_len);
 }
 
 int conv3x3_nstrips(int H, int W) {

@@ -138,6 +138,14 @@ __device__ __forceinline__ float relu_mask(uint32_t bits16, float v) {
 // lane's read of another lane's staged data above that lane's write.
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
+// conv1's share of its image's CA mean (EPI_RELU_POOL with cas_on, training,
+// SRMI_CA_MPART): what the run's epilogues gather for ca_matvec at the run's end
+struct CaPart {
+  float colA[4][4], colB[4][4];  // [c][r]: the lane's sums of column 0 / column W-1 of t
+  float tacc;                    // tid < 64: T over the run's strips, channel tid
+  float* scr;                    // the LDS scratch (ca_scale.hpp layout: bs, cn zeroed)
+};
+
 // Fused epilogue of the v2 kernel (same semantics as conv_epilogue).  A wave holds
 // row `row` of the strip, channel tiles ct0 .. ct0+NCT-1.  NCT < 4: two waves (the
 // channel halves) share the row's LDS staging, so their writes and the full-line
@@ -148,7 +156,8 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
                                                const EpiPre<NPT, EPI, NCT>& e, const float4 (&bias)[NCT], int n,
                                                int cb, int y, int x0, int strip, int nstrips, float* red, int fr,
                                                int fk, int row, int ct0, int tid, char* stage,
-                                               const float4& fs = float4{0.f, 0.f, 0.f, 0.f}) {
+                                               const float4& fs = float4{0.f, 0.f, 0.f, 0.f},
+                                               CaPart* cp = nullptr, bool cpon = false) {
   constexpr bool kShared = NCT < 4;
   const int half_id = ct0 >> 1;  // shared form: which of the two waves of the row
   auto stage_sync = [&]() __attribute__((always_inline)) {
@@ -241,8 +250,29 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       bv[pt][c] = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
       if constexpr (EPI == EPI_RELU_POOL) {  // sums of the bf16 t conv2 reads (ca_scale.hpp)
         const uint2 b = bv[pt][c];
-        ps0[c][0] += bf2f(b.x & 0xFFFFu); ps0[c][1] += bf2f(b.x >> 16);
-        ps0[c][2] += bf2f(b.y & 0xFFFFu); ps0[c][3] += bf2f(b.y >> 16);
+        const float t4[4] = {bf2f(b.x & 0xFFFFu), bf2f(b.x >> 16), bf2f(b.y & 0xFFFFu), bf2f(b.y >> 16)};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ps0[c][r] += t4[r];
+        if (cpon) {  // (uniform) the image's border columns and corners in this wave's row
+          const bool c0 = pt == 0 && fr == 0 && x0 == 0;
+          const bool cw = pt == NPT - 1 && fr == 15 && x0 + NPT * 16 == p.W;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (pt == 0) cp->colA[c][r] += c0 ? t4[r] : 0.f;
+            if (pt == NPT - 1) cp->colB[c][r] += cw ? t4[r] : 0.f;
+          }
+          const int ch = (ct0 + c) * 16 + fk * 4;
+          if (y == 0 || y == p.H - 1) {
+            float* cn = cp->scr + 512;  // (0,0) (0,W-1) (H-1,0) (H-1,W-1)
+            const int l = y == 0 ? 0 : 2;
+            if (c0) *reinterpret_cast<float4*>(cn + l * 64 + ch) = make_float4(t4[0], t4[1], t4[2], t4[3]);
+            if (cw) *reinterpret_cast<float4*>(cn + (l + 1) * 64 + ch) = make_float4(t4[0], t4[1], t4[2], t4[3]);
+            if (y == 0 && y == p.H - 1) {  // (a one-row image: its row is both)
+              if (c0) *reinterpret_cast<float4*>(cn + 2 * 64 + ch) = make_float4(t4[0], t4[1], t4[2], t4[3]);
+              if (cw) *reinterpret_cast<float4*>(cn + 3 * 64 + ch) = make_float4(t4[0], t4[1], t4[2], t4[3]);
+            }
+          }
+        }
       }
     }
   }
@@ -453,6 +483,14 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       if (tid < 64) {
         const float sum = red[tid] + red[128 + tid] + red[256 + tid] + red[384 + tid];
         p.part[((size_t)n * nstrips + strip) * p.part_stride + cb * 64 + tid] = sum;
+        if constexpr (EPI == EPI_RELU_POOL) {
+          if (cpon) {  // T over the run, and the per-row sums (red) of the image's first / last row
+            cp->tacc += sum;
+            const int y0 = y - row;
+            if (y0 == 0) cp->scr[256 + tid] = red[tid];
+            if (y0 + kTH - 1 == p.H - 1) cp->scr[256 + 64 + tid] = red[(kTH - 1) * 128 + tid];
+          }
+        }
       } else if (kPart2 && tid < 128) {
         const int c = tid - 64;
         const float sum = red[64 + c] + red[192 + c] + red[320 + c] + red[448 + c];
@@ -530,6 +568,22 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   // prologue's wait and land under those MFMAs
   [[maybe_unused]] CaScalePre cq;
   constexpr bool kCas = epi_cr<EPI>() && NW == 8;  // (the scale needs 512 threads)
+  // conv1 with cas_on (training, SRMI_CA_MPART): its share of the image's CA mean
+  constexpr bool kMp = EPI == EPI_RELU_POOL && NW == 8;
+  // conv2 reading those (the training EPI_CA_RESID_U under SRMI_CA_MPART; the launch
+  // refuses cas_on without mpart there) or computing the scale from t (the inference one)
+  constexpr bool kFromMp = EPI == EPI_CA_RESID_U && SRMI_CA_MPART;
+  [[maybe_unused]] CaPart cpart;
+  [[maybe_unused]] const bool cpon = kMp && p.cas_on;
+  if constexpr (kMp) {
+    cpart.scr = reinterpret_cast<float*>(smem + S::TOTAL);
+    cpart.tacc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cpart.colA[c][r] = cpart.colB[c][r] = 0.f;
+    if (cpon) cpart.scr[256 + threadIdx.x] = 0.f;  // bs and cn (published by the prologue barrier)
+  }
 
   // LDS-DMA of one 4-row input group into its ring slot: one wave instruction per
   // 8 pixels (1 KiB), swizzle applied on the source side, halo lanes read the zero
@@ -608,7 +662,16 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   }
   __syncthreads();
   if constexpr (kCas) {
-    if (p.cas_on) ca_scale_load_t(p.cas, n, p.H, p.W, cq);
+    if constexpr (kFromMp) {
+      // (the MLP weights too: conv2 has the registers here, and the finish's first
+      //  barrier would otherwise wait for them)
+      if (p.cas_on) {
+        ca_mpart_load(p.cas, n, cq);
+        ca_scale_load_params(p.cas, cq);
+      }
+    } else {
+      if (p.cas_on) ca_scale_load_t(p.cas, n, p.H, p.W, cq);
+    }
 #ifdef SRMI_TLAT  // diagnostic: the latency of the scale's t operands alone (scale stamps 8, 9)
     if (p.cas.stamps && tid == 0) p.cas.stamps[blockIdx.x * 64 + 8] = __builtin_amdgcn_s_memtime();
     wait_vm<0>();
@@ -696,9 +759,12 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
       if (p.cas_on && k == k0) {  // the image's scale (every wave: uniform), before the first epilogue
         // scratch beyond the body's LDS (the launch adds kCaScaleFloats floats); the first
         // workgroup of the image writes its record m | z1 | s for backward
-        ca_scale_load_params(p.cas, cq);  // (L2-resident; consumed after the finish's first barriers)
+        if constexpr (!kFromMp) ca_scale_load_params(p.cas, cq);  // (L2-resident; used after two barriers)
         float* sm = reinterpret_cast<float*>(smem + S::TOTAL);
-        ca_scale_finish<false>(p.cas, cq, n, p.H, p.W, sm, wl, ry == 0 && sx == 0 && cb == 0 && !tail_part);
+        if constexpr (kFromMp)  // from conv1's partial means
+          ca_scale_from_mpart(p.cas, cq, n, p.H * p.W, sm, ry == 0 && sx == 0 && cb == 0 && !tail_part);
+        else
+          ca_scale_finish<false>(p.cas, cq, n, p.H, p.W, sm, wl, ry == 0 && sx == 0 && cb == 0 && !tail_part);
         fs = *reinterpret_cast<const float4*>(sm + kCaScaleS + 4 * (lane & 15));
       }
     }
@@ -709,15 +775,56 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if constexpr (kMp) {
+      if (cpon && k == k1 - 1) {  // every wave is past its last filter read: conv2's filter
+        const uint32_t wbase = lds_u32(wl);  // image into the filter slot for the run-end matvec
+        for (int i = wv_s; i < 72; i += NW) {
+          const int tap = i >> 3, r8 = 8 * (i & 7) + (lane >> 3), c = (lane & 7) ^ (r8 & 7);
+          glds16(p.cas.wimg + ((size_t)(tap * 64 + r8)) * 64 + c * 8, wbase + (uint32_t)i * 1024u);
+        }
+      }
+    }
     conv_epilogue2<NPT, EPI, NCT>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx,
                                                                nsy * nsx, red, fr, fk, row, ct0,
-                                  tid, ring + (k % 3) * S::GROUPB + row * TW * 128, fs);
+                                  tid, ring + (k % 3) * S::GROUPB + row * TW * 128, fs, &cpart, kMp && cpon);
     STAMP(sj + 3);
     // LDS-only barrier: this strip's global stores stay in flight into the next strip
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     STAMP(sj + 4);
+  }
+  if constexpr (kMp) {
+    if (cpon) {  // the run's share of the image's CA mean: border columns over the 4 rows,
+                 // then ca_matvec on conv2's filter image -> mpart[n][run]
+      float* scr = cpart.scr;
+      float* colacc = scr + 768;  // [4 rows][2][64]
+#pragma unroll
+      for (int c = 0; c < NCT; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ch = (ct0 + c) * 16 + fk * 4 + r;
+          if (fr == 0) colacc[(row * 2 + 0) * 64 + ch] = cpart.colA[c][r];
+          if (fr == 15) colacc[(row * 2 + 1) * 64 + ch] = cpart.colB[c][r];
+        }
+      if (tid < 64) scr[tid] = cpart.tacc;  // T in the first of ca_matvec's four partial rows
+      else if (tid < 256) scr[tid] = 0.f;
+      wait_vm<0>();  // this wave's pieces of the filter image (and its last strip's stores)
+      STAMP(57);
+      __syncthreads();
+      STAMP(58);
+      if (tid < 128) {
+        const int l = tid >> 6, ch = tid & 63;
+        scr[256 + (2 + l) * 64 + ch] = ((colacc[(0 * 2 + l) * 64 + ch] + colacc[(1 * 2 + l) * 64 + ch]) +
+                                        colacc[(2 * 2 + l) * 64 + ch]) + colacc[(3 * 2 + l) * 64 + ch];
+      }
+      __syncthreads();
+      STAMP(59);
+      const float a = ca_matvec<false>(scr, scr + 256, scr + 512, wl, tid);
+      const int runs_per_col = (nsy + run_len - 1) / run_len;
+      if ((tid & 7) == 0) p.cas.mpart[((size_t)n * p.cas.nruns + sx * runs_per_col + ry) * 64 + (tid >> 3)] = a;
+      STAMP(60);
+    }
   }
   STAMP(61);
 }

@@ -193,6 +193,7 @@ struct srmi_engine {
   bf16_t* PS[3];  // pixel-shuffle outputs (scale s: [N][h*2^k][w*2^k][64])
   float *rec, *brec;
   float *ppool, *pacc;
+  float* mpart;  // conv1's partial CA means [N][runs per image <= nstrips][64] (SRMI_CA_MPART)
   // backward
   float *GAf, *GBf, *dRESf;
   bf16_t *GAb, *GBb, *DU, *DZ, *dRESb;
@@ -277,6 +278,7 @@ static size_t carve(srmi_engine* e, char* base) {
     e->rec = cv.take<float>((size_t)(e->train ? nl * nb : 1) * N * 160);
     e->brec = e->train ? cv.take<float>((size_t)nl * nb * N * 224) : nullptr;  // [N][160] + dm[N][64]
     e->ppool = cv.take<float>((size_t)N * nstrips * 64);
+    e->mpart = e->train ? cv.take<float>((size_t)N * nstrips * 64) : nullptr;
     e->pacc = cv.take<float>((size_t)N * nstrips * 128);
   }
   e->lpart_n = 1024;
@@ -596,10 +598,19 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
         }
         if (ca_fwd_mode(e)) {  // training: the CA forward inside conv2
           uint8_t* lo = reinterpret_cast<uint8_t*>(e->Hf);  // the pair's lo8 remainder (as below)
-          RC(conv_fwd(e, r.c1, e->hb(g, b - 1), n, h, w, EPI_RELU_POOL, e->Tm(g, b), nullptr, nullptr, e->ppool, 1.f,
-                      st));
+          ConvParams c1 = fwd_params(e, r.c1, e->hb(g, b - 1), n, h, w, e->Tm(g, b), nullptr, nullptr, e->ppool, 1.f);
           ConvParams c2 = fwd_params(e, r.c2, e->Tm(g, b), n, h, w, e->Um(g, b), nullptr, b == 1 ? rin : nullptr,
                                      nullptr, 1.f);
+          // SRMI_CA_MPART: conv1's workgroups leave their share of the CA mean (the matvec
+          // on conv2's bf16 filter image) for conv2, which then reads no t border lines
+          const int nruns = SRMI_CA_MPART ? conv64_runs_per_image(c1) : 0;
+          if (SRMI_CA_MPART) {
+            c1.cas.mpart = e->mpart;
+            c1.cas.nruns = nruns;
+            c1.cas.wimg = c2.w;
+            c1.cas_on = 1;
+          }
+          RC(conv3x3_launch(c1, EPI_RELU_POOL, st));
           c2.r1h = b == 1 ? nullptr : e->hb(g, b - 1);
           c2.r1l = b == 1 ? nullptr : lo;
           c2.yph = e->hb(g, b);
@@ -607,6 +618,10 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
           const CaScale cas{e->Tm(g, b), e->ppool, nstrips, prm + r.ca_w1, prm + r.ca_b1, prm + r.ca_w2,
                             prm + r.ca_b2, e->pbias + r.c2.pb_off, 64 / R, e->recp(g, b)};
           c2.cas = cas;
+          if (SRMI_CA_MPART) {
+            c2.cas.mpart = e->mpart;
+            c2.cas.nruns = nruns;
+          }
           c2.cas_on = 1;
           RC(conv3x3_launch(c2, EPI_CA_RESID_U, st));
           continue;

@@ -29,8 +29,8 @@ enum Epi {
                        // h' out as the pair yph / ypl, s = escale[n * escale_stride + c]
   // the training RCAB's conv2 (the CA forward without a pass of its own):
   EPI_CA_RESID_U = 10, // u = acc + b -> bf16 yb (saved for backward), h' = h + s[c] bf16(u) as
-                       // in EPI_CA_RESID; s computed in the prologue from conv1's t (cas_on,
-                       // ca_scale.hpp) or read from escale
+                       // in EPI_CA_RESID; s computed after the first strip's MFMAs (cas_on,
+                       // ca_scale.hpp: from conv1's partial means, or from t) or read from escale
 };
 
 // The CA scale of an RCAB from its conv1 output t (ca_scale.hpp): mean(u) of u =
@@ -44,6 +44,12 @@ struct CaScale {
   int CR;
   float* rec;         // out: m | z1 | s per image [N][128 + CR]
   unsigned long long* stamps;  // diagnostic build only: phase stamps of ca_scale_finish (null)
+  // Partial means (training, SRMI_CA_MPART): conv1 (EPI_RELU_POOL with cas_on) writes, per
+  // workgroup (run) of an image, the matvec of its rows' share of S_tap (ca_matvec) into
+  // mpart [N][nruns][64]; conv2 then sums them instead of computing the scale from t.
+  float* mpart;
+  int nruns;           // workgroups per image of conv1's launch (conv64_runs_per_image)
+  const bf16_t* wimg;  // conv2's packed bf16 filter image (conv1 loads it for the matvec)
 };
 
 struct ConvParams {
@@ -85,6 +91,7 @@ unsigned long long* conv3x3_stamps_for(int epi);  // (diagnostic build: SRMI_STA
 int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st);  // dispatches p.f32
 int conv3x3_f32_launch(const ConvParams& p, int epi, hipStream_t st);
 int conv3x3_nstrips(int H, int W);
+int conv64_runs_per_image(const ConvParams& p);  // workgroups per image of a 48-wide v2 launch
 
 struct ReduceSet {  // one slab reduction: slabs -> torch-layout dW (and db)
   const float* slab;

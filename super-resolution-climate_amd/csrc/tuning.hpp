@@ -49,6 +49,12 @@
 #define SRMI_CA_FWD 1
 #endif
 
+// the training CA mean from conv1's partial means (ca_scale.hpp ca_matvec in conv1's run
+// end, conv2 sums them: 1) or conv2 computing it from t's border lines (0)
+#ifndef SRMI_CA_MPART
+#define SRMI_CA_MPART 1
+#endif
+
 // waves per workgroup of the exact-fp32 conv (conv_f32.hip)
 #ifndef SRMI_F32_NW
 #define SRMI_F32_NW 8

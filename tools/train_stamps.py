@@ -78,6 +78,12 @@ def main():
             if np.all(cs[:, 9]):  # (diagnostic build SRMI_TLAT: the t operands' latency alone)
                 row("  t loads: barrier + issue", cs[:, 8] - body[:, 1])
                 row("  t loads: latency", cs[:, 9] - cs[:, 8])
+        if epi == 8 and np.all(body[:, 60]):  # conv1's run end: its share of the CA mean (SRMI_CA_MPART)
+            last = max(j for j in range(11) if np.all(body[:, 2 + 5 * j + 4]))
+            row("run end: colsums + wait (DMA, stores)", body[:, 57] - body[:, 2 + 5 * last + 4])
+            row("run end: barrier", body[:, 58] - body[:, 57])
+            row("run end: column reduce + barrier", body[:, 59] - body[:, 58])
+            row("run end: matvec + store", body[:, 60] - body[:, 59])
         for j in range(6):
             base = 2 + 5 * j
             if not np.all(body[:, base + 4]):
