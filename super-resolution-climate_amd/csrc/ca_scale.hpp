@@ -124,13 +124,20 @@ __device__ __forceinline__ float sum8(float v) {
 // half's operands are 36 registers), summed over those 8 lanes.  S_tap from T (four
 // partials, summed in fixed order), the border-line sums bs (row 0, row H-1, column 0,
 // column W-1) and the corners cn ((0,0) (0,W-1) (H-1,0) (H-1,W-1)), each [64] in LDS;
-// wl: conv2's bf16 filter image in LDS (swz128, or swz128t with TSW).
-template <bool TSW>
-__device__ __forceinline__ float ca_matvec(const float* red, const float* bs, const float* cn, const char* wl,
-                                           int tid) {
+// wv: the lane's slices of conv2's bf16 filter image (ca_matvec_load_w), in registers.
+// (conv1's run end: its share of the mean, SRMI_CA_MPART)
+__device__ __forceinline__ void ca_matvec_load_w(const bf16_t* wimg, int tid, uint2 (&wv)[2][9]) {
+  const int co = tid >> 3, pc = tid & 7;  // W2[co][ci][tap] at wimg[(tap * 64 + co) * 64 + ci]
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+      wv[h][tap] = *reinterpret_cast<const uint2*>(wimg + ((size_t)(tap * 64 + co)) * 64 + pc * 8 + 4 * h);
+}
+__device__ __forceinline__ float ca_matvec(const float* red, const float* bs, const float* cn,
+                                           const uint2 (&wv)[2][9], int tid) {
   {
-    const int co = tid >> 3, pc = tid & 7;
-    const uint32_t off = TSW ? swz128t(co, pc) : swz128(co, pc);
+    const int pc = tid & 7;
     float a = 0.f;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -155,8 +162,7 @@ __device__ __forceinline__ float ca_matvec(const float* red, const float* bs, co
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {  // tap (dy, dx) reads t[y + dy][x + dx]
         const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-        const uint2 v = *reinterpret_cast<const uint2*>(wl + tap * 8192 + off + 8 * h);
-        const uint32_t w[2] = {v.x, v.y};
+        const uint32_t w[2] = {wv[h][tap].x, wv[h][tap].y};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float sv = T[e];
@@ -165,8 +171,8 @@ __device__ __forceinline__ float ca_matvec(const float* red, const float* bs, co
           if (dx == -1) sv -= b[3][e];  // column W-1
           if (dx == 1) sv -= b[2][e];   // column 0
           if (dy != 0 && dx != 0) sv += k[(dy == -1 ? 2 : 0) + (dx == -1 ? 1 : 0)][e];
-          const float wv = (e & 1) ? bf2f(w[e >> 1] >> 16) : bf2f(w[e >> 1] & 0xFFFFu);
-          a += wv * sv;
+          const float we = (e & 1) ? bf2f(w[e >> 1] >> 16) : bf2f(w[e >> 1] & 0xFFFFu);
+          a += we * sv;
         }
       }
     }

@@ -574,6 +574,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
   // refuses cas_on without mpart there) or computing the scale from t (the inference one)
   constexpr bool kFromMp = EPI == EPI_CA_RESID_U && SRMI_CA_MPART;
   [[maybe_unused]] CaPart cpart;
+  [[maybe_unused]] uint2 w2v[2][9];  // the lane's slices of conv2's filter image (run end)
   [[maybe_unused]] const bool cpon = kMp && p.cas_on;
   if constexpr (kMp) {
     cpart.scr = reinterpret_cast<float*>(smem + S::TOTAL);
@@ -775,14 +776,8 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if constexpr (kMp) {
-      if (cpon && k == k1 - 1) {  // every wave is past its last filter read: conv2's filter
-        const uint32_t wbase = lds_u32(wl);  // image into the filter slot for the run-end matvec
-        for (int i = wv_s; i < 72; i += NW) {
-          const int tap = i >> 3, r8 = 8 * (i & 7) + (lane >> 3), c = (lane & 7) ^ (r8 & 7);
-          glds16(p.cas.wimg + ((size_t)(tap * 64 + r8)) * 64 + c * 8, wbase + (uint32_t)i * 1024u);
-        }
-      }
+    if constexpr (kMp) {  // conv2's filter slices for the run-end matvec, under the last epilogue
+      if (cpon && k == k1 - 1) ca_matvec_load_w(p.cas.wimg, tid, w2v);
     }
     conv_epilogue2<NPT, EPI, NCT>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx,
                                                                nsy * nsx, red, fr, fk, row, ct0,
@@ -809,7 +804,6 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
         }
       if (tid < 64) scr[tid] = cpart.tacc;  // T in the first of ca_matvec's four partial rows
       else if (tid < 256) scr[tid] = 0.f;
-      wait_vm<0>();  // this wave's pieces of the filter image (and its last strip's stores)
       STAMP(57);
       __syncthreads();
       STAMP(58);
@@ -820,7 +814,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
       }
       __syncthreads();
       STAMP(59);
-      const float a = ca_matvec<false>(scr, scr + 256, scr + 512, wl, tid);
+      const float a = ca_matvec(scr, scr + 256, scr + 512, w2v, tid);
       const int runs_per_col = (nsy + run_len - 1) / run_len;
       if ((tid & 7) == 0) p.cas.mpart[((size_t)n * p.cas.nruns + sx * runs_per_col + ry) * 64 + (tid >> 3)] = a;
       STAMP(60);
