@@ -253,24 +253,32 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
         const float t4[4] = {bf2f(b.x & 0xFFFFu), bf2f(b.x >> 16), bf2f(b.y & 0xFFFFu), bf2f(b.y >> 16)};
 #pragma unroll
         for (int r = 0; r < 4; ++r) ps0[c][r] += t4[r];
-        if (cpon) {  // (uniform) the image's border columns and corners in this wave's row
-          const bool c0 = pt == 0 && fr == 0 && x0 == 0;
-          const bool cw = pt == NPT - 1 && fr == 15 && x0 + NPT * 16 == p.W;
+      }
+    }
+  }
+  if constexpr (EPI == EPI_RELU_POOL) {
+    if (cpon) {  // (uniform) the image's border columns and corners in this wave's row, from
+                 // the first and last pixel tiles' bf16 t (outside the loop above: inside it
+                 // the corner stores cost 0.4 K cycles per strip)
+      const bool c0 = fr == 0 && x0 == 0, cw = fr == 15 && x0 + NPT * 16 == p.W;
+      const bool yc = y == 0 || y == p.H - 1;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            if (pt == 0) cp->colA[c][r] += c0 ? t4[r] : 0.f;
-            if (pt == NPT - 1) cp->colB[c][r] += cw ? t4[r] : 0.f;
-          }
-          const int ch = (ct0 + c) * 16 + fk * 4;
-          if (y == 0 || y == p.H - 1) {
-            float* cn = cp->scr + 512;  // (0,0) (0,W-1) (H-1,0) (H-1,W-1)
-            const int l = y == 0 ? 0 : 2;
-            if (c0) *reinterpret_cast<float4*>(cn + l * 64 + ch) = make_float4(t4[0], t4[1], t4[2], t4[3]);
-            if (cw) *reinterpret_cast<float4*>(cn + (l + 1) * 64 + ch) = make_float4(t4[0], t4[1], t4[2], t4[3]);
-            if (y == 0 && y == p.H - 1) {  // (a one-row image: its row is both)
-              if (c0) *reinterpret_cast<float4*>(cn + 2 * 64 + ch) = make_float4(t4[0], t4[1], t4[2], t4[3]);
-              if (cw) *reinterpret_cast<float4*>(cn + 3 * 64 + ch) = make_float4(t4[0], t4[1], t4[2], t4[3]);
-            }
+      for (int c = 0; c < NCT; ++c) {
+        const uint2 a = bv[0][c], b = bv[NPT - 1][c];
+        const float ta[4] = {bf2f(a.x & 0xFFFFu), bf2f(a.x >> 16), bf2f(a.y & 0xFFFFu), bf2f(a.y >> 16)};
+        const float tb[4] = {bf2f(b.x & 0xFFFFu), bf2f(b.x >> 16), bf2f(b.y & 0xFFFFu), bf2f(b.y >> 16)};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          cp->colA[c][r] += c0 ? ta[r] : 0.f;
+          cp->colB[c][r] += cw ? tb[r] : 0.f;
+        }
+        if (yc) {
+          float* cn = cp->scr + 512 + (ct0 + c) * 16 + fk * 4;  // (0,0) (0,W-1) (H-1,0) (H-1,W-1)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {  // e = 0: row 0, 1: row H-1 (both for a one-row image)
+            if (e == 0 ? y != 0 : y != p.H - 1) continue;
+            if (c0) *reinterpret_cast<float4*>(cn + (2 * e) * 64) = make_float4(ta[0], ta[1], ta[2], ta[3]);
+            if (cw) *reinterpret_cast<float4*>(cn + (2 * e + 1) * 64) = make_float4(tb[0], tb[1], tb[2], tb[3]);
           }
         }
       }
