@@ -802,14 +802,14 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
                  // then ca_matvec on conv2's filter image -> mpart[n][run]
       float* scr = cpart.scr;
       float* colacc = scr + 768;  // [4 rows][2][64]
+      if (fr == 0 || fr == 15) {  // (one branch: lanes of column 0 write colA, of W-1 colB)
+        const int l = fr == 0 ? 0 : 1;
 #pragma unroll
-      for (int c = 0; c < NCT; ++c)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ch = (ct0 + c) * 16 + fk * 4 + r;
-          if (fr == 0) colacc[(row * 2 + 0) * 64 + ch] = cpart.colA[c][r];
-          if (fr == 15) colacc[(row * 2 + 1) * 64 + ch] = cpart.colB[c][r];
-        }
+        for (int c = 0; c < NCT; ++c)
+          *reinterpret_cast<float4*>(colacc + (row * 2 + l) * 64 + (ct0 + c) * 16 + fk * 4) =
+              l == 0 ? make_float4(cpart.colA[c][0], cpart.colA[c][1], cpart.colA[c][2], cpart.colA[c][3])
+                     : make_float4(cpart.colB[c][0], cpart.colB[c][1], cpart.colB[c][2], cpart.colB[c][3]);
+      }
       if (tid < 64) scr[tid] = cpart.tacc;  // T in the first of ca_matvec's four partial rows
       else if (tid < 256) scr[tid] = 0.f;
       STAMP(57);
