@@ -19,7 +19,7 @@
 
 namespace srmi {
 
-#ifdef SRMI_STAMPS
+#if defined(SRMI_STAMPS) && !defined(SRMI_NO_CSTAMP)  // (SRMI_NO_CSTAMP: the body's stamps only)
 #define CSTAMP(i)                                                                                           \
   do {                                                                                                      \
     if (c.stamps && threadIdx.x == 0) c.stamps[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memtime();       \
