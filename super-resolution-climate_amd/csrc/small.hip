@@ -1159,7 +1159,17 @@ __global__ void __launch_bounds__(256) ca_fwd_kernel(const T* __restrict__ u, co
   // (unconditional loads at clamped indices -- no divergent branches, so the
   //  compiler's vmcnt accounting stays exact across the stream loads below)
   float pa = 0.f;
-  for (int k = tid >> 6; k < nstrips; k += 4) pa += part[((size_t)n * nstrips + k) * C + (tid & 63)];
+  {  // (the strip records issued at once, as in ca_bwd_du_kernel)
+    constexpr int KU = 4;
+    float pv[KU];
+    const float* pp = part + (size_t)n * nstrips * C + (tid & 63);
+#pragma unroll
+    for (int i = 0; i < KU; ++i) pv[i] = pp[(size_t)min((tid >> 6) + 4 * i, nstrips - 1) * C];
+#pragma unroll
+    for (int i = 0; i < KU; ++i)
+      if ((tid >> 6) + 4 * i < nstrips) pa += pv[i];
+    for (int k = (tid >> 6) + 4 * KU; k < nstrips; k += 4) pa += pp[(size_t)k * C];
+  }
   const int jc = min(j, CR - 1);
   float wa[8], wb[8];
 #pragma unroll
@@ -1326,7 +1336,18 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
   const int j = tid >> 3, pj = tid & 7;
   const int c4 = tid >> 2, p4 = tid & 3, per = CR / 4;
   float pa = 0.f;  // G[c] = sum_p g, ds[c] = sum_p g*u (MLP operands first, see ca_fwd_kernel)
-  for (int k = tid >> 7; k < nstrips; k += 2) pa += part[((size_t)n * nstrips + k) * (2 * C) + (tid & 127)];
+  {  // the strip records: up to 16 issued at once (clamped, unconditional), then summed in
+     // strip order; a plain loop issued them one load and one wait at a time (~0.7 us each)
+    constexpr int KU = 8;
+    float pv[KU];
+    const float* pp = part + (size_t)n * nstrips * (2 * C) + (tid & 127);
+#pragma unroll
+    for (int i = 0; i < KU; ++i) pv[i] = pp[(size_t)min((tid >> 7) + 2 * i, nstrips - 1) * (2 * C)];
+#pragma unroll
+    for (int i = 0; i < KU; ++i)
+      if ((tid >> 7) + 2 * i < nstrips) pa += pv[i];
+    for (int k = (tid >> 7) + 2 * KU; k < nstrips; k += 2) pa += pp[(size_t)k * (2 * C)];
+  }
   const int jc = min(j, CR - 1);
   float wa[8], wb[8];  // W2 column slice (dz1 lane group j), W1 column slice (dm lane group c)
 #pragma unroll
