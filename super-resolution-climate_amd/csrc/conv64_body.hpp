@@ -303,6 +303,19 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
     const auto rph = wt_rsrc(p.yph, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
     const auto rpl = wt_rsrc(p.ypl, (uint32_t)((size_t)p.N * HW * p.Cout));
     const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
+    // every run's u first (the stage's last reads), then the strip-end barrier here (the
+    // body skips its own for these epilogues), then the arithmetic and the stores: the
+    // stores' issue no longer holds every wave at that barrier
+    uint2 ubs[RUNS];
+#pragma unroll
+    for (int q = 0; q < RUNS; ++q) {
+      const int h = q / (RUNS / 2), i = 2 * (q % (RUNS / 2)) + half_id;
+      const int lin = i * 1024 + lane * 16, px = h * HALF + (lin >> 8), c = (lin >> 4) & 15;
+      ubs[q] = *reinterpret_cast<const uint2*>(stage + px * 128 + (((c >> 1) ^ (px & 7)) << 4) + (c & 1) * 8);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -310,8 +323,8 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
         // run i of the half: pixels 4 (i & ..) -- lane = channels 4c..4c+3 of pixel px
         const int i = 2 * j + half_id;
         const int lin = i * 1024 + lane * 16, px = h * HALF + (lin >> 8), c = (lin >> 4) & 15;
-        const uint2 ub = *reinterpret_cast<const uint2*>(stage + px * 128 + (((c >> 1) ^ (px & 7)) << 4) + (c & 1) * 8);
         const int q = h * (RUNS / 2) + j;
+        const uint2 ub = ubs[q];
         float4 hh = e.r1[q / NCT][q % NCT];
         if (p.r1h) hh = pair_decode4(make_uint2(__float_as_uint(hh.x), __float_as_uint(hh.y)), __float_as_uint(hh.z));
         const uint32_t oe = (uint32_t)((pix0 + px) * p.Cout + cb * 64 + c * 4);  // element
@@ -323,8 +336,6 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
         st_wt8(rph, p.yph, oe * 2, hi);
         st_wt4(rpl, p.ypl, oe, lo);
       }
-    // (no closing barrier: the body's barrier after the epilogue orders the staging
-    //  slot's reuse by group k+3's DMA)
     return;
   }
   // fp32 output: staged in LDS in two halves of the row (256 B per pixel,
@@ -792,9 +803,12 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
                                   tid, ring + (k % 3) * S::GROUPB + row * TW * 128, fs, &cpart, kMp && cpon);
     STAMP(sj + 3);
     // LDS-only barrier: this strip's global stores stay in flight into the next strip
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    // (the bf16-staged conv2 epilogues run it themselves, after their last stage reads)
+    if constexpr (!epi_cr_bf16<EPI>()) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
     STAMP(sj + 4);
   }
   if constexpr (kMp) {
