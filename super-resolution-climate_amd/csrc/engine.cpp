@@ -317,9 +317,10 @@ static size_t carve(srmi_engine* e, char* base) {
     e->slab = cv.take<float>(sf);
     e->bslab = cv.take<float>(bf);
     if (rcan) {  // the RCAB filter-gradient slab sets (64-channel convs only)
-      size_t ns = 0;
+      size_t ns = 0;  // (wgrad48: a slab per 48-wide column tile too, as wgrad3x3_nslabs counts)
       for (int n = 1; n <= N; ++n)
-        ns = std::max(ns, (size_t)n * std::max(rcab_row_splits(e, n, 1), rcab_row_splits(e, n, 2)));
+        ns = std::max(ns, (size_t)n * std::max(rcab_row_splits(e, n, 1), rcab_row_splits(e, n, 2)) *
+                              (e->w % 48 == 0 ? e->w / 48 : 1));
       e->slab_r_floats = ns * 64 * 576;
       e->bslab_r_floats = ns * 64;
       for (int q = 0; q < 2; ++q)

@@ -342,15 +342,17 @@ def _engine_variants_agree(lr_hw, flags, grad_tol, fwd_tol=None):
         assert rel_l2(ga[off:off + n], gb[off:off + n]) < 3e-2, name
 
 
-@pytest.mark.parametrize("lr_hw", [(48, 48), (32, 48), (8, 48)])
+@pytest.mark.parametrize("lr_hw", [(48, 48), (32, 48), (8, 48), (24, 96)])
 def test_ca_forward_in_conv2_matches_ca_pass(lr_hw):
-    """The training CA forward inside conv2's launch (the default: conv1 writes t and
-    the per-strip sums of the bf16 t, every conv2 workgroup derives its image's mean(u)
-    from t's statistics and conv2's bf16 filter image, runs the CA MLP and writes u and
-    h' = h + s bf16(u); engine.cpp ca_fwd_mode) against the CA pass of its own
-    (SRMI_FLAG_CA_PASS: conv2 + pool writing u, then ca_fwd).  mean(u) differs only in
-    fp32 summation order, so the forward agrees far below bf16 noise and the gradients
-    (the backward reads the same stored u and record) to that order; both sit within the
-    oracle's drift bounds.  Three tile heights move the border rows between strips."""
+    """The training CA forward inside conv2's launch (the default: conv1 writes t, the
+    per-strip sums of the bf16 t and per workgroup its rows' share of mean(u) -- the
+    matvec on conv2's bf16 filter image, SRMI_CA_MPART; every conv2 workgroup sums the
+    shares, runs the CA MLP and writes u and h' = h + s bf16(u); engine.cpp ca_fwd_mode)
+    against the CA pass of its own (SRMI_FLAG_CA_PASS: conv2 + pool writing u, then
+    ca_fwd).  mean(u) differs only in fp32 summation order, so the forward agrees far
+    below bf16 noise and the gradients (the backward reads the same stored u and record)
+    to that order; both sit within the oracle's drift bounds.  Three tile heights move
+    the border rows between runs; the 96-wide tiles put columns 0 and W-1 (and the
+    corners) in different workgroups."""
     from srmi._lib import SRMI_FLAG_CA_PASS
     _engine_variants_agree(lr_hw, (0, SRMI_FLAG_CA_PASS), 5e-3, fwd_tol=1e-3)
