@@ -95,10 +95,6 @@ __device__ __forceinline__ void ca_scale_load_params(const CaScale& c, CaScalePr
   q.b2 = c.b2[c8];
   q.bc2 = c.bc2[c8];
 }
-__device__ __forceinline__ void ca_scale_load(const CaScale& c, int n, int H, int W, CaScalePre& q) {
-  ca_scale_load_t(c, n, H, W, q);
-  ca_scale_load_params(c, q);
-}
 
 // The partial-mean path (training, SRMI_CA_MPART): conv1's workgroups leave their share of
 // the matvec in c.mpart [N][nruns][64]; conv2 issues the first kCaPreStrips of them (and
