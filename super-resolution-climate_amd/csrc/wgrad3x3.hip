@@ -629,8 +629,9 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
   ConvParams c = cp;
   c.stamps = conv3x3_stamps_for(epi);  // (null in production; the dgrad runs' phase stamps in diagnostic builds)
   WgradParams w = wp;
-  w.stamps = nullptr;
   const dim3 grid(nconv + nwg);
+  // (diagnostic: the filter-gradient body's stamps in a second [grid][64] region)
+  w.stamps = c.stamps ? c.stamps + (size_t)grid.x * 64 : nullptr;
   // conv run k and wgrad chunk k cover the same rows of the same image
   const int runs_per_col = (cp.H / kTH + run_len - 1) / run_len;
   const int paired =

@@ -45,7 +45,18 @@ def main():
         call("srmi_debug_conv_stamps", None)
         flat = buf.view(-1, 64).cpu().numpy().astype(np.int64)
         if epi in (4, 7):  # fused launch: the dgrad runs' blocks among the filter-gradient ones
-            body = flat[:4096][flat[:4096, 0] != 0]
+            # [grid][64] dgrad rows, then [grid][64] filter-gradient rows (the launch's last
+            # block is a filter-gradient one, so its row ends the second region)
+            grid = (int(np.nonzero(flat[:8192, 0])[0][-1]) + 1) // 2
+            wg = flat[grid:2 * grid]
+            wg = wg[(wg[:, 0] != 0) & (wg[:, 63] != 0)]
+            if len(wg):  # the filter-gradient bodies (wgrad48 WSTAMP 0 .. 63)
+                print(f"  ({name[:2]} filter-gradient chunks: {len(wg)}, span median {np.median(wg[:, 63] - wg[:, 0]):.0f}, "
+                      f"p90 {np.percentile(wg[:, 63] - wg[:, 0], 90):.0f}; their start after the launch's first "
+                      f"stamp: median {np.median(wg[:, 0] - flat[:grid, 0][flat[:grid, 0] != 0].min()):.0f})")
+                print(f"    filter-gradient prologue median {np.median(wg[:, 1] - wg[:, 0]):.0f}, main loop median "
+                      f"{np.median(wg[:, 62 if np.all(wg[:, 62]) else 1] - wg[:, 1]):.0f}")
+            body = flat[:grid][flat[:grid, 0] != 0]
             nst = np.array([sum(1 for j in range(11) if r[2 + 5 * j + 4] != 0) for r in body])
             if epi == 7 and (nst == 1).any() and (nst > 1).any():
                 t = body[nst == 1]
