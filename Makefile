@@ -9,7 +9,7 @@ CXXFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-functi
 HIPSRC := $(SRC)/conv3x3.hip $(SRC)/conv_f32.hip $(SRC)/wgrad3x3.hip $(SRC)/small.hip $(SRC)/tiles.hip $(SRC)/rcab_infer.hip
 CPPSRC := $(SRC)/engine.cpp
 OBJS := $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.o,$(HIPSRC)) $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(CPPSRC))
-HDRS := $(SRC)/common.hpp $(SRC)/srmi_internal.hpp $(SRC)/conv64_body.hpp $(SRC)/wgrad_reduce.hpp $(SRC)/ca_scale.hpp include/srmi.h
+HDRS := $(SRC)/tuning.hpp $(SRC)/common.hpp $(SRC)/srmi_internal.hpp $(SRC)/conv64_body.hpp $(SRC)/wgrad_reduce.hpp $(SRC)/ca_scale.hpp include/srmi.h
 
 all: $(OUT)
 

@@ -55,6 +55,13 @@
 #define SRMI_CA_MPART 1
 #endif
 
+// the fused backward's tail strips (wgrad3x3.hip rcab_bwd_kernel): run by the paired
+// filter-gradient workgroup after its chunk (0) or before it (1: +0.2-0.4 % in the step,
+// profiles/r05_ab_tail_first.txt; the chunk's slab stores no longer meet the dgrad runs' loads)
+#ifndef SRMI_FUSE_TAIL_FIRST
+#define SRMI_FUSE_TAIL_FIRST 1
+#endif
+
 // waves per workgroup of the exact-fp32 conv (conv_f32.hip)
 #ifndef SRMI_F32_NW
 #define SRMI_F32_NW 8

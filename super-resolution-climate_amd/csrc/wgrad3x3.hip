@@ -598,11 +598,20 @@ __global__ void __launch_bounds__(NW * 64, 1) rcab_bwd_kernel(ConvParams cp, int
     return;
   }
   const int nch = wp.N * wp.row_splits;
+#if SRMI_FUSE_TAIL_FIRST
+  if (tail > 0) {
+    conv64_body<48, EPI, NW>(cp, run_len, w, smem, tail, true);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave is past its last LDS access of the strips
+  }
+  wgrad48_dispatch<NW>(wp, smem, w % nch, w / nch);
+#else
   wgrad48_dispatch<NW>(wp, smem, w % nch, w / nch);
   if (tail > 0) {
     __syncthreads();  // every wave is past its last LDS read of the chunk
     conv64_body<48, EPI, NW>(cp, run_len, w, smem, tail, true);
   }
+#endif
 }
 
 int rcab_bwd_fusable(const ConvParams& cp, const WgradParams& wp) {
