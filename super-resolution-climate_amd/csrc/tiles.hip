@@ -70,6 +70,69 @@ __global__ void __launch_bounds__(256) region_to_tiles_kernel(const float* __res
   }
 }
 
+// The same with the tile held in registers: 1024 threads, float4 loads, every region
+// element read once (the form above reads it three times with scalar loads: 157 us
+// for the C5 region, 0.84 TB/s).  Needs tx, W multiples of 4 and ty * tx / 4 <= 1024 * KR.
+constexpr int kR2tKR = 12;
+__device__ __forceinline__ float block_sum1024(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; i += 2) s += red[i] + red[i + 1];
+  __syncthreads();
+  return s;
+}
+__global__ void __launch_bounds__(1024) region_to_tiles_reg_kernel(const float* __restrict__ region, int C, int H,
+                                                                   int W, int ty, int tx, int gx,
+                                                                   float* __restrict__ tiles, float* __restrict__ mean,
+                                                                   float* __restrict__ stdv, int* __restrict__ bad) {
+  __shared__ float red[16];
+  const int c = blockIdx.x, t = blockIdx.y;
+  const int y0 = (t / gx) * ty, x0 = (t % gx) * tx;
+  const float* src = region + (size_t)c * H * W + (size_t)y0 * W + x0;
+  const int tx4 = tx >> 2, n4 = ty * tx4, n = ty * tx;
+  float4 v[kR2tKR];
+  float s = 0.f;
+  int nonfinite = 0;
+#pragma unroll
+  for (int j = 0; j < kR2tKR; ++j) {
+    const int i = threadIdx.x + j * 1024;
+    v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < n4) {
+      const int r = i / tx4, q = i - r * tx4;
+      v[j] = *reinterpret_cast<const float4*>(src + (size_t)r * W + 4 * q);
+      s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+      nonfinite |= !(isfinite(v[j].x) && isfinite(v[j].y) && isfinite(v[j].z) && isfinite(v[j].w));
+    }
+  }
+  const float m = block_sum1024(s, red) / (float)n;
+  float qs = 0.f;
+#pragma unroll
+  for (int j = 0; j < kR2tKR; ++j) {
+    if (threadIdx.x + j * 1024 < n4) {
+      const float a = v[j].x - m, b = v[j].y - m, cc = v[j].z - m, d = v[j].w - m;
+      qs += (a * a + b * b) + (cc * cc + d * d);
+    }
+  }
+  const float sd = sqrtf(block_sum1024(qs, red) / (float)n);
+  const float inv = 1.f / sd;
+  float4* dst = reinterpret_cast<float4*>(tiles + ((size_t)t * C + c) * n);
+#pragma unroll
+  for (int j = 0; j < kR2tKR; ++j) {
+    const int i = threadIdx.x + j * 1024;
+    if (i < n4) dst[i] = make_float4((v[j].x - m) * inv, (v[j].y - m) * inv, (v[j].z - m) * inv, (v[j].w - m) * inv);
+  }
+  const int anybad = __syncthreads_or(nonfinite);
+  if (threadIdx.x == 0) {
+    mean[(size_t)t * C + c] = m;
+    stdv[(size_t)t * C + c] = sd;
+    if (bad && anybad) atomicOr(&bad[t], 1);
+  }
+}
+
 int region_to_tiles_launch(const float* region, int C, int H, int W, int ty, int tx, float* tiles, float* mean,
                            float* stdv, int* bad, hipStream_t st) {
   if (C < 1 || ty < 1 || tx < 1 || H < ty || W < tx) return SRMI_ERR_SHAPE;
@@ -78,8 +141,14 @@ int region_to_tiles_launch(const float* region, int C, int H, int W, int ty, int
     const hipError_t e = hipMemsetAsync(bad, 0, sizeof(int) * gy * gx, st);
     if (e != hipSuccess) return -(int)e;
   }
-  hipLaunchKernelGGL(region_to_tiles_kernel, dim3(C, gy * gx), dim3(256), 0, st, region, C, H, W, ty, tx, gx, tiles,
-                     mean, stdv, bad);
+  const bool reg = tx % 4 == 0 && W % 4 == 0 && (size_t)ty * (tx / 4) <= (size_t)1024 * kR2tKR &&
+                   ((uintptr_t)region & 15) == 0 && ((uintptr_t)tiles & 15) == 0;
+  if (reg)
+    hipLaunchKernelGGL(region_to_tiles_reg_kernel, dim3(C, gy * gx), dim3(1024), 0, st, region, C, H, W, ty, tx, gx,
+                       tiles, mean, stdv, bad);
+  else
+    hipLaunchKernelGGL(region_to_tiles_kernel, dim3(C, gy * gx), dim3(256), 0, st, region, C, H, W, ty, tx, gx, tiles,
+                       mean, stdv, bad);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

@@ -25,10 +25,11 @@ def rel_l2(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
-def test_region_tiles_kernels():
+@pytest.mark.parametrize("wextra", [3, 4])  # W % 4 != 0: the scalar kernel; == 0: the register-resident one
+def test_region_tiles_kernels(wextra):
     d = dev()
     rng = np.random.RandomState(4)
-    region = (rng.randn(2, 3 * 40 + 7, 2 * 56 + 3) * 3 + 1).astype(np.float32)
+    region = (rng.randn(2, 3 * 40 + 7, 2 * 56 + wextra) * 3 + 1).astype(np.float32)
     C, H, W = region.shape
     ty, tx = 40, 56
     n = (H // ty) * (W // tx)
