@@ -692,13 +692,15 @@ int tail_wgrad_reduce_launch(const float* slab, int nslab, int C, float* gw, flo
 // ====================================================================== resampling
 // bicubic (A = -0.75, align_corners = False) at 1/scale: the source coordinate
 // scale*d + (scale-1)/2 is half-way between samples -> separable [-3,19,19,-3]/32
+// grid (ceil(h w / 256), NC): 32-bit index arithmetic within one plane (64-bit
+// divisions of a flat index cost more than the loads)
 __global__ void downsample_kernel(const float* __restrict__ hr, int NC, int H, int W, int scale,
                                   float* __restrict__ lr) {
   const int h = H / scale, w = W / scale;
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (size_t)NC * h * w) return;
-  const int x = idx % w, y = (idx / w) % h;
-  const size_t nc = idx / ((size_t)w * h);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= h * w) return;
+  const int x = i % w, y = i / w;
+  const size_t nc = blockIdx.y, idx = nc * h * w + i;
   const float k[4] = {-3.f / 32.f, 19.f / 32.f, 19.f / 32.f, -3.f / 32.f};
   const int sy = y * scale + scale / 2 - 2, sx = x * scale + scale / 2 - 2;
   const float* src = hr + nc * H * W;
@@ -719,8 +721,9 @@ __global__ void downsample_kernel(const float* __restrict__ hr, int NC, int H, i
 
 int downsample_launch(const float* hr, int N, int C, int H, int W, int scale, float* lr, hipStream_t st) {
   if (scale < 2 || H % scale || W % scale) return SRMI_ERR_SHAPE;
-  const size_t tot = (size_t)N * C * (H / scale) * (W / scale);
-  hipLaunchKernelGGL(downsample_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, hr, N * C, H, W, scale, lr);
+  const int plane = (H / scale) * (W / scale);
+  if (N * C > 65535) return SRMI_ERR_SHAPE;
+  hipLaunchKernelGGL(downsample_kernel, dim3((plane + 255) / 256, N * C), dim3(256), 0, st, hr, N * C, H, W, scale, lr);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
@@ -740,10 +743,10 @@ __device__ __forceinline__ void cubic_w(float t, float* c) {
 __global__ void upsample_kernel(const float* __restrict__ lr, int NC, int h, int w, int scale,
                                 float* __restrict__ hr) {
   const int H = h * scale, W = w * scale;
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (size_t)NC * H * W) return;
-  const int X = idx % W, Y = (idx / W) % H;
-  const size_t nc = idx / ((size_t)W * H);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // grid (ceil(H W / 256), NC)
+  if (i >= H * W) return;
+  const int X = i % W, Y = i / W;
+  const size_t nc = blockIdx.y, idx = nc * H * W + i;
   const float inv = 1.f / (float)scale;
   const float sy = inv * (Y + 0.5f) - 0.5f, sx = inv * (X + 0.5f) - 0.5f;
   const int iy = (int)floorf(sy), ix = (int)floorf(sx);
@@ -767,8 +770,9 @@ __global__ void upsample_kernel(const float* __restrict__ lr, int NC, int h, int
 }
 
 int upsample_launch(const float* lr, int N, int C, int h, int w, int scale, float* hr, hipStream_t st) {
-  const size_t tot = (size_t)N * C * h * scale * w * scale;
-  hipLaunchKernelGGL(upsample_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, lr, N * C, h, w, scale, hr);
+  const int plane = h * scale * w * scale;
+  if (N * C > 65535) return SRMI_ERR_SHAPE;
+  hipLaunchKernelGGL(upsample_kernel, dim3((plane + 255) / 256, N * C), dim3(256), 0, st, lr, N * C, h, w, scale, hr);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
@@ -970,6 +974,43 @@ __global__ void __launch_bounds__(256) tile_loss_sums_kernel(const float* __rest
   if (threadIdx.x == 0) sums[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// the same with 1024 threads and float4 loads, 4 in flight per thread (tile_elems % 4
+// == 0, 16-byte aligned operands): the 256-thread scalar form above is latency bound
+// at one workgroup per tile (C5: 441 tiles of 36864 elements, 78 us)
+__global__ void __launch_bounds__(1024) tile_loss_sums_v4_kernel(const float4* __restrict__ y,
+                                                                  const float4* __restrict__ t, long long tile_v4,
+                                                                  int kind, float eps, float* __restrict__ sums) {
+  __shared__ float red[16];
+  const size_t base = (size_t)blockIdx.x * (size_t)tile_v4;
+  auto term = [&](float d) { return kind == LOSS_MEAN ? sqrtf(d * d + eps) : d * d; };
+  float s = 0.f;
+  long long i = threadIdx.x;
+  for (; i + 3 * 1024 < tile_v4; i += 4 * 1024) {
+    float4 a[4], c[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = y[base + i + u * 1024];
+      c[u] = t[base + i + u * 1024];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      s += (term(a[u].x - c[u].x) + term(a[u].y - c[u].y)) + (term(a[u].z - c[u].z) + term(a[u].w - c[u].w));
+  }
+  for (; i < tile_v4; i += 1024) {
+    const float4 a = y[base + i], c = t[base + i];
+    s += (term(a.x - c.x) + term(a.y - c.y)) + (term(a.z - c.z) + term(a.w - c.w));
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) r += red[k] + red[k + 1];
+    sums[blockIdx.x] = r;
+  }
+}
+
 __global__ void __launch_bounds__(256) batch_loss_mean_kernel(const float* __restrict__ sums, int ntiles,
                                                               long long tile_elems, int bs, int kind,
                                                               float* __restrict__ out) {
@@ -995,7 +1036,11 @@ __global__ void __launch_bounds__(256) batch_loss_mean_kernel(const float* __res
 int batch_losses_launch(const float* y, const float* t, int ntiles, long long tile_elems, int bs, int kind, float eps,
                         float* work, float* out, hipStream_t st) {
   if (ntiles < 1 || tile_elems < 1 || bs < 1 || (ntiles + bs - 1) / bs > 1024) return SRMI_ERR_SHAPE;
-  hipLaunchKernelGGL(tile_loss_sums_kernel, dim3(ntiles), dim3(256), 0, st, y, t, tile_elems, kind, eps, work);
+  if (tile_elems % 4 == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)t & 15) == 0)
+    hipLaunchKernelGGL(tile_loss_sums_v4_kernel, dim3(ntiles), dim3(1024), 0, st, reinterpret_cast<const float4*>(y),
+                       reinterpret_cast<const float4*>(t), tile_elems / 4, kind, eps, work);
+  else
+    hipLaunchKernelGGL(tile_loss_sums_kernel, dim3(ntiles), dim3(256), 0, st, y, t, tile_elems, kind, eps, work);
   SRMI_CHECK_LAUNCH();
   hipLaunchKernelGGL(batch_loss_mean_kernel, dim3(1), dim3(256), 0, st, work, ntiles, tile_elems, bs, kind, out);
   SRMI_CHECK_LAUNCH();

@@ -25,13 +25,15 @@ def rel_l2(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
-@pytest.mark.parametrize("wextra", [3, 4])  # W % 4 != 0: the scalar kernel; == 0: the register-resident one
-def test_region_tiles_kernels(wextra):
+# W % 4 != 0: the scalar region_to_tiles; == 0: the register-resident one.  tx % 4 != 0:
+# the scalar tiles_to_region; == 0: the float4 one
+@pytest.mark.parametrize("wextra,tx", [(3, 56), (4, 56), (3, 55)])
+def test_region_tiles_kernels(wextra, tx):
     d = dev()
     rng = np.random.RandomState(4)
     region = (rng.randn(2, 3 * 40 + 7, 2 * 56 + wextra) * 3 + 1).astype(np.float32)
     C, H, W = region.shape
-    ty, tx = 40, 56
+    ty = 40
     n = (H // ty) * (W // tx)
     rg = torch.tensor(region, device=d)
     tiles = torch.empty(n, C, ty, tx, device=d)

@@ -429,6 +429,23 @@ def test_batch_losses_beyond_1024_tiles_one_batch():
         call("srmi_batch_losses", ptr(y), ptr(t), n, te, 1, _lib.SRMI_LOSS_RMSE, 1e-6, ptr(work), ptr(out), S())
 
 
+@pytest.mark.parametrize("te", [50, 4 * (2 * 4096 + 777)])  # the scalar kernel; the float4 one past its unrolled loop
+@pytest.mark.parametrize("kind", [0, 1])
+def test_tile_loss_sums_both_kernels(te, kind):
+    d = dev()
+    n = 7
+    g = torch.Generator(device="cpu").manual_seed(5)
+    y = torch.randn(n, te, generator=g).to(d)
+    t = torch.randn(n, te, generator=g).to(d)
+    work = torch.zeros(n, device=d)
+    out = torch.zeros(1 + n, device=d)
+    call("srmi_batch_losses", ptr(y), ptr(t), n, te, 1, kind, 1e-6, ptr(work), ptr(out), S())
+    torch.cuda.synchronize()
+    dd = y.double() - t.double()
+    ref = (dd * dd).sum(dim=1) if kind == 0 else torch.sqrt(dd * dd + 1e-6).sum(dim=1)
+    assert rel_l2(work, ref) < 1e-6
+
+
 def test_adam_matches_reference():
     import os
     d = dev()
