@@ -576,8 +576,8 @@ __global__ void __launch_bounds__(kWgradNW * 64, 1) wgrad48_kernel(WgradParams p
 //
 // tail > 0 (paired map only): the filter-gradient half finishes earlier than the
 // dgrad half (F1: 24.7 vs 36.9 us at C2), so the last `tail` strips of dgrad run k
-// move to the workgroup of chunk k, which runs them after its chunk (same rows, same
-// XCD), with its own filter prologue.
+// move to the workgroup of chunk k, which runs them before its chunk (same rows, same
+// XCD), with its own filter prologue (SRMI_FUSE_TAIL_FIRST; after it: 0).
 template <int EPI, int NW>
 __global__ void __launch_bounds__(NW * 64, 1) rcab_bwd_kernel(ConvParams cp, int run_len, int nconv, WgradParams wp,
                                                               int nwg, int paired, int tail) {
