@@ -132,7 +132,10 @@ int srmi_backward(srmi_engine* e, const float* params, const float* lr, const fl
  * residual group's gradient all-reduce right behind that group, srmi.trainer): stages
  * 0 = tail conv, upsamplers and body tail; 1 .. nlayers = residual groups nlayers-1 ..
  * 0; nlayers + 1 = head (RCAN; EDSR has one stage).  srmi_backward_stages runs stages
- * first .. last (in order, each exactly once per backward); group_events as above. */
+ * first .. last (in order, each exactly once per backward); group_events as above.
+ * The engine tracks the next stage: `first` must be it (0 after a forward or a
+ * completed backward), else SRMI_ERR_ARG and nothing is enqueued; srmi_backward is
+ * refused while a staged backward is half-way through. */
 int srmi_backward_stage_count(srmi_engine* e);
 int srmi_backward_stages(srmi_engine* e, const float* params, const float* lr, const float* sr, const float* hr,
                          const float* loss4, const float* dy, float* grads, void** group_events, int first, int last,
@@ -158,7 +161,9 @@ int srmi_rmse_finalize(float* loss4, void* stream);
  * sres/controller/dual_trainer.py:196-198): loss4[0] = sum sqrt(d^2 + eps) (this
  * rank), loss4[1] = count_global; dy (optional, like pred) = d / sqrt(d^2 + eps) /
  * count_global -- the upstream gradient srmi_backward takes.  Finalise with
- * srmi_loss_finalize(loss4, SRMI_LOSS_MEAN): loss4[3] = loss4[0] / loss4[1]. */
+ * srmi_loss_finalize(loss4, SRMI_LOSS_MEAN): loss4[3] = loss4[0] / loss4[1].
+ * loss4 NULL (dy required): dy only, no loss sums (the trainer takes the loss from
+ * srmi_tile_loss_parts). */
 #define SRMI_LOSS_RMSE 0
 #define SRMI_LOSS_MEAN 1
 int srmi_charbonnier_partial(srmi_engine* e, const float* pred, const float* target, size_t n, double count_global,

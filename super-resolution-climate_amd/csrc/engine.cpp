@@ -217,6 +217,10 @@ struct srmi_engine {
   int max_cob = 0, max_cib = 0;  // largest Cout / 64, Cin / 64 of the packed convs
   bool tables_uploaded = false;
   int last_n = 0;
+  // the backward stage srmi_backward_stages must run next (0 after a forward or a
+  // completed backward): the gradient-stream buffers and the slab parity carry over
+  // from one stage to the next, so a skipped, repeated or reordered stage is refused
+  int next_stage = 0;
   const float* probe_prm = nullptr;  // the parameters of the last backward / inference forward (srmi_engine_probe)
 
   bf16_t* at(bf16_t* base, size_t elems) const {
@@ -666,6 +670,7 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
   }
   RC(tail_fwd_launch(cur, prm + P.tail.w, prm + P.tail.b, n, e->Co, H, W, sr, e->f32, st));
   e->last_n = n;
+  e->next_stage = 0;
   if (!e->train) e->probe_prm = prm;  // (srmi_engine_probe which = 3)
   return 0;
 }
@@ -884,6 +889,7 @@ int srmi_backward(srmi_engine* e, const float* params, const float* lr, const fl
                   const float* loss4, const float* dy, float* grads, void** group_events, void* stream) {
   if (!e || !e->train || !params || !lr || !grads || e->last_n < 1) return SRMI_ERR_ARG;
   if (!dy && (!sr || !hr || !loss4)) return SRMI_ERR_ARG;
+  if (e->next_stage != 0) return SRMI_ERR_ARG;  // a staged backward is half-way through
   return backward_impl(e, params, lr, sr, hr, loss4, dy, grads, group_events, S_(stream));
 }
 
@@ -896,7 +902,10 @@ int srmi_backward_stages(srmi_engine* e, const float* params, const float* lr, c
   if (!dy && (!sr || !hr || !loss4)) return SRMI_ERR_ARG;
   const int ns = backward_stages(e);
   if (first < 0 || last >= ns || first > last || (ns == 1 && (first != 0 || last != 0))) return SRMI_ERR_ARG;
-  return backward_impl(e, params, lr, sr, hr, loss4, dy, grads, group_events, S_(stream), first, last);
+  if (first != e->next_stage) return SRMI_ERR_ARG;  // stages run in order, each once per backward
+  RC(backward_impl(e, params, lr, sr, hr, loss4, dy, grads, group_events, S_(stream), first, last));
+  e->next_stage = last + 1 == ns ? 0 : last + 1;
+  return 0;
 }
 
 int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
@@ -959,9 +968,9 @@ int srmi_rmse_finalize(float* loss4, void* stream) {
 
 int srmi_charbonnier_partial(srmi_engine* e, const float* pred, const float* target, size_t n, double count_global,
                              float eps, float* loss4, float* dy, void* stream) {
-  if (!e || !pred || !target || !loss4 || count_global <= 0) return SRMI_ERR_ARG;
-  RC(charb_partial_launch(pred, target, n, eps, count_global, dy, e->lpart, e->lpart_n, S_(stream)));
-  return sqerr_finish_launch(e->lpart, e->lpart_n, count_global, loss4, S_(stream));
+  if (!e || !pred || !target || (!loss4 && !dy) || count_global <= 0) return SRMI_ERR_ARG;
+  RC(charb_partial_launch(pred, target, n, eps, count_global, dy, loss4 ? e->lpart : nullptr, e->lpart_n, S_(stream)));
+  return loss4 ? sqerr_finish_launch(e->lpart, e->lpart_n, count_global, loss4, S_(stream)) : 0;
 }
 
 int srmi_loss_finalize(float* loss4, int kind, void* stream) {

@@ -11,9 +11,10 @@
 //            conv2's bf16 filter image in LDS, the CA MLP                      ca_scale_finish
 // against the three launches of the training forward (conv1; conv2 + pool writing u;
 // the CA pass reading u, h and writing h'): per image 0.6 MB less traffic and no
-// elementwise pass.  It differs from them in summation order (m from t's statistics
-// instead of the pooled fp32 u) and in adding the fp32 u to h (the three launches add
-// bf16(u)): both within bf16 noise of the fp64 oracle
+// elementwise pass.  It differs from them in summation order only (m from t's
+// statistics instead of the pooled u): like them it rounds u to bf16 before
+// h' = h + s * bf16(u) (SRMI_INFER_BF16U=1, the default; the =0 variant adds the fp32 u
+// instead), within bf16 noise of the fp64 oracle
 // (test_fused_inference_rcab_matches_three_launches_and_oracle).
 // (write-back stores and the deferred conv1 epilogue: tuning.hpp SRMI_INFER_*)
 #define SRMI_TU_INFER 1

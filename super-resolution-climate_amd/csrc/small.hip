@@ -900,6 +900,7 @@ __global__ void __launch_bounds__(256) charb_partial_kernel(const float* __restr
     s += r;
     if (dy) dy[i] = d / r * inv_count;
   }
+  if (!partial) return;  // dy only (uniform branch: no barrier is skipped by part of the block)
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();

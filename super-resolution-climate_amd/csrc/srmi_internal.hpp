@@ -192,9 +192,6 @@ int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float
 int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* part, int nstrips, const float* w1,
                       const float* b1, const float* w2, const float* b2, int CR, const float* h_in, const void* hi_in,
                       const void* lo_in, void* hi_out, void* lo_out, float* rec, hipStream_t st);
-// the CA scale of every image of an RCAB as its own launch (a 512-thread workgroup per
-// image; conv2's filter pack wpack, forward layout): the A/B alternative to computing it
-// in the conv2 prologue
 // records of consecutive RCABs Ncap images apart (the engine capacity), N summed
 int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int Ncap, int C, int R,
                                   const long long* offs, float* grads, hipStream_t st);

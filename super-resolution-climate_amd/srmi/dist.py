@@ -62,12 +62,41 @@ def init_from_env(backend: Optional[str] = None, force: bool = False) -> DistInf
     return DistInfo(rank, world, local, force=force and world <= 1)
 
 
-def shard_range(global_batch: int, info: DistInfo) -> Tuple[int, int]:
-    """Contiguous tile shard of this rank."""
-    if global_batch % info.world:
-        raise ValueError(f"global batch {global_batch} not divisible by world size {info.world}")
-    per = global_batch // info.world
-    return info.rank * per, (info.rank + 1) * per
+def shard_range(global_batch: int, info: DistInfo, rank: Optional[int] = None) -> Tuple[int, int]:
+    """Contiguous tile shard [a, b) of this rank.  A batch that does
+    not divide (the short last batch of a time slice, TileBatchIterator,
+    sres/data/tiles.py:55-72) is split as evenly as it goes: the first
+    global_batch % world ranks take one tile more, and a rank may get none."""
+    if global_batch < 0:
+        raise ValueError(f"negative batch {global_batch}")
+    r = info.rank if rank is None else rank
+    base, rem = divmod(global_batch, info.world)
+    a = r * base + min(r, rem)
+    return a, a + base + (1 if r < rem else 0)
+
+
+def shard_capacity(global_batch: int, info: DistInfo) -> int:
+    """The largest shard of a global batch (the per-rank trainer batch it needs)."""
+    return -(-global_batch // info.world)
+
+
+def broadcast_ints(values: Sequence[int], info: DistInfo, device: Optional[torch.device] = None) -> List[int]:
+    """rank 0's integers on every rank (len(values) must agree across ranks).  RCCL
+    needs a device tensor; gloo takes either."""
+    if not info.enabled or not values:
+        return list(values)
+    dev = device if (device is not None and dist.get_backend() == "nccl") else torch.device("cpu")
+    t = torch.tensor(list(values), dtype=torch.int64, device=dev)
+    dist.broadcast(t, 0)
+    return [int(x) for x in t.cpu().tolist()]
+
+
+def barrier(info: DistInfo, device: Optional[torch.device] = None) -> None:
+    if info.enabled:
+        if dist.get_backend() == "nccl" and device is not None and device.type == "cuda":
+            dist.barrier(device_ids=[device.index if device.index is not None else torch.cuda.current_device()])
+        else:
+            dist.barrier()
 
 
 def allreduce_sum_(t: torch.Tensor, info: DistInfo):

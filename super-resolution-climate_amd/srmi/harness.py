@@ -15,6 +15,10 @@ CSV and the validation-checkpoint policy of the reference's ModelTrainer.
   sres/data/tiles.py:48-74), the time-slice loss = mean of the batch losses
   (accumulate_loss, tiles.py:25-28), a train checkpoint after EVERY time slice
   (:330) and a loss record per time slice, flushed every 32 (:275, :331).
+  Data parallel (the trainer's DistInfo, world > 1): every rank follows rank 0's
+  shuffled batch order, steps its shard of each batch (srmi.dist.shard_range; the
+  short last batch too, a rank may get no tile), and only rank 0 writes the
+  checkpoint and the loss records while the others wait at a barrier.
 """
 from __future__ import annotations
 
@@ -196,13 +200,31 @@ def train_timeslices(trainer, timeslices: Sequence[Callable[[], torch.Tensor]], 
     (refresh_state False) restores the trainer and (epoch0, itime0) from the train
     checkpoint; after every time slice the train checkpoint is saved (with its
     .backup) and the loss record written; on_epoch_end(epoch, loss) stands for
-    record_eval (evaluation on the validation set, TiledInference.evaluate)."""
+    record_eval (evaluation on the validation set, TiledInference.evaluate).
+
+    Data parallel (trainer.info.world > 1; every rank calls this with the same time
+    slices): rank 0 shuffles the batch starts with `rng` -- exactly the order one
+    process would use -- and broadcasts them, so the ranks step the same global
+    batches; each rank steps its shard_range of every batch with
+    trainer.step(tiles, shard=(t0, gb)), so the loss and gradient scale are those of
+    the whole batch (srmi.trainer) and a short last batch of gb < world tiles leaves
+    some ranks with none.  trainer.batch must hold ceil(batch_size / world) tiles.
+    Only rank 0 clears, saves and records; a barrier follows each of its writes."""
+    from .dist import DistInfo, barrier, broadcast_ints, shard_capacity, shard_range
+    info = getattr(trainer, "info", None) or DistInfo()
+    dev = getattr(trainer, "device", None)
+    lead = info.rank == 0
+    if info.enabled and trainer.batch < shard_capacity(batch_size, info):
+        raise ValueError(f"trainer batch {trainer.batch} < the {shard_capacity(batch_size, info)}-tile shard of "
+                         f"a {batch_size}-tile batch over {info.world} ranks")
     epoch0, itime0, epoch_loss, interp_l = 1, 0, 0.0, 0.0
     if refresh_state:
-        if store is not None:
-            store.clear()
-        if records is not None:
-            records.refresh_state()
+        if lead:
+            if store is not None:
+                store.clear()
+            if records is not None:
+                records.refresh_state()
+        barrier(info, dev)
     elif store is not None:
         state = store.load(trainer, "train", update_model=True)
         if state is None:
@@ -218,22 +240,35 @@ def train_timeslices(trainer, timeslices: Sequence[Callable[[], torch.Tensor]], 
     for epoch in range(epoch0, nepochs):
         for itime in range(itime0, nts):
             tiles = timeslices[itime]()
+            ntiles = tiles.shape[0]
+            nb = len(range(0, ntiles, batch_size))
+            starts = batch_starts(ntiles, batch_size, True, rng) if lead else [0] * nb
+            starts = broadcast_ints(starts, info, dev)  # rank 0's order on every rank
             losses, ilosses = [], []
-            for start in batch_starts(tiles.shape[0], batch_size, True, rng):
-                out = trainer.step(tiles[start:start + batch_size])
+            for start in starts:
+                gb = min(batch_size, ntiles - start)
+                if info.enabled:
+                    a, e = shard_range(gb, info)
+                    out = trainer.step(tiles[start + a:start + e], shard=(a, gb))
+                else:
+                    out = trainer.step(tiles[start:start + gb])
                 losses.append(out["loss"].clone())  # (views of the trainer's loss record)
                 ilosses.append(out["interp_loss"].clone())
             # accumulate_loss: mean of the batch losses (one host sync per time slice)
             epoch_loss = float(torch.cat(losses).double().mean()) if losses else math.nan
             interp_l = float(torch.cat(ilosses).double().mean()) if ilosses else math.nan
+            if lead:
+                if store is not None:
+                    store.save(trainer, epoch, itime, "train", epoch_loss)
+                if records is not None:
+                    records.record_losses("train", epoch - 1 + itime / nts, epoch_loss, interp_l,
+                                          flush=((itime + 1) % LOSSREC_FLUSH_PERIOD == 0))
             if store is not None:
-                store.save(trainer, epoch, itime, "train", epoch_loss)
-            if records is not None:
-                records.record_losses("train", epoch - 1 + itime / nts, epoch_loss, interp_l,
-                                      flush=((itime + 1) % LOSSREC_FLUSH_PERIOD == 0))
+                barrier(info, dev)  # the checkpoint is complete before any rank goes on
         if on_epoch_end is not None:
             on_epoch_end(epoch, epoch_loss)
         itime0 = 0
-    if records is not None:
+    if records is not None and lead:
         records.flush()
+    barrier(info, dev)
     return {"prediction": epoch_loss, "interpolated": interp_l}

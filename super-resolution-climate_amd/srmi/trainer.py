@@ -19,7 +19,7 @@ gradients are all-reduced as described in srmi/dist.py.
 from __future__ import annotations
 
 import math
-from typing import Dict, Optional
+from typing import Dict, Optional, Tuple
 
 import torch
 
@@ -148,11 +148,15 @@ class FusedTrainer:
                      if self.ds > 1 else None)
         self.loss4 = torch.zeros(4, dtype=torch.float32, device=self.device)
         self.iloss4 = torch.zeros(4, dtype=torch.float32, device=self.device)
-        self.mloss4 = torch.zeros((micro, 4), dtype=torch.float32, device=self.device)   # per micro-batch
-        # the loss sums as per-tile parts (srmi_tile_loss_parts): the step's loss -- and the
-        # gradient scale 1/(count L) -- does not depend on the micro-batch split
-        self.lparts = torch.zeros(batch * TILE_LOSS_SUB, dtype=torch.float32, device=self.device)
-        self.iparts = torch.zeros(batch * TILE_LOSS_SUB, dtype=torch.float32, device=self.device)
+        # the loss sums as per-tile parts (srmi_tile_loss_parts) of the GLOBAL batch, in
+        # global tile order: [loss parts | interp parts] of the step's gb tiles.  The
+        # step's loss -- and the gradient scale 1/(count L) -- then depends neither on the
+        # micro-batch split nor, data parallel, on how the batch is sharded over ranks:
+        # every rank writes its tiles' parts into a zeroed array, one SUM all-reduce
+        # (x + 0 is exact) hands every rank all of them, and every rank sums them in the
+        # order one process would.
+        self.gcap = batch * self.info.world
+        self.gparts = torch.zeros(2 * self.gcap * TILE_LOSS_SUB, dtype=torch.float32, device=self.device)
         self.streams = [None] + [engine_stream(self.device) for _ in range(micro - 1)]
         self.dp_staged = not dp_reducer_stream
         self.reducer = GradReducer(self.eng.table, spec.arch, spec.nlayers, self.info, self.device,
@@ -179,26 +183,46 @@ class FusedTrainer:
         call("srmi_tile_loss_parts", ptr(pred), ptr(target), nt, te, self.loss_kind, CHARBONNIER_EPS,
              ptr(parts[t0 * TILE_LOSS_SUB:]), torch.cuda.current_stream(self.device).cuda_stream)
 
-    def _reduce_loss(self, loss4, parts, b, count):
-        """loss4 of the whole (global) batch from its b tiles' parts in tile order,
-        all-reduced over ranks, finalised -- one launch without data parallelism."""
+    def _reduce_losses(self, gb, count, icount):
+        """loss4 / iloss4 of the whole (global) batch from its gb tiles' parts in tile
+        order, finalised (data parallel: after the all-reduce of the parts)."""
         st = torch.cuda.current_stream(self.device).cuda_stream
+        n = gb * TILE_LOSS_SUB
         if self.info.enabled:
-            call("srmi_loss_from_parts", ptr(parts), b, float(count), -1, ptr(loss4), st)
-            allreduce_sum_(loss4[0:1], self.info)
-            Engine.loss_finalize(loss4, self.loss_kind)
-        else:
-            call("srmi_loss_from_parts", ptr(parts), b, float(count), self.loss_kind, ptr(loss4), st)
+            allreduce_sum_(self.gparts[:2 * n if self.interp_loss else n], self.info)
+        call("srmi_loss_from_parts", ptr(self.gparts), gb, float(count), self.loss_kind, ptr(self.loss4), st)
+        if self.interp_loss:
+            call("srmi_loss_from_parts", ptr(self.gparts[n:]), gb, float(icount), self.loss_kind, ptr(self.iloss4),
+                 st)
 
-    def step(self, hr: torch.Tensor) -> Dict[str, torch.Tensor]:
+    def _shard(self, b: int, shard: Optional[Tuple[int, int]]) -> Tuple[int, int]:
+        """(t0, gb): this call's tiles are tiles t0 .. t0 + b - 1 of a gb-tile global
+        batch.  Default: the whole batch (one process) or, data parallel, equal shards
+        in rank order."""
+        if shard is None:
+            return (self.info.rank * b, self.info.world * b) if self.info.enabled else (0, b)
+        t0, gb = int(shard[0]), int(shard[1])
+        if not self.info.enabled and (t0, gb) != (0, b):
+            raise ValueError(f"shard {shard} of a {b}-tile batch without data parallelism")
+        if t0 < 0 or t0 + b > gb or gb < 1 or gb > self.gcap:
+            raise ValueError(f"shard {shard} of {b} tiles outside a global batch of 1..{self.gcap} tiles")
+        return t0, gb
+
+    def step(self, hr: torch.Tensor, shard: Optional[Tuple[int, int]] = None) -> Dict[str, torch.Tensor]:
         """hr: this rank's HR tiles [b, C, H, W] fp32 on the device (already normalised),
         b <= the trainer's batch (a short last batch of a time slice, as the
-        reference's TileBatchIterator yields, sres/data/tiles.py:55-72)."""
+        reference's TileBatchIterator yields, sres/data/tiles.py:55-72).
+
+        Data parallel, shard = (t0, gb): hr holds tiles t0 .. t0 + b - 1 of the step's
+        gb-tile global batch (srmi.dist.shard_range; a rank of a short last batch may
+        hold none, b = 0, and still takes part in every collective and the Adam step);
+        the default is equal shards in rank order."""
         b = hr.shape[0]
-        if b < 1 or b > self.batch:
-            raise ValueError(f"batch {b} outside 1..{self.batch}")
+        if b < (0 if self.info.enabled else 1) or b > self.batch:
+            raise ValueError(f"batch {b} outside {0 if self.info.enabled else 1}..{self.batch}")
+        t0, gb = self._shard(b, shard)
         s = self.spec.scale
-        if self.ds > 1:  # apply_network: downsample(input, scale_factor=ds) first (:561-563)
+        if self.ds > 1 and b:  # apply_network: downsample(input, scale_factor=ds) first (:561-563)
             got = tuple(interp_size(n, 1.0 / self.ds) for n in hr.shape[2:])
             if got != tuple(self.hrds.shape[2:]):
                 raise ValueError(f"data_downsample={self.ds}: HR tiles {tuple(hr.shape[2:])} give {got}, "
@@ -207,14 +231,19 @@ class FusedTrainer:
         mb = (b + self.micro - 1) // self.micro
         sls = [slice(min(b, k * mb), min(b, (k + 1) * mb)) for k in range(self.micro)]
         main = torch.cuda.current_stream(self.device)
-        if self.tindx is not None:  # apply_network's index_select of the target channels
+        if self.tindx is not None and b:  # apply_network's index_select of the target channels
             tgt = torch.index_select(hr, 1, self.tindx, out=self.tgt[:b])
             if self.tgt_b is not None:
                 self.tgt_b[:b].copy_(tgt.expand(-1, hr.shape[1], -1, -1))
         else:
             tgt = hr
-        count = float(tgt.numel()) * self.info.world
-        icount = float(hr.numel()) * self.info.world
+        # element counts of the global batch: target tiles (Co x HR) and interp tiles (C x HR)
+        count = float(gb) * self.sr[0].numel()
+        icount = float(gb) * self.lrbuf[0].numel() * s * s
+        n = gb * TILE_LOSS_SUB
+        lparts, iparts = self.gparts[:n], self.gparts[n:2 * n]
+        if self.info.enabled:  # the other ranks' tiles' parts stay 0 here
+            self.gparts[:2 * n].zero_()
         for st in self.streams[1:]:
             st.wait_stream(main)
         # forward + loss partials per micro-batch (an empty micro-batch adds nothing)
@@ -225,19 +254,16 @@ class FusedTrainer:
             with self._ctx(k):
                 downsample(hr[sl], s, out=self.lrbuf[sl], mode=self.dmode)
                 eng.forward(self.params, self.lrbuf[sl], out=self.sr[sl])
-                if self.dy is not None:  # Charbonnier: the elementwise upstream gradient
-                    eng.charbonnier_partial(self.sr[sl], tgt[sl], self.mloss4[k], count, CHARBONNIER_EPS,
-                                            dy=self.dy[sl])
-                self._loss_parts(self.sr[sl], tgt[sl], self.lparts, sl.start)
+                if self.dy is not None:  # Charbonnier: the elementwise upstream gradient only
+                    eng.charbonnier_partial(self.sr[sl], tgt[sl], None, count, CHARBONNIER_EPS, dy=self.dy[sl])
+                self._loss_parts(self.sr[sl], tgt[sl], lparts, t0 + sl.start)
                 if self.interp_loss:  # self.loss(btarget, binterp), dual_trainer.py:316-317
                     up = upsample(self.lrbuf[sl], s, out=self.up[sl], mode=self.umode)
                     itgt = hr[sl] if self.tgt_b is None else self.tgt_b[sl]
-                    self._loss_parts(itgt, up, self.iparts, sl.start)
+                    self._loss_parts(itgt, up, iparts, t0 + sl.start)
         for st in self.streams[1:]:
             main.wait_stream(st)
-        self._reduce_loss(self.loss4, self.lparts, b, count)
-        if self.interp_loss:
-            self._reduce_loss(self.iloss4, self.iparts, b, icount)
+        self._reduce_losses(gb, count, icount)
         for st in self.streams[1:]:
             st.wait_stream(main)
         # backward per micro-batch with the global loss scale.  Data parallel: the

@@ -236,3 +236,98 @@ def test_multirank_tiled_inference_world2_bit_identical_to_one_rank():
         assert el == ref_l
         for k, v in ref_res.items():
             np.testing.assert_array_equal(er[k], v.cpu().numpy())
+
+
+def _harness_worker(rank, port, q, root, flat_np):
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "super-resolution-climate_amd"), ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                      LOCAL_RANK="0")
+    import torch.distributed as dist
+    from oracle import rcan_oracle as ro
+    from srmi.dist import init_from_env
+    from srmi.harness import CheckpointStore, LossRecords, train_timeslices
+    from srmi.trainer import FusedTrainer
+    info = init_from_env("gloo")
+    d = torch.device("cuda", 0)
+    torch.cuda.set_device(d)
+    slices = [torch.tensor(ro.synthetic_hr(13, 2, 192, 60 + i)).to(d) for i in range(2)]
+    # ceil(4 / 2) = 2 tiles per rank, as two micro-batch engines of one tile
+    tr = FusedTrainer(_spec(), 2, (48, 48), device=d, params=torch.tensor(flat_np, device=d), micro=2, info=info)
+    rec = []
+    step = tr.step
+
+    def recording_step(hr, shard=None):
+        p = tr.params.clone()
+        out = step(hr, shard=shard)
+        torch.cuda.synchronize()
+        rec.append((p.cpu().numpy(), float(out["loss"]), float(out["interp_loss"]), tr.grads.cpu().numpy(),
+                    hr.shape[0], shard))
+        return out
+    tr.step = recording_step
+    out = train_timeslices(tr, [lambda i=i: slices[i] for i in range(2)], 2, 4,
+                           store=CheckpointStore(root, "dp"), records=LossRecords(root, "ds", "t", "m"),
+                           refresh_state=True, rng=random.Random(3))
+    q.put((rank, rec, out, tr.params.cpu().numpy()))
+    dist.destroy_process_group()
+
+
+def test_train_timeslices_world2_matches_one_process(tmp_path):
+    """C3's training loop (dual_trainer.py:301-331; TileBatchIterator tiles.py:55-72)
+    on the HIP path at world 2 (gloo, both ranks on cuda:0): 2 time slices of 13 tiles
+    at batch_size 4, so every slice ends with a 1-tile batch that rank 1 has no tile
+    of.  Replayed step by step in one process (its params set to the ranks' params
+    before each step): every loss is bit-identical (the global batch's per-tile loss
+    parts, all-reduced and summed in tile order), the gradients agree to fp32 summation
+    order (2e-4 rel-L2), the replicas stay identical after Adam, and rank 0 alone wrote
+    one checkpoint (+ backup) and one CSV row per time slice."""
+    import multiprocessing as mp
+    from oracle import rcan_oracle as ro
+    from srmi.engine import param_table
+    from srmi.harness import LossRecords, train_timeslices
+    from srmi.trainer import FusedTrainer, default_init_
+    spec = _spec()
+    table = param_table(spec)
+    flat = torch.empty(sum(t[2] for t in table))
+    default_init_(flat, table, seed=9)
+    root = str(tmp_path / "dp")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 41000 + random.randint(0, 2000)
+    ps = [ctx.Process(target=_harness_worker, args=(r, port, q, root, flat.numpy())) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=200) for _ in ps], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    (_, rec0, out0, p0), (_, rec1, out1, p1) = res
+    assert len(rec0) == len(rec1) == 8
+    np.testing.assert_array_equal(p0, p1)
+    assert out0 == out1
+    assert [r[4] for r in rec1].count(0) == 2   # rank 1 had no tile of either 1-tile batch
+    assert all(r0[1] == r1[1] for r0, r1 in zip(rec0, rec1))
+    # one process, same rng, each step from the ranks' params
+    d = torch.device("cuda", 0)
+    slices = [torch.tensor(ro.synthetic_hr(13, 2, 192, 60 + i)).to(d) for i in range(2)]
+    one = FusedTrainer(spec, 4, (48, 48), device=d, params=flat.to(d), micro=1)
+    step, k = one.step, [0]
+
+    def replay(hr, shard=None):
+        p_dp, l_dp, il_dp, g_dp, _, _ = rec0[k[0]]
+        one.params.copy_(torch.tensor(p_dp, device=d))
+        for e in one.engines:
+            e.pack(one.params)
+        out = step(hr, shard=shard)
+        torch.cuda.synchronize()
+        assert float(out["loss"]) == l_dp and float(out["interp_loss"]) == il_dp, k[0]
+        g = one.grads.cpu().numpy()
+        assert np.linalg.norm(g_dp - g) / np.linalg.norm(g) < 2e-4, k[0]
+        k[0] += 1
+        return out
+    one.step = replay
+    train_timeslices(one, [lambda i=i: slices[i] for i in range(2)], 2, 4, rng=random.Random(3))
+    assert k[0] == 8
+    assert sorted(os.listdir(os.path.join(root, "checkpoints"))) == ["dp.train.backup.pt", "dp.train.pt"]
+    rows = LossRecords(root, "ds", "t", "m").load_results()
+    assert [r[1] for r in rows] == ["0.000", "0.500"]

@@ -356,3 +356,46 @@ def test_ca_forward_in_conv2_matches_ca_pass(lr_hw):
     corners) in different workgroups."""
     from srmi._lib import SRMI_FLAG_CA_PASS
     _engine_variants_agree(lr_hw, (0, SRMI_FLAG_CA_PASS), 5e-3, fwd_tol=1e-3)
+
+
+@pytest.mark.parametrize("arch", ["rcan", "edsr"])
+def test_backward_stages_one_at_a_time_and_order_checked(arch):
+    """srmi_backward_stages run one stage per call gives the gradients of one
+    srmi_backward bit for bit; a stage skipped, repeated or out of order -- or a whole
+    backward while a staged one is half-way -- is refused (SRMI_ERR_ARG), since the
+    gradient-stream buffers and slab parity carry over from stage to stage."""
+    from srmi._lib import SrmiError
+    from srmi.trainer import default_init_
+    d = dev()
+    # RCAN 4x 48 -> 192, 2 variables; EDSR 8x 32 -> 256, 4 variables (C4's shapes)
+    spec, C, T = (spec_of("rcan", 2, 2, 2), 2, 192) if arch == "rcan" else (spec_of("edsr", 4, 2, scale=8), 4, 256)
+    table = _table(spec)
+    flat = torch.empty(sum(t[2] for t in table), device=d)
+    default_init_(flat, table, seed=4)
+    hr = torch.tensor(ro.synthetic_hr(2, C, T, 8)).to(d)
+    tr = FusedTrainer(spec, 2, (T // spec.scale,) * 2, device=d, params=flat, micro=1)
+    tr.step(hr)  # the engine's last forward, loss4 and sr
+    eng = tr.eng
+    ns = eng.stage_count
+    assert ns == (spec.nlayers + 2 if arch == "rcan" else 1)
+    kw = dict(sr=tr.sr, hr=hr, loss4=tr.loss4)
+    g_full = torch.zeros_like(tr.grads)
+    eng.backward(tr.params, tr.lrbuf, g_full, **kw)
+    g_st = torch.zeros_like(tr.grads)
+    for s in range(ns):
+        eng.backward(tr.params, tr.lrbuf, g_st, stages=(s, s), **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(g_full, g_st)
+    if arch == "rcan":
+        with pytest.raises(SrmiError):  # stage 1 before stage 0
+            eng.backward(tr.params, tr.lrbuf, g_st, stages=(1, 1), **kw)
+        eng.backward(tr.params, tr.lrbuf, g_st, stages=(0, 0), **kw)
+        with pytest.raises(SrmiError):  # stage 0 again
+            eng.backward(tr.params, tr.lrbuf, g_st, stages=(0, 0), **kw)
+        with pytest.raises(SrmiError):  # stage 2 skips stage 1
+            eng.backward(tr.params, tr.lrbuf, g_st, stages=(2, 2), **kw)
+        with pytest.raises(SrmiError):  # a whole backward half-way through
+            eng.backward(tr.params, tr.lrbuf, g_st, **kw)
+        eng.backward(tr.params, tr.lrbuf, g_st, stages=(1, ns - 1), **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(g_full, g_st)

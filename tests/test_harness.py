@@ -133,3 +133,115 @@ def test_oracle_batch_loss_mean_and_evaluate():
     assert abs(float(ro.single_product_loss(p, t, "charbonnier")) - np.sqrt(1 + 1e-6)) < 1e-7
     with pytest.raises(Exception):
         ro.single_product_loss(p, t, "l1")
+
+
+def test_shard_range_uneven_batches():
+    """shard_range splits any batch over the ranks, contiguously and in rank order, the
+    first gb % world ranks one tile longer (a short last batch leaves ranks empty)."""
+    from srmi.dist import DistInfo, shard_capacity, shard_range
+    for world in (1, 2, 3, 8):
+        for gb in range(0, 20):
+            got = [shard_range(gb, DistInfo(rank=r, world=world)) for r in range(world)]
+            assert got[0][0] == 0 and got[-1][1] == gb
+            assert all(got[r][1] == got[r + 1][0] for r in range(world - 1))
+            sizes = [b - a for a, b in got]
+            assert max(sizes) - min(sizes) <= 1 and max(sizes) == shard_capacity(gb, DistInfo(world=world))
+    assert shard_range(1, DistInfo(rank=1, world=2)) == (1, 1)
+    assert shard_range(16, DistInfo(rank=1, world=2)) == (8, 16)
+
+
+class _DPStepTrainer:
+    """A stand-in for FusedTrainer's data-parallel contract: step(tiles, shard=(t0, gb))
+    with this rank's tiles t0.. of a gb-tile global batch; the loss is a whole-batch
+    quantity formed by one all-reduce (the mean of the tiles' values)."""
+
+    def __init__(self, info, batch):
+        self.info, self.batch, self.device = info, batch, torch.device("cpu")
+        self.seen, self.t, self.loaded = [], 0, None
+
+    def step(self, hr, shard=None):
+        import torch.distributed as dist
+        b = hr.shape[0]
+        t0, gb = shard if shard is not None else (0, b)
+        assert b <= self.batch
+        ids = [int(x) for x in hr[:, 0, 0, 0].tolist()]
+        self.seen.append((t0, gb, ids))
+        s = hr.double().sum().reshape(1)
+        if self.info.enabled:
+            dist.all_reduce(s)
+        self.t += 1
+        loss = (s / (gb * hr[0].numel() if b else gb * 4)).float()
+        return {"loss": loss, "interp_loss": 2 * loss}
+
+    def checkpoint(self, epoch=0, itime=0, loss=0.0):
+        return dict(epoch=epoch, itime=itime, model_state_dict={"t": torch.tensor([self.t])},
+                    optimizer_state_dict={}, loss=loss)
+
+    def load_checkpoint(self, state):
+        self.loaded = state
+
+
+def _slices():
+    # time slice i: 13 tiles [13, 1, 2, 2], tile k filled with 100 i + k
+    return [torch.arange(100 * i, 100 * i + 13, dtype=torch.float32)[:, None, None, None].expand(13, 1, 2, 2).clone()
+            for i in range(2)]
+
+
+def _dp_harness_rank(rank, world, port, root, q):
+    import sys
+    sys.path[:0] = [os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                 "super-resolution-climate_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    from srmi.dist import init_from_env
+    from srmi.harness import CheckpointStore, LossRecords, train_timeslices
+    info = init_from_env("gloo")
+    tr = _DPStepTrainer(info, 2)
+    sl = _slices()
+    store = CheckpointStore(root, "v")
+    rec = LossRecords(root, "ds", "task", "m")
+    # every rank passes its own rng: only rank 0's is drawn from (the others' order is broadcast)
+    out = train_timeslices(tr, [lambda i=i: sl[i] for i in range(2)], 3, 4, store=store, records=rec,
+                           refresh_state=True, rng=random.Random(11 if rank == 0 else 1000 + rank))
+    files = sorted(os.listdir(os.path.join(root, "checkpoints")))
+    q.put((rank, tr.seen, out, files))
+    dist.destroy_process_group()
+
+
+def test_train_timeslices_data_parallel_world2_gloo(tmp_path):
+    """C3's loop (dual_trainer.py:301-331 over TileBatchIterator, tiles.py:55-72) at
+    world 2: both ranks step rank 0's shuffled batch order, each its shard_range of
+    every batch -- the short last batch of 1 tile leaves rank 1 empty -- the shards of
+    a batch are exactly its tiles, the losses are the one-process losses, and one
+    checkpoint (+ backup) and one CSV row per time slice come from rank 0 alone."""
+    import multiprocessing as mp
+    from srmi.dist import DistInfo
+    from srmi.harness import LossRecords, train_timeslices
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 39000 + random.randint(0, 2000)
+    root = str(tmp_path / "dp")
+    ps = [ctx.Process(target=_dp_harness_rank, args=(r, 2, port, root, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in ps], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # the one-process run with rank 0's rng
+    one = _DPStepTrainer(DistInfo(), 4)
+    sl = _slices()
+    ref = train_timeslices(one, [lambda i=i: sl[i] for i in range(2)], 3, 4, rng=random.Random(11))
+    (_, seen0, out0, files), (_, seen1, out1, _) = res
+    assert len(seen0) == len(seen1) == len(one.seen) == 2 * 2 * 4  # 2 epochs x 2 slices x 4 batches
+    for (a0, g0, i0), (a1, g1, i1), (_, g, ids) in zip(seen0, seen1, one.seen):
+        assert g0 == g1 == g and a0 == 0 and a1 == len(i0)
+        assert i0 + i1 == ids                      # the shards are the batch, in order
+        assert len(i0) - len(i1) in (0, 1)
+    assert any(len(i1) == 0 for _, _, i1 in seen1)  # the 1-tile last batch: rank 1 had no tile
+    assert out0 == out1 and abs(out0["prediction"] - ref["prediction"]) < 1e-6
+    assert files == ["v.train.backup.pt", "v.train.pt"]
+    rows = LossRecords(root, "ds", "task", "m").load_results()
+    assert [r[1] for r in rows] == ["0.000", "0.500", "1.000", "1.500"]  # one row per time slice
+    st = torch.load(os.path.join(root, "checkpoints", "v.train.pt"), weights_only=True)
+    assert st["epoch"] == 2 and st["itime"] == 1
