@@ -42,8 +42,10 @@ class NetSpec:
     def from_parms(arch: str, parms: Dict, dtype: str = "bf16") -> "NetSpec":
         if parms.get("kernel_size", 3) != 3:
             raise _lib.SrmiError("srmi supports kernel_size 3 only")
-        if parms.get("batch_norm", False):
-            raise _lib.SrmiError("srmi supports batch_norm: False only (the reference configs)")
+        # RCAN ignores batch_norm: its RCABs are built with bn=False (sres/model/rcan/
+        # network.py:70); EDSR's ResBlocks take it (edsr/network.py:15), unsupported here
+        if parms.get("batch_norm", False) and arch != "rcan":
+            raise _lib.SrmiError("srmi's EDSR supports batch_norm: False only (the reference configs)")
         if not parms.get("bias", True):
             raise _lib.SrmiError("srmi supports bias: True only (the reference configs)")
         return NetSpec(arch=arch, nchannels_in=int(parms["nchannels_in"]), nchannels_out=int(parms["nchannels_out"]),

@@ -325,3 +325,14 @@ def test_round_robin_tile_gather_world_gloo(world):
     exp = np.arange(11, dtype=np.float32)[:, None] * np.array([[1.0, -1.0]], dtype=np.float32)
     for _, out in res:
         np.testing.assert_array_equal(out, exp)
+
+
+def test_netspec_batch_norm_rcan_ignored_edsr_refused():
+    """RCAN's RCABs hard-code bn=False (sres/model/rcan/network.py:70), so the key is
+    ignored, as the reference does; EDSR passes it to its ResBlocks (edsr/network.py:15)."""
+    from srmi import _lib
+    from srmi.engine import NetSpec
+    parms = dict(nchannels_in=2, nchannels_out=2, nfeatures=64, nlayers=10, nblocks=20, scale=4, batch_norm=True)
+    assert NetSpec.from_parms("rcan", parms) == NetSpec.from_parms("rcan", dict(parms, batch_norm=False))
+    with pytest.raises(_lib.SrmiError, match="batch_norm"):
+        NetSpec.from_parms("edsr", dict(parms, nblocks=0, scale=8))
