@@ -692,38 +692,41 @@ int tail_wgrad_reduce_launch(const float* slab, int nslab, int C, float* gw, flo
 // ====================================================================== resampling
 // bicubic (A = -0.75, align_corners = False) at 1/scale: the source coordinate
 // scale*d + (scale-1)/2 is half-way between samples -> separable [-3,19,19,-3]/32
-// grid (ceil(h w / 256), NC): 32-bit index arithmetic within one plane (64-bit
-// divisions of a flat index cost more than the loads)
+// grid (ceil(h w / 256), min(NC, 65535)), planes blockIdx.y, + gridDim.y, ...: 32-bit
+// index arithmetic within one plane (64-bit divisions of a flat index cost more than
+// the loads), any number of planes
+constexpr int kMaxGridY = 65535;
 __global__ void downsample_kernel(const float* __restrict__ hr, int NC, int H, int W, int scale,
                                   float* __restrict__ lr) {
   const int h = H / scale, w = W / scale;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= h * w) return;
   const int x = i % w, y = i / w;
-  const size_t nc = blockIdx.y, idx = nc * h * w + i;
   const float k[4] = {-3.f / 32.f, 19.f / 32.f, 19.f / 32.f, -3.f / 32.f};
   const int sy = y * scale + scale / 2 - 2, sx = x * scale + scale / 2 - 2;
-  const float* src = hr + nc * H * W;
-  float acc = 0.f;
+  for (size_t nc = blockIdx.y; nc < (size_t)NC; nc += gridDim.y) {
+    const float* src = hr + nc * H * W;
+    float acc = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int yy = min(max(sy + i, 0), H - 1);
-    float rsum = 0.f;
+    for (int i = 0; i < 4; ++i) {
+      const int yy = min(max(sy + i, 0), H - 1);
+      float rsum = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int xx = min(max(sx + j, 0), W - 1);
-      rsum += k[j] * src[(size_t)yy * W + xx];
+      for (int j = 0; j < 4; ++j) {
+        const int xx = min(max(sx + j, 0), W - 1);
+        rsum += k[j] * src[(size_t)yy * W + xx];
+      }
+      acc += k[i] * rsum;
     }
-    acc += k[i] * rsum;
+    lr[nc * h * w + i] = acc;
   }
-  lr[idx] = acc;
 }
 
 int downsample_launch(const float* hr, int N, int C, int H, int W, int scale, float* lr, hipStream_t st) {
-  if (scale < 2 || H % scale || W % scale) return SRMI_ERR_SHAPE;
+  if (scale < 2 || H % scale || W % scale || N < 1 || C < 1) return SRMI_ERR_SHAPE;
   const int plane = (H / scale) * (W / scale);
-  if (N * C > 65535) return SRMI_ERR_SHAPE;
-  hipLaunchKernelGGL(downsample_kernel, dim3((plane + 255) / 256, N * C), dim3(256), 0, st, hr, N * C, H, W, scale, lr);
+  const int gy = N * C < kMaxGridY ? N * C : kMaxGridY;
+  hipLaunchKernelGGL(downsample_kernel, dim3((plane + 255) / 256, gy), dim3(256), 0, st, hr, N * C, H, W, scale, lr);
   SRMI_CHECK_LAUNCH();
   return 0;
 }
@@ -743,36 +746,38 @@ __device__ __forceinline__ void cubic_w(float t, float* c) {
 __global__ void upsample_kernel(const float* __restrict__ lr, int NC, int h, int w, int scale,
                                 float* __restrict__ hr) {
   const int H = h * scale, W = w * scale;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // grid (ceil(H W / 256), NC)
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // grid as downsample_kernel's
   if (i >= H * W) return;
   const int X = i % W, Y = i / W;
-  const size_t nc = blockIdx.y, idx = nc * H * W + i;
   const float inv = 1.f / (float)scale;
   const float sy = inv * (Y + 0.5f) - 0.5f, sx = inv * (X + 0.5f) - 0.5f;
   const int iy = (int)floorf(sy), ix = (int)floorf(sx);
   float wy[4], wx[4];
   cubic_w(sy - iy, wy);
   cubic_w(sx - ix, wx);
-  const float* src = lr + nc * h * w;
-  float acc = 0.f;
+  for (size_t nc = blockIdx.y; nc < (size_t)NC; nc += gridDim.y) {
+    const float* src = lr + nc * h * w;
+    float acc = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int yy = min(max(iy - 1 + i, 0), h - 1);
-    float rsum = 0.f;
+    for (int i = 0; i < 4; ++i) {
+      const int yy = min(max(iy - 1 + i, 0), h - 1);
+      float rsum = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int xx = min(max(ix - 1 + j, 0), w - 1);
-      rsum += wx[j] * src[(size_t)yy * w + xx];
+      for (int j = 0; j < 4; ++j) {
+        const int xx = min(max(ix - 1 + j, 0), w - 1);
+        rsum += wx[j] * src[(size_t)yy * w + xx];
+      }
+      acc += wy[i] * rsum;
     }
-    acc += wy[i] * rsum;
+    hr[nc * H * W + i] = acc;
   }
-  hr[idx] = acc;
 }
 
 int upsample_launch(const float* lr, int N, int C, int h, int w, int scale, float* hr, hipStream_t st) {
+  if (scale < 1 || N < 1 || C < 1) return SRMI_ERR_SHAPE;
   const int plane = h * scale * w * scale;
-  if (N * C > 65535) return SRMI_ERR_SHAPE;
-  hipLaunchKernelGGL(upsample_kernel, dim3((plane + 255) / 256, N * C), dim3(256), 0, st, lr, N * C, h, w, scale, hr);
+  const int gy = N * C < kMaxGridY ? N * C : kMaxGridY;
+  hipLaunchKernelGGL(upsample_kernel, dim3((plane + 255) / 256, gy), dim3(256), 0, st, lr, N * C, h, w, scale, hr);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

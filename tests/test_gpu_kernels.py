@@ -380,6 +380,27 @@ def test_downsample_upsample_match_reference():
     np.testing.assert_allclose(up.double().cpu().numpy(), gd["up4_out"], rtol=1e-5, atol=1e-5)
 
 
+def test_downsample_upsample_beyond_grid_y_planes():
+    """N * C above the 65535 grid.y limit (a large batch of tiles x channels): the
+    resampling kernels stride over the planes instead of refusing the shape; every
+    plane equals the same plane resampled in a small batch, bit for bit."""
+    d = dev()
+    g = torch.Generator(device="cpu").manual_seed(7)
+    n = 70001
+    x = torch.randn(n, 1, 8, 8, generator=g).to(d)
+    y = torch.empty(n, 1, 2, 2, device=d)
+    call("srmi_downsample", ptr(x), n, 1, 8, 8, 4, ptr(y), S())
+    up = torch.empty(n, 1, 8, 8, device=d)
+    call("srmi_upsample", ptr(y), n, 1, 2, 2, 4, ptr(up), S())
+    for sl in (slice(0, 3), slice(65534, 65537), slice(n - 3, n)):
+        ys = torch.empty(3, 1, 2, 2, device=d)
+        call("srmi_downsample", ptr(x[sl].contiguous()), 3, 1, 8, 8, 4, ptr(ys), S())
+        us = torch.empty(3, 1, 8, 8, device=d)
+        call("srmi_upsample", ptr(ys), 3, 1, 2, 2, 4, ptr(us), S())
+        torch.cuda.synchronize()
+        assert torch.equal(y[sl], ys) and torch.equal(up[sl], us)
+
+
 INTERP_CASES = ["down_linear_4", "down_linear_8", "down_linear_3", "down_linear_1p5", "down_cubic_3",
                 "down_cubic_1p5", "down_cubic_6", "up_linear_4", "up_linear_4b"]
 
