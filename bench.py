@@ -39,6 +39,8 @@ METRIC = "training tiles/sec (48→192, bf16) at 1/2/4/8 MI355X; inference MPix/
 PEAK_BF16_TFLOPS = 2516.6          # 256 CU x 2.4 GHz x 4096 FLOP/clk (MI355X_MICROARCH.md, dense)
 PEAK_FP32_TFLOPS = 157.3           # f32-input MFMA = the f32 vector rate (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
+HBM_ACHIEVABLE_GBS = 6300.0        # MI355X_MICROARCH.md: sustained streaming, not a roofline peak
+RIDGE_FLOP_PER_BYTE = PEAK_BF16_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)   # 314.6
 TRAIN_GFLOP_PER_TILE_C2 = 219.9    # 6 x conv MACs per tile
 EDSR_TRAIN_GFLOP_PER_TILE = 27.4   # C4 EDSR x8 4-var, 6 x 4.57 G MAC
 CONV64_FLOP_PER_TILE = 2 * 64 * 576 * 48 * 48   # one 64->64 3x3 conv at 48x48 (84.93 M MAC)
@@ -169,6 +171,26 @@ F2_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE
 FUSED_FLOP_PER_TILE = 2 * CONV64_FLOP_PER_TILE   # one dgrad conv + one filter-gradient conv
 
 
+def _pmc_step_total(step_ms):
+    """Whole-step HBM traffic from the newest committed summary of
+    tools/pmc_step_total.sh (profiles/rNN_pmc_step.json: FETCH_SIZE x2 + WRITE_SIZE of
+    every dispatch of a run of C2 steps, / steps) over this run's step time: the bytes
+    floor of the step, against the 8 TB/s peak (and the guide's ~6.3 TB/s achievable)."""
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_step*.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+            b = float(d["bytes_per_step"])
+        except Exception:
+            continue
+        ach = b / (step_ms * 1e-3) / 1e9
+        return {"bytes_per_step": round(b), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "frac_of_achievable": round(ach / HBM_ACHIEVABLE_GBS, 4),
+                "floor_ms_at_achievable": round(b / (HBM_ACHIEVABLE_GBS * 1e9) * 1e3, 3),
+                "source": os.path.relpath(f, ROOT),
+                "note": "PMC bytes of one whole step (all kernels) / this run's ms_per_step"}
+    return None
+
+
 def _prof_in_step_us(key):
     """In-step average launch duration (us) of the fused backward kernel `key` (F1 / F2)
     from the newest committed rocprofv3 kernel-trace summary of the bench
@@ -241,28 +263,44 @@ def fused_rooflines(tr, step_ms, reps=20):
         ach_slot = bytes_launch * n_eng / (ms * 1e-3) / 1e9
         tr_ = _pmc_traffic("rcab_bwd_kernel<%d" % (7 if which == 1 else 4))
         prof = _prof_in_step_us(key)
+        # the roof is set by the launch's arithmetic intensity against the ridge point
+        # (bf16 dense peak / HBM peak = 314.6 FLOP/B): F1 (164 FLOP/B) is HBM-bound,
+        # F2 (382 FLOP/B) MFMA-bound
+        ai = flop_launch / bytes_launch
+        mfma_bound = ai > RIDGE_FLOP_PER_BYTE
         rc = None
         if prof:
-            a = bytes_launch / (prof["in_step_avg_us"] * 1e-6) / 1e9
+            sec = prof["in_step_avg_us"] * 1e-6
+            a = (flop_launch / sec / 1e12) if mfma_bound else (bytes_launch / sec / 1e9)
             rc = {"in_step_avg_us": prof["in_step_avg_us"], "achieved": round(a, 1),
-                  "frac": round(a / HBM_PEAK_GBS, 4), "source": prof["source"]}
+                  "frac": round(a / (PEAK_BF16_TFLOPS if mfma_bound else HBM_PEAK_GBS), 4), "source": prof["source"]}
+        budget = tr.engines[0]._cfg.cu_budget or 256
+        a_main, peak = (tf, PEAK_BF16_TFLOPS) if mfma_bound else (ach, HBM_PEAK_GBS)
         out[which] = {
-            "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4),
+            "bound": "mfma" if mfma_bound else "hbm", "achieved": round(a_main, 1), "peak": peak,
+            "unit": "TFLOP/s" if mfma_bound else "GB/s", "frac": round(a_main / peak, 4),
+            "arithmetic_intensity_flop_per_byte": round(ai, 1), "ridge_flop_per_byte": round(RIDGE_FLOP_PER_BYTE, 1),
             "traffic": tr_["bytes"] if tr_ and tr_["bytes"] is not None else None,
             "traffic_source": tr_["source"] if tr_ else None,
             "kernel": "srmi::" + name, "in_step": True,
-            "frac_is": "per launch: algorithmic bytes of one launch / its average duration, the launch alone "
-                       "on the chip (engine 0's stream, in-step grid and CU split)",
+            "frac_is": f"per launch: algorithmic {'flops' if mfma_bound else 'bytes'} of one launch / its average "
+                       f"duration, the launch alone (engine 0's stream, in-step grid and CU split) against the "
+                       f"WHOLE chip's peak.  The launch is sized for a {budget}-CU budget ({budget} of 256 CUs, one "
+                       f"workgroup per CU), so alone it can reach at most ~{budget / 256:.2f} of the chip: "
+                       f"frac_of_budget = frac x 256 / {budget}",
+            "cu_budget": budget, "frac_of_budget": round(a_main / peak * 256 / budget, 4),
             "config": f"one launch of {tiles_per_engine} tiles (micro-batch engine 0), in-step grid and CU split",
             "avg_launch_ms": round(ms1, 4), "bytes_per_launch": bytes_launch, "flop_per_launch": flop_launch,
+            "hbm_gbs": round(ach, 1), "hbm_frac": round(ach / HBM_PEAK_GBS, 4),
             "mfma_tflops": round(tf, 1), "mfma_frac": round(tf / PEAK_BF16_TFLOPS, 4),
             "rocprof_check": rc,
             "mfma_pmc": _pmc_mfma("rcab_bwd_kernel<%d" % (7 if which == 1 else 4)),
             "concurrent": {"launches_per_slot": n_eng, "per_stream_ms": [round(x, 4) for x in per_stream],
-                           "achieved": round(ach_slot, 1), "frac": round(ach_slot / HBM_PEAK_GBS, 4),
+                           "achieved": round(ach_slot, 1), "unit": "GB/s", "frac": round(ach_slot / HBM_PEAK_GBS, 4),
+                           "mfma_frac": round(flop_launch * n_eng / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
                            "note": "all micro-batch engines' launches at once, as in the step: bytes of the "
-                                   "slot / slowest stream's average"},
+                                   "slot / slowest stream's average.  Not rocprof-verifiable: a kernel trace "
+                                   "serialises the two streams"},
             "launches_per_engine_per_step": per_step[which],
             "share_of_step": round(ms * per_step[which] / step_ms, 3),
         }
@@ -669,6 +707,7 @@ def main():
             "loss": loss,
             "roofline": roof,
             "roofline_f2": roof_f2,
+            "step_traffic": _pmc_step_total(step_ms),
             "roofline_conv_fwd": roof_conv,
             "dp_overhead_1rank": dp_probe,
             "cpu_baseline": cpu,

@@ -29,6 +29,13 @@ from srmi.engine import NetSpec, param_table  # noqa: E402
 from srmi.trainer import FusedTrainer  # noqa: E402
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+# fixed per-tensor gradient rel-L2 bars vs the fp32 oracle at C2, independent of the
+# emulation (bf16 drift ~2e-2): every conv tensor within 2e-2; the CA
+# bottleneck MLP's tensors (64 -> 2 -> 64, conv_du.*: a few ReLU units whose gradient
+# sums cancel) within 1e-1 -- the emulated-bf16 oracle alone drifts 5.4e-2 there
+# (profiles/r06_c2_parity.json); the whole gradient vector within 1e-2
+GRAD_CAP_C2 = 2e-2
+GRAD_CAP_C2_CA = 1e-1
 
 
 def dev():
@@ -103,9 +110,32 @@ def test_c2_full_shape_step_vs_fp32_oracle():
         worst = max(worst, e_eng / bound)
     report.sort(key=lambda r: -r[1] / (3.0 * r[2] + 1e-3))
     print("\nC2 grads: emulated-bf16 drift vs engine (worst 5):", report[:5])
+    out_rel, emu_out_rel = rel_l2(tr.sr[:, :, ::2, ::2], out32_sub), rel_l2(oute_sub, out32_sub)
     print(f"C2 loss: engine {loss:.7f} fp32 {l32:.7f} emulated {le:.7f}; output rel-L2 "
-          f"{rel_l2(tr.sr[:, :, ::2, ::2], out32_sub):.3e} (emulated {rel_l2(oute_sub, out32_sub):.3e})")
+          f"{out_rel:.3e} (emulated {emu_out_rel:.3e})")
+    g_all = torch.cat([g32[name].reshape(-1) for name, _, _, _ in table])
+    whole = rel_l2(grads, g_all)
+    path = os.environ.get("SRMI_PARITY_REPORT")
+    if path:  # the committed per-tensor report (profiles/rNN_c2_parity.json)
+        import json
+        eng = np.array([r[1] for r in report])
+        json.dump({"config": "C2: rcan-10-20-64, 2-var, B=64, micro=2, one step from the same weights and tiles",
+                   "reference": "oracle/rcan_oracle.py in exact fp32 on the GPU (TF32 off)",
+                   "emulation": "tests/gpu_oracle.py: the oracle with the engine's bf16 operands, pair stream, bf16 u",
+                   "loss": {"engine": loss, "fp32": l32, "emulated": le, "rel": abs(loss - l32) / l32},
+                   "output_rel_l2": {"engine": out_rel, "emulated": emu_out_rel},
+                   "grad_rel_l2_whole_vector": whole,
+                   "grad_rel_l2_caps": {"conv": GRAD_CAP_C2, "ca_mlp": GRAD_CAP_C2_CA, "whole": 1e-2},
+                   "grad_rel_l2_per_tensor": {"max": float(eng.max()), "median": float(np.median(eng)),
+                                              "p90": float(np.percentile(eng, 90))},
+                   "tensors": [{"name": n_, "engine_vs_fp32": a_, "emulated_vs_fp32": b_, "bound": 3 * b_ + 1e-3}
+                               for n_, a_, b_ in report]}, open(path, "w"), indent=1)
     assert worst <= 1.0, report[:5]
+    # a fixed bar as well (bf16 drift ~2e-2 element-wise): the bound above
+    # follows the emulation, this one does not move with the engine's precision model
+    assert max(r[1] for r in report if "conv_du" not in r[0]) <= GRAD_CAP_C2, report[:5]
+    assert max(r[1] for r in report if "conv_du" in r[0]) <= GRAD_CAP_C2_CA, report[:5]
+    assert whole <= 1e-2, whole
 
 
 def test_full_rcan_grad_samples_vs_golden_b1():

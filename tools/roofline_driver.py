@@ -3,6 +3,8 @@
 
     python tools/roofline_driver.py [--batch 64] [--micro 2] [--steps 2] [--reps 10]
 
+(--reps 0: the steps only -- tools/pmc_step_total.sh sums a whole step's PMC bytes)
+
 The FusedTrainer of bench.py (rcan-10-20-64, 2-var, B tiles of 48x48, micro-batch
 engines) runs `steps` steps, then every engine re-issues its fused backward
 launches (srmi_engine_probe: conv1's dgrad + filter gradient, then conv2's) `reps`
@@ -39,7 +41,7 @@ def main():
         tr.step(hr)
     torch.cuda.synchronize()
     main_st = torch.cuda.current_stream()
-    for which in (1, 2):
+    for which in ((1, 2) if a.reps > 0 else ()):
         for k, eng in enumerate(tr.engines):
             st = tr.streams[k] or main_st
             st.wait_stream(main_st)
