@@ -160,13 +160,13 @@ ACT_F32_PER_TILE = 48 * 48 * 64 * 4
 WGRAD_OUT_BYTES = 64 * 577 * 4           # dW (64x64x9) + db, fp32, once per launch
 # Algorithmic bytes per tile of the two fused RCAB-backward launches (SURVEY.md §8(d),
 # DESIGN.md "Kernels"): what each must move at least, every operand once.
-#  F1 = rcab_bwd_kernel<DG_ACC_CA>: conv1's dgrad (reads dz bf16, reads + writes the
-#       fp32 residual-stream gradient g, reads the CA input u bf16 for the CA sums) and
-#       conv1's filter gradient (reads its input hb bf16; dz already counted)
+#  F1 = rcab_bwd_kernel<DG_ACC_CA16>: conv1's dgrad (reads dz bf16, reads + writes the
+#       in-group gradient stream g -- bf16 since round 6 --, reads the CA input u bf16 for
+#       the CA sums) and conv1's filter gradient (reads its input hb bf16; dz already counted)
 #  F2 = rcab_bwd_kernel<DG_RELUMASK>: conv2's dgrad (reads du bf16, reads the ReLU
 #       output t bf16 as the mask, writes dz bf16) and conv2's filter gradient (t, du
 #       already counted)
-F1_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE + 2 * ACT_F32_PER_TILE
+F1_BYTES_PER_TILE = 5 * ACT_BF16_PER_TILE
 F2_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE
 FUSED_FLOP_PER_TILE = 2 * CONV64_FLOP_PER_TILE   # one dgrad conv + one filter-gradient conv
 
@@ -244,7 +244,7 @@ def fused_rooflines(tr, step_ms, reps=20):
     nl, nb = tr.spec.nlayers, tr.spec.nblocks
     per_step = {1: nl * (nb - 1), 2: nl * nb}
     streams = [tr.streams[k] or main_st for k in range(n_eng)]
-    for which, key, name, bpt in ((1, "F1", "rcab_bwd_kernel<EPI_DG_ACC_CA>", F1_BYTES_PER_TILE),
+    for which, key, name, bpt in ((1, "F1", "rcab_bwd_kernel<EPI_DG_ACC_CA16>", F1_BYTES_PER_TILE),
                                   (2, "F2", "rcab_bwd_kernel<EPI_DG_RELUMASK>", F2_BYTES_PER_TILE)):
         def issue_all(r):
             for k, eng in enumerate(tr.engines):
@@ -261,7 +261,7 @@ def fused_rooflines(tr, step_ms, reps=20):
         ach = bytes_launch / (ms1 * 1e-3) / 1e9
         tf = flop_launch / (ms1 * 1e-3) / 1e12
         ach_slot = bytes_launch * n_eng / (ms * 1e-3) / 1e9
-        tr_ = _pmc_traffic("rcab_bwd_kernel<%d" % (7 if which == 1 else 4))
+        tr_ = _pmc_traffic("rcab_bwd_kernel<%d" % (11 if which == 1 else 4))
         prof = _prof_in_step_us(key)
         # the roof is set by the launch's arithmetic intensity against the ridge point
         # (bf16 dense peak / HBM peak = 314.6 FLOP/B): F1 (164 FLOP/B) is HBM-bound,
@@ -294,7 +294,7 @@ def fused_rooflines(tr, step_ms, reps=20):
             "hbm_gbs": round(ach, 1), "hbm_frac": round(ach / HBM_PEAK_GBS, 4),
             "mfma_tflops": round(tf, 1), "mfma_frac": round(tf / PEAK_BF16_TFLOPS, 4),
             "rocprof_check": rc,
-            "mfma_pmc": _pmc_mfma("rcab_bwd_kernel<%d" % (7 if which == 1 else 4)),
+            "mfma_pmc": _pmc_mfma("rcab_bwd_kernel<%d" % (11 if which == 1 else 4)),
             "concurrent": {"launches_per_slot": n_eng, "per_stream_ms": [round(x, 4) for x in per_stream],
                            "achieved": round(ach_slot, 1), "unit": "GB/s", "frac": round(ach_slot / HBM_PEAK_GBS, 4),
                            "mfma_frac": round(flop_launch * n_eng / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),

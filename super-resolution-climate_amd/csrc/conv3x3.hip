@@ -351,8 +351,12 @@ static int launch_tw(const ConvParams& p, hipStream_t st) {
     // 8 waves (two per SIMD, a wave per row and channel half) at TW = 48
     constexpr int NW = TW == 48 ? 8 : 4;
     hipLaunchKernelGGL((conv64_kernel<TW, EPI, NW>), grid, dim3(NW * 64), Conv2Smem<TW>::TOTAL, st, q, run_len);
+  } else if constexpr (EPI == EPI_DG_ACC_CA16) {
+    return SRMI_ERR_SHAPE;  // (the bf16 gradient stream: the persistent-run body only)
   } else {
-    constexpr int E1 = EPI == EPI_DG_ACC_CA ? EPI_DG_ACC : EPI;  // v1 handles the general form
+    // v1 handles the general form, without the bf16 gradient stream
+    if (EPI == EPI_DG_ACC && (p.r1b || !p.yf)) return SRMI_ERR_SHAPE;
+    constexpr int E1 = EPI == EPI_DG_ACC_CA ? EPI_DG_ACC : EPI;
     dim3 grid((p.H / kTH) * (p.W / TW), p.Cout / 64, p.N);
     hipLaunchKernelGGL((conv3x3_kernel<TW, E1>), grid, dim3(kThreads), ConvSmem<TW>::TOTAL, st, p);
   }
@@ -399,7 +403,11 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
   if (p.Cin % 64 || p.Cout % 64 || p.N <= 0 || p.H % kTH) return SRMI_ERR_SHAPE;
   // operands each epilogue dereferences unconditionally: refuse, never fault
   if (!p.x || !p.w) return SRMI_ERR_ARG;
-  if (epi == EPI_DG_ACC_CA && (!p.r1 || !p.aux || !p.part || p.yb || p.r2 || p.r3 || !p.yf)) return SRMI_ERR_ARG;
+  if (epi == EPI_DG_ACC_CA && (!p.r1 || !p.aux || !p.part || p.yb || p.r2 || p.r3 || !p.yf || p.r1b))
+    return SRMI_ERR_ARG;
+  if (epi == EPI_DG_ACC_CA16 && (!p.r1b || !p.aux || !p.part || !p.yb || p.r1 || p.r2 || p.r3 || p.yf || p.f32))
+    return SRMI_ERR_ARG;
+  if (epi != EPI_DG_ACC && epi != EPI_DG_ACC_CA16 && p.r1b) return SRMI_ERR_ARG;
   switch (epi) {
     case EPI_PS_BF16:
       if (!p.yb) return SRMI_ERR_ARG;
@@ -413,8 +421,9 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
     case EPI_DG_RELUMASK:
       if (!p.aux) return SRMI_ERR_ARG;
       break;
-    case EPI_DG_ACC:
-      if (!p.yf || (p.part && !p.aux)) return SRMI_ERR_ARG;
+    case EPI_DG_ACC:  // (yf may be null with a bf16 yb: the bf16 stream; r1 or r1b, not both)
+      if ((!p.yf && !p.yb) || (p.part && !p.aux) || (p.r1 && p.r1b) || (p.f32 && (p.r1b || !p.yf)))
+        return SRMI_ERR_ARG;
       break;
     case EPI_RELU_POOL:
       if (!p.yb || !p.part || p.f32) return SRMI_ERR_ARG;
@@ -457,6 +466,7 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
     case EPI_DG_ACC: return launch_epi<EPI_DG_ACC>(p, st);
     case EPI_PLAIN_BF16: return launch_epi<EPI_PLAIN_BF16>(p, st);
     case EPI_DG_ACC_CA: return launch_epi<EPI_DG_ACC_CA>(p, st);
+    case EPI_DG_ACC_CA16: return launch_epi<EPI_DG_ACC_CA16>(p, st);
     case EPI_RELU_POOL: return launch_v2_only<EPI_RELU_POOL>(p, st);
     case EPI_CA_RESID_U: return launch_v2_only<EPI_CA_RESID_U>(p, st);
     default: return SRMI_ERR_ARG;

@@ -60,6 +60,7 @@ struct EpiPre {
   float4 r1[NPT][NCT];     // (DG_ACC_CA, DG_ACC: the gradient streams' 16-byte chunks of the
   uint2 aux[NPT][NCT];     //  wave's 1 KiB store runs, and u's 8 bytes beside them -- see
   float4 r2[NPT][NCT];     //  conv_epilogue2)
+  uint2 gb[NPT][NCT];      // (DG_ACC_CA16: the bf16 gradient stream's 8 bytes of the run)
 };
 
 // the gradient-stream epilogues (DG_ACC_CA, DG_ACC) add their fp32 operands to the
@@ -78,7 +79,10 @@ constexpr bool epi_cr_bf16() {
 }
 template <int EPI>
 constexpr bool epi_run() {
-  return EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC || epi_cr<EPI>();
+  return EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC_CA16 || EPI == EPI_DG_ACC || epi_cr<EPI>();
+}
+__device__ __forceinline__ float4 unpack_bf16x4(uint32_t a, uint32_t b) {
+  return make_float4(bf2f(a & 0xFFFFu), bf2f(a >> 16), bf2f(b & 0xFFFFu), bf2f(b >> 16));
 }
 
 // one (pt, c) element (idx = pt * NCT + c), issued one or two per K-step
@@ -86,7 +90,7 @@ template <int NPT, int EPI, int NCT>
 __device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT, EPI, NCT>& e, int n, int cb, int y,
                                                  int x0, int fr, int fk, int ct0, int idx) {
   if constexpr (EPI == EPI_RESID || EPI == EPI_DG_ACC || EPI == EPI_DG_RELUMASK || EPI == EPI_DG_ACC_CA ||
-                epi_cr<EPI>()) {
+                EPI == EPI_DG_ACC_CA16 || epi_cr<EPI>()) {
     const int pt = idx / NCT, c = idx % NCT;
     const size_t HW = (size_t)p.H * p.W;
     const size_t pix = (size_t)n * HW + (size_t)y * p.W + x0 + pt * 16 + fr;
@@ -118,9 +122,17 @@ __device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT
       } else if constexpr (EPI == EPI_DG_ACC_CA) {
         e.r1[pt][c] = *reinterpret_cast<const float4*>(p.r1 + oc);  // (load q = idx at [q / NCT][q % NCT])
         e.aux[pt][c] = *reinterpret_cast<const uint2*>(p.aux + oc);
+      } else if constexpr (EPI == EPI_DG_ACC_CA16) {
+        e.gb[pt][c] = *reinterpret_cast<const uint2*>(p.r1b + oc);  // 512 contiguous bytes per wave
+        e.aux[pt][c] = *reinterpret_cast<const uint2*>(p.aux + oc);
       } else {  // DG_ACC: every operand optional (uniform branches)
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        e.r1[pt][c] = p.r1 ? *reinterpret_cast<const float4*>(p.r1 + oc) : z;
+        if (p.r1b) {  // the bf16 stream's raw bits in .x / .y, decoded in the store loop
+          const uint2 gq = *reinterpret_cast<const uint2*>(p.r1b + oc);
+          e.r1[pt][c] = make_float4(__uint_as_float(gq.x), __uint_as_float(gq.y), 0.f, 0.f);
+        } else {
+          e.r1[pt][c] = p.r1 ? *reinterpret_cast<const float4*>(p.r1 + oc) : z;
+        }
         e.r2[pt][c] = p.r2 ? *reinterpret_cast<const float4*>(p.r2 + oc) : z;
         e.aux[pt][c] = p.part ? *reinterpret_cast<const uint2*>(p.aux + oc) : make_uint2(0, 0);
       }
@@ -172,7 +184,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
   const size_t HW = (size_t)p.H * p.W;
   [[maybe_unused]] const auto rfa = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
   constexpr bool kPart1 = (EPI == EPI_POOL_BF16 || EPI == EPI_RELU_POOL);
-  constexpr bool kPart2 = (EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_CA);
+  constexpr bool kPart2 = (EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC_CA16);
   float ps0[NCT][4], ps1[NCT][4];
   // fp32 output staged through LDS (DG_ACC, whose epilogue also reads r2/r3 from
   // global memory, measured faster with direct stores)
@@ -386,7 +398,16 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             // g += dx in the run layout; the lane's channels 4c..4c+3 (c = lane & 15)
             // are the same in every run, so its sums accumulate in registers
             const int q = h * (kShared ? RUNS / 2 : RUNS) + j;
-            const float4 gg = e.r1[q / NCT][q % NCT];
+            float4 gg;
+            if constexpr (EPI == EPI_DG_ACC_CA16) {
+              const uint2 gq = e.gb[q / NCT][q % NCT];
+              gg = unpack_bf16x4(gq.x, gq.y);
+            } else {
+              gg = e.r1[q / NCT][q % NCT];
+              if constexpr (EPI == EPI_DG_ACC) {
+                if (p.r1b) gg = unpack_bf16x4(__float_as_uint(gg.x), __float_as_uint(gg.y));
+              }
+            }
             const uint2 uu = e.aux[q / NCT][q % NCT];
             val.x += gg.x; val.y += gg.y; val.z += gg.z; val.w += gg.w;
             if constexpr (EPI == EPI_DG_ACC) {
@@ -398,17 +419,27 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
                 val.x += g3.x; val.y += g3.y; val.z += g3.z; val.w += g3.w;
               }
             }
+            // the bf16 gradient stream (DG_ACC_CA16, or DG_ACC without an fp32 output): g is
+            // rounded once, and the CA sums and the store take that stored value
+            if (EPI == EPI_DG_ACC_CA16 || (EPI == EPI_DG_ACC && !p.yf)) {  // (uniform)
+              const uint32_t a = pack2(val.x, val.y), b = pack2(val.z, val.w);
+              val = unpack_bf16x4(a, b);
+            }
             ps0[0][0] += val.x; ps0[0][1] += val.y; ps0[0][2] += val.z; ps0[0][3] += val.w;
             ps1[0][0] += val.x * bf2f(uu.x & 0xFFFFu);
             ps1[0][1] += val.y * bf2f(uu.x >> 16);
             ps1[0][2] += val.z * bf2f(uu.y & 0xFFFFu);
             ps1[0][3] += val.w * bf2f(uu.y >> 16);
           }
-          st_wt16(rf, p.yf, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 4), val);
+          const uint32_t oel = (uint32_t)((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4);  // element
+          if constexpr (EPI == EPI_DG_ACC_CA16) {  // 512 contiguous bytes per instruction
+            st_wt8(rbb, p.yb, oel * 2, make_uint2(pack2(val.x, val.y), pack2(val.z, val.w)));
+            continue;
+          }
+          if (EPI != EPI_DG_ACC || p.yf) st_wt16(rf, p.yf, oel * 4, val);
           if constexpr (EPI == EPI_DG_ACC) {
-            if (p.yb)  // its bf16 copy: 512 contiguous bytes per instruction
-              st_wt8(rbb, p.yb, (uint32_t)(((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4) * 2),
-                     make_uint2(pack2(val.x, val.y), pack2(val.z, val.w)));
+            if (p.yb)  // its bf16 copy (or, yf null, the stream itself): 512 contiguous bytes per instruction
+              st_wt8(rbb, p.yb, oel * 2, make_uint2(pack2(val.x, val.y), pack2(val.z, val.w)));
           }
         }
         stage_sync();
@@ -449,7 +480,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
     }
   }
   if constexpr (kRun) {
-   if (EPI == EPI_DG_ACC_CA || p.part) {  // (uniform)
+   if (EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC_CA16 || p.part) {  // (uniform)
     // lanes l, l ^ 16, l ^ 32, l ^ 48 hold the same 4 channels: fixed-order xor
     // sums, then one 64-channel partial per wave in red[wave][2][64], summed over
     // the waves in wave order

@@ -433,7 +433,7 @@ static int conv_fwd(srmi_engine* e, const ConvRef& c, const bf16_t* x, int n, in
 // dgrad of conv c: input dy (Cout channels, PS layout if c.ps), output Cin channels
 static ConvParams dgrad_params(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n, int H, int W, int* epi,
                                bf16_t* yb, float* yf, const float* r1, const float* r2, const float* r3,
-                               const bf16_t* aux, float* part, float alpha) {
+                               const bf16_t* aux, float* part, float alpha, const bf16_t* r1b = nullptr) {
   ConvParams p{};
   p.x = dy;
   p.w = e->at(e->packs, c.d_off);
@@ -448,6 +448,7 @@ static ConvParams dgrad_params(srmi_engine* e, const ConvRef& c, const bf16_t* d
   p.yb = yb;
   p.yf = yf;
   p.r1 = r1;
+  p.r1b = r1b;
   p.r2 = r2;
   p.r3 = r3;
   p.aux = aux;
@@ -456,8 +457,11 @@ static ConvParams dgrad_params(srmi_engine* e, const ConvRef& c, const bf16_t* d
   p.alpha = alpha;
   p.zeros = e->zeros;
   p.cu_budget = e->cu_budget;
+  // the hot RCAB cases: specialised epilogues without runtime operand checks
   if (*epi == EPI_DG_ACC && r1 && aux && part && !yb && !r2 && !r3 && yf && c.cout == 64 && !c.ps)
-    *epi = EPI_DG_ACC_CA;  // the hot RCAB case: specialised epilogue without runtime operand checks
+    *epi = EPI_DG_ACC_CA;
+  if (*epi == EPI_DG_ACC && r1b && !r1 && aux && part && yb && !r2 && !r3 && !yf && c.cout == 64 && !c.ps)
+    *epi = EPI_DG_ACC_CA16;  // (the bf16 engine's in-group gradient stream)
   return p;
 }
 
@@ -737,6 +741,11 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
     // The filter gradients write the slab set of their RCAB's parity; the last
     // RCAB of a group reduces its own slabs before the group's event.
     const int rs2 = rcab_row_splits(e, n, 2), rs1 = rcab_row_splits(e, n, 1);
+    // the gradient stream INSIDE a residual group (w.r.t. every RCAB output): bf16 in the
+    // bf16 engine, in the buffer of the group input gradient's bf16 copy (ghb: the group's
+    // first RCAB reads it and overwrites it in place with that copy), fp32 (ghf) in the
+    // exact-fp32 engine.  The group input gradient itself stays fp32.
+    const bool g16 = !e->f32;
     for (int g = nl - 1; g >= 0; --g) {
       const int stage = nl - g;
       // the gradient streams swap after every group: the state group g starts from
@@ -749,8 +758,8 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
       int it = (nl - 1 - g) * nb;  // RCAB counter (slab-set parity)
       const ConvRef& gt = P.group_tail[g];
       RC(conv_wgrad(e, gt, e->hb(g, nb), gRb, n, h, w, grads, true, 1.f, st));
-      RC(conv_dgrad(e, gt, gRb, n, h, w, EPI_DG_ACC, nullptr, ghf, nullptr, nullptr, nullptr, e->Um(g, nb), e->pacc,
-                    1.f, st));
+      RC(conv_dgrad(e, gt, gRb, n, h, w, EPI_DG_ACC, g16 ? ghb : nullptr, g16 ? nullptr : ghf, nullptr, nullptr,
+                    nullptr, e->Um(g, nb), e->pacc, 1.f, st));
       ReduceSet prev2{}, prev1{};
       bool have_prev = false;
       for (int b = nb; b >= 1; --b) {
@@ -758,8 +767,9 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         const int q = it++ & 1;
         bf16_t* du = e->DU;
         bf16_t* dz = e->DZ;
-        RC(ca_bwd_du_launch(ghf, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du,
-                            e->brecp(g, b), e->f32, st, have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
+        RC(ca_bwd_du_launch(g16 ? static_cast<const void*>(ghb) : ghf, g16, e->pacc, nstrips, e->recp(g, b),
+                            prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du, e->brecp(g, b), e->f32, st,
+                            have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
         ReduceSet red2, red1;
         WgradParams wp;
         int epi = EPI_DG_RELUMASK;
@@ -770,9 +780,16 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         RC(dgrad_with_wgrad(e, cp, epi, wp, 2, st));
         const bool last = (b == 1);
         epi = EPI_DG_ACC;
-        cp = dgrad_params(e, r.c1, dz, n, h, w, &epi, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
-                          (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
-                          last ? nullptr : e->pacc, 1.f);
+        // g += dgrad(dz): in the group's first RCAB into the group input gradient (fp32 +
+        // its bf16 copy, with the group's skip gradient gR), else the in-group stream
+        if (g16)
+          cp = dgrad_params(e, r.c1, dz, n, h, w, &epi, ghb, last ? ghf : nullptr, nullptr, last ? gRf : nullptr,
+                            (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
+                            last ? nullptr : e->pacc, 1.f, ghb);
+        else
+          cp = dgrad_params(e, r.c1, dz, n, h, w, &epi, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
+                            (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
+                            last ? nullptr : e->pacc, 1.f);
         RC(wgrad_params(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, rs1, e->slab_r[q][1],
                         e->bslab_r[q][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red1));
         RC(dgrad_with_wgrad(e, cp, epi, wp, 1, st));
@@ -945,8 +962,12 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
   } else {
     const bool last = (b == 1);
     epi = EPI_DG_ACC;
-    cp = dgrad_params(e, r.c1, e->DZ, n, h, w, &epi, last ? e->GAb : nullptr, ghf, ghf, last ? e->GAf : nullptr,
-                      nullptr, last ? nullptr : e->Um(0, b - 1), last ? nullptr : e->pacc, 1.f);
+    if (!e->f32)  // the bf16 in-group gradient stream, as backward_impl issues it
+      cp = dgrad_params(e, r.c1, e->DZ, n, h, w, &epi, e->GBb, last ? ghf : nullptr, nullptr, last ? e->GAf : nullptr,
+                        nullptr, last ? nullptr : e->Um(0, b - 1), last ? nullptr : e->pacc, 1.f, e->GBb);
+    else
+      cp = dgrad_params(e, r.c1, e->DZ, n, h, w, &epi, last ? e->GAb : nullptr, ghf, ghf, last ? e->GAf : nullptr,
+                        nullptr, last ? nullptr : e->Um(0, b - 1), last ? nullptr : e->pacc, 1.f);
     RC(wgrad_params(e, r.c1, e->hb(0, b - 1), e->DZ, n, h, w, grads, true, 1.f, rcab_row_splits(e, n, 1),
                     e->slab_r[0][1], e->bslab_r[0][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red));
   }
@@ -1119,7 +1140,8 @@ int srmi_ca_forward_pair(const void* u, const float* part, int nstrips, const fl
 int srmi_ca_backward(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
                      const float* w2, int N, int HW, int C, int R, void* du, float* brec, int dtype, void* stream) {
   if (dtype != SRMI_DTYPE_BF16 && dtype != SRMI_DTYPE_F32) return SRMI_ERR_ARG;
-  return ca_bwd_du_launch(g, part, nstrips, rec, w1, w2, N, HW, C, R, du, brec, dtype == SRMI_DTYPE_F32, S_(stream));
+  return ca_bwd_du_launch(g, 0, part, nstrips, rec, w1, w2, N, HW, C, R, du, brec, dtype == SRMI_DTYPE_F32,
+                          S_(stream));
 }
 
 int srmi_head_forward(const float* lr, const float* w, const float* b, int N, int C, int H, int W, float* x0f,

@@ -1359,14 +1359,15 @@ int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1
 // backward while its g loads are in flight; block 0 of the image writes
 // brec per image: dz2[C] dz1[CR] dbconv2[C]; followed (after all N images) by
 // dm[N][C] = W1^T dz1 (the gradient of the pooled mean).
-// du = g * s + dm / HW  (operand type)
+// du = g * s + dm / HW  (operand type T); g fp32, or (TG = bf16_t) the bf16 engine's
+// in-group gradient stream
 //
 // Rows blockIdx.y >= N of the grid (nred > 0) carry the fixed-order slab
 // reductions of the previous RCAB's two filter gradients (r0, r1: nred blocks
 // each, 256-thread wgrad_reduce_body): both are memory-bound passes of many small
 // blocks, so the reduction rides in this launch instead of a launch of its own.
-template <typename T>
-__global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict__ g, const float* __restrict__ part,
+template <typename T, typename TG>
+__global__ void __launch_bounds__(256) ca_bwd_du_kernel(const TG* __restrict__ g, const float* __restrict__ part,
                                                         int nstrips, const float* __restrict__ rec,
                                                         const float* __restrict__ w1, const float* __restrict__ w2,
                                                         int N, int HW, int C, int CR, T* __restrict__ du,
@@ -1412,11 +1413,16 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
   const size_t nv = (size_t)HW * C / 8;
   const size_t v0 = ((size_t)blockIdx.x * kCaVec) * blockDim.x + tid;
   float4 g0[kCaVec], g1[kCaVec];
+  [[maybe_unused]] uint4 gq[kCaVec];
 #pragma unroll
   for (int k = 0; k < kCaVec; ++k) {  // clamped, unconditional (tail lanes store nothing)
     const size_t e = base + min(v0 + (size_t)k * blockDim.x, nv - 1) * 8;
-    g0[k] = *reinterpret_cast<const float4*>(g + e);
-    g1[k] = *reinterpret_cast<const float4*>(g + e + 4);
+    if constexpr (sizeof(TG) == 2) {
+      gq[k] = *reinterpret_cast<const uint4*>(g + e);  // 8 bf16, decoded where used
+    } else {
+      g0[k] = *reinterpret_cast<const float4*>(g + e);
+      g1[k] = *reinterpret_cast<const float4*>(g + e + 4);
+    }
   }
   __builtin_amdgcn_sched_barrier(0);
   red[tid >> 7][tid & 127] = pa;
@@ -1468,6 +1474,10 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
     float dmh[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) dmh[i] = dm[c0 + i] * (1.f / (float)HW);
+    if constexpr (sizeof(TG) == 2) {
+      g0[k] = make_float4(bf2f(gq[k].x & 0xFFFFu), bf2f(gq[k].x >> 16), bf2f(gq[k].y & 0xFFFFu), bf2f(gq[k].y >> 16));
+      g1[k] = make_float4(bf2f(gq[k].z & 0xFFFFu), bf2f(gq[k].z >> 16), bf2f(gq[k].w & 0xFFFFu), bf2f(gq[k].w >> 16));
+    }
     const float o[8] = {g0[k].x * s[c0 + 0] + dmh[0], g0[k].y * s[c0 + 1] + dmh[1], g0[k].z * s[c0 + 2] + dmh[2],
                         g0[k].w * s[c0 + 3] + dmh[3], g1[k].x * s[c0 + 4] + dmh[4], g1[k].y * s[c0 + 5] + dmh[5],
                         g1[k].z * s[c0 + 6] + dmh[6], g1[k].w * s[c0 + 7] + dmh[7]};
@@ -1481,9 +1491,10 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const float* __restrict_
   }
 }
 
-int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
+int ca_bwd_du_launch(const void* g, int g16, const float* part, int nstrips, const float* rec, const float* w1,
                      const float* w2, int N, int HW, int C, int R, void* du, float* brec, int f32, hipStream_t st,
                      const ReduceSet* red0, const ReduceSet* red1) {
+  if (f32 && g16) return SRMI_ERR_ARG;
   if (C != 64 || C % R || (C / R) > 32 || (C / R) % 4 || (HW * C) % 8) return SRMI_ERR_SHAPE;
   if ((red0 == nullptr) != (red1 == nullptr)) return SRMI_ERR_ARG;
   if (red0 && (red0->Cout != red1->Cout)) return SRMI_ERR_SHAPE;
@@ -1494,11 +1505,14 @@ int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float
   const ReduceSet& a = red0 ? *red0 : none;
   const ReduceSet& b = red1 ? *red1 : none;
   if (f32)
-    hipLaunchKernelGGL(ca_bwd_du_kernel<float>, grid, dim3(256), 0, st, g, part, nstrips, rec, w1, w2, N, HW, C,
-                       C / R, static_cast<float*>(du), brec, a, b, nred);
+    hipLaunchKernelGGL((ca_bwd_du_kernel<float, float>), grid, dim3(256), 0, st, static_cast<const float*>(g), part,
+                       nstrips, rec, w1, w2, N, HW, C, C / R, static_cast<float*>(du), brec, a, b, nred);
+  else if (g16)
+    hipLaunchKernelGGL((ca_bwd_du_kernel<bf16_t, bf16_t>), grid, dim3(256), 0, st, static_cast<const bf16_t*>(g),
+                       part, nstrips, rec, w1, w2, N, HW, C, C / R, static_cast<bf16_t*>(du), brec, a, b, nred);
   else
-    hipLaunchKernelGGL(ca_bwd_du_kernel<bf16_t>, grid, dim3(256), 0, st, g, part, nstrips, rec, w1, w2, N, HW, C,
-                       C / R, static_cast<bf16_t*>(du), brec, a, b, nred);
+    hipLaunchKernelGGL((ca_bwd_du_kernel<bf16_t, float>), grid, dim3(256), 0, st, static_cast<const float*>(g), part,
+                       nstrips, rec, w1, w2, N, HW, C, C / R, static_cast<bf16_t*>(du), brec, a, b, nred);
   SRMI_CHECK_LAUNCH();
   return 0;
 }

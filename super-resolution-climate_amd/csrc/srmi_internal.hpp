@@ -19,7 +19,9 @@ enum Epi {
   EPI_RESID = 2,       // y = alpha*(acc + b) + r1                  -> fp32 (opt) + bf16
   EPI_PS_BF16 = 3,     // y = acc + b, PixelShuffle(2) scatter      -> bf16 [2H][2W][64]
   EPI_DG_RELUMASK = 4, // dz = acc * (aux > 0)                      -> bf16
-  EPI_DG_ACC = 5,      // g = acc + r1 + r2 + r3 (+ sums of g, g*aux) -> fp32 + bf16
+  EPI_DG_ACC = 5,      // g = acc + r1 + r2 + r3 (+ sums of g, g*aux) -> fp32 + bf16; r1 may be the
+                       // bf16 r1b instead, and yf may be null (bf16 yb only: the sums then use
+                       // the rounded bf16 g, the stream's stored value)
   EPI_PLAIN_BF16 = 6,  // y = acc (+ b)                              -> bf16
   EPI_DG_ACC_CA = 7,   // g = acc + r1, sums of g and g*aux; r1/aux/part non-null, no yb/r2/r3
                        // (the hot RCAB case of EPI_DG_ACC, specialised: no runtime operand checks)
@@ -31,6 +33,9 @@ enum Epi {
   EPI_CA_RESID_U = 10, // u = acc + b -> bf16 yb (saved for backward), h' = h + s[c] bf16(u) as
                        // in EPI_CA_RESID; s computed after the first strip's MFMAs (cas_on,
                        // ca_scale.hpp: from conv1's partial means, or from t) or read from escale
+  // the bf16 engine's in-group gradient stream (the hot RCAB conv1 dgrad, F1):
+  EPI_DG_ACC_CA16 = 11, // g = bf16(acc + r1b) -> bf16 yb (in place over r1b allowed), sums of
+                        // that bf16 g and g*aux; r1b / aux / part / yb non-null, no yf / r1 / r2 / r3
 };
 
 // The CA scale of an RCAB from its conv1 output t (ca_scale.hpp): mean(u) of u =
@@ -61,6 +66,7 @@ struct ConvParams {
   bf16_t* yb;          // bf16 output
   float* yf;           // fp32 output
   const float* r1;
+  const bf16_t* r1b;   // (DG_ACC_CA16, DG_ACC) the gradient-stream operand in bf16 instead of r1
   const float* r2;
   const float* r3;
   const bf16_t* aux;   // relu output t (RELUMASK) / CA input u (DG_ACC sums)
@@ -183,7 +189,8 @@ int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1
                   void* hb_out, float* rec, int f32, hipStream_t st, const void* hi_in = nullptr,
                   const void* lo_in = nullptr, void* lo_out = nullptr);
 // red0/red1 (both or neither): two slab reductions carried in the same launch
-int ca_bwd_du_launch(const float* g, const float* part, int nstrips, const float* rec, const float* w1,
+// g: fp32, or (g16) the bf16 engine's in-group gradient stream in bf16
+int ca_bwd_du_launch(const void* g, int g16, const float* part, int nstrips, const float* rec, const float* w1,
                      const float* w2, int N, int HW, int C, int R, void* du, float* brec, int f32, hipStream_t st,
                      const ReduceSet* red0 = nullptr, const ReduceSet* red1 = nullptr);
 // inference RCAB, one launch with a workgroup per image (rcab_infer.hip): c1 = conv1

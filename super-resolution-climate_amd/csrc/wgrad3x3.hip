@@ -656,12 +656,17 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
                          nconv, w, nwg, paired, tail);
       break;
     case EPI_DG_ACC_CA:
-      if (!c.r1 || !c.aux || !c.part || c.yb || c.r2 || c.r3 || !c.yf) return SRMI_ERR_ARG;
+      if (!c.r1 || !c.aux || !c.part || c.yb || c.r2 || c.r3 || !c.yf || c.r1b) return SRMI_ERR_ARG;
       hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len,
                          nconv, w, nwg, paired, tail);
       break;
+    case EPI_DG_ACC_CA16:
+      if (!c.r1b || !c.aux || !c.part || !c.yb || c.r1 || c.r2 || c.r3 || c.yf) return SRMI_ERR_ARG;
+      hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA16, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len,
+                         nconv, w, nwg, paired, tail);
+      break;
     case EPI_DG_ACC:
-      if (!c.yf || (c.part && !c.aux)) return SRMI_ERR_ARG;
+      if ((!c.yf && !c.yb) || (c.part && !c.aux) || (c.r1 && c.r1b)) return SRMI_ERR_ARG;
       hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len, nconv, w, nwg, paired, tail);
       break;
     default:

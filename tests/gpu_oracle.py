@@ -18,7 +18,12 @@ run as unfold + rocBLAS GEMM) and no reduced-precision math.
 * the residual stream INSIDE a residual group is the pair hi + lo (bf16 hi plus an
   8-bit remainder, common.hpp pair codec): 16 significant bits, rounded after every
   CA add (h = pair16(h + out)); the group input, the
-  group-tail / body-tail outputs and the whole gradient stream stay fp32.
+  group-tail / body-tail outputs stay fp32;
+* the gradient stream INSIDE a residual group -- the gradient w.r.t. every RCAB's
+  output -- is bf16 (the group-tail dgrad and every RCAB's conv1 dgrad store it rounded,
+  EPI_DG_ACC_CA16, and the CA backward reads it): rounded where it arrives at an RCAB
+  output (after autograd has summed the identity and conv paths); the gradient of the
+  group input and every other gradient stay fp32.
 Rounding is straight-through in backward, as in the engine (the stored values are
 what backward reads; the gradient of an add is the identity).  The model's drift
 from the fp32 oracle is the reference's own drift under the engine's arithmetic,
@@ -92,6 +97,18 @@ def pair16(h: torch.Tensor) -> torch.Tensor:
     return bits.view(torch.float32).to(h.dtype)
 
 
+class _GradBf16(torch.autograd.Function):
+    """Identity forward; backward rounds the (summed) incoming gradient to bf16."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _bf(g)
+
+
 class _StraightPair16(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
@@ -107,7 +124,7 @@ def _emul_rcab_forward(self, x):
     b = self.body
     u = b[2](b[1](b[0](x)))
     s = b[3].conv_du(u.mean(dim=(2, 3), keepdim=True))
-    return _StraightPair16.apply(_StraightBf16.apply(u) * s + x)
+    return _GradBf16.apply(_StraightPair16.apply(_StraightBf16.apply(u) * s + x))
 
 
 class _EmulConv(nn.Module):

@@ -17,8 +17,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def child(mode, prio, pre, steps):
-    sys.path.insert(0, os.path.join(HERE, "..", "super-resolution-climate_amd"))
-    sys.path.insert(0, os.path.join(HERE, ".."))
+    sys.path.insert(0, os.path.join(HERE, "..", "..", "super-resolution-climate_amd"))
+    sys.path.insert(0, os.path.join(HERE, "..", ".."))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     import torch
     from srmi.dist import init_from_env

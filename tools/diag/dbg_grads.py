@@ -6,7 +6,7 @@ printed instead of stopping at the first over its bound).  Debug aid.
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "super-resolution-climate_amd"), ROOT]
 
 import numpy as np  # noqa: E402

@@ -7,7 +7,7 @@ streams sit on different hardware queues, ~2T when they share one.  Stream kinds
   hi[i]       high-priority pool streams
   cumask[i]   hipExtStreamCreateWithCUMask with every CU enabled
   plain[i]    hipStreamCreateWithFlags(NonBlocking)
-    python tools/dbg_queues.py [--pg]     (--pg: a one-rank RCCL group first)
+    python tools/diag/dbg_queues.py [--pg]     (--pg: a one-rank RCCL group first)
 """
 import ctypes as C
 import os

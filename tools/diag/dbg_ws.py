@@ -2,7 +2,7 @@
 variants / micro-batch splits from the engine workspaces (carve order of engine.cpp)."""
 import os
 import sys
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "super-resolution-climate_amd"), ROOT]
 import torch  # noqa: E402
 from oracle import rcan_oracle as ro  # noqa: E402

@@ -35,7 +35,7 @@ def main(trace, bench_log, out):
     n_eng = 1
     if line and line.get("roofline"):
         n_eng = line["roofline"].get("concurrent", {}).get("launches_per_slot", 1)
-    for key, pat, rk in (("F1", "rcab_bwd_kernel<7", "roofline"), ("F2", "rcab_bwd_kernel<4", "roofline_f2")):
+    for key, pat, rk in (("F1", "rcab_bwd_kernel<11", "roofline"), ("F2", "rcab_bwd_kernel<4", "roofline_f2")):
         d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows if pat in r["Kernel_Name"]]
         if not d:
             continue
