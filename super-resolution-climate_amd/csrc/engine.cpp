@@ -244,6 +244,8 @@ struct srmi_engine {
 // CU budget split in halves), so their row chunks are sized for HALF the engine's
 // budget: fewer, longer chunks write fewer partial slabs (at C2 2 x 24-row chunks
 // per image instead of 3 x 16).
+constexpr bool kSlab16 = SRMI_SLAB16 != 0;  // bf16 RCAB filter-gradient slabs (tuning.hpp)
+
 static int engine_cus(const srmi_engine* e) { return e->cu_budget > 0 ? e->cu_budget : 256; }
 // CU shares of the two parts of a fused launch, in percent of the engine budget taken
 // by the filter gradient: after the ReLU-mask dgrad of conv2 (FUSE_WG2) and after the
@@ -476,7 +478,7 @@ static int conv_dgrad(srmi_engine* e, const ConvRef& c, const bf16_t* dy, int n,
 // reduction into grads is returned in *red
 static int wgrad_params(srmi_engine* e, const ConvRef& c, const bf16_t* x, const bf16_t* dy, int n, int H, int W,
                         float* grads, bool with_bias, float alpha, int row_splits, float* slab, float* bslab,
-                        size_t cap, size_t bcap, WgradParams* out, ReduceSet* red) {
+                        size_t cap, size_t bcap, WgradParams* out, ReduceSet* red, bool slab16 = false) {
   WgradParams p{};
   p.x = x;
   p.dy = dy;
@@ -491,11 +493,13 @@ static int wgrad_params(srmi_engine* e, const ConvRef& c, const bf16_t* x, const
   p.slab = slab;
   p.bslab = bslab;
   p.zeros = e->zeros;
+  // bf16 weight slabs only where the wgrad48 body writes them (layout 1)
+  p.slab16 = slab16 && !e->f32 && wgrad3x3_slab_layout(p) == 1;
   const size_t ns = (size_t)wgrad3x3_nslabs(p);
   if (ns * c.cout * 576 > cap || ns * c.cout > bcap) return SRMI_ERR_WORKSPACE;
   *out = p;
   *red = ReduceSet{p.slab, p.bslab, (int)ns, c.cout, c.ps, wgrad3x3_slab_layout(p), alpha, grads + c.w,
-                   with_bias ? grads + c.b : nullptr};
+                   with_bias ? grads + c.b : nullptr, p.slab16};
   return 0;
 }
 
@@ -776,7 +780,7 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         ConvParams cp = dgrad_params(e, r.c2, du, n, h, w, &epi, dz, nullptr, nullptr, nullptr, nullptr, e->Tm(g, b),
                                      nullptr, 1.f);
         RC(wgrad_params(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, rs2, e->slab_r[q][0], e->bslab_r[q][0],
-                        e->slab_r_floats, e->bslab_r_floats, &wp, &red2));
+                        e->slab_r_floats, e->bslab_r_floats, &wp, &red2, kSlab16));
         RC(dgrad_with_wgrad(e, cp, epi, wp, 2, st));
         const bool last = (b == 1);
         epi = EPI_DG_ACC;
@@ -791,7 +795,7 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
                             (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
                             last ? nullptr : e->pacc, 1.f);
         RC(wgrad_params(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, rs1, e->slab_r[q][1],
-                        e->bslab_r[q][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red1));
+                        e->bslab_r[q][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red1, kSlab16));
         RC(dgrad_with_wgrad(e, cp, epi, wp, 1, st));
         prev2 = red2;
         prev1 = red1;
@@ -958,7 +962,7 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
     cp = dgrad_params(e, r.c2, e->DU, n, h, w, &epi, e->DZ, nullptr, nullptr, nullptr, nullptr, e->Tm(0, b), nullptr,
                       1.f);
     RC(wgrad_params(e, r.c2, e->Tm(0, b), e->DU, n, h, w, grads, false, 1.f, rcab_row_splits(e, n, 2),
-                    e->slab_r[0][0], e->bslab_r[0][0], e->slab_r_floats, e->bslab_r_floats, &wp, &red));
+                    e->slab_r[0][0], e->bslab_r[0][0], e->slab_r_floats, e->bslab_r_floats, &wp, &red, kSlab16));
   } else {
     const bool last = (b == 1);
     epi = EPI_DG_ACC;
@@ -969,7 +973,7 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
       cp = dgrad_params(e, r.c1, e->DZ, n, h, w, &epi, last ? e->GAb : nullptr, ghf, ghf, last ? e->GAf : nullptr,
                         nullptr, last ? nullptr : e->Um(0, b - 1), last ? nullptr : e->pacc, 1.f);
     RC(wgrad_params(e, r.c1, e->hb(0, b - 1), e->DZ, n, h, w, grads, true, 1.f, rcab_row_splits(e, n, 1),
-                    e->slab_r[0][1], e->bslab_r[0][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red));
+                    e->slab_r[0][1], e->bslab_r[0][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red, kSlab16));
   }
   for (int i = 0; i < reps; ++i) RC(dgrad_with_wgrad(e, cp, epi, wp, which, S_(stream)));
   return 0;

@@ -1376,10 +1376,9 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const TG* __restrict__ g
   if ((int)blockIdx.y >= N) {
     const int id = ((int)blockIdx.y - N) * (int)gridDim.x + (int)blockIdx.x;
     if (id < nred)
-      wgrad_reduce_body<16>(r0.slab, r0.bslab, r0.nslab, r0.Cout, r0.ps, r0.layout, r0.alpha, r0.gw, r0.gb, id);
+      wgrad_reduce_body<16>(r0, id);
     else if (id < 2 * nred)
-      wgrad_reduce_body<16>(r1.slab, r1.bslab, r1.nslab, r1.Cout, r1.ps, r1.layout, r1.alpha, r1.gw, r1.gb,
-                            id - nred);
+      wgrad_reduce_body<16>(r1, id - nred);
     return;
   }
   __shared__ float red[2][128], s[64], dz2[64], dz1[32], dm[64];

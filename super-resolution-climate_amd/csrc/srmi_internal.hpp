@@ -100,12 +100,13 @@ int conv3x3_nstrips(int H, int W);
 int conv64_runs_per_image(const ConvParams& p);  // workgroups per image of a 48-wide v2 launch
 
 struct ReduceSet {  // one slab reduction: slabs -> torch-layout dW (and db)
-  const float* slab;
+  const float* slab;   // (slab16: bf16 slabs at this address)
   const float* bslab;
   int nslab, Cout, ps, layout;
   float alpha;
   float* gw;
   float* gb;
+  int slab16;          // the weight slabs are bf16 (WgradParams.slab16); the bias slabs stay fp32
 };
 
 // weight gradient of a 3x3 conv: slab[s][Cout][9][64] + bias slab[s][Cout]
@@ -121,6 +122,8 @@ struct WgradParams {
   const void* zeros;   // >= 16 zero bytes in global memory (DMA source for padding)
   unsigned long long* stamps;  // diagnostic (null in production)
   int f32;             // exact-fp32 mode: x, dy point at fp32 data
+  int slab16;          // (wgrad48 body) weight slabs stored as bf16 at `slab` (the RCAB filter
+                       // gradients of the bf16 engine: half the slab bytes); bias slabs fp32
 };
 void wgrad3x3_set_debug_stamps(unsigned long long* buf);
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st);  // dispatches p.f32

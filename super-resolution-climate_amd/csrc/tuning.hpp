@@ -62,6 +62,12 @@
 #define SRMI_FUSE_TAIL_FIRST 1
 #endif
 
+// the RCAB filter gradients' partial slabs (the fused backward's wgrad48 body) stored as
+// bf16 and summed in fp32 by the reduction (1), or fp32 (0): half the slab bytes
+#ifndef SRMI_SLAB16
+#define SRMI_SLAB16 1
+#endif
+
 // waves per workgroup of the exact-fp32 conv (conv_f32.hip)
 #ifndef SRMI_F32_NW
 #define SRMI_F32_NW 8

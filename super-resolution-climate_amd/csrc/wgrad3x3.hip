@@ -512,15 +512,21 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   const size_t soff = (size_t)chunk * Cout * 576 + (size_t)cb * (64 * 576);
   // (write-through: the slab leaves the XCD's L2 while the other waves still
   //  compute, instead of in the dirty-line flush at the end of the launch)
-  [[maybe_unused]] const auto rsl = wt_rsrc(p.slab, (uint32_t)((size_t)(chunk + 1) * Cout * 576 * 4));
+  // (slab16: the same order in bf16, 512 contiguous bytes per store instruction)
+  const uint32_t esz = p.slab16 ? 2u : 4u;
+  [[maybe_unused]] const auto rsl = wt_rsrc(p.slab, (uint32_t)((size_t)(chunk + 1) * Cout * 576 * esz));
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int ct = 0; ct < NCA; ++ct) {
       const int J = J0 + t, w4 = J / 9, t4 = J % 9, s4 = (ctile(ct) - w4) & 3;
-      const float4 v = make_float4(acc[ct][t][0], acc[ct][t][1], acc[ct][t][2], acc[ct][t][3]);
       const size_t o = soff + (size_t)w4 * (9 * 4 * 256) + ((t4 * 4 + s4) * 64 + lane) * 4;
-      st_wt16(rsl, p.slab, (uint32_t)(o * 4), v);
+      if (p.slab16)  // (uniform)
+        st_wt8(rsl, p.slab, (uint32_t)(o * 2),
+               make_uint2(pack2(acc[ct][t][0], acc[ct][t][1]), pack2(acc[ct][t][2], acc[ct][t][3])));
+      else
+        st_wt16(rsl, p.slab, (uint32_t)(o * 4),
+                make_float4(acc[ct][t][0], acc[ct][t][1], acc[ct][t][2], acc[ct][t][3]));
     }
   if (kBias && (lane & 15) == 0) {
 #pragma unroll
@@ -709,21 +715,21 @@ int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
 }
 
 __global__ void __launch_bounds__(kRedQ * kRedPh) wgrad_reduce_kernel(ReduceSet r) {
-  wgrad_reduce_body<kRedPh>(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb, blockIdx.x);
+  wgrad_reduce_body<kRedPh>(r, blockIdx.x);
 }
 
 // two independent reductions in one launch (blockIdx.y selects the set): the two
 // filter gradients of an RCAB on the side stream share one launch and one boundary
 __global__ void __launch_bounds__(kRedQ * kRedPh) wgrad_reduce2_kernel(ReduceSet r0, ReduceSet r1) {
   const ReduceSet& r = blockIdx.y ? r1 : r0;
-  wgrad_reduce_body<kRedPh>(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb, blockIdx.x);
+  wgrad_reduce_body<kRedPh>(r, blockIdx.x);
 }
 
 int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, int layout, float alpha,
                         float* gw, float* gb, hipStream_t st) {
   if (Cout % 64) return SRMI_ERR_SHAPE;
   const int blocks = wgrad_reduce_blocks(Cout);
-  const ReduceSet r{slab, bslab, nslab, Cout, ps, layout, alpha, gw, gb};
+  const ReduceSet r{slab, bslab, nslab, Cout, ps, layout, alpha, gw, gb, 0};
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(kRedQ * kRedPh), 0, st, r);
   SRMI_CHECK_LAUNCH();
   return 0;

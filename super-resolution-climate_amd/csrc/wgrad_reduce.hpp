@@ -19,10 +19,15 @@ inline int wgrad_reduce_blocks(int Cout) { return Cout * 576 / (4 * kRedQ) + (Co
 
 // PH = slab phases per block (blockDim = kRedQ * PH: 32 -> 512 threads, 16 -> 256);
 // bid = this block's index within the reduction's wgrad_reduce_blocks(Cout)
+// slab16: the weight slabs are bf16 (4 values per 8-byte load), summed in fp32
 template <int PH>
-__device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab, const float* __restrict__ bslab,
-                                                  int nslab, int Cout, int ps, int layout, float alpha,
-                                                  float* __restrict__ gw, float* __restrict__ gb, int bid) {
+__device__ __forceinline__ void wgrad_reduce_body(const ReduceSet& rs, int bid) {
+  const float* __restrict__ slab = rs.slab;
+  const float* __restrict__ bslab = rs.bslab;
+  const int nslab = rs.nslab, Cout = rs.Cout, ps = rs.ps, layout = rs.layout;
+  const float alpha = rs.alpha;
+  float* __restrict__ gw = rs.gw;
+  float* __restrict__ gb = rs.gb;
   __shared__ float4 red[PH][kRedQ], red2[4][kRedQ];
   const int per = Cout * 576;
   const int nwb = per / (4 * kRedQ);  // weight blocks (per % 64 == 0 since Cout % 64 == 0)
@@ -46,7 +51,24 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ slab
   float4 a[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (valid) {
+  if (valid && is_w && rs.slab16) {  // (uniform) bf16 weight slabs: the same order and sums
+    const uint16_t* src16 = reinterpret_cast<const uint16_t*>(slab) + o4;
+    constexpr int U = 4;
+    for (int k = ph; k < nslab; k += U * PH) {
+      uint2 v[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int sl = k + j * PH;
+        v[j] = *reinterpret_cast<const uint2*>(src16 + (size_t)min(sl, nslab - 1) * stride);
+        if (sl >= nslab) v[j] = make_uint2(0u, 0u);  // (bf16 +0)
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        a[j].x += bf2f(v[j].x & 0xFFFFu); a[j].y += bf2f(v[j].x >> 16);
+        a[j].z += bf2f(v[j].y & 0xFFFFu); a[j].w += bf2f(v[j].y >> 16);
+      }
+    }
+  } else if (valid) {
     // phase ph sums slabs ph, ph + PH, ... -- U loads in flight per round,
     // clamped + zeroed past the end (adding 0.f is exact; no divergent branch)
     constexpr int U = 4;
