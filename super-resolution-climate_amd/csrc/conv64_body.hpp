@@ -77,9 +77,14 @@ template <int EPI>
 constexpr bool epi_cr_bf16() {
   return EPI == EPI_CA_RESID_U || (EPI == EPI_CA_RESID && SRMI_INFER_BF16U);
 }
+// the bf16 in-group gradient stream's epilogues (with / without the stream's input r1b)
+template <int EPI>
+constexpr bool epi_g16() {
+  return EPI == EPI_DG_ACC_CA16 || EPI == EPI_DG_CA16;
+}
 template <int EPI>
 constexpr bool epi_run() {
-  return EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC_CA16 || EPI == EPI_DG_ACC || epi_cr<EPI>();
+  return EPI == EPI_DG_ACC_CA || epi_g16<EPI>() || EPI == EPI_DG_ACC || epi_cr<EPI>();
 }
 __device__ __forceinline__ float4 unpack_bf16x4(uint32_t a, uint32_t b) {
   return make_float4(bf2f(a & 0xFFFFu), bf2f(a >> 16), bf2f(b & 0xFFFFu), bf2f(b >> 16));
@@ -90,7 +95,7 @@ template <int NPT, int EPI, int NCT>
 __device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT, EPI, NCT>& e, int n, int cb, int y,
                                                  int x0, int fr, int fk, int ct0, int idx) {
   if constexpr (EPI == EPI_RESID || EPI == EPI_DG_ACC || EPI == EPI_DG_RELUMASK || EPI == EPI_DG_ACC_CA ||
-                EPI == EPI_DG_ACC_CA16 || epi_cr<EPI>()) {
+                epi_g16<EPI>() || epi_cr<EPI>()) {
     const int pt = idx / NCT, c = idx % NCT;
     const size_t HW = (size_t)p.H * p.W;
     const size_t pix = (size_t)n * HW + (size_t)y * p.W + x0 + pt * 16 + fr;
@@ -122,8 +127,9 @@ __device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT
       } else if constexpr (EPI == EPI_DG_ACC_CA) {
         e.r1[pt][c] = *reinterpret_cast<const float4*>(p.r1 + oc);  // (load q = idx at [q / NCT][q % NCT])
         e.aux[pt][c] = *reinterpret_cast<const uint2*>(p.aux + oc);
-      } else if constexpr (EPI == EPI_DG_ACC_CA16) {
-        e.gb[pt][c] = *reinterpret_cast<const uint2*>(p.r1b + oc);  // 512 contiguous bytes per wave
+      } else if constexpr (epi_g16<EPI>()) {
+        if constexpr (EPI == EPI_DG_ACC_CA16)
+          e.gb[pt][c] = *reinterpret_cast<const uint2*>(p.r1b + oc);  // 512 contiguous bytes per wave
         e.aux[pt][c] = *reinterpret_cast<const uint2*>(p.aux + oc);
       } else {  // DG_ACC: every operand optional (uniform branches)
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -184,7 +190,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
   const size_t HW = (size_t)p.H * p.W;
   [[maybe_unused]] const auto rfa = wt_rsrc(p.yf, (uint32_t)((size_t)p.N * HW * p.Cout * 4));
   constexpr bool kPart1 = (EPI == EPI_POOL_BF16 || EPI == EPI_RELU_POOL);
-  constexpr bool kPart2 = (EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC_CA16);
+  constexpr bool kPart2 = (EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_CA || epi_g16<EPI>());
   float ps0[NCT][4], ps1[NCT][4];
   // fp32 output staged through LDS (DG_ACC, whose epilogue also reads r2/r3 from
   // global memory, measured faster with direct stores)
@@ -402,6 +408,8 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             if constexpr (EPI == EPI_DG_ACC_CA16) {
               const uint2 gq = e.gb[q / NCT][q % NCT];
               gg = unpack_bf16x4(gq.x, gq.y);
+            } else if constexpr (EPI == EPI_DG_CA16) {
+              gg = make_float4(0.f, 0.f, 0.f, 0.f);
             } else {
               gg = e.r1[q / NCT][q % NCT];
               if constexpr (EPI == EPI_DG_ACC) {
@@ -421,7 +429,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             }
             // the bf16 gradient stream (DG_ACC_CA16, or DG_ACC without an fp32 output): g is
             // rounded once, and the CA sums and the store take that stored value
-            if (EPI == EPI_DG_ACC_CA16 || (EPI == EPI_DG_ACC && !p.yf)) {  // (uniform)
+            if (epi_g16<EPI>() || (EPI == EPI_DG_ACC && !p.yf)) {  // (uniform)
               const uint32_t a = pack2(val.x, val.y), b = pack2(val.z, val.w);
               val = unpack_bf16x4(a, b);
             }
@@ -432,7 +440,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             ps1[0][3] += val.w * bf2f(uu.y >> 16);
           }
           const uint32_t oel = (uint32_t)((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4);  // element
-          if constexpr (EPI == EPI_DG_ACC_CA16) {  // 512 contiguous bytes per instruction
+          if constexpr (epi_g16<EPI>()) {  // 512 contiguous bytes per instruction
             st_wt8(rbb, p.yb, oel * 2, make_uint2(pack2(val.x, val.y), pack2(val.z, val.w)));
             continue;
           }
@@ -480,7 +488,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
     }
   }
   if constexpr (kRun) {
-   if (EPI == EPI_DG_ACC_CA || EPI == EPI_DG_ACC_CA16 || p.part) {  // (uniform)
+   if (EPI == EPI_DG_ACC_CA || epi_g16<EPI>() || p.part) {  // (uniform)
     // lanes l, l ^ 16, l ^ 32, l ^ 48 hold the same 4 channels: fixed-order xor
     // sums, then one 64-channel partial per wave in red[wave][2][64], summed over
     // the waves in wave order

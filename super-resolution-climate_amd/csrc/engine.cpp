@@ -464,6 +464,8 @@ static ConvParams dgrad_params(srmi_engine* e, const ConvRef& c, const bf16_t* d
     *epi = EPI_DG_ACC_CA;
   if (*epi == EPI_DG_ACC && r1b && !r1 && aux && part && yb && !r2 && !r3 && !yf && c.cout == 64 && !c.ps)
     *epi = EPI_DG_ACC_CA16;  // (the bf16 engine's in-group gradient stream)
+  if (*epi == EPI_DG_ACC && !r1b && !r1 && aux && part && yb && !r2 && !r3 && !yf && c.cout == 64 && !c.ps)
+    *epi = EPI_DG_CA16;  // (the group tail's dgrad: the stream's start)
   return p;
 }
 
@@ -510,11 +512,11 @@ static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const b
   WgradParams p;
   ReduceSet r;
   const int rc = wgrad_params(e, c, x, dy, n, H, W, grads, with_bias, alpha, choose_row_splits(n, H, c.cout, e->cu_budget),
-                              e->slab, e->bslab, e->slab_floats, e->bslab_floats, &p, &r);
+                              e->slab, e->bslab, e->slab_floats, e->bslab_floats, &p, &r, kSlab16);
   if (rc) return rc;
   const int rc2 = wgrad3x3_launch(p, st);
   if (rc2) return rc2;
-  return wgrad_reduce_launch(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb, st);
+  return wgrad_reduce_launch(r.slab, r.bslab, r.nslab, r.Cout, r.ps, r.layout, r.alpha, r.gw, r.gb, st, r.slab16);
 }
 
 // a dgrad conv and the filter gradient of the same conv (independent, both reading

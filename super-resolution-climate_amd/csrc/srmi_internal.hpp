@@ -36,6 +36,7 @@ enum Epi {
   // the bf16 engine's in-group gradient stream (the hot RCAB conv1 dgrad, F1):
   EPI_DG_ACC_CA16 = 11, // g = bf16(acc + r1b) -> bf16 yb (in place over r1b allowed), sums of
                         // that bf16 g and g*aux; r1b / aux / part / yb non-null, no yf / r1 / r2 / r3
+  EPI_DG_CA16 = 12,     // the same without r1b: g = bf16(acc) (the group tail's dgrad starts the stream)
 };
 
 // The CA scale of an RCAB from its conv1 output t (ca_scale.hpp): mean(u) of u =
@@ -141,7 +142,7 @@ int wgrad_reduce2_launch(const ReduceSet& r0, const ReduceSet& r1, hipStream_t s
 int rcab_bwd_fusable(const ConvParams& cp, const WgradParams& wp);
 int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradParams& wp, hipStream_t st);
 int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, int layout, float alpha,
-                        float* gw, float* gb, hipStream_t st);
+                        float* gw, float* gb, hipStream_t st, int slab16 = 0);
 
 // small-channel kernels (head / tail), bicubic resampling, loss, CA, Adam, packing
 // f32 != 0: the operand-type outputs / inputs below are fp32 (exact-fp32 engine mode)

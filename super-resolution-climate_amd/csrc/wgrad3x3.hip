@@ -726,10 +726,10 @@ __global__ void __launch_bounds__(kRedQ * kRedPh) wgrad_reduce2_kernel(ReduceSet
 }
 
 int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, int layout, float alpha,
-                        float* gw, float* gb, hipStream_t st) {
-  if (Cout % 64) return SRMI_ERR_SHAPE;
+                        float* gw, float* gb, hipStream_t st, int slab16) {
+  if (Cout % 64 || (slab16 && layout != 1)) return SRMI_ERR_SHAPE;
   const int blocks = wgrad_reduce_blocks(Cout);
-  const ReduceSet r{slab, bslab, nslab, Cout, ps, layout, alpha, gw, gb, 0};
+  const ReduceSet r{slab, bslab, nslab, Cout, ps, layout, alpha, gw, gb, slab16};
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(kRedQ * kRedPh), 0, st, r);
   SRMI_CHECK_LAUNCH();
   return 0;
