@@ -244,7 +244,11 @@ struct srmi_engine {
 // CU budget split in halves), so their row chunks are sized for HALF the engine's
 // budget: fewer, longer chunks write fewer partial slabs (at C2 2 x 24-row chunks
 // per image instead of 3 x 16).
-constexpr bool kSlab16 = SRMI_SLAB16 != 0;  // bf16 RCAB filter-gradient slabs (tuning.hpp)
+// bf16 partial slabs for the RCAB filter gradients (tuning.hpp).  The other filter
+// gradients (group / body tails, upsamplers: 26 launches per step) keep fp32 slabs:
+// bf16 there measured +0.3 % (noise) and doubled the split dependence of their sums
+// (one engine of 16 tiles vs 2 x 2 engines of 4: 2.4e-4 rel-L2 of the gradient)
+constexpr bool kSlab16 = SRMI_SLAB16 != 0;
 
 static int engine_cus(const srmi_engine* e) { return e->cu_budget > 0 ? e->cu_budget : 256; }
 // CU shares of the two parts of a fused launch, in percent of the engine budget taken
@@ -512,7 +516,7 @@ static int conv_wgrad(srmi_engine* e, const ConvRef& c, const bf16_t* x, const b
   WgradParams p;
   ReduceSet r;
   const int rc = wgrad_params(e, c, x, dy, n, H, W, grads, with_bias, alpha, choose_row_splits(n, H, c.cout, e->cu_budget),
-                              e->slab, e->bslab, e->slab_floats, e->bslab_floats, &p, &r, kSlab16);
+                              e->slab, e->bslab, e->slab_floats, e->bslab_floats, &p, &r);
   if (rc) return rc;
   const int rc2 = wgrad3x3_launch(p, st);
   if (rc2) return rc2;
