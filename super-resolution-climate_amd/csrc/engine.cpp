@@ -767,11 +767,31 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
       if (stage < s_lo || stage > s_hi) continue;
       int it = (nl - 1 - g) * nb;  // RCAB counter (slab-set parity)
       const ConvRef& gt = P.group_tail[g];
-      RC(conv_wgrad(e, gt, e->hb(g, nb), gRb, n, h, w, grads, true, 1.f, st));
-      RC(conv_dgrad(e, gt, gRb, n, h, w, EPI_DG_ACC, g16 ? ghb : nullptr, g16 ? nullptr : ghf, nullptr, nullptr,
-                    nullptr, e->Um(g, nb), e->pacc, 1.f, st));
       ReduceSet prev2{}, prev1{};
       bool have_prev = false;
+      // group tail: its dgrad (the bf16 stream's start, with the CA sums of RCAB nb) and its
+      // filter gradient as one fused launch, like the RCABs' (into the slab set of the
+      // parity RCAB nb does not use; the reduction rides in RCAB nb's CA-backward launch),
+      // else (exact fp32, unfusable shapes) the two launches and the reduction in turn
+      {
+        int epi = EPI_DG_ACC;
+        const ConvParams cp = dgrad_params(e, gt, gRb, n, h, w, &epi, g16 ? ghb : nullptr, g16 ? nullptr : ghf,
+                                           nullptr, nullptr, nullptr, e->Um(g, nb), e->pacc, 1.f);
+        WgradParams wp{};
+        const int qt = (it & 1) ^ 1;
+        if (g16)
+          RC(wgrad_params(e, gt, e->hb(g, nb), gRb, n, h, w, grads, true, 1.f, rs1, e->slab_r[qt][0],
+                          e->bslab_r[qt][0], e->slab_r_floats, e->bslab_r_floats, &wp, &prev2));
+        if (g16 && rcab_bwd_fusable(cp, wp)) {
+          RC(dgrad_with_wgrad(e, cp, epi, wp, 1, st));
+          prev1 = ReduceSet{};  // (no second reduction: gw = gb = null)
+          prev1.Cout = prev2.Cout;
+          have_prev = true;
+        } else {
+          RC(conv_wgrad(e, gt, e->hb(g, nb), gRb, n, h, w, grads, true, 1.f, st));
+          RC(conv3x3_launch(cp, epi, st));
+        }
+      }
       for (int b = nb; b >= 1; --b) {
         const RCABRef& r = P.groups[g][b - 1];
         const int q = it++ & 1;

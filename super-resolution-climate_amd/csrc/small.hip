@@ -1497,10 +1497,12 @@ int ca_bwd_du_launch(const void* g, int g16, const float* part, int nstrips, con
   if (C != 64 || C % R || (C / R) > 32 || (C / R) % 4 || (HW * C) % 8) return SRMI_ERR_SHAPE;
   if ((red0 == nullptr) != (red1 == nullptr)) return SRMI_ERR_ARG;
   if (red0 && (red0->Cout != red1->Cout)) return SRMI_ERR_SHAPE;
+  // (a set with neither gw nor gb -- the group tail's single reduction -- adds no blocks)
+  const bool two = red1 && (red1->gw || red1->gb);
   const int gx = ca_grid_x(HW, C);
   const ReduceSet none{};
   const int nred = red0 ? wgrad_reduce_blocks(red0->Cout) : 0;
-  const dim3 grid(gx, N + (2 * nred + gx - 1) / gx);
+  const dim3 grid(gx, N + ((two ? 2 : 1) * nred + gx - 1) / gx);
   const ReduceSet& a = red0 ? *red0 : none;
   const ReduceSet& b = red1 ? *red1 : none;
   if (f32)

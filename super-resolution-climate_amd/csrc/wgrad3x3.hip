@@ -671,6 +671,11 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
       hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA16, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len,
                          nconv, w, nwg, paired, tail);
       break;
+    case EPI_DG_CA16:
+      if (!c.aux || !c.part || !c.yb || c.r1 || c.r1b || c.r2 || c.r3 || c.yf) return SRMI_ERR_ARG;
+      hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_CA16, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len,
+                         nconv, w, nwg, paired, tail);
+      break;
     case EPI_DG_ACC:
       if ((!c.yf && !c.yb) || (c.part && !c.aux) || (c.r1 && c.r1b)) return SRMI_ERR_ARG;
       hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len, nconv, w, nwg, paired, tail);
