@@ -351,7 +351,7 @@ static int launch_tw(const ConvParams& p, hipStream_t st) {
     // 8 waves (two per SIMD, a wave per row and channel half) at TW = 48
     constexpr int NW = TW == 48 ? 8 : 4;
     hipLaunchKernelGGL((conv64_kernel<TW, EPI, NW>), grid, dim3(NW * 64), Conv2Smem<TW>::TOTAL, st, q, run_len);
-  } else if constexpr (EPI == EPI_DG_ACC_CA16 || EPI == EPI_DG_CA16) {
+  } else if constexpr (EPI == EPI_DG_ACC_CA16 || EPI == EPI_DG_CA16 || EPI == EPI_DG_ACC_G1) {
     return SRMI_ERR_SHAPE;  // (the bf16 gradient stream: the persistent-run body only)
   } else {
     // v1 handles the general form, without the bf16 gradient stream
@@ -409,7 +409,9 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
     return SRMI_ERR_ARG;
   if (epi == EPI_DG_CA16 && (!p.aux || !p.part || !p.yb || p.r1 || p.r1b || p.r2 || p.r3 || p.yf || p.f32))
     return SRMI_ERR_ARG;
-  if (epi != EPI_DG_ACC && epi != EPI_DG_ACC_CA16 && p.r1b) return SRMI_ERR_ARG;
+  if (epi == EPI_DG_ACC_G1 && (!p.r1b || !p.r2 || !p.yf || !p.yb || p.r1 || p.aux || p.part || p.f32))
+    return SRMI_ERR_ARG;
+  if (epi != EPI_DG_ACC && epi != EPI_DG_ACC_CA16 && epi != EPI_DG_ACC_G1 && p.r1b) return SRMI_ERR_ARG;
   switch (epi) {
     case EPI_PS_BF16:
       if (!p.yb) return SRMI_ERR_ARG;
@@ -470,6 +472,7 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
     case EPI_DG_ACC_CA: return launch_epi<EPI_DG_ACC_CA>(p, st);
     case EPI_DG_ACC_CA16: return launch_epi<EPI_DG_ACC_CA16>(p, st);
     case EPI_DG_CA16: return launch_epi<EPI_DG_CA16>(p, st);
+    case EPI_DG_ACC_G1: return launch_epi<EPI_DG_ACC_G1>(p, st);
     case EPI_RELU_POOL: return launch_v2_only<EPI_RELU_POOL>(p, st);
     case EPI_CA_RESID_U: return launch_v2_only<EPI_CA_RESID_U>(p, st);
     default: return SRMI_ERR_ARG;

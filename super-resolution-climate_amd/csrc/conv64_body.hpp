@@ -84,7 +84,7 @@ constexpr bool epi_g16() {
 }
 template <int EPI>
 constexpr bool epi_run() {
-  return EPI == EPI_DG_ACC_CA || epi_g16<EPI>() || EPI == EPI_DG_ACC || epi_cr<EPI>();
+  return EPI == EPI_DG_ACC_CA || epi_g16<EPI>() || EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_G1 || epi_cr<EPI>();
 }
 __device__ __forceinline__ float4 unpack_bf16x4(uint32_t a, uint32_t b) {
   return make_float4(bf2f(a & 0xFFFFu), bf2f(a >> 16), bf2f(b & 0xFFFFu), bf2f(b >> 16));
@@ -95,7 +95,7 @@ template <int NPT, int EPI, int NCT>
 __device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT, EPI, NCT>& e, int n, int cb, int y,
                                                  int x0, int fr, int fk, int ct0, int idx) {
   if constexpr (EPI == EPI_RESID || EPI == EPI_DG_ACC || EPI == EPI_DG_RELUMASK || EPI == EPI_DG_ACC_CA ||
-                epi_g16<EPI>() || epi_cr<EPI>()) {
+                epi_g16<EPI>() || EPI == EPI_DG_ACC_G1 || epi_cr<EPI>()) {
     const int pt = idx / NCT, c = idx % NCT;
     const size_t HW = (size_t)p.H * p.W;
     const size_t pix = (size_t)n * HW + (size_t)y * p.W + x0 + pt * 16 + fr;
@@ -127,6 +127,9 @@ __device__ __forceinline__ void epi_prefetch_one(const ConvParams& p, EpiPre<NPT
       } else if constexpr (EPI == EPI_DG_ACC_CA) {
         e.r1[pt][c] = *reinterpret_cast<const float4*>(p.r1 + oc);  // (load q = idx at [q / NCT][q % NCT])
         e.aux[pt][c] = *reinterpret_cast<const uint2*>(p.aux + oc);
+      } else if constexpr (EPI == EPI_DG_ACC_G1) {
+        e.gb[pt][c] = *reinterpret_cast<const uint2*>(p.r1b + oc);
+        e.r2[pt][c] = *reinterpret_cast<const float4*>(p.r2 + oc);
       } else if constexpr (epi_g16<EPI>()) {
         if constexpr (EPI == EPI_DG_ACC_CA16)
           e.gb[pt][c] = *reinterpret_cast<const uint2*>(p.r1b + oc);  // 512 contiguous bytes per wave
@@ -410,6 +413,9 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
               gg = unpack_bf16x4(gq.x, gq.y);
             } else if constexpr (EPI == EPI_DG_CA16) {
               gg = make_float4(0.f, 0.f, 0.f, 0.f);
+            } else if constexpr (EPI == EPI_DG_ACC_G1) {
+              const uint2 gq = e.gb[q / NCT][q % NCT];
+              gg = unpack_bf16x4(gq.x, gq.y);
             } else {
               gg = e.r1[q / NCT][q % NCT];
               if constexpr (EPI == EPI_DG_ACC) {
@@ -418,7 +424,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             }
             const uint2 uu = e.aux[q / NCT][q % NCT];
             val.x += gg.x; val.y += gg.y; val.z += gg.z; val.w += gg.w;
-            if constexpr (EPI == EPI_DG_ACC) {
+            if constexpr (EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_G1) {
               const float4 g2 = e.r2[q / NCT][q % NCT];
               val.x += g2.x; val.y += g2.y; val.z += g2.z; val.w += g2.w;
               if (p.r3) {
@@ -433,11 +439,13 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
               const uint32_t a = pack2(val.x, val.y), b = pack2(val.z, val.w);
               val = unpack_bf16x4(a, b);
             }
-            ps0[0][0] += val.x; ps0[0][1] += val.y; ps0[0][2] += val.z; ps0[0][3] += val.w;
-            ps1[0][0] += val.x * bf2f(uu.x & 0xFFFFu);
-            ps1[0][1] += val.y * bf2f(uu.x >> 16);
-            ps1[0][2] += val.z * bf2f(uu.y & 0xFFFFu);
-            ps1[0][3] += val.w * bf2f(uu.y >> 16);
+            if constexpr (EPI != EPI_DG_ACC_G1) {  // (the CA sums of the RCAB below)
+              ps0[0][0] += val.x; ps0[0][1] += val.y; ps0[0][2] += val.z; ps0[0][3] += val.w;
+              ps1[0][0] += val.x * bf2f(uu.x & 0xFFFFu);
+              ps1[0][1] += val.y * bf2f(uu.x >> 16);
+              ps1[0][2] += val.z * bf2f(uu.y & 0xFFFFu);
+              ps1[0][3] += val.w * bf2f(uu.y >> 16);
+            }
           }
           const uint32_t oel = (uint32_t)((pix0 + h * HALF + lpx) * p.Cout + cb * 64 + c * 4);  // element
           if constexpr (epi_g16<EPI>()) {  // 512 contiguous bytes per instruction
@@ -445,6 +453,9 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
             continue;
           }
           if (EPI != EPI_DG_ACC || p.yf) st_wt16(rf, p.yf, oel * 4, val);
+          if constexpr (EPI == EPI_DG_ACC_G1) {  // the group input gradient's bf16 copy
+            st_wt8(rbb, p.yb, oel * 2, make_uint2(pack2(val.x, val.y), pack2(val.z, val.w)));
+          }
           if constexpr (EPI == EPI_DG_ACC) {
             if (p.yb)  // its bf16 copy (or, yf null, the stream itself): 512 contiguous bytes per instruction
               st_wt8(rbb, p.yb, oel * 2, make_uint2(pack2(val.x, val.y), pack2(val.z, val.w)));
@@ -488,7 +499,7 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
     }
   }
   if constexpr (kRun) {
-   if (EPI == EPI_DG_ACC_CA || epi_g16<EPI>() || p.part) {  // (uniform)
+   if (EPI != EPI_DG_ACC_G1 && (EPI == EPI_DG_ACC_CA || epi_g16<EPI>() || p.part)) {  // (uniform)
     // lanes l, l ^ 16, l ^ 32, l ^ 48 hold the same 4 channels: fixed-order xor
     // sums, then one 64-channel partial per wave in red[wave][2][64], summed over
     // the waves in wave order

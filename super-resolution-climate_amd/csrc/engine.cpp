@@ -470,6 +470,8 @@ static ConvParams dgrad_params(srmi_engine* e, const ConvRef& c, const bf16_t* d
     *epi = EPI_DG_ACC_CA16;  // (the bf16 engine's in-group gradient stream)
   if (*epi == EPI_DG_ACC && !r1b && !r1 && aux && part && yb && !r2 && !r3 && !yf && c.cout == 64 && !c.ps)
     *epi = EPI_DG_CA16;  // (the group tail's dgrad: the stream's start)
+  if (*epi == EPI_DG_ACC && r1b && !r1 && !aux && !part && yb && yf && r2 && c.cout == 64 && !c.ps)
+    *epi = EPI_DG_ACC_G1;  // (the group's first RCAB: the stream's end)
   return p;
 }
 

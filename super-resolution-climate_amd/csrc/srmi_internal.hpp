@@ -37,6 +37,8 @@ enum Epi {
   EPI_DG_ACC_CA16 = 11, // g = bf16(acc + r1b) -> bf16 yb (in place over r1b allowed), sums of
                         // that bf16 g and g*aux; r1b / aux / part / yb non-null, no yf / r1 / r2 / r3
   EPI_DG_CA16 = 12,     // the same without r1b: g = bf16(acc) (the group tail's dgrad starts the stream)
+  EPI_DG_ACC_G1 = 13,   // the group's first RCAB (the stream's end): g = acc + r1b + r2 (+ r3) -> fp32 yf
+                        // + its bf16 copy yb (in place over r1b allowed); no CA sums
 };
 
 // The CA scale of an RCAB from its conv1 output t (ca_scale.hpp): mean(u) of u =

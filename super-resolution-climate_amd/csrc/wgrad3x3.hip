@@ -671,6 +671,11 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
       hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_CA16, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len,
                          nconv, w, nwg, paired, tail);
       break;
+    case EPI_DG_ACC_G1:
+      if (!c.r1b || !c.r2 || !c.yf || !c.yb || c.r1 || c.aux || c.part) return SRMI_ERR_ARG;
+      hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_ACC_G1, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len,
+                         nconv, w, nwg, paired, tail);
+      break;
     case EPI_DG_CA16:
       if (!c.aux || !c.part || !c.yb || c.r1 || c.r1b || c.r2 || c.r3 || c.yf) return SRMI_ERR_ARG;
       hipLaunchKernelGGL((rcab_bwd_kernel<EPI_DG_CA16, kFuseNW>), grid, dim3(kFuseNW * 64), lds, st, c, run_len,
