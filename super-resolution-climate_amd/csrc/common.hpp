@@ -218,15 +218,6 @@ template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-// the same through the builtin: the compiler's waitcnt pass sees it (an asm wait is
-// opaque to it), so loads older than the N newest count as landed afterwards and it adds
-// no waits of its own for them (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4] and
-// lgkmcnt [11:8] left at their maxima)
-template <int N>
-__device__ __forceinline__ void wait_vm_known() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
 
 }  // namespace srmi
 

@@ -693,14 +693,6 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
       if (wv_s + NW * m < NGRP) group_dma_one(gidx, m);
   };
 
-  // DG_ACC_CA16 (F1's dgrad half, bound by the bytes it keeps in flight): the epilogue
-  // operands (g, u: 24 KB each per strip and workgroup) are loaded ONE STRIP AHEAD --
-  // strip k+1's during strip k's K-loop, issued after group k+2's DMA pieces, so the
-  // K-loop's end waits for the DMA with a counted vmcnt and leaves them in flight -- and
-  // strip k0's in the prologue (SRMI_EPI_AHEAD; 0: loaded during their own strip)
-  constexpr bool kAhead = EPI == EPI_DG_ACC_CA16 && SRMI_EPI_AHEAD && NW == 8;
-  constexpr int kAheadLoads = 2 * NPT * NCT;  // VMEM instructions per wave for one strip (g, u)
-  [[maybe_unused]] EpiPre<NPT, EPI, NCT> epc;  // (kAhead) the current strip's operands
   // bias first (read only by the epilogue): its latency hides under the prologue wait
   // instead of following it (~650 cycles per workgroup)
   float4 bias[NCT];
@@ -724,10 +716,6 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     }
     group_dma(k0);  // strip k reads input groups k and k + 1
     group_dma(k0 + 1);
-    if constexpr (kAhead) {
-#pragma unroll
-      for (int i = 0; i < NPT * NCT; ++i) epi_prefetch_one<NPT, EPI, NCT>(p, epc, n, cb, 4 * k0 + row, x0, fr, fk, ct0, i);
-    }
     wait_vm<0>();
   }
   STAMP(1);
@@ -761,16 +749,13 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
 #endif
   }
 
-  // one strip: its K-loop and epilogue.  epcur: the strip's epilogue operands (kAhead:
-  // loaded during the previous strip, or the prologue), epnxt: where the K-loop loads
-  // the next strip's (kAhead) or its own (else; epcur unused)
-  auto strip = [&](const int k, EpiPre<NPT, EPI, NCT>& epcur, EpiPre<NPT, EPI, NCT>& epnxt)
-                   __attribute__((always_inline)) {
+#pragma unroll 1
+  for (int k = k0; k < k1; ++k) {
     const int y = 4 * k + row;
     const bool pf = (k + 1 < k1);
     // group k+2 -> ring slot (k+2)%3, which held group k-1 (last read by strip k-1,
     // released by the barrier that ended it)
-    EpiPre<NPT, EPI, NCT>& ep = epnxt;
+    EpiPre<NPT, EPI, NCT> ep;
     [[maybe_unused]] const int sj = 2 + 5 * min(k - k0, 11);
     STAMP(sj);
 
@@ -810,23 +795,11 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
       // group k+2's DMA pieces and the epilogue operands are issued one or two per
       // K-step, so a full memory queue stalls the wave between MFMA groups only
       if (s < NGW && pf && wv_s + NW * s < NGRP) group_dma_one(k + 2, s);
-      if constexpr (kAhead) {
-        // strip k+1's operands, after every DMA piece of this K-loop; unconditional (the
-        // last strip reloads its own rows, unused) so that the count of loads behind them
-        // is static and the K-loop's counted wait is exact for the compiler too
-        constexpr int s0 = NGW;
-        const int yn = pf ? y + 4 : y;
-        if (s >= s0 && 2 * (s - s0) < NPT * NCT)
-          epi_prefetch_one<NPT, EPI, NCT>(p, ep, n, cb, yn, x0, fr, fk, ct0, 2 * (s - s0));
-        if (s >= s0 && 2 * (s - s0) + 1 < NPT * NCT)
-          epi_prefetch_one<NPT, EPI, NCT>(p, ep, n, cb, yn, x0, fr, fk, ct0, 2 * (s - s0) + 1);
-      } else {
-        // the epilogue operands, two per K-step from the first one: a whole strip of
-        // MFMAs to land (spread over K-steps 2..13, the heavy fp32 epilogue of
-        // DG_ACC_CA waited on its last ones at the end of the K-loop: +1.3 % step)
-        if (2 * s < NPT * NCT) epi_prefetch_one<NPT, EPI, NCT>(p, ep, n, cb, y, x0, fr, fk, ct0, 2 * s);
-        if (2 * s + 1 < NPT * NCT) epi_prefetch_one<NPT, EPI, NCT>(p, ep, n, cb, y, x0, fr, fk, ct0, 2 * s + 1);
-      }
+      // the epilogue operands, two per K-step from the first one: a whole strip of
+      // MFMAs to land (spread over K-steps 2..13, the heavy fp32 epilogue of
+      // DG_ACC_CA waited on its last ones at the end of the K-loop: +1.3 % step)
+      if (2 * s < NPT * NCT) epi_prefetch_one<NPT, EPI, NCT>(p, ep, n, cb, y, x0, fr, fk, ct0, 2 * s);
+      if (2 * s + 1 < NPT * NCT) epi_prefetch_one<NPT, EPI, NCT>(p, ep, n, cb, y, x0, fr, fk, ct0, 2 * s + 1);
       __builtin_amdgcn_sched_barrier(0);
       const bool ld = s + LA < 18;
       if (ld) load_step(s + LA, A[(s + LA) % kFragBuf], B[(s + LA) % kFragBuf]);
@@ -849,13 +822,8 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     }
     // group k+2's DMA, the epilogue operands and the previous strip's stores had the
     // whole MFMA phase to land: drain them here, before the epilogue (the barrier at
-    // the end of the strip then publishes group k+2 to every wave).  kAhead: all but
-    // strip k+1's operands, the last kAheadLoads issued (VMEM retires in issue order)
-    if constexpr (kAhead) {
-      wait_vm_known<kAheadLoads>();
-    } else {
-      wait_vm<0>();
-    }
+    // the end of the strip then publishes group k+2 to every wave)
+    wait_vm<0>();
     STAMP(sj + 1);
     if constexpr (kCas) {
       if (p.cas_on && k == k0) {  // the image's scale (every wave: uniform), before the first epilogue
@@ -880,7 +848,7 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
     if constexpr (kMp) {  // conv2's filter slices for the run-end matvec, under the last epilogue
       if (cpon && k == k1 - 1) ca_matvec_load_w(p.cas.wimg, tid, w2v);
     }
-    conv_epilogue2<NPT, EPI, NCT>(p, acc, kAhead ? epcur : ep, bias, n, cb, y, x0, k * nsx + sx,
+    conv_epilogue2<NPT, EPI, NCT>(p, acc, ep, bias, n, cb, y, x0, k * nsx + sx,
                                                                nsy * nsx, red, fr, fk, row, ct0,
                                   tid, ring + (k % 3) * S::GROUPB + row * TW * 128, fs, &cpart, kMp && cpon);
     STAMP(sj + 3);
@@ -892,22 +860,6 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
       asm volatile("" ::: "memory");
     }
     STAMP(sj + 4);
-  };
-  if constexpr (kAhead) {
-    // two strips per trip with the operand sets swapping roles: no register copy between
-    // strips (a copy would have to wait for the next strip's loads inside this epilogue)
-    EpiPre<NPT, EPI, NCT> epo;
-#pragma unroll 1
-    for (int k = k0; k < k1; k += 2) {
-      strip(k, epc, epo);
-      if (k + 1 < k1) strip(k + 1, epo, epc);
-    }
-  } else {
-#pragma unroll 1
-    for (int k = k0; k < k1; ++k) {
-      EpiPre<NPT, EPI, NCT> ep;
-      strip(k, ep, ep);
-    }
   }
   if constexpr (kMp) {
     if (cpon) {  // the run's share of the image's CA mean: border columns over the 4 rows,

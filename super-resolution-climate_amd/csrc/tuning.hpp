@@ -68,12 +68,6 @@
 #define SRMI_SLAB16 1
 #endif
 
-// F1's dgrad half (EPI_DG_ACC_CA16): the epilogue operands g, u loaded one strip ahead
-// (conv64_body kAhead), 0 = during their own strip's K-loop
-#ifndef SRMI_EPI_AHEAD
-#define SRMI_EPI_AHEAD 1
-#endif
-
 // waves per workgroup of the exact-fp32 conv (conv_f32.hip)
 #ifndef SRMI_F32_NW
 #define SRMI_F32_NW 8
