@@ -240,16 +240,16 @@ struct srmi_engine {
   float* brecp(int g, int b) const { return brec + (size_t)(g * P.cfg.nblocks + (b - 1)) * N * 224; }
 };
 
-// The RCAB filter gradients run beside their dgrad convs (one fused launch, the
-// CU budget split in halves), so their row chunks are sized for HALF the engine's
-// budget: fewer, longer chunks write fewer partial slabs (at C2 2 x 24-row chunks
-// per image instead of 3 x 16).
 // bf16 partial slabs for the RCAB filter gradients (tuning.hpp).  The other filter
 // gradients (group / body tails, upsamplers: 26 launches per step) keep fp32 slabs:
 // bf16 there measured +0.3 % (noise) and doubled the split dependence of their sums
 // (one engine of 16 tiles vs 2 x 2 engines of 4: 2.4e-4 rel-L2 of the gradient)
 constexpr bool kSlab16 = SRMI_SLAB16 != 0;
 
+// The RCAB filter gradients run beside their dgrad convs (one fused launch, the
+// CU budget split in halves), so their row chunks are sized for HALF the engine's
+// budget: fewer, longer chunks write fewer partial slabs (at C2 2 x 24-row chunks
+// per image instead of 3 x 16).
 static int engine_cus(const srmi_engine* e) { return e->cu_budget > 0 ? e->cu_budget : 256; }
 // CU shares of the two parts of a fused launch, in percent of the engine budget taken
 // by the filter gradient: after the ReLU-mask dgrad of conv2 (FUSE_WG2) and after the
