@@ -196,7 +196,7 @@ def _dp_harness_rank(rank, world, port, root, q):
     from srmi.dist import init_from_env
     from srmi.harness import CheckpointStore, LossRecords, train_timeslices
     info = init_from_env("gloo")
-    tr = _DPStepTrainer(info, 2)
+    tr = _DPStepTrainer(info, -(-4 // world))
     sl = _slices()
     store = CheckpointStore(root, "v")
     rec = LossRecords(root, "ds", "task", "m")
@@ -208,20 +208,22 @@ def _dp_harness_rank(rank, world, port, root, q):
     dist.destroy_process_group()
 
 
-def test_train_timeslices_data_parallel_world2_gloo(tmp_path):
+@pytest.mark.parametrize("world", [2, 3])
+def test_train_timeslices_data_parallel_gloo(tmp_path, world):
     """C3's loop (dual_trainer.py:301-331 over TileBatchIterator, tiles.py:55-72) at
-    world 2: both ranks step rank 0's shuffled batch order, each its shard_range of
-    every batch -- the short last batch of 1 tile leaves rank 1 empty -- the shards of
-    a batch are exactly its tiles, the losses are the one-process losses, and one
-    checkpoint (+ backup) and one CSV row per time slice come from rank 0 alone."""
+    world 2 and 3: every rank steps rank 0's shuffled batch order, each its shard_range
+    of every batch -- the short last batch of 1 tile leaves the other ranks empty (and
+    at world 3 the 4-tile batches split 2 / 1 / 1) -- the shards of a batch are exactly
+    its tiles, the losses are the one-process losses, and one checkpoint (+ backup) and
+    one CSV row per time slice come from rank 0 alone."""
     import multiprocessing as mp
     from srmi.dist import DistInfo
     from srmi.harness import LossRecords, train_timeslices
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 39000 + random.randint(0, 2000)
+    port = 39000 + random.randint(0, 2000) + 2500 * (world - 2)
     root = str(tmp_path / "dp")
-    ps = [ctx.Process(target=_dp_harness_rank, args=(r, 2, port, root, q)) for r in range(2)]
+    ps = [ctx.Process(target=_dp_harness_rank, args=(r, world, port, root, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = sorted([q.get(timeout=120) for _ in ps], key=lambda t: t[0])
@@ -232,14 +234,23 @@ def test_train_timeslices_data_parallel_world2_gloo(tmp_path):
     one = _DPStepTrainer(DistInfo(), 4)
     sl = _slices()
     ref = train_timeslices(one, [lambda i=i: sl[i] for i in range(2)], 3, 4, rng=random.Random(11))
-    (_, seen0, out0, files), (_, seen1, out1, _) = res
-    assert len(seen0) == len(seen1) == len(one.seen) == 2 * 2 * 4  # 2 epochs x 2 slices x 4 batches
-    for (a0, g0, i0), (a1, g1, i1), (_, g, ids) in zip(seen0, seen1, one.seen):
-        assert g0 == g1 == g and a0 == 0 and a1 == len(i0)
-        assert i0 + i1 == ids                      # the shards are the batch, in order
-        assert len(i0) - len(i1) in (0, 1)
-    assert any(len(i1) == 0 for _, _, i1 in seen1)  # the 1-tile last batch: rank 1 had no tile
-    assert out0 == out1 and abs(out0["prediction"] - ref["prediction"]) < 1e-6
+    seens = [r[1] for r in res]
+    files = res[0][3]
+    assert all(len(sn) == len(one.seen) == 2 * 2 * 4 for sn in seens)  # 2 epochs x 2 slices x 4 batches
+    for j, (_, g, ids) in enumerate(one.seen):
+        parts = [sn[j] for sn in seens]
+        assert all(pg == g for _, pg, _ in parts)
+        got, t0 = [], 0
+        for a, _, i in parts:               # rank order, contiguous, balanced
+            assert a == t0
+            t0 += len(i)
+            got += i
+        assert got == ids                   # the shards are the batch, in order
+        sizes = [len(i) for _, _, i in parts]
+        assert max(sizes) - min(sizes) <= 1 and sizes == sorted(sizes, reverse=True)
+    assert any(len(sn[j][2]) == 0 for sn in seens[1:] for j in range(len(one.seen)))  # empty shards occur
+    outs = [r[2] for r in res]
+    assert all(o == outs[0] for o in outs) and abs(outs[0]["prediction"] - ref["prediction"]) < 1e-6
     assert files == ["v.train.backup.pt", "v.train.pt"]
     rows = LossRecords(root, "ds", "task", "m").load_results()
     assert [r[1] for r in rows] == ["0.000", "0.500", "1.000", "1.500"]  # one row per time slice
