@@ -223,7 +223,9 @@ int srmi_axpy(float* y, const float* x, float a, size_t n, void* stream);
 /* forward conv: x NHWC [N][H][W][Cin], packed filters (srmi_pack_conv),
  * epi: 0 relu, 1 + channel sums (part[N][strips][64]), 2 alpha*(y+b)+r1
  * -> yf fp32 (opt) + yb, 3 PixelShuffle(2), 4 dgrad * (aux > 0), 5 dgrad + r1 + r2
- * + r3 -> yf (+ sums of g, g*aux), 6 plain (+ bias)                           */
+ * + r3 -> yf (+ sums of g, g*aux), 6 plain (+ bias).  (The engine's own epilogues
+ * 7-13 -- the CA forward, the bf16 in-group gradient stream -- take operands this
+ * entry point does not pass; they are reached through srmi_forward / _backward.)  */
 int srmi_conv3x3(const void* x, const void* wpack, const float* bias, int N, int H, int W, int Cin, int Cout,
                  int in_unshuffle, int epi, void* yb, float* yf, const float* r1, const float* r2, const float* r3,
                  const void* aux, float* part, float alpha, int dtype, void* stream);
