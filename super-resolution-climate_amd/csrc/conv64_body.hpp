@@ -82,11 +82,6 @@ template <int EPI>
 constexpr bool epi_g16() {
   return EPI == EPI_DG_ACC_CA16 || EPI == EPI_DG_CA16;
 }
-// ... staged once as bf16 (SRMI_G16_STAGE16; the 8-wave body, NCT = 2)
-template <int EPI, int NCT>
-constexpr bool epi_g16_stage16() {
-  return epi_g16<EPI>() && SRMI_G16_STAGE16 && NCT < 4;
-}
 template <int EPI>
 constexpr bool epi_run() {
   return EPI == EPI_DG_ACC_CA || epi_g16<EPI>() || EPI == EPI_DG_ACC || EPI == EPI_DG_ACC_G1 || epi_cr<EPI>();
@@ -266,10 +261,6 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
         bv[pt][c] = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         continue;
       }
-      if constexpr (epi_g16_stage16<EPI, NCT>()) {  // dx rounded to bf16, staged once as bf16
-        bv[pt][c] = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        continue;
-      }
       if constexpr (kRun) {
         fv[pt][c] = make_float4(v[0], v[1], v[2], v[3]);  // dx; g is added in the store loop
         continue;  // no bf16 copy
@@ -368,63 +359,9 @@ __device__ __forceinline__ void conv_epilogue2(const ConvParams& p, f32x4 (&acc)
       }
     return;
   }
-  // the bf16 in-group gradient stream (SRMI_G16_STAGE16): dx staged once as bf16 (128 B
-  // per pixel, chunk-swizzled, the whole strip row: one barrier instead of the fp32
-  // path's two halves and four), read back in the run layout, g = bf16(bf16(dx) + g),
-  // the CA sums of that stored g; the CA sums' cross-wave reduction follows below
-  if constexpr (epi_g16_stage16<EPI, NCT>()) {
-    constexpr int HALF = NPT * 8, RUNS = HALF / 4;
-    static_assert(kShared, "the 8-wave body");
-#pragma unroll
-    for (int pt = 0; pt < NPT; ++pt)
-#pragma unroll
-      for (int c = 0; c < NCT; ++c) {
-        const int px = pt * 16 + fr, c16 = (ct0 + c) * 2 + (fk >> 1);
-        *reinterpret_cast<uint2*>(stage + px * 128 + ((c16 ^ (px & 7)) << 4) + (fk & 1) * 8) = bv[pt][c];
-      }
-    stage_sync();
-    const auto rbb = wt_rsrc(p.yb, (uint32_t)((size_t)p.N * HW * p.Cout * 2));
-    const size_t pix0 = (size_t)n * HW + (size_t)y * p.W + x0;
-    uint2 dxs[RUNS];
-#pragma unroll
-    for (int q = 0; q < RUNS; ++q) {
-      const int h = q / (RUNS / 2), i = 2 * (q % (RUNS / 2)) + half_id;
-      const int lin = i * 1024 + lane * 16, px = h * HALF + (lin >> 8), c = (lin >> 4) & 15;
-      dxs[q] = *reinterpret_cast<const uint2*>(stage + px * 128 + (((c >> 1) ^ (px & 7)) << 4) + (c & 1) * 8);
-    }
-    // the stage's last reads before the barrier that releases the ring slot (the body
-    // skips its own strip-end barrier for this epilogue)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int j = 0; j < RUNS / 2; ++j) {
-        const int i = 2 * j + half_id;
-        const int lin = i * 1024 + lane * 16, px = h * HALF + (lin >> 8), c = (lin >> 4) & 15;
-        const int q = h * (RUNS / 2) + j;
-        float4 val = unpack_bf16x4(dxs[q].x, dxs[q].y);
-        if constexpr (EPI == EPI_DG_ACC_CA16) {
-          const uint2 gq = e.gb[q / NCT][q % NCT];
-          const float4 gg = unpack_bf16x4(gq.x, gq.y);
-          val.x += gg.x; val.y += gg.y; val.z += gg.z; val.w += gg.w;
-        }
-        const uint32_t a = pack2(val.x, val.y), b = pack2(val.z, val.w);
-        val = unpack_bf16x4(a, b);
-        const uint2 uu = e.aux[q / NCT][q % NCT];
-        ps0[0][0] += val.x; ps0[0][1] += val.y; ps0[0][2] += val.z; ps0[0][3] += val.w;
-        ps1[0][0] += val.x * bf2f(uu.x & 0xFFFFu);
-        ps1[0][1] += val.y * bf2f(uu.x >> 16);
-        ps1[0][2] += val.z * bf2f(uu.y & 0xFFFFu);
-        ps1[0][3] += val.w * bf2f(uu.y >> 16);
-        const uint32_t oe = (uint32_t)((pix0 + px) * p.Cout + cb * 64 + c * 4);  // element
-        st_wt8(rbb, p.yb, oe * 2, make_uint2(a, b));
-      }
-  }
   // fp32 output: staged in LDS in two halves of the row (256 B per pixel,
   // chunk-swizzled) and written back as 1 KiB contiguous runs (full lines)
-  if constexpr (kF && !epi_g16_stage16<EPI, NCT>()) {
+  if constexpr (kF) {
     if (kRun || p.yf) {
       constexpr int HALF = NPT * 8;  // pixels per half
       constexpr int RUNS = HALF / 4;  // 1 KiB runs per half
@@ -916,8 +853,8 @@ __device__ __forceinline__ void conv64_body(const ConvParams& p, int run_len, in
                                   tid, ring + (k % 3) * S::GROUPB + row * TW * 128, fs, &cpart, kMp && cpon);
     STAMP(sj + 3);
     // LDS-only barrier: this strip's global stores stay in flight into the next strip
-    // (the bf16-staged epilogues run it themselves, after their last stage reads)
-    if constexpr (!epi_cr_bf16<EPI>() && !epi_g16_stage16<EPI, NCT>()) {
+    // (the bf16-staged conv2 epilogues run it themselves, after their last stage reads)
+    if constexpr (!epi_cr_bf16<EPI>()) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");

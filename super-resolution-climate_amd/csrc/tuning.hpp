@@ -68,12 +68,6 @@
 #define SRMI_SLAB16 1
 #endif
 
-// the bf16 gradient stream's epilogues (EPI_DG_ACC_CA16, EPI_DG_CA16): the dgrad output
-// rounded to bf16 and staged once as bf16 (1), or staged as fp32 in two halves (0)
-#ifndef SRMI_G16_STAGE16
-#define SRMI_G16_STAGE16 1
-#endif
-
 // waves per workgroup of the exact-fp32 conv (conv_f32.hip)
 #ifndef SRMI_F32_NW
 #define SRMI_F32_NW 8

@@ -23,9 +23,7 @@ run as unfold + rocBLAS GEMM) and no reduced-precision math.
   output -- is bf16 (the group-tail dgrad and every RCAB's conv1 dgrad store it rounded,
   EPI_DG_ACC_CA16, and the CA backward reads it): rounded where it arrives at an RCAB
   output (after autograd has summed the identity and conv paths); the gradient of the
-  group input and every other gradient stay fp32.  Inside that stream, the dgrad of
-  every RCAB's conv1 but the group's first is rounded to bf16 before it is added (its
-  epilogue stages it once as bf16, SRMI_G16_STAGE16): g = bf16(bf16(dx) + g).
+  group input and every other gradient stay fp32.
 Rounding is straight-through in backward, as in the engine (the stored values are
 what backward reads; the gradient of an add is the identity).  The model's drift
 from the fp32 oracle is the reference's own drift under the engine's arithmetic,
@@ -129,25 +127,14 @@ def _emul_rcab_forward(self, x):
     return _GradBf16.apply(_StraightPair16.apply(_StraightBf16.apply(u) * s + x))
 
 
-class _Bf16OperandConvDx16(_Bf16OperandConv):
-    """The same with its input gradient rounded to bf16 (the in-group RCABs' conv1)."""
-
-    @staticmethod
-    def backward(ctx, dy):
-        dx, dw, db, _ = _Bf16OperandConv.backward(ctx, dy)
-        return _bf(dx), dw, db, None
-
-
 class _EmulConv(nn.Module):
-    def __init__(self, conv: nn.Conv2d, dx16: bool = False):
+    def __init__(self, conv: nn.Conv2d):
         super().__init__()
         self.conv = conv
-        self.dx16 = dx16
 
     def forward(self, x):
         c = self.conv
-        fn = _Bf16OperandConvDx16 if self.dx16 else _Bf16OperandConv
-        return fn.apply(x, c.weight, c.bias, c.padding)
+        return _Bf16OperandConv.apply(x, c.weight, c.bias, c.padding)
 
 
 def bf16_operand_emulation(model: nn.Module, pair_stream: bool = True) -> nn.Module:
@@ -155,17 +142,11 @@ def bf16_operand_emulation(model: nn.Module, pair_stream: bool = True) -> nn.Mod
     and, with pair_stream, give every RCAB the engine's CA product and in-group pair
     residual stream (module docstring)."""
     import types
-    from oracle.rcan_oracle import _RCAB, _RG
-    # conv1 of every RCAB but a residual group's first: dgrad rounded to bf16 (module docstring)
-    dx16 = set()
-    if pair_stream:
-        for mod in model.modules():
-            if isinstance(mod, _RG):
-                dx16 |= {id(r.body[0]) for r in list(mod.body)[1:] if isinstance(r, _RCAB)}
+    from oracle.rcan_oracle import _RCAB
     for name, mod in list(model.named_modules()):
         for cname, child in list(mod.named_children()):
             if isinstance(child, nn.Conv2d) and child.kernel_size == (3, 3) and child.in_channels == 64:
-                setattr(mod, cname, _EmulConv(child, dx16=id(child) in dx16))
+                setattr(mod, cname, _EmulConv(child))
     if pair_stream:
         for mod in model.modules():
             if isinstance(mod, _RCAB):
