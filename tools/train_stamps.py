@@ -35,7 +35,7 @@ def main():
     for _ in range(3):
         tr.step(hr)
     torch.cuda.synchronize()
-    for epi, name in ((8, "conv1 RELU_POOL"), (10, "conv2 CA_RESID_U"), (7, "F1 dgrad runs (DG_ACC_CA)"),
+    for epi, name in ((8, "conv1 RELU_POOL"), (10, "conv2 CA_RESID_U"), (11, "F1 dgrad runs (DG_ACC_CA16)"),
                       (4, "F2 dgrad runs (DG_RELUMASK, deferred)")):
         buf = torch.zeros(2 * 4096 * 64, dtype=torch.int64, device=d)
         os.environ["SRMI_STAMP_EPI"] = str(epi)
@@ -44,7 +44,7 @@ def main():
         torch.cuda.synchronize()
         call("srmi_debug_conv_stamps", None)
         flat = buf.view(-1, 64).cpu().numpy().astype(np.int64)
-        if epi in (4, 7):  # fused launch: the dgrad runs' blocks among the filter-gradient ones
+        if epi in (4, 7, 11):  # fused launch: the dgrad runs' blocks among the filter-gradient ones
             # [grid][64] dgrad rows, then [grid][64] filter-gradient rows (the launch's last
             # block is a filter-gradient one, so its row ends the second region)
             grid = (int(np.nonzero(flat[:8192, 0])[0][-1]) + 1) // 2
@@ -58,7 +58,7 @@ def main():
                       f"{np.median(wg[:, 62 if np.all(wg[:, 62]) else 1] - wg[:, 1]):.0f}")
             body = flat[:grid][flat[:grid, 0] != 0]
             nst = np.array([sum(1 for j in range(11) if r[2 + 5 * j + 4] != 0) for r in body])
-            if epi == 7 and (nst == 1).any() and (nst > 1).any():
+            if epi in (7, 11) and (nst == 1).any() and (nst > 1).any():
                 t = body[nst == 1]
                 print(f"  (F1 tail strips run by the filter-gradient workgroups: {len(t)}, span median "
                       f"{np.median(t[:, 61] - t[:, 0]):.0f}, prologue {np.median(t[:, 1] - t[:, 0]):.0f})")
