@@ -71,6 +71,8 @@ def parse():
                     help="A/B: the DP all-reduce on a reducer stream of its own (the event-driven schedule)")
     ap.add_argument("--ca-pass", action="store_true",
                     help="A/B: the training CA forward as a pass of its own after conv2 (SRMI_FLAG_CA_PASS)")
+    ap.add_argument("--du-pass", action="store_true",
+                    help="A/B: the CA backward writes du for the conv2 backward to read (SRMI_FLAG_DU_PASS)")
     ap.add_argument("--no-rcab-infer", action="store_true",
                     help="A/B: inference RCABs as three launches (SRMI_FLAG_NO_RCAB_INFER)")
     return ap.parse_args()
@@ -493,7 +495,7 @@ def dp_overhead_probe(args, reps=2):
             "--no-dp-probe", "--steps", str(args.steps), "--warmup", str(args.warmup), "--batch", str(args.batch)]
     if args.micro is not None:
         base += ["--micro", str(args.micro)]
-    for flag in ("ca_pass", "dp_reducer_stream"):
+    for flag in ("ca_pass", "du_pass", "dp_reducer_stream"):
         if getattr(args, flag):
             base += ["--" + flag.replace("_", "-")]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
@@ -601,8 +603,8 @@ def main():
                                                                            2 if args.no_rcab_infer else 0)}
         print(json.dumps(rec), flush=True)
         return
-    from srmi._lib import SRMI_FLAG_CA_PASS
-    flags = SRMI_FLAG_CA_PASS if args.ca_pass else 0
+    from srmi._lib import SRMI_FLAG_CA_PASS, SRMI_FLAG_DU_PASS
+    flags = (SRMI_FLAG_CA_PASS if args.ca_pass else 0) | (SRMI_FLAG_DU_PASS if args.du_pass else 0)
     spec = NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=10, nblocks=20,
                    cbottleneck=2, scale=4, flags=flags)
     tr = FusedTrainer(spec, B, (48, 48), lr=1e-4, interp_loss=not args.no_interp_loss, info=info, device=dev, seed=0,
@@ -695,7 +697,7 @@ def main():
         rec = {
             "metric": METRIC, "value": round(value, 2), "unit": "tiles/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "step_times": step_stats,
-            "ca_pass": bool(args.ca_pass),
+            "ca_pass": bool(args.ca_pass), "du_pass": bool(args.du_pass),
             "host_enqueue_ms_per_step": round(1000 * t_host / args.steps, 3),
             "host_enqueue_idle_ms_per_step": round(host_idle_ms, 3), "micro": micro, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",

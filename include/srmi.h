@@ -90,6 +90,10 @@ typedef struct srmi_model_config {
  * a pass of its own after conv2 (conv1, conv2 + pool writing u, CA pass) instead of inside
  * conv2's launch */
 #define SRMI_FLAG_CA_PASS 4
+/* training backward (A/B, tests): SRMI_FLAG_DU_PASS has the CA backward write du = g s +
+   dm / HW to memory for the conv2 backward to read (round 6), instead of the fused conv2
+   backward forming du from the bf16 gradient stream in LDS (the same values, bit for bit) */
+#define SRMI_FLAG_DU_PASS 16
 
 typedef struct srmi_param_info {
   long long offset; /* element offset in the flat fp32 parameter buffer     */

@@ -38,6 +38,17 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
 }
 
+// du = bf16(g s + dmh) of 8 bf16 channels (the CALayer backward's du, ca_bwd_du_kernel;
+// dmh = dm / HW): one fma per channel, so every producer of du rounds the same value
+__device__ __forceinline__ uint4 du_from_g8(uint4 gq, const float (&s)[8], const float (&m)[8]) {
+  const uint32_t w[4] = {gq.x, gq.y, gq.z, gq.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    o[q] = pack2(fmaf(bf2f(w[q] & 0xFFFFu), s[2 * q], m[2 * q]), fmaf(bf2f(w[q] >> 16), s[2 * q + 1], m[2 * q + 1]));
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // The pair: a value as hi = bf16(h) plus an 8-bit remainder lo -- 16 significant bits
 // in 3 bytes (the bf16 engine's residual stream inside a residual group).  In the fp32
 // bit pattern A = (T << 16) + L of h (bit patterns of one sign are monotonic integers):

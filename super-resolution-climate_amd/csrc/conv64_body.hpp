@@ -575,7 +575,8 @@ template <int EPI>
 constexpr bool conv64_defers() {
   return ((SRMI_DEFER & 1) && EPI == EPI_RELU_BF16) || ((SRMI_DEFER & 2) && EPI == EPI_POOL_BF16) ||
          ((SRMI_DEFER & 4) && EPI == EPI_DG_RELUMASK) || ((SRMI_DEFER & 8) && EPI == EPI_DG_ACC_CA) ||
-         ((SRMI_DEFER & 16) && EPI == EPI_RELU_POOL) || ((SRMI_DEFER & 32) && EPI == EPI_CA_RESID);
+         ((SRMI_DEFER & 16) && EPI == EPI_RELU_POOL) || ((SRMI_DEFER & 32) && EPI == EPI_CA_RESID) ||
+         ((SRMI_DEFER & (64 | 128)) && EPI == EPI_DG_ACC_CA16);
   // (EPI_CA_RESID_U: the non-deferred body only)
 }
 template <int TW, int EPI>
@@ -942,6 +943,7 @@ struct DeferOps {
   uint4 t[NPT];      // DG_RELUMASK: the ReLU output t, 8 bf16 (permuted rows)
   float4 g[NPT][2];  // DG_ACC_CA: gradient stream in (natural rows)
   uint2 u[NPT][2];   // DG_ACC_CA: the CA input u
+  uint4 uq[NPT];     // DG_ACC_CA16: the CA input u, 8 bf16 (permuted rows; the stream g in t)
 };
 
 template <int TW, int EPI>
@@ -951,8 +953,14 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
   using S = Conv2Smem<TW>;
   constexpr int NPT = TW / 16;
   constexpr bool kPerm = EPI != EPI_DG_ACC_CA;  // bf16 output: permuted filter rows
-  constexpr bool kPart = EPI == EPI_POOL_BF16 || EPI == EPI_DG_ACC_CA || EPI == EPI_RELU_POOL;
+  constexpr bool kG16 = EPI == EPI_DG_ACC_CA16;  // the bf16 gradient stream: g in / out as 8 bf16 per lane
+  constexpr bool kPart = EPI == EPI_POOL_BF16 || EPI == EPI_DG_ACC_CA || EPI == EPI_RELU_POOL || kG16;
   constexpr bool kCA = EPI == EPI_DG_ACC_CA;
+  constexpr bool kS1 = kCA || kG16;  // the second channel sum (g * u)
+  // DG_ACC_CA16 with SRMI_DEFER bit 128: this body's register-direct epilogue, run right
+  // after its own strip's K-loop (operands loaded at the strip's first K-steps) instead of
+  // inside the next strip's: no LDS staging, one barrier per strip
+  constexpr bool kImm = kG16 && (SRMI_DEFER & 128);
   constexpr bool kCR = EPI == EPI_CA_RESID;  // h' = h + s u: 8 contiguous channels per lane (permuted rows)
   constexpr int ES = 10;  // K-step of the first deferred epilogue tile
   char* wl = smem;
@@ -1013,6 +1021,36 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     for (int m = 0; m < NGW; ++m)
       if (wv_s + NW * m < NGRP) group_dma_one(gidx, m);
   };
+  // (DG_RELUMASK with gx_s: x is the gradient stream g) du = bf16(g s + dm / HW) formed in
+  // place on the wave's own DMA pieces of a group once they landed, before the barrier that
+  // publishes them; the padding (zero page) stays zero.  A lane's 16 B are the channels
+  // 8 cc .. 8 cc + 7 of its pixel in every piece (the swizzle (lane & 7) ^ (q & 7), q = 8 i +
+  // lane / 8)
+  [[maybe_unused]] const bool gx = EPI == EPI_DG_RELUMASK && p.gx_s != nullptr;  // (uniform)
+  [[maybe_unused]] float gxs[8], gxm[8];
+  if constexpr (EPI == EPI_DG_RELUMASK) {
+    if (gx) {
+      const int cc = (lane & 7) ^ (lane >> 3);
+      const float* sp = p.gx_s + (size_t)n * p.gx_s_stride + cc * 8;
+      const float* mp = p.gx_m + (size_t)n * 64 + cc * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        gxs[i] = sp[i];
+        gxm[i] = mp[i] * p.gx_inv_hw;
+      }
+    }
+  }
+  auto gx_group = [&](int gidx) __attribute__((always_inline)) {
+    const int slot = gidx % 3, y0 = 4 * gidx - 3;
+#pragma unroll
+    for (int m = 0; m < NGW; ++m) {
+      const int i = wv_s + NW * m;
+      if (i < NGRP && ((okx >> m) & 1u) && y0 + lrr[m] >= 0 && y0 + lrr[m] < p.H) {
+        uint4* q = reinterpret_cast<uint4*>(ring + (slot * 4 * (TW + 2)) * 128 + i * 1024 + lane * 16);
+        *q = du_from_g8(*q, gxs, gxm);
+      }
+    }
+  };
 
   // channel of accumulator row (c, r) of this lane, and the lane's channel bases
   auto chan = [&](int c, int rr) -> int { return kPerm ? ct0 * 16 + 8 * fk + 4 * c + rr : (ct0 + c) * 16 + 4 * fk + rr; };
@@ -1036,6 +1074,12 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     group_dma(k0);
     group_dma(k0 + 1);
     wait_vm<0>();
+    if constexpr (EPI == EPI_DG_RELUMASK) {
+      if (gx) {
+        gx_group(k0);
+        gx_group(k0 + 1);
+      }
+    }
   }
   STAMP(1);
   // A-fragment rows: lane fr of tile c reads the filter row of the channel its
@@ -1065,12 +1109,18 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
   DeferOps<NPT> ops;     // operands of the pending epilogue
 
   // operand loads of the epilogue of strip kp (pixel row 4 kp + row), load slot i
-  constexpr int NLD = (EPI == EPI_DG_RELUMASK || kCR) ? NPT : (kCA ? NPT * NCT : 0);
+  constexpr int NLD = (EPI == EPI_DG_RELUMASK || kCR) ? NPT : ((kCA || kG16) ? NPT * 2 : 0);
   auto op_load = [&](int kp, int i) __attribute__((always_inline)) {
     const int yy = 4 * kp + row;
     if constexpr (EPI == EPI_DG_RELUMASK) {
       const size_t pix = (size_t)n * HW + (size_t)yy * p.W + x0 + i * 16 + fr;
       ops.t[i] = *reinterpret_cast<const uint4*>(p.aux + pix * p.Cout + cb * 64 + chan(0, 0));
+    } else if constexpr (kG16) {  // load i: tile i / 2, g (even) or u (odd), 16 B each
+      const int pt = i >> 1;
+      const size_t pix = (size_t)n * HW + (size_t)yy * p.W + x0 + pt * 16 + fr;
+      const size_t o = pix * p.Cout + cb * 64 + chan(0, 0);
+      if (i & 1) ops.uq[pt] = *reinterpret_cast<const uint4*>(p.aux + o);
+      else ops.t[pt] = *reinterpret_cast<const uint4*>(p.r1b + o);
     } else if constexpr (kCA) {
       const int pt = i / NCT, c = i % NCT;
       const size_t pix = (size_t)n * HW + (size_t)yy * p.W + x0 + pt * 16 + fr;
@@ -1097,6 +1147,10 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
 #pragma unroll
     for (int c = 0; c < NCT; ++c) pin4(accp[pt][c]);
     if constexpr (EPI == EPI_DG_RELUMASK) pin4u(ops.t[pt]);
+    if constexpr (kG16) {
+      pin4u(ops.t[pt]);
+      pin4u(ops.uq[pt]);
+    }
     if constexpr (kCR) {
       if (p.r1h) {
         pin4u(ops.t[pt]);
@@ -1142,6 +1196,24 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
       const uint32_t oe = (uint32_t)(pix * p.Cout + cb * 64 + chan(0, 0));
       st_wt16(rph, p.yph, oe * 2, make_uint4(h0.x, h0.y, h1.x, h1.y));
       st_wt8(rpl, p.ypl, oe, make_uint2(l0, l1));
+    } else if constexpr (kG16) {
+      // g = bf16(acc + g_in): the CA sums take the rounded (stored) value, as conv_epilogue2
+      const uint32_t gw[4] = {ops.t[pt].x, ops.t[pt].y, ops.t[pt].z, ops.t[pt].w};
+      const uint32_t uw[4] = {ops.uq[pt].x, ops.uq[pt].y, ops.uq[pt].z, ops.uq[pt].w};
+      uint32_t ow[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 v = accp[pt][q >> 1];
+        const float a = v[2 * (q & 1)] + bf2f(gw[q] & 0xFFFFu), b = v[2 * (q & 1) + 1] + bf2f(gw[q] >> 16);
+        ow[q] = pack2(a, b);
+        const float ra = bf2f(ow[q] & 0xFFFFu), rb = bf2f(ow[q] >> 16);
+        const int c = q >> 1, r0 = 2 * (q & 1);
+        ps0[c][r0] += ra;
+        ps0[c][r0 + 1] += rb;
+        ps1[c][r0] += ra * bf2f(uw[q] & 0xFFFFu);
+        ps1[c][r0 + 1] += rb * bf2f(uw[q] >> 16);
+      }
+      st_defer(rout, p.yb, (uint32_t)((pix * p.Cout + cb * 64 + chan(0, 0)) * 2), make_uint4(ow[0], ow[1], ow[2], ow[3]));
     } else if constexpr (kPerm) {
       float o[8];
 #pragma unroll
@@ -1196,10 +1268,10 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
       for (int rr = 0; rr < 4; ++rr) {
         const float s0 = sum16(ps0[c][rr]);
         float s1 = 0.f;
-        if constexpr (kCA) s1 = sum16(ps1[c][rr]);
+        if constexpr (kS1) s1 = sum16(ps1[c][rr]);
         if (fr == 0) {
           rb[(row * 2 + 0) * 64 + chan(c, rr)] = s0;
-          if constexpr (kCA) rb[(row * 2 + 1) * 64 + chan(c, rr)] = s1;
+          if constexpr (kS1) rb[(row * 2 + 1) * 64 + chan(c, rr)] = s1;
         }
       }
   };
@@ -1209,7 +1281,7 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     const size_t rec = ((size_t)n * nstrips_all + kp * nsx + sx) * p.part_stride;
     if (tid < 64) {
       p.part[rec + cb * 64 + tid] = rb[tid] + rb[128 + tid] + rb[256 + tid] + rb[384 + tid];
-    } else if (kCA && tid < 128) {
+    } else if (kS1 && tid < 128) {
       const int c = tid - 64;
       p.part[rec + 64 + c] = rb[64 + c] + rb[192 + c] + rb[320 + c] + rb[448 + c];
     }
@@ -1228,7 +1300,7 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     constexpr bool LAST = decltype(last_tag)::value;
     const int y = 4 * k + row;
     const bool pf = (k + 1 < k1);
-    const bool red_store = kPart && (k - 2 >= k0) && tid < (kCA ? 128 : 64);
+    const bool red_store = kPart && (k - (kImm ? 1 : 2) >= k0) && tid < (kS1 ? 128 : 64);
     [[maybe_unused]] const int sj = 2 + 5 * min(k - k0, 11);
     STAMP(sj);
     uint32_t boff[3][3][2];
@@ -1264,11 +1336,11 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
       // 0-2), group k+2's DMA (0-3), the deferred stores (K-steps ES..), the
       // previous-but-one strip's partial record (17): the DMA is waited for at the
       // end with a count of the stores behind it
-      if constexpr (PREV && NLD > 0) {
+      if constexpr ((PREV || kImm) && NLD > 0) {
         constexpr int PER = (NLD + 2) / 3;
 #pragma unroll
         for (int i = 0; i < PER; ++i)
-          if (st < 3 && st * PER + i < NLD) op_load(k - 1, st * PER + i);
+          if (st < 3 && st * PER + i < NLD) op_load(kImm ? k : k - 1, st * PER + i);
       }
       if (st < NGW && pf && wv_s + NW * st < NGRP) group_dma_one(k + 2, st);
       __builtin_amdgcn_sched_barrier(0);
@@ -1293,7 +1365,7 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
           if (st == ES + NPT) part_rows(k - 1);
       }
       if constexpr (kPart)
-        if (st == 17 && red_store) part_store(k - 2);
+        if (st == 17 && red_store) part_store(kImm ? k - 1 : k - 2);
       if constexpr (LAST && NLD > 0) {
         // the exposed epilogue's operands, behind this strip's last MFMAs
         constexpr int PER = (NLD + 1) / 2;
@@ -1307,13 +1379,27 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     // group k+2 has landed once only this strip's deferred stores (and the partial
     // record) may still be in flight behind it
     constexpr int NST = PREV ? (kCR ? 2 * NPT : (kPerm ? NPT : NPT * NCT)) : 0;
-    if (!pf) {
+    if constexpr (kImm) {
+      // the strip's own epilogue: its operands, group k+2 and the partial record landed
+      wait_vm<0>();
+#pragma unroll
+      for (int i = 0; i < NPT; ++i)
+#pragma unroll
+        for (int j = 0; j < NCT; ++j) accp[i][j] = acc[i][j];
+      zero_ps();
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt) epi_tile(k, pt);
+      part_rows(k);
+    } else if (!pf) {
       // no DMA in this strip: nothing to wait for (the loads of the exposed
       // epilogue are waited for where they are used)
     } else if (red_store) {
       wait_vm<NST + 1>();
     } else {
       wait_vm<NST>();
+    }
+    if constexpr (EPI == EPI_DG_RELUMASK) {
+      if (gx && pf) gx_group(k + 2);  // (its pieces landed: the wait above)
     }
     STAMP(sj + 2);
 #ifdef SRMI_STAMPS
@@ -1334,6 +1420,13 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
   };
   using T = std::true_type;
   using F = std::false_type;
+  if constexpr (kImm) {
+#pragma unroll 1
+    for (int k = k0; k < k1; ++k) strip(k, F{}, F{});
+    part_store(k1 - 1);  // (its rows' sums published by the last strip's barrier)
+    STAMP(61);
+    return;
+  }
   if (k1 - k0 == 1) {
     strip(k0, F{}, T{});
   } else {

@@ -84,7 +84,7 @@ int build_plan(const srmi_model_config* cfg, Plan& P) {
   if (c.arch == SRMI_ARCH_RCAN && (c.nblocks < 1 || c.reduction < 1 || 64 % c.reduction)) return SRMI_ERR_ARG;
   if (c.arch != SRMI_ARCH_RCAN && c.arch != SRMI_ARCH_EDSR) return SRMI_ERR_ARG;
   if (c.dtype != SRMI_DTYPE_BF16 && c.dtype != SRMI_DTYPE_F32) return SRMI_ERR_ARG;
-  if (c.flags & ~(SRMI_FLAG_NO_RCAB_INFER | SRMI_FLAG_CA_PASS)) return SRMI_ERR_ARG;  // (retired bits refused)
+  if (c.flags & ~(SRMI_FLAG_NO_RCAB_INFER | SRMI_FLAG_CA_PASS | SRMI_FLAG_DU_PASS)) return SRMI_ERR_ARG;  // (retired bits refused)
   P = Plan();
   P.cfg = c;
   const int F = 64;
@@ -799,9 +799,6 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         const int q = it++ & 1;
         bf16_t* du = e->DU;
         bf16_t* dz = e->DZ;
-        RC(ca_bwd_du_launch(g16 ? static_cast<const void*>(ghb) : ghf, g16, e->pacc, nstrips, e->recp(g, b),
-                            prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du, e->brecp(g, b), e->f32, st,
-                            have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
         ReduceSet red2, red1;
         WgradParams wp;
         int epi = EPI_DG_RELUMASK;
@@ -809,6 +806,22 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
                                      nullptr, 1.f);
         RC(wgrad_params(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, rs2, e->slab_r[q][0], e->bslab_r[q][0],
                         e->slab_r_floats, e->bslab_r_floats, &wp, &red2, kSlab16));
+        // du = bf16(g s + dm / HW) formed by the fused conv2 backward from the bf16 stream
+        // on its input rings (the CA backward then runs its MLP only), or written by the
+        // CA backward and read back (SRMI_FLAG_DU_PASS, exact fp32, unfusable shapes)
+        const bool du_fused = g16 && !(P.cfg.flags & SRMI_FLAG_DU_PASS) && rcab_bwd_du_from_g() &&
+                              epi == EPI_DG_RELUMASK && rcab_bwd_fusable(cp, wp);
+        if (du_fused) {
+          const int CR = 64 / R;
+          cp.x = wp.dy = ghb;
+          cp.gx_s = wp.gx_s = e->recp(g, b) + 64 + CR;  // s in the forward record m | z1 | s
+          cp.gx_s_stride = wp.gx_s_stride = 128 + CR;
+          cp.gx_m = wp.gx_m = e->brecp(g, b) + (size_t)n * (128 + CR);  // dm [n][64] after the records
+          cp.gx_inv_hw = wp.gx_inv_hw = 1.f / (float)HW;
+        }
+        RC(ca_bwd_du_launch(g16 ? static_cast<const void*>(ghb) : ghf, g16, e->pacc, nstrips, e->recp(g, b),
+                            prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du_fused ? nullptr : du, e->brecp(g, b),
+                            e->f32, st, have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
         RC(dgrad_with_wgrad(e, cp, epi, wp, 2, st));
         const bool last = (b == 1);
         epi = EPI_DG_ACC;

@@ -1360,13 +1360,15 @@ int ca_fwd_launch(const void* u, const float* part, int nstrips, const float* w1
 // brec per image: dz2[C] dz1[CR] dbconv2[C]; followed (after all N images) by
 // dm[N][C] = W1^T dz1 (the gradient of the pooled mean).
 // du = g * s + dm / HW  (operand type T); g fp32, or (TG = bf16_t) the bf16 engine's
-// in-group gradient stream
+// in-group gradient stream.  DU = false (du null): the MLP backward and brec only, one
+// block per image -- the next fused backward launch forms du from g itself (ConvParams
+// gx_*, du_from_g8: the same fma and rounding)
 //
 // Rows blockIdx.y >= N of the grid (nred > 0) carry the fixed-order slab
 // reductions of the previous RCAB's two filter gradients (r0, r1: nred blocks
 // each, 256-thread wgrad_reduce_body): both are memory-bound passes of many small
 // blocks, so the reduction rides in this launch instead of a launch of its own.
-template <typename T, typename TG>
+template <typename T, typename TG, bool DU = true>
 __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const TG* __restrict__ g, const float* __restrict__ part,
                                                         int nstrips, const float* __restrict__ rec,
                                                         const float* __restrict__ w1, const float* __restrict__ w2,
@@ -1414,7 +1416,7 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const TG* __restrict__ g
   float4 g0[kCaVec], g1[kCaVec];
   [[maybe_unused]] uint4 gq[kCaVec];
 #pragma unroll
-  for (int k = 0; k < kCaVec; ++k) {  // clamped, unconditional (tail lanes store nothing)
+  for (int k = 0; k < (DU ? kCaVec : 0); ++k) {  // clamped, unconditional (tail lanes store nothing)
     const size_t e = base + min(v0 + (size_t)k * blockDim.x, nv - 1) * 8;
     if constexpr (sizeof(TG) == 2) {
       gq[k] = *reinterpret_cast<const uint4*>(g + e);  // 8 bf16, decoded where used
@@ -1464,6 +1466,7 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const TG* __restrict__ g
     }
     if (tid < CR) br[C + tid] = dz1[tid];
   }
+  if constexpr (!DU) return;
   const auto rdu = wt_rsrc(du, (uint32_t)((size_t)gridDim.y * HW * C * sizeof(T)));  // lane-contiguous: write-through
 #pragma unroll
   for (int k = 0; k < kCaVec; ++k) {
@@ -1477,9 +1480,10 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const TG* __restrict__ g
       g0[k] = make_float4(bf2f(gq[k].x & 0xFFFFu), bf2f(gq[k].x >> 16), bf2f(gq[k].y & 0xFFFFu), bf2f(gq[k].y >> 16));
       g1[k] = make_float4(bf2f(gq[k].z & 0xFFFFu), bf2f(gq[k].z >> 16), bf2f(gq[k].w & 0xFFFFu), bf2f(gq[k].w >> 16));
     }
-    const float o[8] = {g0[k].x * s[c0 + 0] + dmh[0], g0[k].y * s[c0 + 1] + dmh[1], g0[k].z * s[c0 + 2] + dmh[2],
-                        g0[k].w * s[c0 + 3] + dmh[3], g1[k].x * s[c0 + 4] + dmh[4], g1[k].y * s[c0 + 5] + dmh[5],
-                        g1[k].z * s[c0 + 6] + dmh[6], g1[k].w * s[c0 + 7] + dmh[7]};
+    const float o[8] = {fmaf(g0[k].x, s[c0 + 0], dmh[0]), fmaf(g0[k].y, s[c0 + 1], dmh[1]),
+                        fmaf(g0[k].z, s[c0 + 2], dmh[2]), fmaf(g0[k].w, s[c0 + 3], dmh[3]),
+                        fmaf(g1[k].x, s[c0 + 4], dmh[4]), fmaf(g1[k].y, s[c0 + 5], dmh[5]),
+                        fmaf(g1[k].z, s[c0 + 6], dmh[6]), fmaf(g1[k].w, s[c0 + 7], dmh[7])};
     if constexpr (sizeof(T) == 2) {
       const uint4 ob = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
       st_wt16(rdu, du, (uint32_t)((base + v * 8) * 2), ob);
@@ -1499,7 +1503,8 @@ int ca_bwd_du_launch(const void* g, int g16, const float* part, int nstrips, con
   if (red0 && (red0->Cout != red1->Cout)) return SRMI_ERR_SHAPE;
   // (a set with neither gw nor gb -- the group tail's single reduction -- adds no blocks)
   const bool two = red1 && (red1->gw || red1->gb);
-  const int gx = ca_grid_x(HW, C);
+  if (!du && (f32 || !g16)) return SRMI_ERR_ARG;  // (du from g: the bf16 stream only)
+  const int gx = du ? ca_grid_x(HW, C) : 1;
   const ReduceSet none{};
   const int nred = red0 ? wgrad_reduce_blocks(red0->Cout) : 0;
   const dim3 grid(gx, N + ((two ? 2 : 1) * nred + gx - 1) / gx);
@@ -1508,6 +1513,9 @@ int ca_bwd_du_launch(const void* g, int g16, const float* part, int nstrips, con
   if (f32)
     hipLaunchKernelGGL((ca_bwd_du_kernel<float, float>), grid, dim3(256), 0, st, static_cast<const float*>(g), part,
                        nstrips, rec, w1, w2, N, HW, C, C / R, static_cast<float*>(du), brec, a, b, nred);
+  else if (g16 && !du)
+    hipLaunchKernelGGL((ca_bwd_du_kernel<bf16_t, bf16_t, false>), grid, dim3(256), 0, st, static_cast<const bf16_t*>(g),
+                       part, nstrips, rec, w1, w2, N, HW, C, C / R, static_cast<bf16_t*>(du), brec, a, b, nred);
   else if (g16)
     hipLaunchKernelGGL((ca_bwd_du_kernel<bf16_t, bf16_t>), grid, dim3(256), 0, st, static_cast<const bf16_t*>(g),
                        part, nstrips, rec, w1, w2, N, HW, C, C / R, static_cast<bf16_t*>(du), brec, a, b, nred);

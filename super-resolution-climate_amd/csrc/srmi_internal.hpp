@@ -92,6 +92,14 @@ struct ConvParams {
   // (and the first one of the image writes cas.rec); cas_on = 0: s from escale
   CaScale cas;
   int cas_on;
+  // (EPI_DG_RELUMASK, the deferred 8-wave body) x is the bf16 gradient stream g and the
+  // conv reads du = bf16(g s[c] + dm[c] / HW), the CALayer backward's du (ca_bwd_du_kernel),
+  // formed on the input ring in LDS: gx_s = s of image n at gx_s + n * gx_s_stride (the
+  // forward record), gx_m = dm [N][64]; null = x is read as it is
+  const float* gx_s;
+  int gx_s_stride;
+  const float* gx_m;
+  float gx_inv_hw;
 };
 
 void conv3x3_set_debug_stamps(unsigned long long* buf);
@@ -127,6 +135,12 @@ struct WgradParams {
   int f32;             // exact-fp32 mode: x, dy point at fp32 data
   int slab16;          // (wgrad48 body) weight slabs stored as bf16 at `slab` (the RCAB filter
                        // gradients of the bf16 engine: half the slab bytes); bias slabs fp32
+  // (wgrad48 body, IN_PLAIN, Cout == 64) dy is g and the filter gradient takes du formed
+  // from it in LDS, as ConvParams.gx_* (null = dy read as it is)
+  const float* gx_s;
+  int gx_s_stride;
+  const float* gx_m;
+  float gx_inv_hw;
 };
 void wgrad3x3_set_debug_stamps(unsigned long long* buf);
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st);  // dispatches p.f32
@@ -143,6 +157,8 @@ int wgrad_reduce2_launch(const ReduceSet& r0, const ReduceSet& r1, hipStream_t s
 // sized for conv_cus CUs) beside the filter gradient wp of the same conv (wgrad48)
 int rcab_bwd_fusable(const ConvParams& cp, const WgradParams& wp);
 int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradParams& wp, hipStream_t st);
+// the fused conv2 backward (EPI_DG_RELUMASK) of this build forms du from g (ConvParams gx_*)
+bool rcab_bwd_du_from_g();
 int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Cout, int ps, int layout, float alpha,
                         float* gw, float* gb, hipStream_t st, int slab16 = 0);
 

@@ -16,7 +16,7 @@
 #endif
 
 // Deferred conv epilogues (conv64_body.hpp conv64_defers), a bit mask: 1 RELU, 2 POOL,
-// 4 DG_RELUMASK, 8 DG_ACC_CA, 16 RELU_POOL, 32 CA_RESID.  Training: only DG_RELUMASK
+// 4 DG_RELUMASK, 8 DG_ACC_CA, 16 RELU_POOL, 32 CA_RESID, 64 DG_ACC_CA16.  Training: only DG_RELUMASK
 // gains in the step; inference (an image is one run of 12 strips): conv1's RELU_POOL
 // (CA_RESID deferred measured 5 % slower: its pair codec competes with the next strip's
 // MFMA issue).
@@ -25,6 +25,12 @@
 #endif
 #ifndef SRMI_INFER_DEFER
 #define SRMI_INFER_DEFER 16
+#endif
+
+// F1 (EPI_DG_ACC_CA16) with its epilogue deferred (SRMI_TRAIN_DEFER bit 64): dgrad strips
+// per run handed to the paired filter-gradient workgroup
+#ifndef SRMI_F1_DEFER_TAIL
+#define SRMI_F1_DEFER_TAIL 0
 #endif
 
 // the inference conv2's h' = h + s u with u rounded to bf16 (as the training conv2 and

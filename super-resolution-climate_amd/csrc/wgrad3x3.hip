@@ -418,6 +418,39 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
     else wait_vm<0>();
   };
 
+  // (gx_s: dy is the gradient stream g) du = bf16(g s + dm / HW) formed in place on this
+  // wave's own dY groups of a pair once they landed, before the barrier that publishes
+  // them (as the dgrad's input ring, conv64_body_defer); s and dm / HW of the image in an
+  // LDS table past the rings.  A lane's 16 B of group g are channels 8 c .. 8 c + 7, c =
+  // cl0 (g even) / cl1 (g odd)
+  const bool gx = p.gx_s != nullptr;  // (uniform)
+  float* const gxt = reinterpret_cast<float*>(smem + LDS);  // [s 64][dmh 64]
+  auto gx_pair = [&](int P) __attribute__((always_inline)) {
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int k = wave_s + 4 * m, rr = k / GD, g = k - rr * GD;
+      const int c = (g & 1) ? cl1 : cl0;
+      float sv[8], mv[8];
+      const float4 s0 = *reinterpret_cast<const float4*>(gxt + c * 8);
+      const float4 s1 = *reinterpret_cast<const float4*>(gxt + c * 8 + 4);
+      const float4 m0 = *reinterpret_cast<const float4*>(gxt + 64 + c * 8);
+      const float4 m1 = *reinterpret_cast<const float4*>(gxt + 64 + c * 8 + 4);
+      sv[0] = s0.x; sv[1] = s0.y; sv[2] = s0.z; sv[3] = s0.w; sv[4] = s1.x; sv[5] = s1.y; sv[6] = s1.z; sv[7] = s1.w;
+      mv[0] = m0.x; mv[1] = m0.y; mv[2] = m0.z; mv[3] = m0.w; mv[4] = m1.x; mv[5] = m1.y; mv[6] = m1.z; mv[7] = m1.w;
+      uint4* q = reinterpret_cast<uint4*>(smem + ((2 * P + rr) & (RD - 1)) * DSLOT + g * 1024 + lane * 16);
+      *q = du_from_g8(*q, sv, mv);
+    }
+  };
+  if (gx) {  // (8 waves: by waves 4 and 5, which issue no DMA, so the wait for these loads
+             //  does not drain the prologue's groups)
+    const int tt = NW == 8 ? tid - 256 : tid;
+    if (tt >= 0 && tt < 64) {
+      gxt[tt] = p.gx_s[(size_t)n * p.gx_s_stride + tt];
+    } else if (tt >= 64 && tt < 128) {
+      gxt[tt] = p.gx_m[(size_t)n * 64 + tt - 64] * p.gx_inv_hw;
+    }
+  }
+
   // prologue: input rows -1, 0 and pairs 0 .. PF-1; wait for the rows and pair 0
   if constexpr (kMain) {
 #pragma unroll
@@ -425,7 +458,11 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
       if (wave_s + 4 * m < 2 * GX) dma(0, wave_s + 4 * m, true);
     for (int P = 0; P < PF && P < np; ++P) dma_pair_part(P, 0, 7);
   }
+  if (gx) __syncthreads();  // (the table)
   wait_groups(min(PF, np) - 1, 0);
+  if constexpr (kMain) {
+    if (gx) gx_pair(0);
+  }
   __syncthreads();
   WSTAMP(1);
 
@@ -490,6 +527,9 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
           // flight may stay: pair j+2 (whole) and the 5 groups of pair j+PF issued above.
           if (j + 2 < np) wait_groups(1, pf ? 5 : 0);
           else wait_groups(0, 0);
+          if constexpr (kMain) {
+            if (gx && more) gx_pair(j + 1);
+          }
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
@@ -620,6 +660,8 @@ __global__ void __launch_bounds__(NW * 64, 1) rcab_bwd_kernel(ConvParams cp, int
 #endif
 }
 
+bool rcab_bwd_du_from_g() { return conv64_defers<EPI_DG_RELUMASK>(); }
+
 int rcab_bwd_fusable(const ConvParams& cp, const WgradParams& wp) {
   return !cp.f32 && !wp.f32 && cp.Cin == 64 && cp.Cout == 64 && cp.in_mode == IN_PLAIN && cp.W == 48 &&
          cp.H % 4 == 0 && wp.W == 48 && wp.Cout == 64 && wp.dy_mode == IN_PLAIN && wp.row_splits > 0 &&
@@ -636,11 +678,19 @@ static bool slab_range_ok(const WgradParams& p, int nslabs) {
 
 int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradParams& wp, hipStream_t st) {
   if (!rcab_bwd_fusable(cp, wp)) return SRMI_ERR_SHAPE;
+  // du formed from the gradient stream g (gx_*): both roles together, in the deferred
+  // ReLU-mask dgrad (conv64_body_defer) beside a 64-channel filter gradient
+  if ((cp.gx_s != nullptr) != (wp.gx_s != nullptr) || (cp.gx_m != nullptr) != (wp.gx_m != nullptr) ||
+      (cp.gx_s != nullptr) != (cp.gx_m != nullptr))
+    return SRMI_ERR_ARG;
+  if (cp.gx_s && (epi != EPI_DG_RELUMASK || !conv64_defers<EPI_DG_RELUMASK>() || cp.x != wp.dy))
+    return SRMI_ERR_ARG;
   if (!slab_range_ok(wp, wp.N * wp.row_splits)) return SRMI_ERR_SHAPE;
   const int run_len = conv64_run_len(cp, 48, conv_cus);
   const int nconv = conv64_blocks(cp, 48, run_len);
   const int nwg = wp.N * wp.row_splits * (wp.Cout / 64);
   const int lds = Conv2Smem<48>::TOTAL > v4::LDS ? Conv2Smem<48>::TOTAL : v4::LDS;
+  static_assert(Conv2Smem<48>::TOTAL >= v4::LDS + 512, "the filter gradient's du table (gx) past its rings");
   ConvParams c = cp;
   c.stamps = conv3x3_stamps_for(epi);  // (null in production; the dgrad runs' phase stamps in diagnostic builds)
   WgradParams w = wp;
@@ -653,8 +703,9 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
       nconv == nwg && cp.N == wp.N && runs_per_col == wp.row_splits && run_len * kTH == wp.H / wp.row_splits;
   // dgrad strips per run handed to the paired filter-gradient workgroup (see the kernel)
   // (one strip in F1; none in F2, whose ReLU-mask strip is cheaper than the extra
-  // filter prologue: DESIGN.md section 3)
-  const int tail = !paired ? 0 : std::min(run_len - 1, epi == EPI_DG_RELUMASK ? 0 : 1);
+  //  filter prologue, nor in F1 with its epilogue deferred: SRMI_F1_DEFER_TAIL)
+  const bool f1_defer = epi == EPI_DG_ACC_CA16 && conv64_defers<EPI_DG_ACC_CA16>();
+  const int tail = !paired ? 0 : std::min(run_len - 1, epi == EPI_DG_RELUMASK ? 0 : (f1_defer ? SRMI_F1_DEFER_TAIL : 1));
   switch (epi) {
     case EPI_DG_RELUMASK:
       if (!c.aux) return SRMI_ERR_ARG;
@@ -704,6 +755,7 @@ int wgrad3x3_nslabs(const WgradParams& p) { return p.N * p.row_splits * (use_wgr
 int wgrad3x3_slab_layout(const WgradParams& p) { return use_wgrad48(p) ? 1 : 0; }
 
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
+  if (p.gx_s) return SRMI_ERR_ARG;  // (du formed from g: the fused backward launch only)
   if (p.f32) return wgrad_f32_launch(p, st);
   if (p.Cout % 64 || p.H % p.row_splits || (p.H / p.row_splits) % 4) return SRMI_ERR_SHAPE;
   if (p.dy_mode == IN_UNSHUF && p.Cout != 256) return SRMI_ERR_SHAPE;

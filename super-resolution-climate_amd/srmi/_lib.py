@@ -19,6 +19,7 @@ SRMI_ARCH_EDSR = 1
 SRMI_DTYPE_BF16 = 0
 SRMI_FLAG_NO_RCAB_INFER = 2
 SRMI_FLAG_CA_PASS = 4
+SRMI_FLAG_DU_PASS = 16
 SRMI_DTYPE_F32 = 1
 SRMI_LOSS_RMSE = 0
 SRMI_LOSS_MEAN = 1

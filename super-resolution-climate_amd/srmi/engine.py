@@ -36,7 +36,7 @@ class NetSpec:
     scale: int = 4
     res_scale: float = 1.0
     dtype: str = "bf16"   # engine operand type: "bf16" (bf16 MFMA operands) or "fp32" (exact fp32)
-    flags: int = 0        # srmi_model_config.flags (SRMI_FLAG_CA_PASS, SRMI_FLAG_NO_RCAB_INFER: A/B and tests)
+    flags: int = 0        # srmi_model_config.flags (SRMI_FLAG_CA_PASS, SRMI_FLAG_DU_PASS, SRMI_FLAG_NO_RCAB_INFER: A/B and tests)
 
     @staticmethod
     def from_parms(arch: str, parms: Dict, dtype: str = "bf16") -> "NetSpec":

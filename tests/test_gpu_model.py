@@ -358,6 +358,19 @@ def test_ca_forward_in_conv2_matches_ca_pass(lr_hw):
     _engine_variants_agree(lr_hw, (0, SRMI_FLAG_CA_PASS), 5e-3, fwd_tol=1e-3)
 
 
+@pytest.mark.parametrize("lr_hw", [(48, 48), (32, 48), (8, 48), (24, 96)])
+def test_du_from_g_matches_du_pass(lr_hw):
+    """The CALayer backward's du = bf16(g s + dm / HW) formed by the fused conv2 backward
+    on its input rings in LDS, from the bf16 gradient stream g (the default: the dgrad's
+    ring groups and the filter gradient's dY rows, each wave on its own DMA pieces) against
+    du written by the CA backward and read back (SRMI_FLAG_DU_PASS): the same fma and
+    rounding, so the whole step is bit-identical.  Three tile heights change the runs'
+    and row bands' boundaries (and the image-border halo rows the transform must leave
+    zero); the 96-wide tiles take the unfused launches in both engines."""
+    from srmi._lib import SRMI_FLAG_DU_PASS
+    _engine_variants_agree(lr_hw, (0, SRMI_FLAG_DU_PASS), 0)
+
+
 @pytest.mark.parametrize("arch", ["rcan", "edsr"])
 def test_backward_stages_one_at_a_time_and_order_checked(arch):
     """srmi_backward_stages run one stage per call gives the gradients of one
