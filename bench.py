@@ -165,9 +165,9 @@ WGRAD_OUT_BYTES = 64 * 577 * 4           # dW (64x64x9) + db, fp32, once per lau
 #  F1 = rcab_bwd_kernel<DG_ACC_CA16>: conv1's dgrad (reads dz bf16, reads + writes the
 #       in-group gradient stream g -- bf16 since round 6 --, reads the CA input u bf16 for
 #       the CA sums) and conv1's filter gradient (reads its input hb bf16; dz already counted)
-#  F2 = rcab_bwd_kernel<DG_RELUMASK>: conv2's dgrad (reads du bf16, reads the ReLU
-#       output t bf16 as the mask, writes dz bf16) and conv2's filter gradient (t, du
-#       already counted)
+#  F2 = rcab_bwd_kernel<DG_RELUMASK>: conv2's dgrad (reads the bf16 stream g -- du =
+#       g s + dm / HW formed in LDS since round 6; before, du bf16 --, reads the ReLU output
+#       t bf16 as the mask, writes dz bf16) and conv2's filter gradient (t, g already counted)
 F1_BYTES_PER_TILE = 5 * ACT_BF16_PER_TILE
 F2_BYTES_PER_TILE = 3 * ACT_BF16_PER_TILE
 FUSED_FLOP_PER_TILE = 2 * CONV64_FLOP_PER_TILE   # one dgrad conv + one filter-gradient conv

@@ -1004,6 +1004,15 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
                       1.f);
     RC(wgrad_params(e, r.c2, e->Tm(0, b), e->DU, n, h, w, grads, false, 1.f, rcab_row_splits(e, n, 2),
                     e->slab_r[0][0], e->bslab_r[0][0], e->slab_r_floats, e->bslab_r_floats, &wp, &red, kSlab16));
+    // (as backward_impl: du formed from the bf16 stream in the fused launch)
+    if (!e->f32 && !(e->P.cfg.flags & SRMI_FLAG_DU_PASS) && rcab_bwd_du_from_g() && rcab_bwd_fusable(cp, wp)) {
+      const int CR = 64 / e->P.cfg.reduction;
+      cp.x = wp.dy = e->GBb;
+      cp.gx_s = wp.gx_s = e->recp(0, b) + 64 + CR;
+      cp.gx_s_stride = wp.gx_s_stride = 128 + CR;
+      cp.gx_m = wp.gx_m = e->brecp(0, b) + (size_t)n * (128 + CR);
+      cp.gx_inv_hw = wp.gx_inv_hw = 1.f / (float)(h * w);
+    }
   } else {
     const bool last = (b == 1);
     epi = EPI_DG_ACC;
