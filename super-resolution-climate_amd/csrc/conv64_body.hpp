@@ -1040,16 +1040,16 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
       }
     }
   }
-  auto gx_group = [&](int gidx) __attribute__((always_inline)) {
-    const int slot = gidx % 3, y0 = 4 * gidx - 3;
-#pragma unroll
-    for (int m = 0; m < NGW; ++m) {
-      const int i = wv_s + NW * m;
-      if (i < NGRP && ((okx >> m) & 1u) && y0 + lrr[m] >= 0 && y0 + lrr[m] < p.H) {
-        uint4* q = reinterpret_cast<uint4*>(ring + (slot * 4 * (TW + 2)) * 128 + i * 1024 + lane * 16);
-        *q = du_from_g8(*q, gxs, gxm);
-      }
+  auto gx_piece = [&](int gidx, int m) __attribute__((always_inline)) {
+    const int slot = gidx % 3, y0 = 4 * gidx - 3, i = wv_s + NW * m;
+    if (i < NGRP && ((okx >> m) & 1u) && y0 + lrr[m] >= 0 && y0 + lrr[m] < p.H) {
+      uint4* q = reinterpret_cast<uint4*>(ring + (slot * 4 * (TW + 2)) * 128 + i * 1024 + lane * 16);
+      *q = du_from_g8(*q, gxs, gxm);
     }
+  };
+  auto gx_group = [&](int gidx) __attribute__((always_inline)) {
+#pragma unroll
+    for (int m = 0; m < NGW; ++m) gx_piece(gidx, m);
   };
 
   // channel of accumulator row (c, r) of this lane, and the lane's channel bases
@@ -1366,6 +1366,19 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
       }
       if constexpr (kPart)
         if (st == 17 && red_store) part_store(kImm ? k - 1 : k - 2);
+      if constexpr (EPI == EPI_DG_RELUMASK) {
+        // du of group k+2 (gx), one DMA piece per K-step behind that step's MFMAs over the
+        // strip's last K-steps: the pieces (issued at K-steps 0-3) have landed once only
+        // the deferred stores of K-steps ES.. may still be in flight behind them
+        constexpr int GXS = 18 - NGW;
+        if (SRMI_GX_INLOOP && gx && pf && st >= GXS) {
+          if (st == GXS) {
+            if constexpr (PREV) wait_vm<NPT>();
+            else wait_vm<0>();
+          }
+          gx_piece(k + 2, st - GXS);
+        }
+      }
       if constexpr (LAST && NLD > 0) {
         // the exposed epilogue's operands, behind this strip's last MFMAs
         constexpr int PER = (NLD + 1) / 2;
@@ -1398,7 +1411,7 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     } else {
       wait_vm<NST>();
     }
-    if constexpr (EPI == EPI_DG_RELUMASK) {
+    if constexpr (EPI == EPI_DG_RELUMASK && !SRMI_GX_INLOOP) {
       if (gx && pf) gx_group(k + 2);  // (its pieces landed: the wait above)
     }
     STAMP(sj + 2);

@@ -33,6 +33,13 @@
 #define SRMI_F1_DEFER_TAIL 0
 #endif
 
+// du formed from g in the fused conv2 backward (ConvParams / WgradParams gx_*): 1 = behind
+// the MFMAs of the strip's last K-steps (dgrad) / of a pair's first K-step (filter
+// gradient), 0 = after the wait for the pieces, before the barrier that publishes them
+#ifndef SRMI_GX_INLOOP
+#define SRMI_GX_INLOOP 1
+#endif
+
 // the inference conv2's h' = h + s u with u rounded to bf16 (as the training conv2 and
 // the round-3 three-launch inference did; staged once as bf16, one barrier), 0 = fp32 u
 // (staged as fp32 in two halves, four barriers)

@@ -412,6 +412,8 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
     else if (n == 13) wait_vm<13>();
     else if (n == 12) wait_vm<12>();
     else if (n == 11) wait_vm<11>();
+    else if (n == 10) wait_vm<10>();
+    else if (n == 9) wait_vm<9>();
     else if (n == 7) wait_vm<7>();
     else if (n == 6) wait_vm<6>();
     else if (n == 5) wait_vm<5>();
@@ -522,12 +524,21 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
           if constexpr (NRD > NPAIR) __builtin_amdgcn_sched_group_barrier(0x100, NRD - NPAIR, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (kMain) {
+          // (gx) du of pair j+1 behind K-step 0's MFMAs: in flight may stay pair j+2 and the
+          // 3 groups of pair j+PF issued above; the barrier of K-step 1 publishes it
+          if (SRMI_GX_INLOOP && kc == 0 && gx && more) {
+            if (j + 2 < np) wait_groups(1, pf ? 3 : 0);
+            else wait_groups(0, 0);
+            gx_pair(j + 1);
+          }
+        }
         if (kc == 1) {
           // pair j+1 must have landed before K-step 2 reads its first fragments.  In
           // flight may stay: pair j+2 (whole) and the 5 groups of pair j+PF issued above.
           if (j + 2 < np) wait_groups(1, pf ? 5 : 0);
           else wait_groups(0, 0);
-          if constexpr (kMain) {
+          if constexpr (kMain && !SRMI_GX_INLOOP) {
             if (gx && more) gx_pair(j + 1);
           }
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

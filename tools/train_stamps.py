@@ -29,7 +29,7 @@ from srmi.trainer import FusedTrainer  # noqa: E402
 def main():
     d = torch.device("cuda", 0)
     spec = NetSpec(arch="rcan", nchannels_in=2, nchannels_out=2, nfeatures=64, nlayers=10, nblocks=20,
-                   cbottleneck=2, scale=4)
+                   cbottleneck=2, scale=4, flags=int(os.environ.get("STAMPS_FLAGS", "0")))  # (16: SRMI_FLAG_DU_PASS)
     tr = FusedTrainer(spec, 64, (48, 48), lr=1e-4, info=DistInfo(), device=d, seed=0, micro=2)
     hr = torch.tensor(bench.synthetic_hr(64, 2, 192, 1234)).to(d)
     for _ in range(3):
