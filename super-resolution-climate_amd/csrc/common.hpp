@@ -40,12 +40,17 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 
 // du = bf16(g s + dmh) of 8 bf16 channels (the CALayer backward's du, ca_bwd_du_kernel;
 // dmh = dm / HW): one fma per channel, so every producer of du rounds the same value
+// (two channels per packed fma: v_pk_fma_f32, the same fma per element)
 __device__ __forceinline__ uint4 du_from_g8(uint4 gq, const float (&s)[8], const float (&m)[8]) {
   const uint32_t w[4] = {gq.x, gq.y, gq.z, gq.w};
   uint32_t o[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
-    o[q] = pack2(fmaf(bf2f(w[q] & 0xFFFFu), s[2 * q], m[2 * q]), fmaf(bf2f(w[q] >> 16), s[2 * q + 1], m[2 * q + 1]));
+  for (int q = 0; q < 4; ++q) {
+    const f32x2 x = {__uint_as_float(w[q] << 16), __uint_as_float(w[q] & 0xFFFF0000u)};
+    const f32x2 sv = {s[2 * q], s[2 * q + 1]}, mv = {m[2 * q], m[2 * q + 1]};
+    const f32x2 r = __builtin_elementwise_fma(x, sv, mv);
+    o[q] = pack2(r.x, r.y);
+  }
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
 

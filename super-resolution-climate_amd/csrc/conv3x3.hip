@@ -403,7 +403,7 @@ int conv3x3_launch(const ConvParams& p, int epi, hipStream_t st) {
   if (p.Cin % 64 || p.Cout % 64 || p.N <= 0 || p.H % kTH) return SRMI_ERR_SHAPE;
   // operands each epilogue dereferences unconditionally: refuse, never fault
   if (!p.x || !p.w) return SRMI_ERR_ARG;
-  if (p.gx_s) return SRMI_ERR_ARG;  // (du formed from g: the fused backward launch only)
+  if (p.gx.rec) return SRMI_ERR_ARG;  // (du formed from g: the fused backward launch only)
   if (epi == EPI_DG_ACC_CA && (!p.r1 || !p.aux || !p.part || p.yb || p.r2 || p.r3 || !p.yf || p.r1b))
     return SRMI_ERR_ARG;
   if (epi == EPI_DG_ACC_CA16 && (!p.r1b || !p.aux || !p.part || !p.yb || p.r1 || p.r2 || p.r3 || p.yf || p.f32))

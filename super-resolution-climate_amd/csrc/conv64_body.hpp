@@ -4,6 +4,7 @@
 #pragma once
 #include <type_traits>
 
+#include "ca_bwd.hpp"
 #include "ca_scale.hpp"
 
 #include "common.hpp"
@@ -1021,35 +1022,37 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     for (int m = 0; m < NGW; ++m)
       if (wv_s + NW * m < NGRP) group_dma_one(gidx, m);
   };
-  // (DG_RELUMASK with gx_s: x is the gradient stream g) du = bf16(g s + dm / HW) formed in
-  // place on the wave's own DMA pieces of a group once they landed, before the barrier that
-  // publishes them; the padding (zero page) stays zero.  A lane's 16 B are the channels
-  // 8 cc .. 8 cc + 7 of its pixel in every piece (the swizzle (lane & 7) ^ (q & 7), q = 8 i +
-  // lane / 8)
-  [[maybe_unused]] const bool gx = EPI == EPI_DG_RELUMASK && p.gx_s != nullptr;  // (uniform)
+  // (DG_RELUMASK with p.gx: x is the gradient stream g) the image's CALayer backward MLP in
+  // the prologue (ca_bwd.hpp; its operands issued behind the DMA, the first run of the image
+  // writes the record) or its s and dm read, then du = bf16(g s + dm / HW) formed in place on
+  // the wave's own DMA pieces of a group once they landed, before the barrier that publishes
+  // them; the padding (zero page) stays zero.  A lane's 16 B are the channels 8 cc .. 8 cc + 7
+  // of its pixel in every piece (the swizzle (lane & 7) ^ (q & 7), q = 8 i + lane / 8)
+  [[maybe_unused]] const bool gx = EPI == EPI_DG_RELUMASK && p.gx.rec != nullptr;  // (uniform)
   [[maybe_unused]] float gxs[8], gxm[8];
-  if constexpr (EPI == EPI_DG_RELUMASK) {
-    if (gx) {
-      const int cc = (lane & 7) ^ (lane >> 3);
-      const float* sp = p.gx_s + (size_t)n * p.gx_s_stride + cc * 8;
-      const float* mp = p.gx_m + (size_t)n * 64 + cc * 8;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        gxs[i] = sp[i];
-        gxm[i] = mp[i] * p.gx_inv_hw;
-      }
-    }
-  }
+  [[maybe_unused]] CaBwdPre cbq;
+  auto gx_ok = [&](int gidx, int m) __attribute__((always_inline)) -> bool {
+    const int y0 = 4 * gidx - 3;
+    return wv_s + NW * m < NGRP && ((okx >> m) & 1u) && y0 + lrr[m] >= 0 && y0 + lrr[m] < p.H;
+  };
+  auto gx_ptr = [&](int gidx, int m) __attribute__((always_inline)) -> uint4* {
+    return reinterpret_cast<uint4*>(ring + ((gidx % 3) * 4 * (TW + 2)) * 128 + (wv_s + NW * m) * 1024 + lane * 16);
+  };
   auto gx_piece = [&](int gidx, int m) __attribute__((always_inline)) {
-    const int slot = gidx % 3, y0 = 4 * gidx - 3, i = wv_s + NW * m;
-    if (i < NGRP && ((okx >> m) & 1u) && y0 + lrr[m] >= 0 && y0 + lrr[m] < p.H) {
-      uint4* q = reinterpret_cast<uint4*>(ring + (slot * 4 * (TW + 2)) * 128 + i * 1024 + lane * 16);
+    if (gx_ok(gidx, m)) {
+      uint4* q = gx_ptr(gidx, m);
       *q = du_from_g8(*q, gxs, gxm);
     }
   };
+  // a group's pieces: every read first, then the arithmetic and the writes
   auto gx_group = [&](int gidx) __attribute__((always_inline)) {
+    uint4 v[NGW];
 #pragma unroll
-    for (int m = 0; m < NGW; ++m) gx_piece(gidx, m);
+    for (int m = 0; m < NGW; ++m)
+      if (gx_ok(gidx, m)) v[m] = *gx_ptr(gidx, m);
+#pragma unroll
+    for (int m = 0; m < NGW; ++m)
+      if (gx_ok(gidx, m)) *gx_ptr(gidx, m) = du_from_g8(v[m], gxs, gxm);
   };
 
   // channel of accumulator row (c, r) of this lane, and the lane's channel bases
@@ -1073,11 +1076,39 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
     }
     group_dma(k0);
     group_dma(k0 + 1);
+    [[maybe_unused]] const int cc = (lane & 7) ^ (lane >> 3);
+    if constexpr (EPI == EPI_DG_RELUMASK) {
+      if (gx) {
+        if (p.gx.mlp) {
+          if (tid < 256) ca_bwd_load(p.gx, n, tid, cbq);
+        } else {
+          const float* sp = p.gx.rec + (size_t)n * (128 + p.gx.CR) + 64 + p.gx.CR + cc * 8;
+          const float* mp = p.gx.brec + (size_t)p.gx.N * (128 + p.gx.CR) + (size_t)n * 64 + cc * 8;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            gxs[i] = sp[i];
+            gxm[i] = mp[i] * p.gx.inv_hw;
+          }
+        }
+      }
+    }
     wait_vm<0>();
     if constexpr (EPI == EPI_DG_RELUMASK) {
       if (gx) {
+        STAMP(32);
+        if (p.gx.mlp) {
+          float* sm = reinterpret_cast<float*>(smem + S::TOTAL);
+          ca_bwd_mlp(p.gx, n, tid < 256 ? tid : -1, cbq, sm, ry == 0 && sx == 0 && cb == 0 && !tail_part);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            gxs[i] = sm[kCaBwdS + cc * 8 + i];
+            gxm[i] = sm[kCaBwdDm + cc * 8 + i] * p.gx.inv_hw;
+          }
+        }
+        STAMP(33);
         gx_group(k0);
         gx_group(k0 + 1);
+        STAMP(34);
       }
     }
   }
@@ -1320,6 +1351,7 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
       for (int j = 0; j < NCT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (PREV) zero_ps();
     bf16x8 A[kFragBuf][NCT], B[kFragBuf][NPT];
+    [[maybe_unused]] uint4 gxv[NGW];  // (gx) group k+2's pieces, read one K-step ahead
     auto load_step = [&](int st, bf16x8 (&a)[NCT], bf16x8 (&b)[NPT]) __attribute__((always_inline)) {
       const int tap = st >> 1, kk = st & 1, ky = tap / 3, kx = tap % 3;
 #pragma unroll
@@ -1368,15 +1400,20 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
         if (st == 17 && red_store) part_store(kImm ? k - 1 : k - 2);
       if constexpr (EPI == EPI_DG_RELUMASK) {
         // du of group k+2 (gx), one DMA piece per K-step behind that step's MFMAs over the
-        // strip's last K-steps: the pieces (issued at K-steps 0-3) have landed once only
-        // the deferred stores of K-steps ES.. may still be in flight behind them
+        // strip's last K-steps, each piece read one K-step ahead: the pieces (issued at
+        // K-steps 0-3) have landed once only the deferred stores of K-steps ES.. may still
+        // be in flight behind them
         constexpr int GXS = 18 - NGW;
-        if (SRMI_GX_INLOOP && gx && pf && st >= GXS) {
-          if (st == GXS) {
+        if (SRMI_GX_INLOOP && gx && pf && st >= GXS - 1) {
+          if (st == GXS - 1) {
             if constexpr (PREV) wait_vm<NPT>();
             else wait_vm<0>();
+            if (gx_ok(k + 2, 0)) gxv[0] = *gx_ptr(k + 2, 0);
+          } else {
+            const int m = st - GXS;
+            if (m + 1 < NGW && gx_ok(k + 2, m + 1)) gxv[m + 1 < NGW ? m + 1 : 0] = *gx_ptr(k + 2, m + 1);
+            if (gx_ok(k + 2, m)) *gx_ptr(k + 2, m) = du_from_g8(gxv[m], gxs, gxm);
           }
-          gx_piece(k + 2, st - GXS);
         }
       }
       if constexpr (LAST && NLD > 0) {

@@ -202,8 +202,13 @@ struct srmi_engine {
   size_t slab_floats, bslab_floats;
   // RCAB filter-gradient slabs: [RCAB parity][conv2, conv1] (the reduction of RCAB
   // i runs in RCAB i+1's CA-backward launch, while RCAB i+1 writes the other parity)
-  float *slab_r[2][2] = {}, *bslab_r[2][2] = {};
+  // the RCAB filter gradients' slab sets of one residual group: set (b, c) = RCAB b's conv2
+  // (c = 0) / conv1 (c = 1) filter gradient, b = 1 .. nblocks; (0, 0) the group tail's.  One
+  // per launch, so the reductions can wait for the group's end (one launch for all)
+  std::vector<float*> slab_sets, bslab_sets;
   size_t slab_r_floats = 0, bslab_r_floats = 0;
+  float* slab_r(int b, int c) const { return slab_sets[(size_t)b * 2 + c]; }
+  float* bslab_r(int b, int c) const { return bslab_sets[(size_t)b * 2 + c]; }
   float* lpart;
   int lpart_n;
   float* zeros;  // 256 zero bytes (DMA padding source)
@@ -333,11 +338,14 @@ static size_t carve(srmi_engine* e, char* base) {
                               (e->w % 48 == 0 ? e->w / 48 : 1));
       e->slab_r_floats = ns * 64 * 576;
       e->bslab_r_floats = ns * 64;
-      for (int q = 0; q < 2; ++q)
-        for (int c = 0; c < 2; ++c) {
-          e->slab_r[q][c] = cv.take<float>(e->slab_r_floats);
-          e->bslab_r[q][c] = cv.take<float>(e->bslab_r_floats);
-        }
+      const int nsets = (P.cfg.nblocks + 1) * 2;
+      e->slab_sets.assign(nsets, nullptr);
+      e->bslab_sets.assign(nsets, nullptr);
+      for (int i = 0; i < nsets; ++i) {
+        if (i == 1) continue;  // (the group tail has one filter gradient)
+        e->slab_sets[i] = cv.take<float>(e->slab_r_floats);
+        e->bslab_sets[i] = cv.take<float>(e->bslab_r_floats);
+      }
     }
   }
   e->packs = act(P.pack_elems);
@@ -767,23 +775,29 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
       gRb = sw ? e->GBb : e->GAb;
       ghb = sw ? e->GAb : e->GBb;
       if (stage < s_lo || stage > s_hi) continue;
-      int it = (nl - 1 - g) * nb;  // RCAB counter (slab-set parity)
       const ConvRef& gt = P.group_tail[g];
+      // the filter-gradient reductions: collected for one launch at the group's end (or, with
+      // the CA backward's MLP as a launch of its own (SRMI_F2_MLP 0), riding in that launch)
       ReduceSet prev2{}, prev1{};
       bool have_prev = false;
+      std::vector<ReduceSet> group_sets;
+      auto defer_prev = [&]() {
+        if (!have_prev) return;
+        if (prev2.gw || prev2.gb) group_sets.push_back(prev2);
+        if (prev1.gw || prev1.gb) group_sets.push_back(prev1);
+        have_prev = false;
+      };
       // group tail: its dgrad (the bf16 stream's start, with the CA sums of RCAB nb) and its
-      // filter gradient as one fused launch, like the RCABs' (into the slab set of the
-      // parity RCAB nb does not use; the reduction rides in RCAB nb's CA-backward launch),
-      // else (exact fp32, unfusable shapes) the two launches and the reduction in turn
+      // filter gradient as one fused launch, like the RCABs' (slab set (0, 0), reduced with the
+      // RCABs'), else (exact fp32, unfusable shapes) the two launches and the reduction in turn
       {
         int epi = EPI_DG_ACC;
         const ConvParams cp = dgrad_params(e, gt, gRb, n, h, w, &epi, g16 ? ghb : nullptr, g16 ? nullptr : ghf,
                                            nullptr, nullptr, nullptr, e->Um(g, nb), e->pacc, 1.f);
         WgradParams wp{};
-        const int qt = (it & 1) ^ 1;
         if (g16)
-          RC(wgrad_params(e, gt, e->hb(g, nb), gRb, n, h, w, grads, true, 1.f, rs1, e->slab_r[qt][0],
-                          e->bslab_r[qt][0], e->slab_r_floats, e->bslab_r_floats, &wp, &prev2));
+          RC(wgrad_params(e, gt, e->hb(g, nb), gRb, n, h, w, grads, true, 1.f, rs1, e->slab_r(0, 0),
+                          e->bslab_r(0, 0), e->slab_r_floats, e->bslab_r_floats, &wp, &prev2));
         if (g16 && rcab_bwd_fusable(cp, wp)) {
           RC(dgrad_with_wgrad(e, cp, epi, wp, 1, st));
           prev1 = ReduceSet{};  // (no second reduction: gw = gb = null)
@@ -796,7 +810,6 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
       }
       for (int b = nb; b >= 1; --b) {
         const RCABRef& r = P.groups[g][b - 1];
-        const int q = it++ & 1;
         bf16_t* du = e->DU;
         bf16_t* dz = e->DZ;
         ReduceSet red2, red1;
@@ -804,24 +817,32 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         int epi = EPI_DG_RELUMASK;
         ConvParams cp = dgrad_params(e, r.c2, du, n, h, w, &epi, dz, nullptr, nullptr, nullptr, nullptr, e->Tm(g, b),
                                      nullptr, 1.f);
-        RC(wgrad_params(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, rs2, e->slab_r[q][0], e->bslab_r[q][0],
+        RC(wgrad_params(e, r.c2, e->Tm(g, b), du, n, h, w, grads, false, 1.f, rs2, e->slab_r(b, 0), e->bslab_r(b, 0),
                         e->slab_r_floats, e->bslab_r_floats, &wp, &red2, kSlab16));
-        // du = bf16(g s + dm / HW) formed by the fused conv2 backward from the bf16 stream
-        // on its input rings (the CA backward then runs its MLP only), or written by the
-        // CA backward and read back (SRMI_FLAG_DU_PASS, exact fp32, unfusable shapes)
+        // The CALayer backward inside the fused conv2 backward (both its roles run the
+        // image's MLP in their prologue and form du = bf16(g s + dm / HW) from the bf16
+        // stream on their input rings; ca_bwd.hpp), or as a launch of its own writing du
+        // (SRMI_FLAG_DU_PASS, exact fp32, unfusable shapes) that the conv2 backward reads
         const bool du_fused = g16 && !(P.cfg.flags & SRMI_FLAG_DU_PASS) && rcab_bwd_du_from_g() &&
                               epi == EPI_DG_RELUMASK && rcab_bwd_fusable(cp, wp);
         if (du_fused) {
-          const int CR = 64 / R;
           cp.x = wp.dy = ghb;
-          cp.gx_s = wp.gx_s = e->recp(g, b) + 64 + CR;  // s in the forward record m | z1 | s
-          cp.gx_s_stride = wp.gx_s_stride = 128 + CR;
-          cp.gx_m = wp.gx_m = e->brecp(g, b) + (size_t)n * (128 + CR);  // dm [n][64] after the records
-          cp.gx_inv_hw = wp.gx_inv_hw = 1.f / (float)HW;
+          cp.gx = wp.gx = CaBwdIn{e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, 64 / R,
+                                  e->brecp(g, b), n, 1.f / (float)HW, SRMI_F2_MLP};
+          if (SRMI_F2_MLP) {
+            defer_prev();
+          } else {  // the MLP launch (brec, dm), the previous pair's reductions riding in it
+            RC(ca_bwd_du_launch(ghb, 1, e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R,
+                                nullptr, e->brecp(g, b), 0, st, have_prev ? &prev2 : nullptr,
+                                have_prev ? &prev1 : nullptr));
+            have_prev = false;
+          }
+        } else {  // (its reductions, too, at the group's end: the same sums as the default path's)
+          defer_prev();
+          RC(ca_bwd_du_launch(g16 ? static_cast<const void*>(ghb) : ghf, g16, e->pacc, nstrips, e->recp(g, b),
+                              prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du, e->brecp(g, b), e->f32, st, nullptr,
+                              nullptr));
         }
-        RC(ca_bwd_du_launch(g16 ? static_cast<const void*>(ghb) : ghf, g16, e->pacc, nstrips, e->recp(g, b),
-                            prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du_fused ? nullptr : du, e->brecp(g, b),
-                            e->f32, st, have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
         RC(dgrad_with_wgrad(e, cp, epi, wp, 2, st));
         const bool last = (b == 1);
         epi = EPI_DG_ACC;
@@ -835,14 +856,15 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
           cp = dgrad_params(e, r.c1, dz, n, h, w, &epi, last ? ghb : nullptr, ghf, ghf, last ? gRf : nullptr,
                             (last && g == 0) ? e->dRESf : nullptr, last ? nullptr : e->Um(g, b - 1),
                             last ? nullptr : e->pacc, 1.f);
-        RC(wgrad_params(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, rs1, e->slab_r[q][1],
-                        e->bslab_r[q][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red1, kSlab16));
+        RC(wgrad_params(e, r.c1, e->hb(g, b - 1), dz, n, h, w, grads, true, 1.f, rs1, e->slab_r(b, 1),
+                        e->bslab_r(b, 1), e->slab_r_floats, e->bslab_r_floats, &wp, &red1, kSlab16));
         RC(dgrad_with_wgrad(e, cp, epi, wp, 1, st));
         prev2 = red2;
         prev1 = red1;
         have_prev = true;
       }
-      RC(wgrad_reduce2_launch(prev2, prev1, st));
+      defer_prev();
+      if (!group_sets.empty()) RC(wgrad_reduce_sets_launch(group_sets.data(), (int)group_sets.size(), st));
       RC(ca_param_grads_batched_launch(e->recp(g, 1), e->brecp(g, 1), nb, n, e->N, 64, R, e->d_caoffs + (size_t)g * nb * 5,
                                        grads, st));
       // the group's gradients are final here (one stream): the hook for a bucketed
@@ -1003,15 +1025,15 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
     cp = dgrad_params(e, r.c2, e->DU, n, h, w, &epi, e->DZ, nullptr, nullptr, nullptr, nullptr, e->Tm(0, b), nullptr,
                       1.f);
     RC(wgrad_params(e, r.c2, e->Tm(0, b), e->DU, n, h, w, grads, false, 1.f, rcab_row_splits(e, n, 2),
-                    e->slab_r[0][0], e->bslab_r[0][0], e->slab_r_floats, e->bslab_r_floats, &wp, &red, kSlab16));
-    // (as backward_impl: du formed from the bf16 stream in the fused launch)
+                    e->slab_r(b, 0), e->bslab_r(b, 0), e->slab_r_floats, e->bslab_r_floats, &wp, &red, kSlab16));
+    // (as backward_impl: the CA backward and du inside the fused launch; its record and dm
+    //  go to brec, which the engine's next backward rewrites)
     if (!e->f32 && !(e->P.cfg.flags & SRMI_FLAG_DU_PASS) && rcab_bwd_du_from_g() && rcab_bwd_fusable(cp, wp)) {
-      const int CR = 64 / e->P.cfg.reduction;
+      if (!e->probe_prm) return SRMI_ERR_ARG;
       cp.x = wp.dy = e->GBb;
-      cp.gx_s = wp.gx_s = e->recp(0, b) + 64 + CR;
-      cp.gx_s_stride = wp.gx_s_stride = 128 + CR;
-      cp.gx_m = wp.gx_m = e->brecp(0, b) + (size_t)n * (128 + CR);
-      cp.gx_inv_hw = wp.gx_inv_hw = 1.f / (float)(h * w);
+      cp.gx = wp.gx = CaBwdIn{e->pacc, conv3x3_nstrips(h, w), e->recp(0, b), e->probe_prm + r.ca_w1,
+                              e->probe_prm + r.ca_w2, 64 / e->P.cfg.reduction, e->brecp(0, b), n, 1.f / (float)(h * w),
+                              SRMI_F2_MLP};
     }
   } else {
     const bool last = (b == 1);
@@ -1023,7 +1045,7 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
       cp = dgrad_params(e, r.c1, e->DZ, n, h, w, &epi, last ? e->GAb : nullptr, ghf, ghf, last ? e->GAf : nullptr,
                         nullptr, last ? nullptr : e->Um(0, b - 1), last ? nullptr : e->pacc, 1.f);
     RC(wgrad_params(e, r.c1, e->hb(0, b - 1), e->DZ, n, h, w, grads, true, 1.f, rcab_row_splits(e, n, 1),
-                    e->slab_r[0][1], e->bslab_r[0][1], e->slab_r_floats, e->bslab_r_floats, &wp, &red, kSlab16));
+                    e->slab_r(b, 1), e->bslab_r(b, 1), e->slab_r_floats, e->bslab_r_floats, &wp, &red, kSlab16));
   }
   for (int i = 0; i < reps; ++i) RC(dgrad_with_wgrad(e, cp, epi, wp, which, S_(stream)));
   return 0;

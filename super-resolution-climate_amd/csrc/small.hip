@@ -15,6 +15,7 @@
 #include "common.hpp"
 #include "srmi_internal.hpp"
 #include "wgrad_reduce.hpp"
+#include "ca_bwd.hpp"
 
 namespace srmi {
 
@@ -1383,32 +1384,11 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const TG* __restrict__ g
       wgrad_reduce_body<16>(r1, id - nred);
     return;
   }
-  __shared__ float red[2][128], s[64], dz2[64], dz1[32], dm[64];
+  __shared__ float sm[kCaBwdScratch];
   const int n = blockIdx.y, tid = threadIdx.x;
-  const float* r = rec + (size_t)n * (2 * C + CR);
-  const int j = tid >> 3, pj = tid & 7;
-  const int c4 = tid >> 2, p4 = tid & 3, per = CR / 4;
-  float pa = 0.f;  // G[c] = sum_p g, ds[c] = sum_p g*u (MLP operands first, see ca_fwd_kernel)
-  {  // the strip records: up to 16 issued at once (clamped, unconditional), then summed in
-     // strip order; a plain loop issued them one load and one wait at a time (~0.7 us each)
-    constexpr int KU = 8;
-    float pv[KU];
-    const float* pp = part + (size_t)n * nstrips * (2 * C) + (tid & 127);
-#pragma unroll
-    for (int i = 0; i < KU; ++i) pv[i] = pp[(size_t)min((tid >> 7) + 2 * i, nstrips - 1) * (2 * C)];
-#pragma unroll
-    for (int i = 0; i < KU; ++i)
-      if ((tid >> 7) + 2 * i < nstrips) pa += pv[i];
-    for (int k = (tid >> 7) + 2 * KU; k < nstrips; k += 2) pa += pp[(size_t)k * (2 * C)];
-  }
-  const int jc = min(j, CR - 1);
-  float wa[8], wb[8];  // W2 column slice (dz1 lane group j), W1 column slice (dm lane group c)
-#pragma unroll
-  for (int i = 0; i < 8; ++i) wa[i] = w2[(pj * 8 + i) * CR + jc];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) wb[i] = w1[(p4 * per + min(i, per - 1)) * C + c4];
-  const float zj = r[C + jc];
-  const float svl = r[C + CR + (tid & 63)];
+  const CaBwdIn cb{part, nstrips, rec, w1, w2, CR, brec, N, 1.f / (float)HW};
+  CaBwdPre q;  // the MLP operands first (ca_bwd.hpp), then the stream's loads behind them
+  ca_bwd_load(cb, n, tid, q);
   __builtin_amdgcn_sched_barrier(0);
   const size_t base = (size_t)n * HW * C;
   const size_t nv = (size_t)HW * C / 8;
@@ -1426,46 +1406,9 @@ __global__ void __launch_bounds__(256) ca_bwd_du_kernel(const TG* __restrict__ g
     }
   }
   __builtin_amdgcn_sched_barrier(0);
-  red[tid >> 7][tid & 127] = pa;
-  s[tid & 63] = svl;  // (unconditional: the load cannot sink past the stream loads)
-  lds_barrier();
-  float G = 0.f, sv = 0.f;
-  if (tid < C) {
-    G = red[0][tid] + red[1][tid];
-    const float ds = red[0][C + tid] + red[1][C + tid];
-    sv = s[tid];
-    dz2[tid] = ds * sv * (1.f - sv);
-  }
-  lds_barrier();
-  {  // dz1[j] = relu'(z1[j]) sum_c W2[c][j] dz2[c]
-    float a = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a += wa[i] * dz2[pj * 8 + i];
-    a += __shfl_xor(a, 1, 64);
-    a += __shfl_xor(a, 2, 64);
-    a += __shfl_xor(a, 4, 64);
-    if (j < CR && pj == 0) dz1[j] = (zj > 0.f) ? a : 0.f;
-  }
-  lds_barrier();
-  {  // dm[c] = sum_j W1[j][c] dz1[j]
-    float a = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      if (i < per) a += wb[i] * dz1[p4 * per + i];
-    a += __shfl_xor(a, 1, 64);
-    a += __shfl_xor(a, 2, 64);
-    if (p4 == 0) dm[c4] = a;
-  }
-  lds_barrier();
-  if (blockIdx.x == 0) {
-    float* br = brec + (size_t)n * (2 * C + CR);
-    if (tid < C) {
-      br[tid] = dz2[tid];
-      brec[(size_t)N * (2 * C + CR) + (size_t)n * C + tid] = dm[tid];
-      br[C + CR + tid] = sv * G + dm[tid];  // conv2 bias grad: sum_p du
-    }
-    if (tid < CR) br[C + tid] = dz1[tid];
-  }
+  ca_bwd_mlp(cb, n, tid, q, sm, blockIdx.x == 0);
+  const float* s = sm + kCaBwdS;
+  const float* dm = sm + kCaBwdDm;
   if constexpr (!DU) return;
   const auto rdu = wt_rsrc(du, (uint32_t)((size_t)gridDim.y * HW * C * sizeof(T)));  // lane-contiguous: write-through
 #pragma unroll

@@ -60,6 +60,24 @@ struct CaScale {
   const bf16_t* wimg;  // conv2's packed bf16 filter image (conv1 loads it for the matvec)
 };
 
+// The CALayer backward of an RCAB (reference network.py:31-47, 61-64) as the fused conv2
+// backward runs it (ca_bwd.hpp): the MLP backward of each image from the producer's
+// per-strip sums, then du = bf16(g s[c] + dm[c] / HW) formed from the bf16 gradient stream
+// g on the launch's input rings in LDS (null rec = off: x / dy is read as it is)
+struct CaBwdIn {
+  const float* part;   // sum_p g | sum_p g u per strip [N][nstrips][128] (F1's CA sums)
+  int nstrips;
+  const float* rec;    // the forward record m | z1 | s [N][128 + CR]
+  const float* w1;     // conv_du.0 weight [CR][64]
+  const float* w2;     // conv_du.2 weight [64][CR]
+  int CR;
+  float* brec;         // out, one workgroup per image: dz2 | dz1 | dbconv2 [N][128 + CR], then dm [N][64]
+  int N;
+  float inv_hw;        // 1 / (H W)
+  int mlp;             // 1: every workgroup runs its image's MLP (ca_bwd_mlp; the first dgrad run
+                       // of the image writes brec); 0: s and dm are read (rec, brec: an MLP launch ran)
+};
+
 struct ConvParams {
   const bf16_t* x;     // input (logical NHWC [N][H][W][Cin])
   const bf16_t* w;     // packed filters [Cin/64][9][Cout][64]
@@ -93,13 +111,8 @@ struct ConvParams {
   CaScale cas;
   int cas_on;
   // (EPI_DG_RELUMASK, the deferred 8-wave body) x is the bf16 gradient stream g and the
-  // conv reads du = bf16(g s[c] + dm[c] / HW), the CALayer backward's du (ca_bwd_du_kernel),
-  // formed on the input ring in LDS: gx_s = s of image n at gx_s + n * gx_s_stride (the
-  // forward record), gx_m = dm [N][64]; null = x is read as it is
-  const float* gx_s;
-  int gx_s_stride;
-  const float* gx_m;
-  float gx_inv_hw;
+  // conv reads the CALayer backward's du formed from it on the input ring (CaBwdIn)
+  CaBwdIn gx;
 };
 
 void conv3x3_set_debug_stamps(unsigned long long* buf);
@@ -136,11 +149,8 @@ struct WgradParams {
   int slab16;          // (wgrad48 body) weight slabs stored as bf16 at `slab` (the RCAB filter
                        // gradients of the bf16 engine: half the slab bytes); bias slabs fp32
   // (wgrad48 body, IN_PLAIN, Cout == 64) dy is g and the filter gradient takes du formed
-  // from it in LDS, as ConvParams.gx_* (null = dy read as it is)
-  const float* gx_s;
-  int gx_s_stride;
-  const float* gx_m;
-  float gx_inv_hw;
+  // from it in LDS, as ConvParams.gx
+  CaBwdIn gx;
 };
 void wgrad3x3_set_debug_stamps(unsigned long long* buf);
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st);  // dispatches p.f32
@@ -153,6 +163,8 @@ int wgrad3x3_slab_layout(const WgradParams& p);
 // ps != 0 un-permutes the packed PixelShuffle channel order (c'' = 64q + c -> 4c + q)
 
 int wgrad_reduce2_launch(const ReduceSet& r0, const ReduceSet& r1, hipStream_t st);
+// n independent slab reductions (equal Cout) in one launch (blockIdx.y selects the set)
+int wgrad_reduce_sets_launch(const ReduceSet* sets, int n, hipStream_t st);
 // fused RCAB backward launch: dgrad conv (epi RELUMASK / DG_ACC_CA / DG_ACC, its runs
 // sized for conv_cus CUs) beside the filter gradient wp of the same conv (wgrad48)
 int rcab_bwd_fusable(const ConvParams& cp, const WgradParams& wp);

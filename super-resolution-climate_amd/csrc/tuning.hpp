@@ -40,6 +40,13 @@
 #define SRMI_GX_INLOOP 1
 #endif
 
+// the CALayer backward with du formed in the fused conv2 backward: its MLP in that launch's
+// prologue (every workgroup, 1; the filter-gradient reductions then wait for the group's end)
+// or in a small launch of its own before it (0; the reductions ride in it)
+#ifndef SRMI_F2_MLP
+#define SRMI_F2_MLP 1
+#endif
+
 // the inference conv2's h' = h + s u with u rounded to bf16 (as the training conv2 and
 // the round-3 three-launch inference did; staged once as bf16, one barrier), 0 = fp32 u
 // (staged as fp32 in two halves, four barriers)

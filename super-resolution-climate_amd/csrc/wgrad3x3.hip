@@ -21,6 +21,7 @@
 // in a fixed order (deterministic) into the torch-layout gradient.
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "common.hpp"
 #include "conv64_body.hpp"
@@ -425,31 +426,40 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   // them (as the dgrad's input ring, conv64_body_defer); s and dm / HW of the image in an
   // LDS table past the rings.  A lane's 16 B of group g are channels 8 c .. 8 c + 7, c =
   // cl0 (g even) / cl1 (g odd)
-  const bool gx = p.gx_s != nullptr;  // (uniform)
+  const bool gx = p.gx.rec != nullptr;  // (uniform)
   float* const gxt = reinterpret_cast<float*>(smem + LDS);  // [s 64][dmh 64]
   auto gx_pair = [&](int P) __attribute__((always_inline)) {
+    // (a wave's three dY groups of a pair are g = k % 6 of one parity: one channel chunk c)
+    static_assert(GD % 2 == 0, "g = k - rr GD keeps the parity of k = wave + 4 m");
+    const int c = (wave_s & 1) ? cl1 : cl0;
+    float sv[8], mv[8];
+    const float4 s0 = *reinterpret_cast<const float4*>(gxt + c * 8);
+    const float4 s1 = *reinterpret_cast<const float4*>(gxt + c * 8 + 4);
+    const float4 m0 = *reinterpret_cast<const float4*>(gxt + 64 + c * 8);
+    const float4 m1 = *reinterpret_cast<const float4*>(gxt + 64 + c * 8 + 4);
+    sv[0] = s0.x; sv[1] = s0.y; sv[2] = s0.z; sv[3] = s0.w; sv[4] = s1.x; sv[5] = s1.y; sv[6] = s1.z; sv[7] = s1.w;
+    mv[0] = m0.x; mv[1] = m0.y; mv[2] = m0.z; mv[3] = m0.w; mv[4] = m1.x; mv[5] = m1.y; mv[6] = m1.z; mv[7] = m1.w;
+    uint4* q[3];
+    uint4 v[3];
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
       const int k = wave_s + 4 * m, rr = k / GD, g = k - rr * GD;
-      const int c = (g & 1) ? cl1 : cl0;
-      float sv[8], mv[8];
-      const float4 s0 = *reinterpret_cast<const float4*>(gxt + c * 8);
-      const float4 s1 = *reinterpret_cast<const float4*>(gxt + c * 8 + 4);
-      const float4 m0 = *reinterpret_cast<const float4*>(gxt + 64 + c * 8);
-      const float4 m1 = *reinterpret_cast<const float4*>(gxt + 64 + c * 8 + 4);
-      sv[0] = s0.x; sv[1] = s0.y; sv[2] = s0.z; sv[3] = s0.w; sv[4] = s1.x; sv[5] = s1.y; sv[6] = s1.z; sv[7] = s1.w;
-      mv[0] = m0.x; mv[1] = m0.y; mv[2] = m0.z; mv[3] = m0.w; mv[4] = m1.x; mv[5] = m1.y; mv[6] = m1.z; mv[7] = m1.w;
-      uint4* q = reinterpret_cast<uint4*>(smem + ((2 * P + rr) & (RD - 1)) * DSLOT + g * 1024 + lane * 16);
-      *q = du_from_g8(*q, sv, mv);
+      q[m] = reinterpret_cast<uint4*>(smem + ((2 * P + rr) & (RD - 1)) * DSLOT + g * 1024 + lane * 16);
+      v[m] = *q[m];
     }
+#pragma unroll
+    for (int m = 0; m < 3; ++m) *q[m] = du_from_g8(v[m], sv, mv);
   };
-  if (gx) {  // (8 waves: by waves 4 and 5, which issue no DMA, so the wait for these loads
-             //  does not drain the prologue's groups)
-    const int tt = NW == 8 ? tid - 256 : tid;
-    if (tt >= 0 && tt < 64) {
-      gxt[tt] = p.gx_s[(size_t)n * p.gx_s_stride + tt];
-    } else if (tt >= 64 && tt < 128) {
-      gxt[tt] = p.gx_m[(size_t)n * 64 + tt - 64] * p.gx_inv_hw;
+  // the image's CALayer backward MLP (ca_bwd.hpp) by waves 4-7 (8 waves), which issue no
+  // DMA: the compiler's wait for its operands then drains no DMA group of the prologue
+  const int mt = NW == 8 ? tid - 256 : tid;  // MLP thread
+  CaBwdPre cbq;
+  if (gx && mt >= 0) {
+    if (p.gx.mlp) {
+      ca_bwd_load(p.gx, n, mt, cbq);
+    } else if (mt < 128) {  // (s and dm read: an MLP launch ran)
+      gxt[mt] = mt < 64 ? p.gx.rec[(size_t)n * (128 + p.gx.CR) + 64 + p.gx.CR + mt]
+                        : p.gx.brec[(size_t)p.gx.N * (128 + p.gx.CR) + (size_t)n * 64 + mt - 64] * p.gx.inv_hw;
     }
   }
 
@@ -460,7 +470,14 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
       if (wave_s + 4 * m < 2 * GX) dma(0, wave_s + 4 * m, true);
     for (int P = 0; P < PF && P < np; ++P) dma_pair_part(P, 0, 7);
   }
-  if (gx) __syncthreads();  // (the table)
+  if (gx) {
+    if (p.gx.mlp) {
+      float* sm = reinterpret_cast<float*>(smem + LDS + 512);
+      ca_bwd_mlp(p.gx, n, mt, cbq, sm, false);
+      if (mt >= 0 && mt < 128) gxt[mt] = mt < 64 ? sm[kCaBwdS + mt] : sm[kCaBwdDm + mt - 64] * p.gx.inv_hw;
+    }
+    __syncthreads();  // (the table)
+  }
   wait_groups(min(PF, np) - 1, 0);
   if constexpr (kMain) {
     if (gx) gx_pair(0);
@@ -691,17 +708,21 @@ int rcab_bwd_launch(const ConvParams& cp, int epi, int conv_cus, const WgradPara
   if (!rcab_bwd_fusable(cp, wp)) return SRMI_ERR_SHAPE;
   // du formed from the gradient stream g (gx_*): both roles together, in the deferred
   // ReLU-mask dgrad (conv64_body_defer) beside a 64-channel filter gradient
-  if ((cp.gx_s != nullptr) != (wp.gx_s != nullptr) || (cp.gx_m != nullptr) != (wp.gx_m != nullptr) ||
-      (cp.gx_s != nullptr) != (cp.gx_m != nullptr))
+  if ((cp.gx.rec != nullptr) != (wp.gx.rec != nullptr) ||
+      (cp.gx.rec && std::memcmp(&cp.gx, &wp.gx, sizeof(CaBwdIn)) != 0))
     return SRMI_ERR_ARG;
-  if (cp.gx_s && (epi != EPI_DG_RELUMASK || !conv64_defers<EPI_DG_RELUMASK>() || cp.x != wp.dy))
+  if (cp.gx.rec && (epi != EPI_DG_RELUMASK || !conv64_defers<EPI_DG_RELUMASK>() || cp.x != wp.dy ||
+                    !cp.gx.part || !cp.gx.w1 || !cp.gx.w2 || !cp.gx.brec || cp.gx.CR < 4 || cp.gx.CR > 32 ||
+                    cp.gx.CR % 4 || cp.Cin != 64))
     return SRMI_ERR_ARG;
   if (!slab_range_ok(wp, wp.N * wp.row_splits)) return SRMI_ERR_SHAPE;
   const int run_len = conv64_run_len(cp, 48, conv_cus);
   const int nconv = conv64_blocks(cp, 48, run_len);
   const int nwg = wp.N * wp.row_splits * (wp.Cout / 64);
-  const int lds = Conv2Smem<48>::TOTAL > v4::LDS ? Conv2Smem<48>::TOTAL : v4::LDS;
-  static_assert(Conv2Smem<48>::TOTAL >= v4::LDS + 512, "the filter gradient's du table (gx) past its rings");
+  // (+ the CA backward MLP's scratch of the dgrad runs past their body's LDS, ca_bwd.hpp;
+  //  the filter gradient's du table and MLP scratch sit past its rings)
+  const int lds = (Conv2Smem<48>::TOTAL > v4::LDS ? Conv2Smem<48>::TOTAL : v4::LDS) + (cp.gx.rec ? kCaBwdScratch * 4 : 0);
+  static_assert(Conv2Smem<48>::TOTAL >= v4::LDS + 512 + kCaBwdScratch * 4, "the filter gradient's du table and MLP scratch");
   ConvParams c = cp;
   c.stamps = conv3x3_stamps_for(epi);  // (null in production; the dgrad runs' phase stamps in diagnostic builds)
   WgradParams w = wp;
@@ -766,7 +787,7 @@ int wgrad3x3_nslabs(const WgradParams& p) { return p.N * p.row_splits * (use_wgr
 int wgrad3x3_slab_layout(const WgradParams& p) { return use_wgrad48(p) ? 1 : 0; }
 
 int wgrad3x3_launch(const WgradParams& p, hipStream_t st) {
-  if (p.gx_s) return SRMI_ERR_ARG;  // (du formed from g: the fused backward launch only)
+  if (p.gx.rec) return SRMI_ERR_ARG;  // (du formed from g: the fused backward launch only)
   if (p.f32) return wgrad_f32_launch(p, st);
   if (p.Cout % 64 || p.H % p.row_splits || (p.H / p.row_splits) % 4) return SRMI_ERR_SHAPE;
   if (p.dy_mode == IN_UNSHUF && p.Cout != 256) return SRMI_ERR_SHAPE;
@@ -805,6 +826,30 @@ int wgrad_reduce_launch(const float* slab, const float* bslab, int nslab, int Co
   const ReduceSet r{slab, bslab, nslab, Cout, ps, layout, alpha, gw, gb, slab16};
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(kRedQ * kRedPh), 0, st, r);
   SRMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// up to kRedSets reductions of one launch, passed by value (kernel arguments, no upload)
+constexpr int kRedSets = 42;
+struct ReduceSets {
+  ReduceSet s[kRedSets];
+};
+__global__ void __launch_bounds__(kRedQ * kRedPh) wgrad_reduce_sets_kernel(ReduceSets r) {
+  wgrad_reduce_body<kRedPh>(r.s[blockIdx.y], blockIdx.x);
+}
+
+int wgrad_reduce_sets_launch(const ReduceSet* sets, int n, hipStream_t st) {
+  for (int i0 = 0; i0 < n; i0 += kRedSets) {
+    const int m = std::min(kRedSets, n - i0);
+    ReduceSets r{};
+    for (int i = 0; i < m; ++i) {
+      if (sets[i0 + i].Cout != sets[i0].Cout || sets[i0].Cout % 64) return SRMI_ERR_SHAPE;
+      r.s[i] = sets[i0 + i];
+    }
+    hipLaunchKernelGGL(wgrad_reduce_sets_kernel, dim3(wgrad_reduce_blocks(sets[i0].Cout), m), dim3(kRedQ * kRedPh), 0,
+                       st, r);
+    SRMI_CHECK_LAUNCH();
+  }
   return 0;
 }
 

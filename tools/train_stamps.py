@@ -81,6 +81,10 @@ def main():
             print(f"  {nm:30s} median {np.median(v):8.0f}  p90 {np.percentile(v, 90):8.0f}  "
                   f"share {np.median(v) / np.median(tot):6.3f}")
         row("prologue", body[:, 1] - body[:, 0])
+        if epi == 4 and np.all(body[:, 34]):  # (du from g: the CA backward MLP and the first du groups)
+            row("  start -> DMA landed", body[:, 32] - body[:, 0])
+            row("  CA backward MLP", body[:, 33] - body[:, 32])
+            row("  du of the first two groups", body[:, 34] - body[:, 33])
         if epi == 10:
             for i, nm in enumerate(("  scale: T + border lines", "  scale: barrier 1", "  scale: S_tap + matvec",
                                     "  scale: barrier 2", "  scale: z1 + s", "  scale: barrier 3")):
