@@ -1038,12 +1038,6 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
   auto gx_ptr = [&](int gidx, int m) __attribute__((always_inline)) -> uint4* {
     return reinterpret_cast<uint4*>(ring + ((gidx % 3) * 4 * (TW + 2)) * 128 + (wv_s + NW * m) * 1024 + lane * 16);
   };
-  auto gx_piece = [&](int gidx, int m) __attribute__((always_inline)) {
-    if (gx_ok(gidx, m)) {
-      uint4* q = gx_ptr(gidx, m);
-      *q = du_from_g8(*q, gxs, gxm);
-    }
-  };
   // a group's pieces: every read first, then the arithmetic and the writes
   auto gx_group = [&](int gidx) __attribute__((always_inline)) {
     uint4 v[NGW];
@@ -1404,7 +1398,19 @@ __device__ __forceinline__ void conv64_body_defer(const ConvParams& p, int run_l
         // K-steps 0-3) have landed once only the deferred stores of K-steps ES.. may still
         // be in flight behind them
         constexpr int GXS = 18 - NGW;
-        if (SRMI_GX_INLOOP && gx && pf && st >= GXS - 1) {
+        if (SRMI_GX_INLOOP == 2 && gx && pf && st >= 17 - 2 * NGW) {
+          // (variant: a piece every other K-step from K-step 18 - 2 NGW, each read the step
+          //  before; the wait at 17 - 2 NGW also takes the deferred epilogue's operands)
+          constexpr int G0 = 17 - 2 * NGW;
+          const int m = (st - G0) >> 1;
+          if (st == G0) wait_vm<0>();
+          if (((st - G0) & 1) == 0) {
+            if (gx_ok(k + 2, m)) gxv[m < NGW ? m : 0] = *gx_ptr(k + 2, m);
+          } else if (gx_ok(k + 2, m)) {
+            *gx_ptr(k + 2, m) = du_from_g8(gxv[m < NGW ? m : 0], gxs, gxm);
+          }
+        }
+        if (SRMI_GX_INLOOP == 1 && gx && pf && st >= GXS - 1) {
           if (st == GXS - 1) {
             if constexpr (PREV) wait_vm<NPT>();
             else wait_vm<0>();

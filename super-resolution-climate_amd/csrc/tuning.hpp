@@ -33,11 +33,14 @@
 #define SRMI_F1_DEFER_TAIL 0
 #endif
 
-// du formed from g in the fused conv2 backward (ConvParams / WgradParams gx_*): 1 = behind
-// the MFMAs of the strip's last K-steps (dgrad) / of a pair's first K-step (filter
-// gradient), 0 = after the wait for the pieces, before the barrier that publishes them
+// du formed from g in the fused conv2 backward (ConvParams / WgradParams gx): where the
+// dgrad forms it on group k+2's ring pieces -- 2 = one piece every other K-step from K-step
+// 18 - 2 x pieces, each read the K-step before (profiles/r06_ab_gx_spread.txt: +0.2-0.4 %),
+// 1 = one piece per K-step over the last K-steps, 0 = after the strip's wait for the pieces,
+// before the barrier that publishes them; the filter gradient forms a pair's dY rows behind
+// the MFMAs of the pair before's first K-step (1, 2) or before its barrier (0)
 #ifndef SRMI_GX_INLOOP
-#define SRMI_GX_INLOOP 1
+#define SRMI_GX_INLOOP 2
 #endif
 
 // the CALayer backward with du formed in the fused conv2 backward: its MLP in that launch's

@@ -544,7 +544,7 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
         if constexpr (kMain) {
           // (gx) du of pair j+1 behind K-step 0's MFMAs: in flight may stay pair j+2 and the
           // 3 groups of pair j+PF issued above; the barrier of K-step 1 publishes it
-          if (SRMI_GX_INLOOP && kc == 0 && gx && more) {
+          if (SRMI_GX_INLOOP != 0 && kc == 0 && gx && more) {
             if (j + 2 < np) wait_groups(1, pf ? 3 : 0);
             else wait_groups(0, 0);
             gx_pair(j + 1);

@@ -336,3 +336,24 @@ def test_netspec_batch_norm_rcan_ignored_edsr_refused():
     assert NetSpec.from_parms("rcan", parms) == NetSpec.from_parms("rcan", dict(parms, batch_norm=False))
     with pytest.raises(_lib.SrmiError, match="batch_norm"):
         NetSpec.from_parms("edsr", dict(parms, nblocks=0, scale=8))
+
+
+def test_flag_constants_match_header():
+    """The Python names of srmi_model_config.flags bits are the header's values, and the
+    engine refuses the retired bits (0 and 3) and any unknown bit."""
+    import ctypes as C
+    from srmi import _lib
+    from srmi.engine import NetSpec
+    hdr = open(os.path.join(ROOT, "include", "srmi.h")).read()
+    defs = dict((k, int(v)) for k, v in re.findall(r"#define (SRMI_FLAG_[A-Z_]+) (\d+)", hdr))
+    assert set(defs) == {"SRMI_FLAG_NO_RCAB_INFER", "SRMI_FLAG_CA_PASS", "SRMI_FLAG_DU_PASS"}
+    for k, v in defs.items():
+        assert getattr(_lib, k) == v, k
+    tb = C.c_size_t()
+    for bad in (1, 8, 32):
+        cfg = NetSpec(arch="rcan", nchannels_in=2, nchannels_out=2, nlayers=1, nblocks=2, flags=bad).cstruct(4, 48, 48)
+        with pytest.raises(_lib.SrmiError):
+            _lib.call("srmi_workspace_size", C.byref(cfg), 1, C.byref(tb))
+    cfg = NetSpec(arch="rcan", nchannels_in=2, nchannels_out=2, nlayers=1, nblocks=2,
+                  flags=sum(defs.values())).cstruct(4, 48, 48)
+    _lib.call("srmi_workspace_size", C.byref(cfg), 1, C.byref(tb))
