@@ -151,7 +151,10 @@ int srmi_backward_stages(srmi_engine* e, const float* params, const float* lr, c
  * (+ CA sums) beside conv1's filter gradient; which = 2: the ReLU-mask dgrad of
  * conv2 beside conv2's filter gradient -- on the buffers of the last backward
  * (their contents are overwritten).  RCAN train engines; which = 3: an RCAN
- * inference engine's one-launch RCAB (0, 2) on the buffers of the last forward. */
+ * inference engine's one-launch RCAB (0, 2) on the buffers of the last forward;
+ * which = 4 (nothing launched, reps ignored): 1 if the engine's backward runs the CA
+ * backward inside the fused conv2 backward (du formed from the bf16 gradient stream),
+ * 0 if as a launch of its own (SRMI_FLAG_DU_PASS, exact fp32, unfusable shapes). */
 int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream);
 
 /* RMSE (l2loss, squared=False).  loss4[0] = sum of squares (this rank),

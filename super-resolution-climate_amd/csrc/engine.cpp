@@ -706,6 +706,15 @@ static int forward_impl(srmi_engine* e, const float* prm, const float* lr, float
 // group's gradient all-reduce right behind that group (srmi_backward_stages).
 static int backward_stages(const srmi_engine* e) { return e->P.cfg.arch == SRMI_ARCH_RCAN ? e->P.cfg.nlayers + 2 : 1; }
 
+// The CALayer backward inside the fused conv2 backward (ca_bwd.hpp; SRMI_FLAG_DU_PASS off):
+// the bf16 engine, a fusable 48-wide launch, CR = 64 / reduction in 4 .. 32 and a multiple
+// of 4 (the MLP's thread mapping).  Else the CA backward is a launch of its own.
+static bool du_in_f2(const srmi_engine* e, const ConvParams& cp, const WgradParams& wp, int epi) {
+  const int CR = 64 / e->P.cfg.reduction;
+  return !e->f32 && !(e->P.cfg.flags & SRMI_FLAG_DU_PASS) && rcab_bwd_du_from_g() && epi == EPI_DG_RELUMASK &&
+         rcab_bwd_fusable(cp, wp) && CR % 4 == 0 && CR >= 4 && CR <= 32;
+}
+
 static int backward_impl(srmi_engine* e, const float* prm, const float* lr, const float* sr, const float* hr,
                          const float* loss4, const float* dy, float* grads, void** group_events, hipStream_t st,
                          int s_lo = 0, int s_hi = 1 << 30) {
@@ -823,8 +832,7 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
         // image's MLP in their prologue and form du = bf16(g s + dm / HW) from the bf16
         // stream on their input rings; ca_bwd.hpp), or as a launch of its own writing du
         // (SRMI_FLAG_DU_PASS, exact fp32, unfusable shapes) that the conv2 backward reads
-        const bool du_fused = g16 && !(P.cfg.flags & SRMI_FLAG_DU_PASS) && rcab_bwd_du_from_g() &&
-                              epi == EPI_DG_RELUMASK && rcab_bwd_fusable(cp, wp);
+        const bool du_fused = du_in_f2(e, cp, wp, epi);
         if (du_fused) {
           cp.x = wp.dy = ghb;
           cp.gx = wp.gx = CaBwdIn{e->pacc, nstrips, e->recp(g, b), prm + r.ca_w1, prm + r.ca_w2, 64 / R,
@@ -1009,6 +1017,19 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
                            e->recp(0, 2), S_(stream)));
     return 0;
   }
+  if (which == 4) {  // does the backward form du inside the fused conv2 backward (1) or not (0)
+    if (!e || !e->train || e->P.cfg.arch != SRMI_ARCH_RCAN || e->last_n < 1 || !e->probe_prm) return SRMI_ERR_ARG;
+    const int n = e->last_n, b = e->P.cfg.nblocks >= 2 ? 2 : 1;
+    const RCABRef& r = e->P.groups[0][b - 1];
+    int epi = EPI_DG_RELUMASK;
+    ConvParams cp = dgrad_params(e, r.c2, e->DU, n, e->h, e->w, &epi, e->DZ, nullptr, nullptr, nullptr, nullptr,
+                                 e->Tm(0, b), nullptr, 1.f);
+    WgradParams wp;
+    ReduceSet red;
+    RC(wgrad_params(e, r.c2, e->Tm(0, b), e->DU, n, e->h, e->w, e->slab, false, 1.f, rcab_row_splits(e, n, 2),
+                    e->slab_r(b, 0), e->bslab_r(b, 0), e->slab_r_floats, e->bslab_r_floats, &wp, &red, kSlab16));
+    return du_in_f2(e, cp, wp, epi) ? 1 : 0;
+  }
   if (!e || !e->train || e->P.cfg.arch != SRMI_ARCH_RCAN || e->last_n < 1 || reps < 1) return SRMI_ERR_ARG;
   if (which != 1 && which != 2) return SRMI_ERR_ARG;
   const int n = e->last_n, h = e->h, w = e->w;
@@ -1028,8 +1049,7 @@ int srmi_engine_probe(srmi_engine* e, int which, int reps, void* stream) {
                     e->slab_r(b, 0), e->bslab_r(b, 0), e->slab_r_floats, e->bslab_r_floats, &wp, &red, kSlab16));
     // (as backward_impl: the CA backward and du inside the fused launch; its record and dm
     //  go to brec, which the engine's next backward rewrites)
-    if (!e->f32 && !(e->P.cfg.flags & SRMI_FLAG_DU_PASS) && rcab_bwd_du_from_g() && rcab_bwd_fusable(cp, wp)) {
-      if (!e->probe_prm) return SRMI_ERR_ARG;
+    if (e->probe_prm && du_in_f2(e, cp, wp, epi)) {
       cp.x = wp.dy = e->GBb;
       cp.gx = wp.gx = CaBwdIn{e->pacc, conv3x3_nstrips(h, w), e->recp(0, b), e->probe_prm + r.ca_w1,
                               e->probe_prm + r.ca_w2, 64 / e->P.cfg.reduction, e->brecp(0, b), n, 1.f / (float)(h * w),

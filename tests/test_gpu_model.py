@@ -340,6 +340,7 @@ def _engine_variants_agree(lr_hw, flags, grad_tol, fwd_tol=None):
         rb = rel_l2(gb[off:off + n].view(shape), g_ref[name])
         assert ra <= bound[name] and rb <= bound[name], (name, ra, rb, bound[name])
         assert rel_l2(ga[off:off + n], gb[off:off + n]) < 3e-2, name
+    return trs
 
 
 @pytest.mark.parametrize("lr_hw", [(48, 48), (32, 48), (8, 48), (24, 96)])
@@ -367,8 +368,12 @@ def test_du_from_g_matches_du_pass(lr_hw):
     rounding, so the whole step is bit-identical.  Three tile heights change the runs'
     and row bands' boundaries (and the image-border halo rows the transform must leave
     zero); the 96-wide tiles take the unfused launches in both engines."""
-    from srmi._lib import SRMI_FLAG_DU_PASS
-    _engine_variants_agree(lr_hw, (0, SRMI_FLAG_DU_PASS), 0)
+    from srmi._lib import SRMI_FLAG_DU_PASS, call
+    trs = _engine_variants_agree(lr_hw, (0, SRMI_FLAG_DU_PASS), 0)
+    # the default engine really took the fused path (srmi_engine_probe which = 4), the
+    # du-pass one did not; 96-wide tiles are unfusable in both
+    fused = [call("srmi_engine_probe", t.engines[0]._h, 4, 1, None) for t in trs]
+    assert fused == ([0, 0] if lr_hw[1] == 96 else [1, 0]), fused
 
 
 @pytest.mark.parametrize("arch", ["rcan", "edsr"])
