@@ -207,8 +207,16 @@ struct srmi_engine {
   // per launch, so the reductions can wait for the group's end (one launch for all)
   std::vector<float*> slab_sets, bslab_sets;
   size_t slab_r_floats = 0, bslab_r_floats = 0;
-  float* slab_r(int b, int c) const { return slab_sets[(size_t)b * 2 + c]; }
-  float* bslab_r(int b, int c) const { return bslab_sets[(size_t)b * 2 + c]; }
+  // (SRMI_F2_MLP 0: the reductions ride in the next launch pair's CA-backward launch, so two
+  //  sets per conv alternate -- RCAB b by the parity of b, the group tail the other parity of
+  //  RCAB nblocks' -- and only four sets are ever touched)
+  int slab_idx(int b, int c) const {
+    if (SRMI_F2_MLP) return b * 2 + c;
+    const int q = b == 0 ? ((P.cfg.nblocks & 1) ^ 1) : (b & 1);
+    return (q + 1) * 2 + c;  // (sets 2 .. 5: the group tail's own (0, 1) slot is never allocated)
+  }
+  float* slab_r(int b, int c) const { return slab_sets[slab_idx(b, c)]; }
+  float* bslab_r(int b, int c) const { return bslab_sets[slab_idx(b, c)]; }
   float* lpart;
   int lpart_n;
   float* zeros;  // 256 zero bytes (DMA padding source)
@@ -338,7 +346,7 @@ static size_t carve(srmi_engine* e, char* base) {
                               (e->w % 48 == 0 ? e->w / 48 : 1));
       e->slab_r_floats = ns * 64 * 576;
       e->bslab_r_floats = ns * 64;
-      const int nsets = (P.cfg.nblocks + 1) * 2;
+      const int nsets = SRMI_F2_MLP ? (P.cfg.nblocks + 1) * 2 : 6;  // (slab_idx)
       e->slab_sets.assign(nsets, nullptr);
       e->bslab_sets.assign(nsets, nullptr);
       for (int i = 0; i < nsets; ++i) {
@@ -845,11 +853,16 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
                                 have_prev ? &prev1 : nullptr));
             have_prev = false;
           }
-        } else {  // (its reductions, too, at the group's end: the same sums as the default path's)
+        } else if (SRMI_F2_MLP) {  // (its reductions, too, at the group's end: the default path's sums)
           defer_prev();
           RC(ca_bwd_du_launch(g16 ? static_cast<const void*>(ghb) : ghf, g16, e->pacc, nstrips, e->recp(g, b),
                               prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du, e->brecp(g, b), e->f32, st, nullptr,
                               nullptr));
+        } else {  // (the reductions riding, as the default path's MLP launch carries them)
+          RC(ca_bwd_du_launch(g16 ? static_cast<const void*>(ghb) : ghf, g16, e->pacc, nstrips, e->recp(g, b),
+                              prm + r.ca_w1, prm + r.ca_w2, n, HW, 64, R, du, e->brecp(g, b), e->f32, st,
+                              have_prev ? &prev2 : nullptr, have_prev ? &prev1 : nullptr));
+          have_prev = false;
         }
         RC(dgrad_with_wgrad(e, cp, epi, wp, 2, st));
         const bool last = (b == 1);
