@@ -834,8 +834,11 @@ constexpr int kRedSets = 42;
 struct ReduceSets {
   ReduceSet s[kRedSets];
 };
-__global__ void __launch_bounds__(kRedQ * kRedPh) wgrad_reduce_sets_kernel(ReduceSets r) {
-  wgrad_reduce_body<kRedPh>(r.s[blockIdx.y], blockIdx.x);
+// (64 quads x 8 phases: a thread sums 8 of a launch's 64 slabs with 4 loads in flight, a
+//  block 256 outputs -- a quarter of the blocks of the 16 x 32 form, each latency-bound)
+constexpr int kSetQ = 64, kSetPh = 8;
+__global__ void __launch_bounds__(kSetQ * kSetPh) wgrad_reduce_sets_kernel(ReduceSets r) {
+  wgrad_reduce_body<kSetPh, kSetQ>(r.s[blockIdx.y], blockIdx.x);
 }
 
 int wgrad_reduce_sets_launch(const ReduceSet* sets, int n, hipStream_t st) {
@@ -846,8 +849,8 @@ int wgrad_reduce_sets_launch(const ReduceSet* sets, int n, hipStream_t st) {
       if (sets[i0 + i].Cout != sets[i0].Cout || sets[i0].Cout % 64) return SRMI_ERR_SHAPE;
       r.s[i] = sets[i0 + i];
     }
-    hipLaunchKernelGGL(wgrad_reduce_sets_kernel, dim3(wgrad_reduce_blocks(sets[i0].Cout), m), dim3(kRedQ * kRedPh), 0,
-                       st, r);
+    hipLaunchKernelGGL(wgrad_reduce_sets_kernel, dim3(wgrad_reduce_blocks(sets[i0].Cout, kSetQ), m),
+                       dim3(kSetQ * kSetPh), 0, st, r);
     SRMI_CHECK_LAUNCH();
   }
   return 0;

@@ -15,12 +15,14 @@ namespace srmi {
 // The bias slab ([nslab][Cout]) is handled by the last block(s).
 constexpr int kRedQ = 16, kRedPh = 32;
 // blocks of one slab reduction (Cout * 576 weights + Cout biases, kRedQ quads each)
-inline int wgrad_reduce_blocks(int Cout) { return Cout * 576 / (4 * kRedQ) + (Cout + 4 * kRedQ - 1) / (4 * kRedQ); }
+inline int wgrad_reduce_blocks(int Cout, int Q = kRedQ) { return Cout * 576 / (4 * Q) + (Cout + 4 * Q - 1) / (4 * Q); }
 
 // PH = slab phases per block (blockDim = kRedQ * PH: 32 -> 512 threads, 16 -> 256);
 // bid = this block's index within the reduction's wgrad_reduce_blocks(Cout)
 // slab16: the weight slabs are bf16 (4 values per 8-byte load), summed in fp32
-template <int PH>
+// (Q = output quads per block: kRedQ, or more quads and fewer phases for long runs of
+//  reductions, wgrad_reduce_sets_kernel)
+template <int PH, int Q = kRedQ>
 __device__ __forceinline__ void wgrad_reduce_body(const ReduceSet& rs, int bid) {
   const float* __restrict__ slab = rs.slab;
   const float* __restrict__ bslab = rs.bslab;
@@ -28,22 +30,22 @@ __device__ __forceinline__ void wgrad_reduce_body(const ReduceSet& rs, int bid) 
   const float alpha = rs.alpha;
   float* __restrict__ gw = rs.gw;
   float* __restrict__ gb = rs.gb;
-  __shared__ float4 red[PH][kRedQ], red2[4][kRedQ];
+  __shared__ float4 red[PH][Q], red2[4][Q];
   const int per = Cout * 576;
-  const int nwb = per / (4 * kRedQ);  // weight blocks (per % 64 == 0 since Cout % 64 == 0)
-  const int qd = threadIdx.x % kRedQ, ph = threadIdx.x / kRedQ;
+  const int nwb = per / (4 * Q);  // weight blocks (per % (4 Q) == 0: Cout % 64 == 0, Q | 576)
+  const int qd = threadIdx.x % Q, ph = threadIdx.x / Q;
   const bool is_w = bid < nwb;
   const float* src;
   int stride, o4, valid;
   if (is_w) {
     if (!gw) return;
-    o4 = bid * (4 * kRedQ) + qd * 4;
+    o4 = bid * (4 * Q) + qd * 4;
     src = slab + o4;
     stride = per;
     valid = 1;
   } else {
     if (!gb) return;
-    o4 = (bid - nwb) * (4 * kRedQ) + qd * 4;
+    o4 = (bid - nwb) * (4 * Q) + qd * 4;
     src = bslab + o4;
     stride = Cout;
     valid = o4 < Cout;
