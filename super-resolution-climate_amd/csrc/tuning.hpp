@@ -16,21 +16,24 @@
 #endif
 
 // Deferred conv epilogues (conv64_body.hpp conv64_defers), a bit mask: 1 RELU, 2 POOL,
-// 4 DG_RELUMASK, 8 DG_ACC_CA, 16 RELU_POOL, 32 CA_RESID, 64 DG_ACC_CA16.  Training: only DG_RELUMASK
-// gains in the step; inference (an image is one run of 12 strips): conv1's RELU_POOL
+// 4 DG_RELUMASK, 8 DG_ACC_CA, 16 RELU_POOL, 32 CA_RESID, 64 DG_ACC_CA16; 128: DG_ACC_CA16 in the
+// deferred body's register-direct form but right after its own strip (no LDS staging, one
+// barrier per strip).  Training: DG_RELUMASK and 128 (F1: +0.3 / +0.4 / +0.9 % on three boxes,
+// profiles/r06_ab_f1_epilogue_forms.txt, r06_ab_f1_imm_final.txt) gain in the step; 64 lost;
+// inference (an image is one run of 12 strips): conv1's RELU_POOL
 // (CA_RESID deferred measured 5 % slower: its pair codec competes with the next strip's
 // MFMA issue).
 #ifndef SRMI_TRAIN_DEFER
-#define SRMI_TRAIN_DEFER 4
+#define SRMI_TRAIN_DEFER 132
 #endif
 #ifndef SRMI_INFER_DEFER
 #define SRMI_INFER_DEFER 16
 #endif
 
-// F1 (EPI_DG_ACC_CA16) with its epilogue deferred (SRMI_TRAIN_DEFER bit 64): dgrad strips
-// per run handed to the paired filter-gradient workgroup
+// F1 (EPI_DG_ACC_CA16) in the deferred body (SRMI_TRAIN_DEFER bit 64 or 128): dgrad strips per
+// run handed to the paired filter-gradient workgroup (1, as the staged form's)
 #ifndef SRMI_F1_DEFER_TAIL
-#define SRMI_F1_DEFER_TAIL 0
+#define SRMI_F1_DEFER_TAIL 1
 #endif
 
 // du formed from g in the fused conv2 backward (ConvParams / WgradParams gx): where the
