@@ -200,8 +200,6 @@ struct srmi_engine {
   bf16_t* dPS[3];
   float *slab, *bslab;
   size_t slab_floats, bslab_floats;
-  // RCAB filter-gradient slabs: [RCAB parity][conv2, conv1] (the reduction of RCAB
-  // i runs in RCAB i+1's CA-backward launch, while RCAB i+1 writes the other parity)
   // the RCAB filter gradients' slab sets of one residual group: set (b, c) = RCAB b's conv2
   // (c = 0) / conv1 (c = 1) filter gradient, b = 1 .. nblocks; (0, 0) the group tail's.  One
   // per launch, so the reductions can wait for the group's end (one launch for all)
@@ -771,12 +769,12 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
       RC(conv_dgrad(e, P.body_tail, e->dRESb, n, h, w, EPI_DG_ACC, gRb, gRf, nullptr, nullptr, nullptr, nullptr,
                     nullptr, 1.f, st));
     }
-    // One stream, three launches per RCAB:
-    //   [CA backward -> du (+ the slab reductions of the previous RCAB)]
-    //   [dgrad conv2 -> dz  ||  filter gradient conv2 (t, du)]
+    // One stream, two launches per RCAB:
+    //   [the CA backward (MLP, du from g in LDS) -> dgrad conv2 -> dz || filter gradient conv2 (t, du)]
     //   [dgrad conv1 -> g (+ CA sums of the next RCAB)  ||  filter gradient conv1 (hb, dz)]
-    // The filter gradients write the slab set of their RCAB's parity; the last
-    // RCAB of a group reduces its own slabs before the group's event.
+    // (SRMI_FLAG_DU_PASS, exact fp32, unfusable shapes: a CA-backward launch writing du
+    // first).  The filter gradients write their RCAB's slab sets, reduced by one launch at
+    // the group's end, before the group's event.
     const int rs2 = rcab_row_splits(e, n, 2), rs1 = rcab_row_splits(e, n, 1);
     // the gradient stream INSIDE a residual group (w.r.t. every RCAB output): bf16 in the
     // bf16 engine, in the buffer of the group input gradient's bf16 copy (ghb: the group's

@@ -1,5 +1,6 @@
 // The deterministic slab reduction of the filter gradients (wgrad3x3.hip), shared
-// with the fused CA-backward + reduction launch of small.hip.
+// with the CA-backward launch of small.hip (which carries reductions in the SRMI_F2_MLP 0
+// variant) and the group-end multi-set launch.
 #pragma once
 #include "common.hpp"
 #include "srmi_internal.hpp"
