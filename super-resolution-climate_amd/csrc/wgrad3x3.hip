@@ -245,7 +245,9 @@ constexpr int NGP = 2 * GD + 2 * GX;                             // groups per p
 // 0-3 also issue the DMA (the 4-wave schedule) and the bias gradient; every wave
 // keeps all four output-channel tiles and writes its partial slab in the 4-wave
 // layout, so wgrad_reduce is unchanged.
-template <int WV, int NW = 4>
+// DUG: the instantiation that may form du from g (p.gx, the fused conv2 backward only): the
+// others carry none of its code (F1's launch had 20 SGPR spills with it compiled in)
+template <int WV, int NW = 4, bool DUG = false>
 __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, int chunk, int cb) {
   using namespace v4;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
@@ -426,7 +428,7 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   // them (as the dgrad's input ring, conv64_body_defer); s and dm / HW of the image in an
   // LDS table past the rings.  A lane's 16 B of group g are channels 8 c .. 8 c + 7, c =
   // cl0 (g even) / cl1 (g odd)
-  const bool gx = p.gx.rec != nullptr;  // (uniform)
+  const bool gx = DUG && p.gx.rec != nullptr;  // (uniform)
   float* const gxt = reinterpret_cast<float*>(smem + LDS);  // [s 64][dmh 64]
   auto gx_pair = [&](int P) __attribute__((always_inline)) {
     // (a wave's three dY groups of a pair are g = k % 6 of one parity: one channel chunk c)
@@ -604,20 +606,20 @@ __device__ __forceinline__ void wgrad48_body(const WgradParams& p, char* smem, i
   WSTAMP(63);
 }
 
-template <int NW = 4>
+template <int NW = 4, bool DUG = false>
 __device__ __forceinline__ void wgrad48_dispatch(const WgradParams& p, char* smem, int chunk, int cb) {
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: wgrad48_body<0, NW>(p, smem, chunk, cb); break;
-    case 1: wgrad48_body<1, NW>(p, smem, chunk, cb); break;
-    case 2: wgrad48_body<2, NW>(p, smem, chunk, cb); break;
-    case 3: wgrad48_body<3, NW>(p, smem, chunk, cb); break;
+    case 0: wgrad48_body<0, NW, DUG>(p, smem, chunk, cb); break;
+    case 1: wgrad48_body<1, NW, DUG>(p, smem, chunk, cb); break;
+    case 2: wgrad48_body<2, NW, DUG>(p, smem, chunk, cb); break;
+    case 3: wgrad48_body<3, NW, DUG>(p, smem, chunk, cb); break;
     default:
       if constexpr (NW == 8) {
         switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-          case 4: wgrad48_body<4, NW>(p, smem, chunk, cb); break;
-          case 5: wgrad48_body<5, NW>(p, smem, chunk, cb); break;
-          case 6: wgrad48_body<6, NW>(p, smem, chunk, cb); break;
-          default: wgrad48_body<7, NW>(p, smem, chunk, cb); break;
+          case 4: wgrad48_body<4, NW, DUG>(p, smem, chunk, cb); break;
+          case 5: wgrad48_body<5, NW, DUG>(p, smem, chunk, cb); break;
+          case 6: wgrad48_body<6, NW, DUG>(p, smem, chunk, cb); break;
+          default: wgrad48_body<7, NW, DUG>(p, smem, chunk, cb); break;
         }
       }
       break;
@@ -678,9 +680,9 @@ __global__ void __launch_bounds__(NW * 64, 1) rcab_bwd_kernel(ConvParams cp, int
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // every wave is past its last LDS access of the strips
   }
-  wgrad48_dispatch<NW>(wp, smem, w % nch, w / nch);
+  wgrad48_dispatch<NW, EPI == EPI_DG_RELUMASK>(wp, smem, w % nch, w / nch);
 #else
-  wgrad48_dispatch<NW>(wp, smem, w % nch, w / nch);
+  wgrad48_dispatch<NW, EPI == EPI_DG_RELUMASK>(wp, smem, w % nch, w / nch);
   if (tail > 0) {
     __syncthreads();  // every wave is past its last LDS read of the chunk
     conv64_body<48, EPI, NW>(cp, run_len, w, smem, tail, true);
