@@ -884,8 +884,9 @@ static int backward_impl(srmi_engine* e, const float* prm, const float* lr, cons
       }
       defer_prev();
       if (!group_sets.empty()) RC(wgrad_reduce_sets_launch(group_sets.data(), (int)group_sets.size(), st));
-      RC(ca_param_grads_batched_launch(e->recp(g, 1), e->brecp(g, 1), nb, n, e->N, 64, R, e->d_caoffs + (size_t)g * nb * 5,
-                                       grads, st));
+      // per-RCAB slots of recp / brecp (N x 160 and N x 224 floats at any CR <= 32)
+      RC(ca_param_grads_batched_launch(e->recp(g, 1), e->brecp(g, 1), nb, n, (size_t)e->N * 160, (size_t)e->N * 224,
+                                       64, R, e->d_caoffs + (size_t)g * nb * 5, grads, st));
       // the group's gradients are final here (one stream): the hook for a bucketed
       // all-reduce overlapped with the rest of backward
       if (group_events && group_events[g]) HC(hipEventRecord(reinterpret_cast<hipEvent_t>(group_events[g]), st));

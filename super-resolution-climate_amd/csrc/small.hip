@@ -1473,17 +1473,18 @@ int ca_bwd_du_launch(const void* g, int g16, const float* part, int nstrips, con
 // the conv2 bias grad.  offs[k*5 + {0..4}] = grad offsets of
 // conv_du.0.weight, conv_du.0.bias, conv_du.2.weight, conv_du.2.bias, conv2.bias
 __global__ void __launch_bounds__(256) ca_param_grads_kernel(const float* __restrict__ recs,
-                                                             const float* __restrict__ brecs, int N, int Ncap, int C,
-                                                             int CR, const long long* __restrict__ offs,
+                                                             const float* __restrict__ brecs, int N, size_t rstride,
+                                                             size_t bstride, int C, int CR,
+                                                             const long long* __restrict__ offs,
                                                              float* __restrict__ grads) {
   // blockIdx.y < 2*C*CR/256: one weight gradient per thread; the last y slice
   // does the biases.  Image sums run in a fixed order (deterministic).  The
-  // records of consecutive RCABs are Ncap (the engine's capacity) images apart;
-  // the first N images are summed.
+  // records of consecutive RCABs are rstride / bstride floats apart (the engine's
+  // slots: capacity x the widest record, whatever CR is); the first N images are summed.
   const int k = blockIdx.x;
   const int rs = 2 * C + CR;
-  const float* rec = recs + (size_t)k * Ncap * rs;
-  const float* brec = brecs + (size_t)k * Ncap * (rs + C);  // [N][rs] then dm[N][C]
+  const float* rec = recs + (size_t)k * rstride;
+  const float* brec = brecs + (size_t)k * bstride;  // [N][rs] then dm[N][C]
   const int nw = 2 * C * CR;
   const int o = blockIdx.y * 256 + threadIdx.x;
   if ((int)blockIdx.y * 256 < nw) {
@@ -1536,12 +1537,12 @@ __global__ void __launch_bounds__(256) ca_param_grads_kernel(const float* __rest
   }
 }
 
-int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int Ncap, int C, int R,
-                                  const long long* offs, float* grads, hipStream_t st) {
-  if (N < 1 || N > Ncap) return SRMI_ERR_ARG;
+int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, size_t rstride,
+                                  size_t bstride, int C, int R, const long long* offs, float* grads, hipStream_t st) {
   const int CR = C / R;
+  if (N < 1 || (size_t)N * (2 * C + CR) > rstride || (size_t)N * (3 * C + CR) > bstride) return SRMI_ERR_ARG;
   const int ny = (2 * C * CR + 255) / 256 + 1;
-  hipLaunchKernelGGL(ca_param_grads_kernel, dim3(nblocks, ny), dim3(256), 0, st, recs, brecs, N, Ncap, C, CR, offs,
+  hipLaunchKernelGGL(ca_param_grads_kernel, dim3(nblocks, ny), dim3(256), 0, st, recs, brecs, N, rstride, bstride, C, CR, offs,
                      grads);
   SRMI_CHECK_LAUNCH();
   return 0;

@@ -234,8 +234,8 @@ int rcab_infer_launch(const ConvParams& c1, const ConvParams& c2, const float* p
                       const float* b1, const float* w2, const float* b2, int CR, const float* h_in, const void* hi_in,
                       const void* lo_in, void* hi_out, void* lo_out, float* rec, hipStream_t st);
 // records of consecutive RCABs Ncap images apart (the engine capacity), N summed
-int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, int Ncap, int C, int R,
-                                  const long long* offs, float* grads, hipStream_t st);
+int ca_param_grads_batched_launch(const float* recs, const float* brecs, int nblocks, int N, size_t rstride,
+                                  size_t bstride, int C, int R, const long long* offs, float* grads, hipStream_t st);
 
 int adam_launch(float* p, const float* g, float* m, float* v, size_t n, float lr, float b1, float b2, float eps,
                 float wd, float step_size, float bc2_sqrt, hipStream_t st);

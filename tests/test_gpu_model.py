@@ -297,7 +297,7 @@ def test_checkpoint_resume_matches_uninterrupted():
     assert torch.equal(a.m, c.m) and torch.equal(a.v, c.v)
 
 
-def _engine_variants_agree(lr_hw, flags, grad_tol, fwd_tol=None):
+def _engine_variants_agree(lr_hw, flags, grad_tol, fwd_tol=None, cb=2):
     """One training step of the same weights and tiles through two engine variants
     (srmi_model_config.flags): the forward is untouched (fwd_tol None: bit-identical
     output and loss; else output rel. L2 and loss within fwd_tol), the gradients agree
@@ -308,7 +308,7 @@ def _engine_variants_agree(lr_hw, flags, grad_tol, fwd_tol=None):
     h, w = lr_hw
     C, nl, nb, B = 2, 2, 4, 6
     specs = [NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=nl, nblocks=nb,
-                     cbottleneck=2, scale=4, flags=f) for f in flags]
+                     cbottleneck=cb, scale=4, flags=f) for f in flags]
     table = _table(specs[0])
     flat = torch.empty(sum(t[2] for t in table))
     default_init_(flat, table, seed=21)
@@ -328,7 +328,7 @@ def _engine_variants_agree(lr_hw, flags, grad_tol, fwd_tol=None):
         assert torch.equal(ga, gb)
     else:
         assert rel_l2(ga, gb) < grad_tol
-    model = ro.RCANOracle(nchannels_in=C, nchannels_out=C, nlayers=nl, nblocks=nb, nfeatures=64, cbottleneck=2).double()
+    model = ro.RCANOracle(nchannels_in=C, nchannels_out=C, nlayers=nl, nblocks=nb, nfeatures=64, cbottleneck=cb).double()
     sd = dict(model.named_parameters())
     with torch.no_grad():
         for name, off, n, shape in table:
@@ -374,6 +374,19 @@ def test_du_from_g_matches_du_pass(lr_hw):
     # du-pass one did not; 96-wide tiles are unfusable in both
     fused = [call("srmi_engine_probe", t.engines[0]._h, 4, 1, None) for t in trs]
     assert fused == ([0, 0] if lr_hw[1] == 96 else [1, 0]), fused
+
+
+@pytest.mark.parametrize("cb", [8, 16])
+def test_du_from_g_matches_du_pass_other_bottlenecks(cb):
+    """As above at CA bottlenecks of 64 / 8 = 8 and 64 / 16 = 4 channels (the reference's
+    default is 32): the MLP's thread mapping (ca_bwd.hpp) at every CR the fused path takes.
+    The oracle check also pins the CA parameter gradients of RCABs 2..nb at CR < 32: the
+    batched kernel once stepped between RCABs by N x (2C + CR) floats instead of the
+    engine's N x 160 / N x 224 slots, reading uninitialised memory (bit-different between
+    two engines, and wrong in both)."""
+    from srmi._lib import SRMI_FLAG_DU_PASS, call
+    trs = _engine_variants_agree((48, 48), (0, SRMI_FLAG_DU_PASS), 0, cb=cb)
+    assert [call("srmi_engine_probe", t.engines[0]._h, 4, 1, None) for t in trs] == [1, 0]
 
 
 @pytest.mark.parametrize("arch", ["rcan", "edsr"])
