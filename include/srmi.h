@@ -71,7 +71,8 @@ typedef struct srmi_model_config {
   int nfeatures;     /* model.nfeatures (64)                                */
   int nlayers;       /* RCAN residual groups / EDSR resblocks               */
   int nblocks;       /* RCAN RCABs per group (ignored for EDSR)             */
-  int reduction;     /* RCAN model.cbottleneck (channel-attention reduction) */
+  int reduction;     /* RCAN model.cbottleneck (channel-attention reduction): 64 / reduction
+                        in 4 .. 32 and a multiple of 4 (else SRMI_ERR_UNSUPPORTED) */
   int scale;         /* prod(model.downscale_factors): 2, 4 or 8            */
   float res_scale;   /* EDSR model.res_scale                                */
   int batch;         /* max tiles per call (workspace capacity)             */

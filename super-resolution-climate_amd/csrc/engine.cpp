@@ -82,6 +82,9 @@ int build_plan(const srmi_model_config* cfg, Plan& P) {
   if (c.scale != 2 && c.scale != 4 && c.scale != 8) return SRMI_ERR_UNSUPPORTED;
   if (c.nlayers < 1 || c.batch < 1 || c.lr_h < 4 || c.lr_w < 16) return SRMI_ERR_ARG;
   if (c.arch == SRMI_ARCH_RCAN && (c.nblocks < 1 || c.reduction < 1 || 64 % c.reduction)) return SRMI_ERR_ARG;
+  // the CA kernels take CR = 64 / reduction in 4 .. 32, a multiple of 4 (records sized for 32):
+  // refused here rather than at the first CA launch
+  if (c.arch == SRMI_ARCH_RCAN && (64 / c.reduction > 32 || (64 / c.reduction) % 4)) return SRMI_ERR_UNSUPPORTED;
   if (c.arch != SRMI_ARCH_RCAN && c.arch != SRMI_ARCH_EDSR) return SRMI_ERR_ARG;
   if (c.dtype != SRMI_DTYPE_BF16 && c.dtype != SRMI_DTYPE_F32) return SRMI_ERR_ARG;
   if (c.flags & ~(SRMI_FLAG_NO_RCAB_INFER | SRMI_FLAG_CA_PASS | SRMI_FLAG_DU_PASS)) return SRMI_ERR_ARG;  // (retired bits refused)

@@ -66,6 +66,14 @@ def test_workspace_sizes_are_sane():
     bad = spec.cstruct(64, 47, 48)
     with pytest.raises(_lib.SrmiError):
         _lib.call("srmi_workspace_size", C.byref(bad), 1, C.byref(tb))
+    # CA bottlenecks: CR = 64 / cbottleneck must be 4 .. 32 and a multiple of 4
+    for cb in (4, 8, 16):
+        ok = NetSpec(arch="rcan", nchannels_in=2, nchannels_out=2, nlayers=2, nblocks=2, cbottleneck=cb)
+        _lib.call("srmi_workspace_size", C.byref(ok.cstruct(8, 48, 48)), 1, C.byref(tb))
+    for cb in (1, 32, 64):
+        bad = NetSpec(arch="rcan", nchannels_in=2, nchannels_out=2, nlayers=2, nblocks=2, cbottleneck=cb)
+        with pytest.raises(_lib.SrmiError):
+            _lib.call("srmi_workspace_size", C.byref(bad.cstruct(8, 48, 48)), 1, C.byref(tb))
 
 
 def test_engine_refuses_maps_past_the_32bit_buffer_range():
