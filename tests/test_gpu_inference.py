@@ -170,15 +170,17 @@ def test_tiled_inference_micro_engines_bit_identical(graph):
             assert loss == ref_loss
 
 
-@pytest.mark.parametrize("C,nl,nb,hw,N", [(1, 2, 3, (48, 48), 5), (2, 1, 2, (32, 48), 3), (1, 1, 1, (8, 48), 2)])
-def test_fused_inference_rcab_matches_three_launches_and_oracle(C, nl, nb, hw, N):
+@pytest.mark.parametrize("C,nl,nb,hw,N,cb", [(1, 2, 3, (48, 48), 5, 2), (2, 1, 2, (32, 48), 3, 2), (1, 1, 1, (8, 48), 2, 2),
+                                           (2, 1, 3, (48, 48), 3, 8), (1, 2, 2, (32, 48), 2, 16)])
+def test_fused_inference_rcab_matches_three_launches_and_oracle(C, nl, nb, hw, N, cb):
     """The inference RCAB as one launch with a workgroup per image (rcab_infer.hip:
     conv1 + sums of the bf16 t -> mean(u) from t's statistics with conv2's bf16 filter
     image and the CA MLP -> conv2 whose epilogue writes h + s u; u is never stored)
     against the three launches (SRMI_FLAG_NO_RCAB_INFER: conv1, conv2 + pool, CA pass)
     and the fp64 oracle forward.  The one launch differs from the three only in the
     summation order of mean(u) and in adding the fp32 u to h instead of bf16(u), so
-    both sit within bf16 noise of the oracle and of each other."""
+    both sit within bf16 noise of the oracle and of each other.  cb: the CA bottleneck
+    (CR = 64 / cb = 32, 8, 4)."""
     from srmi._lib import SRMI_FLAG_NO_RCAB_INFER
     from srmi.engine import Engine
     from srmi.trainer import default_init_
@@ -186,7 +188,7 @@ def test_fused_inference_rcab_matches_three_launches_and_oracle(C, nl, nb, hw, N
     out = []
     for flags in (0, SRMI_FLAG_NO_RCAB_INFER):
         spec = NetSpec(arch="rcan", nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=nl, nblocks=nb,
-                       cbottleneck=2, scale=4, flags=flags)
+                       cbottleneck=cb, scale=4, flags=flags)
         table = param_table(spec)
         flat = torch.empty(sum(t[2] for t in table), device=d)
         default_init_(flat, table, seed=3)
@@ -197,7 +199,7 @@ def test_fused_inference_rcab_matches_three_launches_and_oracle(C, nl, nb, hw, N
         out.append(e.forward(flat, lr.to(d)).clone().cpu().double())
     torch.cuda.synchronize()
     model = ro.RCANOracle(nchannels_in=C, nchannels_out=C, nlayers=nl, nblocks=nb, nfeatures=64,
-                          cbottleneck=2).double()
+                          cbottleneck=cb).double()
     sd = dict(model.named_parameters())
     fl = flat.cpu()
     with torch.no_grad():
