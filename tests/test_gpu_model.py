@@ -121,15 +121,15 @@ def test_small_model_step_vs_golden(arch, C, nl, nb, scale, S, B, gname):
     assert abs(loss1 - float(gd["loss1"])) / float(gd["loss1"]) < 2e-3, (loss1, float(gd["loss1"]))
 
 
-@pytest.mark.parametrize("factors,lr", [([2], 48), ([2, 2, 2], 32)])
-def test_rcan_other_scales_vs_oracle(factors, lr):
+@pytest.mark.parametrize("factors,lr,C", [([2], 48, 2), ([2, 2, 2], 32, 2), ([2, 2], 48, 3), ([2, 2], 32, 4)])
+def test_rcan_other_scales_vs_oracle(factors, lr, C):
     """RCAN at downscale_factors [2] and [2, 2, 2] (the headline is [2, 2]: one and three
-    pixel-shuffle stages in the upsampler, sres/model/common/common.py Upsampler) against
-    the fp64 oracle on the same weights and tiles (no golden file: the oracle itself is
-    pinned by the x4 goldens above): loss and every gradient tensor within the bf16
-    drift bounds."""
+    pixel-shuffle stages in the upsampler, sres/model/common/common.py Upsampler), and at
+    x4 with 3 and 4 variables (the goldens hold 1 and 2), against the fp64 oracle on the
+    same weights and tiles (no golden file: the oracle itself is pinned by the goldens
+    above): loss and every gradient tensor within the bf16 drift bounds."""
     d = dev()
-    scale, C, nl, nb, B = int(np.prod(factors)), 2, 2, 2, 2
+    scale, nl, nb, B = int(np.prod(factors)), 2, 2, 2
     model = ro.RCANOracle(nchannels_in=C, nchannels_out=C, nlayers=nl, nblocks=nb, nfeatures=64, cbottleneck=2,
                           downscale_factors=factors)
     ro.init_params_numpy(model, 3)
