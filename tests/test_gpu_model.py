@@ -44,8 +44,8 @@ def flat_from_model(model, table):
     return flat
 
 
-def spec_of(arch, C, nl, nb=0, scale=4, rs=1.0):
-    return NetSpec(arch=arch, nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=nl, nblocks=nb, cbottleneck=2,
+def spec_of(arch, C, nl, nb=0, scale=4, rs=1.0, cb=2):
+    return NetSpec(arch=arch, nchannels_in=C, nchannels_out=C, nfeatures=64, nlayers=nl, nblocks=nb, cbottleneck=cb,
                    scale=scale, res_scale=rs)
 
 
@@ -269,14 +269,16 @@ def test_plugin_module_reference_style_step():
     assert len(meta["keys"]["rcan_small_c2"]) == len(sd)
 
 
-def test_micro_batch_step_matches_single_engine():
+@pytest.mark.parametrize("cb", [2, 8])
+def test_micro_batch_step_matches_single_engine(cb):
     """FusedTrainer(micro=2) -- two half-batch engines on two streams -- computes the
     same step as one engine: the loss comes from per-tile parts summed in tile order
     (srmi_tile_loss_parts / srmi_loss_from_parts), so it is bit-identical whatever the
     split, and the gradients agree up to fp32 summation order.  (A 1-ulp loss
-    difference would scale the bf16 gradient maps and flip roundings: 4e-5.)"""
+    difference would scale the bf16 gradient maps and flip roundings: 4e-5.)  cb: the
+    CA bottleneck (CR = 32, 8; the engines' record slots at a narrower CR)."""
     d = dev()
-    spec = spec_of("rcan", 2, 2, 3)
+    spec = spec_of("rcan", 2, 2, 3, cb=cb)
     table = _table(spec)
     from srmi.trainer import default_init_
     flat = torch.empty(sum(t[2] for t in table), device=d)
